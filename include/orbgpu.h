@@ -1,0 +1,149 @@
+/* orbgpu.h -- C ABI of the MI355X ORB front-end (liborbgpu.so).
+ *
+ * Plain C: pointers, sizes, int status codes, no torch / OpenCV / HIP types in signatures
+ * (streams travel as void*).  One context per stream/thread; no globals.
+ *
+ * Each entry point names the reference interface it replaces (paths relative to the
+ * Lynx-MR/orbslam3lib root, cpp/ = app/src/main/cpp/):
+ *   - ORBextractor ctor + operator()      cpp/include/ORBextractor_old.h:51-59,
+ *                                         cpp/src/ORBextractor_old.cc:411-471, 1088-1191
+ *   - stereo operator()(AHardwareBuffer*) cpp/include/ORBextractor.h:52-57 /
+ *                                         cpp/src/ORBextractor.cc:118-165
+ *   - FastRPC extractFeatures/bfMatchStereo  cpp/inc/orbslam3.idl:15-21 (impl
+ *                                         dsp/src/orbslam_dsp.cpp:866-1087)
+ *   - LynxHardwareAccelerator::{ctor,ExtractORB,BFMatchORB,dtor}
+ *                                         cpp/include/LynxHardwareAcceleration/
+ *                                         LynxHardwareAccelerator.h:45-51
+ *   - ORBmatcher::DescriptorDistance      cpp/include/ORBmatcher.h:44, cpp/src/ORBmatcher.cc:2107
+ *   - cv::BFMatcher(NORM_HAMMING).knnMatch(k=2)  cpp/src/Frame.cc:45,1227
+ *   - mvImagePyramid (public member)      cpp/include/ORBextractor_old.h:80
+ */
+#ifndef ORBGPU_H_
+#define ORBGPU_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ORBGPU_ABI_VERSION 1
+
+/* Status codes (the DSP path returned 1/3/7 and callers ignored them; we never exit()). */
+enum {
+    ORBGPU_OK = 0,
+    ORBGPU_ERR_EMPTY_IMAGE = -1,  /* reference operator() returns -1 on an empty image (:1092) */
+    ORBGPU_ERR_CAPACITY = -2,     /* caller buffer / context capacity too small */
+    ORBGPU_ERR_INVALID = -3,      /* bad argument */
+    ORBGPU_ERR_HIP = -4,          /* HIP runtime error (see orbgpu_last_error) */
+    ORBGPU_ERR_OVERFLOW = -5,     /* device-side workspace overflow (keys / nodes) */
+    ORBGPU_ERR_NO_DEVICE = -6     /* no usable gfx950 device */
+};
+
+/* The 5 ORB parameters of the ORBextractor ctor / Settings.cc:443-451. */
+typedef struct {
+    int32_t nfeatures;
+    float scale_factor;
+    int32_t nlevels;
+    int32_t ini_th_fast;
+    int32_t min_th_fast;
+} orbgpu_params;
+
+/* cv::KeyPoint field layout (28 B): pt.x, pt.y, size, angle, response, octave, class_id. */
+typedef struct {
+    float x, y, size, angle, response;
+    int32_t octave, class_id;
+} orbgpu_keypoint;
+
+typedef struct orbgpu_ctx orbgpu_ctx;
+
+/* Build a context for images up to max_width x max_height and batches of up to max_images
+ * images.  Allocates all device memory once (nothing is allocated per call).  device = HIP
+ * ordinal.  Replaces the ORBextractor ctor + LynxHardwareAccelerator ctor (orbslam3_open). */
+int orbgpu_create(const orbgpu_params* params, int device, int max_width, int max_height,
+                  int max_images, orbgpu_ctx** out_ctx);
+int orbgpu_destroy(orbgpu_ctx* ctx); /* orbslam3_close */
+
+/* Scale tables exactly as the ORBextractor getters return them (GetScaleFactors, ...). */
+int orbgpu_get_scale_tables(const orbgpu_ctx* ctx, float* scale, float* inv_scale,
+                            float* sigma2, float* inv_sigma2, int32_t* features_per_level);
+
+/* ORBextractor::operator()(image, mask, keypoints, descriptors, vLappingArea) on one host
+ * image (u8, row stride `stride`).  Writes *n keypoints (cv::KeyPoint layout) and n x 32 B
+ * descriptors (row i <-> keypoint i), mono first / lapping-area keypoints from the back;
+ * *n_mono = return value of the reference (monoIndex).  cap = capacity of kps/desc. */
+int orbgpu_extract(orbgpu_ctx* ctx, const uint8_t* image, int width, int height, int stride,
+                   int lap0, int lap1, orbgpu_keypoint* kps, uint8_t* desc, int cap, int* n,
+                   int* n_mono);
+
+/* Stereo form (ORBextractor.h:52-57 / IDL extractFeatures): left and right images in one call,
+ * both on the device together. */
+int orbgpu_extract_stereo(orbgpu_ctx* ctx, const uint8_t* left, const uint8_t* right, int width,
+                          int height, int stride, const int lap_left[2], const int lap_right[2],
+                          orbgpu_keypoint* kps_left, uint8_t* desc_left, int* n_left,
+                          int* mono_left, orbgpu_keypoint* kps_right, uint8_t* desc_right,
+                          int* n_right, int* mono_right, int cap);
+
+/* ---- device-resident batch API (the throughput path) --------------------------------------
+ * Images live in the context's HBM input buffer: [n_images][height][width] u8 (pitch = width).
+ * orbgpu_upload_images copies host pixels in (PCIe; not part of the timed hot path).
+ * orbgpu_run_batch runs the whole front-end for n_images images on `stream` (void* hipStream_t,
+ * NULL = the context's own stream) and leaves keypoints/descriptors/counts in HBM.
+ * laps: n_images x {lap0, lap1}, host pointer (copied into the launch arguments). */
+int orbgpu_upload_images(orbgpu_ctx* ctx, const uint8_t* images, int n_images, int width,
+                         int height, int stride);
+uint8_t* orbgpu_device_input(orbgpu_ctx* ctx); /* device pointer of the input buffer */
+int orbgpu_run_batch(orbgpu_ctx* ctx, int n_images, int width, int height, const int32_t* laps,
+                     void* stream);
+/* Copy image i's results to the host (after orbgpu_synchronize or on the same stream). */
+int orbgpu_download_result(orbgpu_ctx* ctx, int image, orbgpu_keypoint* kps, uint8_t* desc,
+                           int cap, int* n, int* n_mono);
+/* Per-image keypoint counts and mono counts of the last batch (host arrays of n_images). */
+int orbgpu_download_counts(orbgpu_ctx* ctx, int n_images, int32_t* n, int32_t* n_mono);
+int orbgpu_synchronize(orbgpu_ctx* ctx);
+
+/* Pyramid level `level` of batch image `image` (mvImagePyramid[level]), optionally blurred
+ * (the GaussianBlur'd working copy, ORBextractor_old.cc:1146-1147). */
+int orbgpu_get_pyramid_level(orbgpu_ctx* ctx, int image, int level, int blurred, uint8_t* dst,
+                             int dst_stride, int* width, int* height);
+
+/* Level keypoints before assembly (level coordinates, octree order, with angle) and their
+ * descriptors: for per-stage parity tests.  counts[nlevels]. */
+int orbgpu_get_level_keypoints(orbgpu_ctx* ctx, int image, orbgpu_keypoint* kps, uint8_t* desc,
+                               int cap, int32_t* counts);
+
+/* ---- Hamming matching ---------------------------------------------------------------------
+ * cv::BFMatcher(NORM_HAMMING).knnMatch(query, train, matches, 2): for each query row the best
+ * and second-best train rows (lexicographic (distance, index): lowest index wins ties);
+ * idx = -1 / dist = INT32_MAX when absent (nt < 2).  Host pointers, n x 32 B each. */
+int orbgpu_match_knn2(orbgpu_ctx* ctx, const uint8_t* query, int nq, const uint8_t* train, int nt,
+                      int32_t* idx1, int32_t* dist1, int32_t* idx2, int32_t* dist2);
+/* Batch stereo matching on device-resident results of the last orbgpu_run_batch: pair p
+ * matches image 2p (query) against image 2p+1 (train), rows [mono..n) of each when
+ * stereo_rows_only != 0 (Frame::ComputeStereoFishEyeMatches, Frame.cc:1142-1148) or all rows.
+ * Results stay in HBM; fetch with orbgpu_download_matches. */
+int orbgpu_match_stereo_batch(orbgpu_ctx* ctx, int n_pairs, int stereo_rows_only, void* stream);
+int orbgpu_download_matches(orbgpu_ctx* ctx, int pair, int32_t* idx1, int32_t* dist1,
+                            int32_t* idx2, int32_t* dist2, int cap, int* nq);
+
+/* ORBmatcher::DescriptorDistance on two 32-byte descriptors (host, no device work). */
+int orbgpu_descriptor_distance(const uint8_t* a, const uint8_t* b);
+
+/* ---- instrumentation ----------------------------------------------------------------------
+ * When enabled, every kernel launch of run_batch/match_stereo_batch is bracketed by HIP events
+ * on its stream; orbgpu_stage_times returns the summed milliseconds and launch counts per
+ * stage since the last reset.  Stage names via orbgpu_stage_name. */
+int orbgpu_set_profiling(orbgpu_ctx* ctx, int enable);
+int orbgpu_num_stages(void);
+const char* orbgpu_stage_name(int stage);
+int orbgpu_stage_times(orbgpu_ctx* ctx, double* ms, int64_t* launches, int max_stages);
+int orbgpu_reset_stage_times(orbgpu_ctx* ctx);
+
+const char* orbgpu_last_error(void);
+int orbgpu_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ORBGPU_H_ */

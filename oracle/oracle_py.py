@@ -1,0 +1,214 @@
+"""ctypes binding of the CPU oracle -- TEST INFRASTRUCTURE ONLY.
+
+Imported only by tests/, __graft_entry__.smoke() (as the checker) and bench.py's cpu_baseline
+leg.  The product path (orbslam3lib_amd) never imports this module.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "build", "liborb_oracle.so")
+
+KP_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                     ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
+
+
+class OracleKP(C.Structure):
+    _fields_ = [("x", C.c_float), ("y", C.c_float), ("size", C.c_float), ("angle", C.c_float),
+                ("response", C.c_float), ("octave", C.c_int32), ("class_id", C.c_int32)]
+
+
+_lib = None
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", HERE])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        _lib = C.CDLL(LIB_PATH)
+        _lib.oracle_fast_atan2.restype = C.c_float
+        _lib.oracle_fast_atan2.argtypes = [C.c_float, C.c_float]
+        _lib.oracle_ic_angle.restype = C.c_float
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def level_sizes(w, h, scale_factor=1.2, nlevels=8):
+    lw = np.zeros(nlevels, np.int32)
+    lh = np.zeros(nlevels, np.int32)
+    lib().oracle_level_sizes(C.c_float(scale_factor), nlevels, w, h, _p(lw), _p(lh))
+    return list(zip(lw.tolist(), lh.tolist()))
+
+
+def pyramid(img, scale_factor=1.2, nlevels=8):
+    h, w = img.shape
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    sizes = level_sizes(w, h, scale_factor, nlevels)
+    out = np.zeros(sum(a * b for a, b in sizes), np.uint8)
+    lib().oracle_pyramid(C.c_float(scale_factor), nlevels, _p(img), w, h, w, _p(out))
+    levels, off = [], 0
+    for lw_, lh_ in sizes:
+        levels.append(out[off:off + lw_ * lh_].reshape(lh_, lw_))
+        off += lw_ * lh_
+    return levels
+
+
+def resize(src, dw, dh):
+    src = np.ascontiguousarray(src, dtype=np.uint8)
+    dst = np.zeros((dh, dw), np.uint8)
+    lib().oracle_resize(_p(src), src.shape[1], src.shape[0], src.shape[1], _p(dst), dw, dh, dw)
+    return dst
+
+
+def blur(img):
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    out = np.zeros_like(img)
+    lib().oracle_gaussian_blur(_p(img), img.shape[1], img.shape[0], _p(out))
+    return out
+
+
+def blur_kernel():
+    k = np.zeros(7, np.int32)
+    lib().oracle_blur_kernel(_p(k))
+    return k.tolist()
+
+
+def resize_simd_end(width):
+    return lib().oracle_resize_simd_end(width)
+
+
+def fast(img, th, roi=None):
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    h, w = img.shape
+    x0, y0, cols, rows = roi if roi else (0, 0, w, h)
+    cap = max(16, cols * rows // 2)
+    out = np.zeros(cap, KP_DTYPE)
+    n = lib().oracle_fast(_p(img), w, x0, y0, cols, rows, th, _p(out), cap)
+    return out[:n]
+
+
+def corner_score(img, x, y, th):
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    return lib().oracle_corner_score(_p(img), img.shape[1], x, y, th)
+
+
+def level_candidates(lvl, ini_th=20, min_th=7):
+    lvl = np.ascontiguousarray(lvl, dtype=np.uint8)
+    cap = lvl.size // 2 + 16
+    out = np.zeros(cap, KP_DTYPE)
+    n = lib().oracle_level_candidates(_p(lvl), lvl.shape[1], lvl.shape[0], ini_th, min_th,
+                                      _p(out), cap)
+    return out[:n]
+
+
+def distribute_octree(keys, minX, maxX, minY, maxY, N):
+    keys = np.ascontiguousarray(keys, dtype=KP_DTYPE)
+    cap = max(16, 4 * max(N, 1) + len(keys))
+    out = np.zeros(cap, KP_DTYPE)
+    m = lib().oracle_distribute_octree(_p(keys), len(keys), minX, maxX, minY, maxY, N, _p(out), cap)
+    return out[:m]
+
+
+def fast_atan2(y, x):
+    return lib().oracle_fast_atan2(float(y), float(x))
+
+
+def ic_angle(img, x, y):
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    return lib().oracle_ic_angle(_p(img), img.shape[1], int(x), int(y))
+
+
+def orb_descriptor(blurred, x, y, angle):
+    blurred = np.ascontiguousarray(blurred, dtype=np.uint8)
+    d = np.zeros(32, np.uint8)
+    lib().oracle_orb_descriptor(_p(blurred), blurred.shape[1], C.c_float(x), C.c_float(y),
+                                C.c_float(angle), _p(d))
+    return d
+
+
+def umax():
+    u = np.zeros(16, np.int32)
+    lib().oracle_umax(_p(u))
+    return u.tolist()
+
+
+def features_per_level(nfeatures, scale_factor=1.2, nlevels=8):
+    o = np.zeros(nlevels, np.int32)
+    lib().oracle_features_per_level(nfeatures, C.c_float(scale_factor), nlevels, _p(o))
+    return o.tolist()
+
+
+def scale_factors(scale_factor=1.2, nlevels=8):
+    arr = [np.zeros(nlevels, np.float32) for _ in range(4)]
+    lib().oracle_scale_factors(C.c_float(scale_factor), nlevels, *[_p(a) for a in arr])
+    return arr
+
+
+def extract(img, nfeatures=1000, scale_factor=1.2, nlevels=8, ini_th=20, min_th=7, lap=(0, 0)):
+    """ORBextractor::operator() -> (keypoints[KP_DTYPE], descriptors[N,32], monoIndex)."""
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    h, w = img.shape
+    cap = 4 * nfeatures + 64 * nlevels
+    kps = np.zeros(cap, KP_DTYPE)
+    desc = np.zeros((cap, 32), np.uint8)
+    n = C.c_int(0)
+    mono = lib().oracle_extract(nfeatures, C.c_float(scale_factor), nlevels, ini_th, min_th,
+                                _p(img), w, h, w, int(lap[0]), int(lap[1]), _p(kps), _p(desc),
+                                cap, C.byref(n))
+    if mono < 0:
+        raise RuntimeError("oracle_extract failed: %d" % mono)
+    return kps[:n.value], desc[:n.value], mono
+
+
+def extract_levels(img, nfeatures=1000, scale_factor=1.2, nlevels=8, ini_th=20, min_th=7):
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    h, w = img.shape
+    cap = 4 * nfeatures + 64 * nlevels
+    kps = np.zeros(cap, KP_DTYPE)
+    desc = np.zeros((cap, 32), np.uint8)
+    cnt = np.zeros(nlevels, np.int32)
+    n = lib().oracle_extract_levels(nfeatures, C.c_float(scale_factor), nlevels, ini_th, min_th,
+                                    _p(img), w, h, w, _p(kps), _p(desc), cap, _p(cnt))
+    if n < 0:
+        raise RuntimeError("oracle_extract_levels failed: %d" % n)
+    out, off = [], 0
+    for c in cnt.tolist():
+        out.append((kps[off:off + c], desc[off:off + c]))
+        off += c
+    return out
+
+
+def descriptor_distance(a, b):
+    a = np.ascontiguousarray(a, dtype=np.uint8)
+    b = np.ascontiguousarray(b, dtype=np.uint8)
+    return lib().oracle_descriptor_distance(_p(a), _p(b))
+
+
+def knn2(q, t):
+    q = np.ascontiguousarray(q, dtype=np.uint8).reshape(-1, 32)
+    t = np.ascontiguousarray(t, dtype=np.uint8).reshape(-1, 32)
+    nq = q.shape[0]
+    i1, d1, i2, d2 = (np.zeros(nq, np.int32) for _ in range(4))
+    lib().oracle_knn2(_p(q), nq, _p(t), t.shape[0], _p(i1), _p(d1), _p(i2), _p(d2))
+    return i1, d1, i2, d2
+
+
+def sort_nodes(size, ulx):
+    size = np.ascontiguousarray(size, dtype=np.int32)
+    ulx = np.ascontiguousarray(ulx, dtype=np.int32)
+    perm = np.zeros(len(size), np.int32)
+    lib().oracle_sort_nodes(_p(size), _p(ulx), len(size), _p(perm))
+    return perm

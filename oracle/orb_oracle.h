@@ -1,0 +1,84 @@
+// orb_oracle.h -- TEST INFRASTRUCTURE ONLY.
+//
+// CPU restatement of the reference CPU ORB front-end (Lynx-MR/orbslam3lib,
+// app/src/main/cpp/src/ORBextractor_old.cc) and of the OpenCV 4.2.0 primitives it calls
+// (cv::resize INTER_LINEAR, cv::FAST TYPE_9_16 + nonmax, cv::GaussianBlur 7x7 sigma 2,
+// cv::fastAtan2, cv::BFMatcher NORM_HAMMING knn).  OpenCV is not present in this image, so
+// the OpenCV parts are restated from its published algorithm; the choices that OpenCV's
+// build configuration leaves open are pinned as named constants below.
+//
+// Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this code,
+// and only as the checker.  The product (liborbgpu.so) never links or calls it.
+#pragma once
+#include <cstddef>
+#include <cstdint>
+
+extern "C" {
+
+// cv::KeyPoint field layout (28 bytes).
+typedef struct {
+    float x, y, size, angle, response;
+    int32_t octave, class_id;
+} oracle_kp;
+
+// Pinned OpenCV-4.2 choices:
+//  * resize vertical pass: 128-bit-SIMD body (VResizeLinearVec_32s8u) for x < simd_end(width),
+//    scalar FixedPtCast tail after it.                     -> oracle_resize_simd_end()
+//  * GaussianBlur 7x7 sigma=2 fixed-point kernel with error diffusion: {18,34,48,56,48,34,18}/256
+//  * cos/sin in computeOrbDescriptor: (float)cos((double)angle)
+//  * no FMA contraction anywhere (-ffp-contract=off)
+int oracle_resize_simd_end(int width);
+void oracle_blur_kernel(int32_t k[7]);
+
+// Full ORBextractor::operator() (ORBextractor_old.cc:1088-1191) on one image.
+// Returns monoIndex (or -1 on empty image, -2 on capacity overflow).  *n_out = N keypoints.
+int oracle_extract(int nfeatures, float scale_factor, int nlevels, int ini_th, int min_th,
+                   const uint8_t* img, int w, int h, int stride, int lap0, int lap1,
+                   oracle_kp* kps, uint8_t* desc, int cap, int* n_out);
+
+// Same, but per level, before assembly: keypoints in level coordinates in octree order with
+// orientation, and their descriptors.  lvl_count[nlevels]; kps/desc packed level after level.
+int oracle_extract_levels(int nfeatures, float scale_factor, int nlevels, int ini_th, int min_th,
+                          const uint8_t* img, int w, int h, int stride,
+                          oracle_kp* kps, uint8_t* desc, int cap, int* lvl_count);
+
+// Pyramid level sizes (canonical ComputePyramid, ORBextractor_old.cc:1333-1339).
+void oracle_level_sizes(float scale_factor, int nlevels, int w, int h, int* lw, int* lh);
+// Whole pyramid, levels packed tightly (pitch = width) one after another into out.
+int oracle_pyramid(float scale_factor, int nlevels, const uint8_t* img, int w, int h, int stride,
+                   uint8_t* out);
+// cv::resize(src, dst, Size(dw,dh), 0, 0, INTER_LINEAR) on CV_8UC1.
+void oracle_resize(const uint8_t* src, int sw, int sh, int sstride, uint8_t* dst, int dw, int dh,
+                   int dstride);
+// cv::GaussianBlur(src, dst, Size(7,7), 2, 2, BORDER_REFLECT_101) on CV_8UC1, tight pitch.
+void oracle_gaussian_blur(const uint8_t* src, int w, int h, uint8_t* dst);
+// cv::FAST(roi, kps, th, true) on an ROI (x0,y0,cols,rows) of an image with row stride.
+int oracle_fast(const uint8_t* img, int stride, int x0, int y0, int cols, int rows, int th,
+                oracle_kp* kps, int cap);
+// FAST score of one pixel as the nonmax buffer would hold it (cornerScore<16>), th-clamped.
+int oracle_corner_score(const uint8_t* img, int stride, int x, int y, int th);
+// Per-level keypoints BEFORE the octree (cell loop of ComputeKeyPointsOctTree, :807-874),
+// coordinates relative to (minBorderX, minBorderY) exactly as vToDistributeKeys holds them.
+int oracle_level_candidates(const uint8_t* lvl, int w, int h, int ini_th, int min_th,
+                            oracle_kp* kps, int cap);
+// DistributeOctTree (ORBextractor_old.cc:557-781) on a candidate list.
+int oracle_distribute_octree(const oracle_kp* keys, int n, int minX, int maxX, int minY, int maxY,
+                             int N, oracle_kp* out, int cap);
+float oracle_fast_atan2(float y, float x);
+float oracle_ic_angle(const uint8_t* img, int stride, int x, int y);
+void oracle_orb_descriptor(const uint8_t* blurred, int stride, float x, float y, float angle,
+                           uint8_t* desc32);
+void oracle_umax(int* umax16);
+void oracle_features_per_level(int nfeatures, float scale_factor, int nlevels, int* out);
+void oracle_scale_factors(float scale_factor, int nlevels, float* scale, float* inv_scale,
+                          float* sigma2, float* inv_sigma2);
+// ORBmatcher::DescriptorDistance (ORBmatcher.cc:2107-2123).
+int oracle_descriptor_distance(const uint8_t* a, const uint8_t* b);
+// cv::BFMatcher(NORM_HAMMING).knnMatch(q, t, m, 2) -> per query (idx1,d1,idx2,d2); idx=-1 absent.
+void oracle_knn2(const uint8_t* q, int nq, const uint8_t* t, int nt, int32_t* idx1, int32_t* d1,
+                 int32_t* idx2, int32_t* d2);
+// Reference-ordered sort (std::sort + compareNodes, ORBextractor_old.cc:540-555,702) on
+// (size, ULx) pairs; writes the permutation of input indices.
+void oracle_sort_nodes(const int32_t* size, const int32_t* ulx, int n, int32_t* perm);
+
+}  // extern "C"

@@ -1,0 +1,319 @@
+"""orbslam3lib_amd -- MI355X-native ORB front-end (Python mirror of the reference interface).
+
+The compute path is liborbgpu.so (HIP kernels for gfx950 behind the C ABI in
+include/orbgpu.h).  This module mirrors the reference's operator surface so the parity tests
+read like the reference's own call sites:
+
+  ORBextractor(nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST)
+      cpp/include/ORBextractor_old.h:51-59; operator() :56-59; getters :62-84; mvImagePyramid :86
+  ORBmatcher.DescriptorDistance(a, b)        cpp/include/ORBmatcher.h:44
+  BFMatcher(NORM_HAMMING).knnMatch(q, t, 2)  cpp/src/Frame.cc:45,1227
+
+There is no CPU fallback: if liborbgpu.so or a gfx950 device is missing, construction raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+__all__ = ["ORBextractor", "ORBmatcher", "BFMatcher", "BatchExtractor", "KEYPOINT_DTYPE",
+           "OrbGpuError", "load_library", "LIB_PATH"]
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liborbgpu.so")
+
+# cv::KeyPoint layout (28 B)
+KEYPOINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                           ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
+
+EXPORTED = [
+    "orbgpu_create", "orbgpu_destroy", "orbgpu_get_scale_tables", "orbgpu_extract",
+    "orbgpu_extract_stereo", "orbgpu_upload_images", "orbgpu_device_input", "orbgpu_run_batch",
+    "orbgpu_download_result", "orbgpu_download_counts", "orbgpu_synchronize",
+    "orbgpu_get_pyramid_level", "orbgpu_get_level_keypoints", "orbgpu_match_knn2",
+    "orbgpu_match_stereo_batch", "orbgpu_download_matches", "orbgpu_descriptor_distance",
+    "orbgpu_set_profiling", "orbgpu_num_stages", "orbgpu_stage_name", "orbgpu_stage_times",
+    "orbgpu_reset_stage_times", "orbgpu_last_error", "orbgpu_abi_version",
+]
+
+
+class OrbGpuError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("orbgpu error %d: %s" % (code, msg))
+        self.code = code
+
+
+class _Params(C.Structure):
+    _fields_ = [("nfeatures", C.c_int32), ("scale_factor", C.c_float), ("nlevels", C.c_int32),
+                ("ini_th_fast", C.c_int32), ("min_th_fast", C.c_int32)]
+
+
+_lib = None
+
+
+def load_library(path: str = LIB_PATH):
+    """Load liborbgpu.so (raises if it has not been built -- no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise OrbGpuError(-6, "liborbgpu.so not built (run `make` or __graft_entry__.build())")
+    lib = C.CDLL(path)
+    lib.orbgpu_last_error.restype = C.c_char_p
+    lib.orbgpu_stage_name.restype = C.c_char_p
+    lib.orbgpu_device_input.restype = C.c_void_p
+    lib.orbgpu_device_input.argtypes = [C.c_void_p]
+    for name in ("orbgpu_destroy", "orbgpu_synchronize", "orbgpu_set_profiling",
+                 "orbgpu_reset_stage_times"):
+        getattr(lib, name).argtypes = [C.c_void_p] + ([C.c_int] if name == "orbgpu_set_profiling" else [])
+    _lib = lib
+    return lib
+
+
+def _check(code):
+    if code < 0:
+        raise OrbGpuError(code, _lib.orbgpu_last_error().decode())
+    return code
+
+
+def _p(a):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+class _Context:
+    def __init__(self, nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST, device, max_width,
+                 max_height, max_images):
+        lib = load_library()
+        self.params = _Params(int(nfeatures), float(scaleFactor), int(nlevels), int(iniThFAST),
+                              int(minThFAST))
+        self.handle = C.c_void_p()
+        _check(lib.orbgpu_create(C.byref(self.params), int(device), int(max_width),
+                                 int(max_height), int(max_images), C.byref(self.handle)))
+        self.nlevels = int(nlevels)
+        self.max_images = int(max_images)
+
+    def close(self):
+        if self.handle:
+            _lib.orbgpu_destroy(self.handle)
+            self.handle = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class ORBextractor:
+    """ORB_SLAM3::ORBextractor on the GPU (cpp/src/ORBextractor_old.cc:411-1191).
+
+    __call__(image, mask=None, vLappingArea=(0, 0)) -> (keypoints, descriptors, monoIndex)
+      keypoints: structured array with cv::KeyPoint fields; descriptors: uint8 [N, 32];
+      monoIndex: number of keypoints outside the lapping area (written first).
+      Returns (empty, None, -1) for an empty image, like the reference (:1092-1093).
+    """
+
+    def __init__(self, nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST, device=0,
+                 max_width=1920, max_height=1080, max_images=2):
+        self.nfeatures = int(nfeatures)
+        self.scaleFactor = float(scaleFactor)
+        self.nlevels = int(nlevels)
+        self.iniThFAST = int(iniThFAST)
+        self.minThFAST = int(minThFAST)
+        self._ctx = _Context(nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST, device,
+                             max_width, max_height, max_images)
+        L = self.nlevels
+        self.mvScaleFactor = np.zeros(L, np.float32)
+        self.mvInvScaleFactor = np.zeros(L, np.float32)
+        self.mvLevelSigma2 = np.zeros(L, np.float32)
+        self.mvInvLevelSigma2 = np.zeros(L, np.float32)
+        self.mnFeaturesPerLevel = np.zeros(L, np.int32)
+        _check(_lib.orbgpu_get_scale_tables(self._ctx.handle, _p(self.mvScaleFactor),
+                                            _p(self.mvInvScaleFactor), _p(self.mvLevelSigma2),
+                                            _p(self.mvInvLevelSigma2), _p(self.mnFeaturesPerLevel)))
+        self._cap = 4 * max(self.nfeatures, 1) * 2 + 64 * L + 4096
+        self._last_n_images = 0
+
+    # getters (ORBextractor_old.h:62-84)
+    def GetLevels(self):
+        return self.nlevels
+
+    def GetScaleFactor(self):
+        return self.scaleFactor
+
+    def GetScaleFactors(self):
+        return self.mvScaleFactor.tolist()
+
+    def GetInverseScaleFactors(self):
+        return self.mvInvScaleFactor.tolist()
+
+    def GetScaleSigmaSquares(self):
+        return self.mvLevelSigma2.tolist()
+
+    def GetInverseScaleSigmaSquares(self):
+        return self.mvInvLevelSigma2.tolist()
+
+    def __call__(self, image, mask=None, vLappingArea=(0, 0)):
+        img = np.asarray(image)
+        if img.size == 0:
+            return np.zeros(0, KEYPOINT_DTYPE), None, -1
+        if img.dtype != np.uint8 or img.ndim != 2:
+            raise OrbGpuError(-3, "image must be CV_8UC1 (2-D uint8)")  # assert :1096
+        img = np.ascontiguousarray(img)
+        h, w = img.shape
+        kps = np.zeros(self._cap, KEYPOINT_DTYPE)
+        desc = np.zeros((self._cap, 32), np.uint8)
+        n, mono = C.c_int(0), C.c_int(0)
+        _check(_lib.orbgpu_extract(self._ctx.handle, _p(img), w, h, w, int(vLappingArea[0]),
+                                   int(vLappingArea[1]), _p(kps), _p(desc), self._cap,
+                                   C.byref(n), C.byref(mono)))
+        self._last_n_images = 1
+        return kps[:n.value], (desc[:n.value] if n.value else None), mono.value
+
+    def extract_stereo(self, left, right, lapLeft=(0, 0), lapRight=(0, 0)):
+        """Stereo operator() (cpp/include/ORBextractor.h:52-57): both eyes in one device pass."""
+        left = np.ascontiguousarray(left, dtype=np.uint8)
+        right = np.ascontiguousarray(right, dtype=np.uint8)
+        h, w = left.shape
+        out = []
+        bufs = [(np.zeros(self._cap, KEYPOINT_DTYPE), np.zeros((self._cap, 32), np.uint8),
+                 C.c_int(0), C.c_int(0)) for _ in range(2)]
+        la = (C.c_int * 2)(*lapLeft)
+        ra = (C.c_int * 2)(*lapRight)
+        (kl, dl, nl, ml), (kr, dr, nr, mr) = bufs
+        _check(_lib.orbgpu_extract_stereo(self._ctx.handle, _p(left), _p(right), w, h, w, la, ra,
+                                          _p(kl), _p(dl), C.byref(nl), C.byref(ml), _p(kr), _p(dr),
+                                          C.byref(nr), C.byref(mr), self._cap))
+        self._last_n_images = 2
+        for k, d, n, m in bufs:
+            out.append((k[:n.value], d[:n.value], m.value))
+        return out
+
+    @property
+    def mvImagePyramid(self):
+        """Levels of the last extracted image (public member, ORBextractor_old.h:86)."""
+        return [self.pyramid_level(0, l) for l in range(self.nlevels)]
+
+    def pyramid_level(self, image, level, blurred=False):
+        w, h = C.c_int(0), C.c_int(0)
+        _check(_lib.orbgpu_get_pyramid_level(self._ctx.handle, image, level, int(blurred), None, 0,
+                                             C.byref(w), C.byref(h)))
+        out = np.zeros((h.value, w.value), np.uint8)
+        _check(_lib.orbgpu_get_pyramid_level(self._ctx.handle, image, level, int(blurred), _p(out),
+                                             w.value, None, None))
+        return out
+
+    def level_keypoints(self, image=0):
+        """Per-level keypoints (level coords, octree order, with angle) + descriptors."""
+        kps = np.zeros(self._cap, KEYPOINT_DTYPE)
+        desc = np.zeros((self._cap, 32), np.uint8)
+        cnt = np.zeros(self.nlevels, np.int32)
+        _check(_lib.orbgpu_get_level_keypoints(self._ctx.handle, image, _p(kps), _p(desc), self._cap,
+                                               _p(cnt)))
+        out, off = [], 0
+        for c in cnt.tolist():
+            out.append((kps[off:off + c], desc[off:off + c]))
+            off += c
+        return out
+
+
+class ORBmatcher:
+    @staticmethod
+    def DescriptorDistance(a, b):
+        """Hamming distance of two 32-byte descriptors (cpp/src/ORBmatcher.cc:2107-2123)."""
+        lib = load_library()
+        a = np.ascontiguousarray(a, dtype=np.uint8).reshape(32)
+        b = np.ascontiguousarray(b, dtype=np.uint8).reshape(32)
+        return lib.orbgpu_descriptor_distance(_p(a), _p(b))
+
+
+class BFMatcher:
+    """cv::BFMatcher(NORM_HAMMING) with knnMatch(k=2) on the GPU."""
+
+    def __init__(self, extractor: ORBextractor):
+        self._ctx = extractor._ctx
+
+    def knnMatch(self, query, train, k=2):
+        """Returns (idx1, dist1, idx2, dist2) int32 arrays; idx = -1 where absent."""
+        if k != 2:
+            raise OrbGpuError(-3, "only k=2 is implemented (the reference uses k=2)")
+        q = np.ascontiguousarray(query, dtype=np.uint8).reshape(-1, 32)
+        t = np.ascontiguousarray(train, dtype=np.uint8).reshape(-1, 32)
+        nq = q.shape[0]
+        out = [np.zeros(nq, np.int32) for _ in range(4)]
+        _check(_lib.orbgpu_match_knn2(self._ctx.handle, _p(q), nq, _p(t), t.shape[0],
+                                      *[_p(o) for o in out]))
+        return tuple(out)
+
+
+class BatchExtractor:
+    """Device-resident batch path (the throughput path used by bench.py).
+
+    upload(images[n,h,w]) -> run(laps) -> results stay in HBM; match_stereo() pairs 2p/2p+1.
+    """
+
+    def __init__(self, nfeatures=2000, scaleFactor=1.2, nlevels=8, iniThFAST=20, minThFAST=7,
+                 device=0, width=640, height=480, max_images=128):
+        self.ctx = _Context(nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST, device, width,
+                            height, max_images)
+        self.width, self.height = int(width), int(height)
+        self.n = 0
+
+    def upload(self, images):
+        imgs = np.ascontiguousarray(images, dtype=np.uint8)
+        n, h, w = imgs.shape
+        _check(_lib.orbgpu_upload_images(self.ctx.handle, _p(imgs), n, w, h, w))
+        self.n, self.height, self.width = n, h, w
+        _check(_lib.orbgpu_synchronize(self.ctx.handle))
+
+    def run(self, laps=None, stream=None):
+        n = self.n
+        lp = None
+        if laps is not None:
+            lp = np.ascontiguousarray(laps, dtype=np.int32).reshape(n, 2)
+        _check(_lib.orbgpu_run_batch(self.ctx.handle, n, self.width, self.height,
+                                     _p(lp) if lp is not None else None,
+                                     C.c_void_p(stream) if stream else None))
+
+    def match_stereo(self, stereo_rows_only=False, stream=None):
+        _check(_lib.orbgpu_match_stereo_batch(self.ctx.handle, self.n // 2, int(stereo_rows_only),
+                                              C.c_void_p(stream) if stream else None))
+
+    def synchronize(self):
+        _check(_lib.orbgpu_synchronize(self.ctx.handle))
+
+    def counts(self):
+        n = np.zeros(self.n, np.int32)
+        m = np.zeros(self.n, np.int32)
+        _check(_lib.orbgpu_download_counts(self.ctx.handle, self.n, _p(n), _p(m)))
+        return n, m
+
+    def result(self, i, cap=65536):
+        kps = np.zeros(cap, KEYPOINT_DTYPE)
+        desc = np.zeros((cap, 32), np.uint8)
+        n, m = C.c_int(0), C.c_int(0)
+        _check(_lib.orbgpu_download_result(self.ctx.handle, i, _p(kps), _p(desc), cap, C.byref(n),
+                                           C.byref(m)))
+        return kps[:n.value], desc[:n.value], m.value
+
+    def matches(self, pair, cap=65536):
+        out = [np.zeros(cap, np.int32) for _ in range(4)]
+        nq = C.c_int(0)
+        _check(_lib.orbgpu_download_matches(self.ctx.handle, pair, *[_p(o) for o in out], cap,
+                                            C.byref(nq)))
+        return tuple(o[:nq.value] for o in out)
+
+    def set_profiling(self, on=True):
+        _check(_lib.orbgpu_set_profiling(self.ctx.handle, int(on)))
+
+    def reset_stage_times(self):
+        _check(_lib.orbgpu_reset_stage_times(self.ctx.handle))
+
+    def stage_times(self):
+        ns = _lib.orbgpu_num_stages()
+        ms = np.zeros(ns, np.float64)
+        cnt = np.zeros(ns, np.int64)
+        _check(_lib.orbgpu_stage_times(self.ctx.handle, _p(ms), _p(cnt), ns))
+        return {_lib.orbgpu_stage_name(i).decode(): (float(ms[i]), int(cnt[i])) for i in range(ns)}

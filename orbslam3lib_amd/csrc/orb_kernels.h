@@ -1,0 +1,122 @@
+// orb_kernels.h -- launch-argument structs shared by orb_kernels.hip and orb_runtime.cpp.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace orbgpu {
+
+constexpr int kMaxLevels = 16;
+constexpr int kMinBorder = 16;   // EDGE_THRESHOLD - 3 (ORBextractor_old.cc:791)
+constexpr int kEdge = 19;        // EDGE_THRESHOLD (:75)
+
+// Per-level geometry, computed on the host (orb_runtime.cpp) from the reference formulas.
+struct LevelGeom {
+    int w, h, pitch;           // plane size; pitch in bytes (level 0: the input's row stride)
+    long long img_stride;      // bytes between images for this level's plane
+    int bpitch;                // blurred plane pitch (multiple of 64)
+    long long bimg_stride;     // bytes between images for the blurred plane
+    int nCols, nRows, wCell, hCell, maxBX, maxBY;  // cell grid (:787-805)
+    int ncells, cell_cap;      // cells in this level, key capacity per cell
+    int cell_first;            // flattened index of this level's first cell
+    long long cellkey_off;     // offset (in keys) of this level's cell-key region in an image
+    int cellcnt_off;           // offset (in cells) of this level's counts in an image
+    int cand_cap;              // ncells * cell_cap
+    int N;                     // mnFeaturesPerLevel[level]
+    int W, H;                  // octree extents maxBorder - minBorder
+    int kp_cap;                // octree output capacity
+    int kp_off;                // offset (in keypoints) in an image's level-keypoint region
+    int oct_cap;               // node capacity of the octree workspace
+    long long oct_off;         // byte offset of this level's octree workspace in an image
+    float scale;               // mvScaleFactor[level]
+    int patch;                 // (int)(PATCH_SIZE * scale) (:882)
+    int tiles_x, tiles_y, tile_first;  // blur tiling (128 x 16)
+    int xtab_off, ytab_off, simd_end;  // resize tables (levels >= 1)
+    int area2;                 // exact 2x downscale: OpenCV switches to INTER_AREA (2x2 mean)
+    int od_blocks, od_first;   // orientation/descriptor blocks for this level
+};
+
+struct BatchArgs {
+    int nlevels, nimages;
+    int ini_th, min_th;
+    LevelGeom lv[kMaxLevels];
+    uint8_t* lvl_base[kMaxLevels];   // plane base of image 0 (level 0 = the input buffer)
+    uint8_t* blur_base[kMaxLevels];
+    const int4* rtab;                // resize tables (x: {sx,sx1,a0,a1}, y: {sy0,sy1,b0,b1})
+    uint32_t* cellkeys;              // [img][cand region]
+    long long cellkeys_img_stride;   // keys
+    int32_t* cellcnt;                // [img][cells]
+    int cellcnt_img_stride;
+    uint8_t* octws;                  // [img][octree workspace]
+    long long octws_img_stride;
+    uint32_t* lvlkey;                // [img][level kps] packed key
+    float* lvlangle;                 // [img][level kps]
+    uint8_t* lvldesc;                // [img][level kps][32]
+    int lvlkp_img_stride;            // keypoints
+    int32_t* lvlcnt;                 // [img][kMaxLevels]
+    int32_t* status;                 // [img][kMaxLevels]
+    void* out_kps;                   // orbgpu_keypoint [img][out_cap]
+    uint8_t* out_desc;               // [img][out_cap][32]
+    int out_cap;
+    int32_t* out_n;                  // [img]
+    int32_t* out_mono;               // [img]
+    const int32_t* laps;             // [img][2]
+    int total_cells, total_tiles, total_od_blocks;
+};
+
+struct MatchArgs {
+    const uint8_t* desc;      // out_desc
+    const int32_t* out_n;
+    const int32_t* out_mono;
+    int out_cap;
+    int stereo_only;
+    int32_t* idx1;
+    int32_t* dist1;
+    int32_t* idx2;
+    int32_t* dist2;           // [pair][out_cap]
+    int32_t* nq;              // [pair]
+};
+
+// Octree workspace layout for one (image, level) with n_cap keys and node capacity C.
+struct OctLayout {
+    long long keys, knode, kq, nodesA, nodesB, childcnt, childpos, divrank, rank2node, rankoff,
+        expoff, undivpos, vsizeA, vsizeB, sortbuf, best, total;
+};
+
+__host__ __device__ inline long long oct_align(long long x) { return (x + 255) & ~255LL; }
+
+__host__ __device__ inline OctLayout oct_layout(int n_cap, int C) {
+    OctLayout L;
+    long long o = 0;
+    L.keys = o; o = oct_align(o + 4LL * n_cap);
+    L.knode = o; o = oct_align(o + 4LL * n_cap);
+    L.kq = o; o = oct_align(o + 1LL * n_cap);
+    L.nodesA = o; o = oct_align(o + 24LL * C);
+    L.nodesB = o; o = oct_align(o + 24LL * C);
+    L.childcnt = o; o = oct_align(o + 16LL * C);
+    L.childpos = o; o = oct_align(o + 16LL * C);
+    L.divrank = o; o = oct_align(o + 4LL * C);
+    L.rank2node = o; o = oct_align(o + 4LL * C);
+    L.rankoff = o; o = oct_align(o + 4LL * C);
+    L.expoff = o; o = oct_align(o + 4LL * C);
+    L.undivpos = o; o = oct_align(o + 4LL * C);
+    L.vsizeA = o; o = oct_align(o + 4LL * C);
+    L.vsizeB = o; o = oct_align(o + 4LL * C);
+    L.sortbuf = o; o = oct_align(o + 12LL * C);
+    L.best = o; o = oct_align(o + 4LL * C);
+    L.total = o;
+    return L;
+}
+
+// Kernel launchers (orb_kernels.hip).  Each returns hipGetLastError() of its launch.
+hipError_t launch_resize(const BatchArgs& a, int level, hipStream_t s);
+hipError_t launch_blur(const BatchArgs& a, hipStream_t s);
+hipError_t launch_fast_cells(const BatchArgs& a, hipStream_t s);
+hipError_t launch_octree(const BatchArgs& a, hipStream_t s);
+hipError_t launch_orient_desc(const BatchArgs& a, hipStream_t s);
+hipError_t launch_finalize(const BatchArgs& a, hipStream_t s);
+hipError_t launch_knn2_pairs(const MatchArgs& m, int npairs, int qblocks, hipStream_t s);
+hipError_t launch_knn2_plain(const uint8_t* q, int nq, const uint8_t* t, int nt, int32_t* i1,
+                             int32_t* d1, int32_t* i2, int32_t* d2, hipStream_t s);
+
+}  // namespace orbgpu

@@ -1,0 +1,502 @@
+// orb_kernels.hip -- gfx950 kernels of the ORB front-end.  Integer/byte work: no MFMA.
+//
+// Pipeline for a batch of B images (all on one stream):
+//   k_resize      x (L-1)  cascaded bilinear pyramid, OpenCV INTER_LINEAR fixed point
+//   k_blur        x 1      7x7 Gaussian (sigma 2, fixed point, REFLECT_101) on every level
+//   k_fast_cells  x 1      one workgroup per (image, level, 35-px cell): FAST-9 strength,
+//                          3x3 nonmax at iniTh / minTh fallback, ordered compaction
+//   k_octree      x 1      one workgroup per (image, level): DistributeOctTree
+//   k_orient_desc x 1      one wave per keypoint: IC_Angle + rBRIEF 256 bit
+//   k_finalize    x 1      one workgroup per image: scale + mono/stereo partition
+//   k_knn2        x 1      Hamming k=2 brute force, query-in-registers / train-in-LDS
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "orb_kernels.h"
+#include "orb_math.h"
+#include "orb_fast_cell.h"
+#include "orb_octree.h"
+#include "orb_pattern_data.h"
+#include "orb_policy.h"
+
+namespace orbgpu {
+
+static_assert(sizeof(BatchArgs) <= 4096, "kernel argument block too large");
+
+// rBRIEF pattern decoded at compile time from the hex data: 256 pairs (x0,y0,x1,y1) int8.
+struct PatternTable {
+    int8_t v[1024];
+};
+constexpr int hexval(char c) { return c <= '9' ? c - '0' : c - 'a' + 10; }
+constexpr PatternTable make_pattern() {
+    PatternTable t{};
+    const char* h = ORBGPU_PATTERN_HEX;
+    for (int i = 0; i < 1024; ++i) t.v[i] = (int8_t)(hexval(h[2 * i]) * 16 + hexval(h[2 * i + 1]));
+    return t;
+}
+__constant__ PatternTable c_pattern = make_pattern();
+
+// umax[] of the ORBextractor ctor (ORBextractor_old.cc:455-470) for HALF_PATCH_SIZE = 15.
+__constant__ int c_umax[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};
+
+// ---------------------------------------------------------------------------------------------
+// k_resize: level l from level l-1 (canonical ComputePyramid, ORBextractor_old.cc:1342-1344 ->
+// cv::resize INTER_LINEAR).  Horizontal: D = S[sx]*a0 + S[sx1]*a1 (int); vertical: OpenCV's
+// 128-bit SIMD body for x < simd_end, FixedPtCast tail after.  Each thread writes 4 pixels.
+__global__ __launch_bounds__(256) void k_resize(BatchArgs a, int l) {
+    const LevelGeom& G = a.lv[l];
+    const LevelGeom& S = a.lv[l - 1];
+    const int img = blockIdx.z;
+    const int dy = blockIdx.y * 4 + (threadIdx.x >> 6);
+    const int dx0 = (blockIdx.x * 64 + (threadIdx.x & 63)) * 4;
+    if (dy >= G.h || dx0 >= G.w) return;
+    const uint8_t* src = a.lvl_base[l - 1] + (long long)img * S.img_stride;
+    uint8_t* dst = a.lvl_base[l] + (long long)img * G.img_stride;
+    if (G.area2) {  // resize.cpp: INTER_LINEAR at exactly 2x is serviced by INTER_AREA fast
+        const uint8_t* s0 = src + (long long)(2 * dy) * S.pitch;
+        const uint8_t* s1 = s0 + S.pitch;
+        uint32_t pk = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int dx = min(dx0 + k, G.w - 1);
+            const int o = (s0[2 * dx] + s0[2 * dx + 1] + s1[2 * dx] + s1[2 * dx + 1] + 2) >> 2;
+            pk |= (uint32_t)o << (8 * k);
+        }
+        *reinterpret_cast<uint32_t*>(dst + (long long)dy * G.pitch + dx0) = pk;
+        return;
+    }
+    const int4 yt = a.rtab[G.ytab_off + dy];
+    const uint8_t* r0 = src + (long long)yt.x * S.pitch;
+    const uint8_t* r1 = src + (long long)yt.y * S.pitch;
+    const int b0 = yt.z, b1 = yt.w;
+    uint32_t packed = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int dx = dx0 + k;
+        int o = 0;
+        if (dx < G.w) {
+            const int4 xt = a.rtab[G.xtab_off + dx];
+            const int D0 = r0[xt.x] * xt.z + r0[xt.y] * xt.w;
+            const int D1 = r1[xt.x] * xt.z + r1[xt.y] * xt.w;
+            if (dx < G.simd_end) {
+                const int s = (((D0 >> 4) * b0) >> 16) + (((D1 >> 4) * b1) >> 16);
+                o = (s + 2) >> 2;
+            } else {
+                o = (D0 * b0 + D1 * b1 + (1 << 21)) >> 22;
+            }
+            o = o < 0 ? 0 : (o > 255 ? 255 : o);
+        }
+        packed |= (uint32_t)o << (8 * k);
+    }
+    *reinterpret_cast<uint32_t*>(dst + (long long)dy * G.pitch + dx0) = packed;
+}
+
+// ---------------------------------------------------------------------------------------------
+// k_blur: cv::GaussianBlur(Size(7,7), 2, 2, BORDER_REFLECT_101) on each level
+// (ORBextractor_old.cc:1146-1147), bit-exact fixed point: kernel {18,34,48,56,48,34,18}/256,
+// horizontal sums exact in u16, vertical (sum + 2^15) >> 16.  Tile 128 x 16, LDS staged.
+__device__ inline int refl101(int p, int n) {
+    p = p < 0 ? -p : p;
+    return p >= n ? 2 * n - p - 2 : p;
+}
+
+__global__ __launch_bounds__(256) void k_blur(BatchArgs a) {
+    constexpr int TW = 128, TH = 16, IW = TW + 6, IH = TH + 6;
+    __shared__ uint8_t tin[IH][IW + 2];
+    __shared__ uint16_t th[IH][TW + 1];
+    const int img = blockIdx.y;
+    int l = 0;
+    while (l + 1 < a.nlevels && (int)blockIdx.x >= a.lv[l + 1].tile_first) ++l;
+    const LevelGeom& G = a.lv[l];
+    const int t = blockIdx.x - G.tile_first;
+    const int ty0 = (t / G.tiles_x) * TH, tx0 = (t % G.tiles_x) * TW;
+    const uint8_t* src = a.lvl_base[l] + (long long)img * G.img_stride;
+    uint8_t* dst = a.blur_base[l] + (long long)img * G.bimg_stride;
+    for (int i = threadIdx.x; i < IH * IW; i += 256) {
+        const int r = i / IW, c = i % IW;
+        const int y = refl101(ty0 + r - 3, G.h), x = refl101(tx0 + c - 3, G.w);
+        tin[r][c] = src[(long long)y * G.pitch + x];
+    }
+    __syncthreads();
+    const int k0 = 18, k1 = 34, k2 = 48, k3 = 56;
+    for (int i = threadIdx.x; i < IH * TW; i += 256) {
+        const int r = i / TW, c = i % TW;
+        const uint8_t* p = &tin[r][c];
+        th[r][c] = (uint16_t)(k0 * (p[0] + p[6]) + k1 * (p[1] + p[5]) + k2 * (p[2] + p[4]) +
+                              k3 * p[3]);
+    }
+    __syncthreads();
+    const int r = threadIdx.x >> 4, c0 = (threadIdx.x & 15) * 8;
+    const int y = ty0 + r;
+    if (y >= G.h || tx0 + c0 >= G.w) return;
+    uint32_t lo = 0, hi = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const int c = c0 + k;
+        const uint32_t s = k0 * ((uint32_t)th[r][c] + th[r + 6][c]) +
+                           k1 * ((uint32_t)th[r + 1][c] + th[r + 5][c]) +
+                           k2 * ((uint32_t)th[r + 2][c] + th[r + 4][c]) + k3 * (uint32_t)th[r + 3][c];
+        const uint32_t o = (s + (1u << 15)) >> 16;
+        if (k < 4) lo |= o << (8 * k);
+        else hi |= o << (8 * (k - 4));
+    }
+    *reinterpret_cast<uint2*>(dst + (long long)y * G.bpitch + tx0 + c0) = make_uint2(lo, hi);
+}
+
+// ---------------------------------------------------------------------------------------------
+// k_fast_cells: one workgroup per (level, cell), image = blockIdx.y.  Restates the cell loop of
+// ComputeKeyPointsOctTree (ORBextractor_old.cc:807-871) with cv::FAST(cell, kps, th, true):
+// detection on [3,rows-3)x[3,cols-3) of the cell ROI, 3x3 nonmax inside the cell only, iniTh
+// then minTh if the cell yields nothing, keys emitted in row-major order.
+__global__ __launch_bounds__(256) void k_fast_cells(BatchArgs a) {
+    __shared__ uint8_t T[kCellMax * kCellMax];
+    __shared__ uint8_t M[kCellMax * kCellMax];
+    __shared__ int scratch[16];
+    __shared__ int s_cnt;
+    const int img = blockIdx.y;
+    int l = 0;
+    while (l + 1 < a.nlevels && (int)blockIdx.x >= a.lv[l + 1].cell_first) ++l;
+    const LevelGeom& G = a.lv[l];
+    const int cell = blockIdx.x - G.cell_first;
+    const int ci = cell / G.nCols, cj = cell % G.nCols;
+    int32_t* cnt_out = a.cellcnt + (long long)img * a.cellcnt_img_stride + G.cellcnt_off + cell;
+    uint32_t* key_out = a.cellkeys + (long long)img * a.cellkeys_img_stride + G.cellkey_off +
+                        (long long)cell * G.cell_cap;
+    CellGeom g;
+    g.iniY = kMinBorder + ci * G.hCell;
+    g.iniX = kMinBorder + cj * G.wCell;
+    g.minBorder = kMinBorder;
+    if (g.iniY >= G.maxBY - 3 || g.iniX >= G.maxBX - 6) {  // :812, :821
+        if (threadIdx.x == 0) *cnt_out = 0;
+        return;
+    }
+    g.rows = min(g.iniY + G.hCell + 6, G.maxBY) - g.iniY;
+    g.cols = min(g.iniX + G.wCell + 6, G.maxBX) - g.iniX;
+    const uint8_t* src = a.lvl_base[l] + (long long)img * G.img_stride + (long long)g.iniY * G.pitch + g.iniX;
+    DevPolicy p{scratch};
+    const int n = fast_cell_run(p, src, G.pitch, g, a.ini_th, a.min_th, T, M, &s_cnt, key_out);
+    if (threadIdx.x == 0) *cnt_out = n;
+}
+
+// ---------------------------------------------------------------------------------------------
+// k_octree: one workgroup per (level, image).  Gathers the level's cell lists in cell order
+// (vToDistributeKeys, :807-871) then runs DistributeOctTree (orb_octree.h).
+__global__ __launch_bounds__(512) void k_octree(BatchArgs a) {
+    __shared__ int scratch[16];
+    __shared__ OctShared sh;
+    const int l = blockIdx.x, img = blockIdx.y;
+    const LevelGeom& G = a.lv[l];
+    DevPolicy p{scratch};
+    const int32_t* cnt = a.cellcnt + (long long)img * a.cellcnt_img_stride + G.cellcnt_off;
+    const uint32_t* ck = a.cellkeys + (long long)img * a.cellkeys_img_stride + G.cellkey_off;
+    uint8_t* ws = a.octws + (long long)img * a.octws_img_stride + G.oct_off;
+    const OctLayout L = oct_layout(G.cand_cap, G.oct_cap);
+    uint32_t* keys = reinterpret_cast<uint32_t*>(ws + L.keys);
+    int32_t* cell_off = reinterpret_cast<int32_t*>(ws + L.childpos);  // scratch before use
+    // exclusive scan of the cell counts
+    int carry = 0;
+    for (int base = 0; base < G.ncells; base += blockDim.x) {
+        const int i = base + threadIdx.x;
+        const int v = i < G.ncells ? cnt[i] : 0;
+        int tot;
+        const int ex = p.scan_excl(v, &tot);
+        if (i < G.ncells) cell_off[i] = carry + ex;
+        carry += tot;
+    }
+    const int n = carry;
+    __syncthreads();
+    {
+        const int lane = threadIdx.x & 63, nw = blockDim.x >> 6;
+        for (int c = threadIdx.x >> 6; c < G.ncells; c += nw) {
+            const int m = cnt[c], o = cell_off[c];
+            for (int k = lane; k < m; k += 64) keys[o + k] = ck[(long long)c * G.cell_cap + k];
+        }
+    }
+    __syncthreads();
+    OctWS w;
+    w.keys = keys;
+    w.n = n;
+    w.cap = G.oct_cap;
+    w.knode = reinterpret_cast<int32_t*>(ws + L.knode);
+    w.kq = ws + L.kq;
+    w.nodesA = reinterpret_cast<OctNode*>(ws + L.nodesA);
+    w.nodesB = reinterpret_cast<OctNode*>(ws + L.nodesB);
+    w.childcnt = reinterpret_cast<int32_t*>(ws + L.childcnt);
+    w.childpos = reinterpret_cast<int32_t*>(ws + L.childpos);
+    w.divrank = reinterpret_cast<int32_t*>(ws + L.divrank);
+    w.rank2node = reinterpret_cast<int32_t*>(ws + L.rank2node);
+    w.rankoff = reinterpret_cast<int32_t*>(ws + L.rankoff);
+    w.expoff = reinterpret_cast<int32_t*>(ws + L.expoff);
+    w.undivpos = reinterpret_cast<int32_t*>(ws + L.undivpos);
+    w.vsizeA = reinterpret_cast<int32_t*>(ws + L.vsizeA);
+    w.vsizeB = reinterpret_cast<int32_t*>(ws + L.vsizeB);
+    w.sortbuf = reinterpret_cast<SortElem*>(ws + L.sortbuf);
+    w.best = reinterpret_cast<uint32_t*>(ws + L.best);
+    w.out_keys = a.lvlkey + (long long)img * a.lvlkp_img_stride + G.kp_off;
+    w.out_cap = G.kp_cap;
+    int r = (n > G.cand_cap) ? -3 : 0;
+    if (r == 0) r = octree_distribute(p, w, &sh, G.W, G.H, G.N);
+    if (threadIdx.x == 0) {
+        a.lvlcnt[img * kMaxLevels + l] = r < 0 ? 0 : r;
+        a.status[img * kMaxLevels + l] = r < 0 ? r : 0;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// k_orient_desc: one wave per keypoint.  IC_Angle on the raw level (ORBextractor_old.cc:78-105)
+// then computeOrbDescriptor on the blurred level (:108-148): a = (float)cos, b = (float)sin of
+// angle*pi/180 (float), sample center[cvRound(x*b + y*a)*step + cvRound(x*a - y*b)].
+__global__ __launch_bounds__(256) void k_orient_desc(BatchArgs a) {
+    const int img = blockIdx.y;
+    int l = 0;
+    while (l + 1 < a.nlevels && (int)blockIdx.x >= a.lv[l + 1].od_first) ++l;
+    const LevelGeom& G = a.lv[l];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int count = a.lvlcnt[img * kMaxLevels + l];
+    const long long kbase = (long long)img * a.lvlkp_img_stride + G.kp_off;
+    const uint8_t* lvl = a.lvl_base[l] + (long long)img * G.img_stride;
+    const uint8_t* blr = a.blur_base[l] + (long long)img * G.bimg_stride;
+    const int stride_k = G.od_blocks * 4;
+    for (int kp = (blockIdx.x - G.od_first) * 4 + wave; kp < count; kp += stride_k) {
+        const uint32_t key = a.lvlkey[kbase + kp];
+        const int x = key_x(key) + kMinBorder, y = key_y(key) + kMinBorder;
+        // moments over the r=15 disc: lane v in [0,31) covers row v-15
+        int m10 = 0, m01 = 0;
+        if (lane < 31) {
+            const int v = lane - 15;
+            const int d = c_umax[v < 0 ? -v : v];
+            const uint8_t* row = lvl + (long long)(y + v) * G.pitch + x;
+            int s = 0, su = 0;
+            for (int u = -d; u <= d; ++u) {
+                const int val = row[u];
+                s += val;
+                su += u * val;
+            }
+            m10 = su;
+            m01 = v * s;
+        }
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            m10 += __shfl_xor(m10, o, 64);
+            m01 += __shfl_xor(m01, o, 64);
+        }
+        const float angle = fast_atan2_deg((float)m01, (float)m10);
+        if (lane == 0) a.lvlangle[kbase + kp] = angle;
+        if (lane < 32) {
+            const float factorPI = (float)(3.14159265358979323846 / 180.0);
+            const float ang = angle * factorPI;
+            const float ca = (float)cos((double)ang), sb = (float)sin((double)ang);
+            const uint8_t* center = blr + (long long)y * G.bpitch + x;
+            const int8_t* pat = c_pattern.v + lane * 32;  // byte `lane`: 8 pairs = 32 int8
+            int val = 0;
+#pragma unroll
+            for (int bit = 0; bit < 8; ++bit) {
+                int t[2];
+#pragma unroll
+                for (int e = 0; e < 2; ++e) {
+                    const float px = (float)pat[4 * bit + 2 * e], py = (float)pat[4 * bit + 2 * e + 1];
+                    const int ry = cv_round(px * sb + py * ca);
+                    const int rx = cv_round(px * ca - py * sb);
+                    t[e] = center[(long long)ry * G.bpitch + rx];
+                }
+                val |= (t[0] < t[1]) << bit;
+            }
+            a.lvldesc[(kbase + kp) * 32 + lane] = (uint8_t)val;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// k_finalize: ORBextractor::operator() assembly (ORBextractor_old.cc:1130-1190): levels in
+// order, pt *= mvScaleFactor[level] for level > 0, keypoints inside [lap0, lap1] written from
+// the back, the others from the front; returns monoIndex.
+struct KP28 {
+    float x, y, size, angle, response;
+    int32_t octave, class_id;
+};
+
+__global__ __launch_bounds__(256) void k_finalize(BatchArgs a) {
+    __shared__ int scratch[16];
+    const int img = blockIdx.x;
+    DevPolicy p{scratch};
+    int total = 0;
+    bool bad = false;
+    for (int l = 0; l < a.nlevels; ++l) {
+        total += a.lvlcnt[img * kMaxLevels + l];
+        bad |= a.status[img * kMaxLevels + l] != 0;
+    }
+    if (bad || total > a.out_cap) {
+        if (threadIdx.x == 0) {
+            a.out_n[img] = bad ? -5 : -2;
+            a.out_mono[img] = 0;
+        }
+        return;
+    }
+    const float lap0 = (float)a.laps[2 * img], lap1 = (float)a.laps[2 * img + 1];
+    KP28* out = reinterpret_cast<KP28*>(a.out_kps) + (long long)img * a.out_cap;
+    uint8_t* od = a.out_desc + (long long)img * a.out_cap * 32;
+    int mono = 0, stereo = 0;
+    for (int l = 0; l < a.nlevels; ++l) {
+        const LevelGeom& G = a.lv[l];
+        const int cnt = a.lvlcnt[img * kMaxLevels + l];
+        const long long kbase = (long long)img * a.lvlkp_img_stride + G.kp_off;
+        for (int base = 0; base < cnt; base += 256) {
+            const int i = base + threadIdx.x;
+            KP28 k;
+            bool st = false;
+            if (i < cnt) {
+                const uint32_t key = a.lvlkey[kbase + i];
+                k.x = (float)(key_x(key) + kMinBorder);
+                k.y = (float)(key_y(key) + kMinBorder);
+                if (l != 0) {
+                    k.x = k.x * G.scale;
+                    k.y = k.y * G.scale;
+                }
+                k.size = (float)G.patch;
+                k.angle = a.lvlangle[kbase + i];
+                k.response = (float)key_resp(key);
+                k.octave = l;
+                k.class_id = -1;
+                st = (k.x >= lap0 && k.x <= lap1);
+            }
+            int tst;
+            const int exs = p.scan_excl(st ? 1 : 0, &tst);
+            const int exm = (int)threadIdx.x - exs;  // earlier lanes of this chunk are all valid
+            if (i < cnt) {
+                const int dst = st ? (total - 1 - (stereo + exs)) : (mono + exm);
+                out[dst] = k;
+                const uint4* s4 = reinterpret_cast<const uint4*>(a.lvldesc + (kbase + i) * 32);
+                uint4* d4 = reinterpret_cast<uint4*>(od + (long long)dst * 32);
+                d4[0] = s4[0];
+                d4[1] = s4[1];
+            }
+            const int chunk = min(256, cnt - base);
+            stereo += tst;
+            mono += chunk - tst;
+        }
+    }
+    if (threadIdx.x == 0) {
+        a.out_n[img] = total;
+        a.out_mono[img] = mono;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Hamming k=2 brute force (cv::BFMatcher NORM_HAMMING knnMatch k=2, batchDistance insertion:
+// a candidate enters if d < dist[1], shifts past entries only while they are > d -> the two
+// lexicographically smallest (distance, train index)).  One query per thread in 8 VGPRs, train
+// descriptors staged through LDS 512 at a time and read as broadcasts.
+constexpr int kTrainChunk = 512;
+
+__device__ inline void knn2_core(const uint8_t* q, int nq, const uint8_t* t, int nt, int qi,
+                                 int32_t* i1, int32_t* d1, int32_t* i2, int32_t* d2,
+                                 uint4 (*tl)[2]) {
+    uint4 qa = make_uint4(0, 0, 0, 0), qb = qa;
+    if (qi < nq) {
+        const uint4* qp = reinterpret_cast<const uint4*>(q + (long long)qi * 32);
+        qa = qp[0];
+        qb = qp[1];
+    }
+    int b1 = 0x7fffffff, b2 = 0x7fffffff, j1 = -1, j2 = -1;
+    for (int base = 0; base < nt; base += kTrainChunk) {
+        const int m = min(kTrainChunk, nt - base);
+        __syncthreads();
+        for (int i = threadIdx.x; i < m; i += blockDim.x) {
+            const uint4* tp = reinterpret_cast<const uint4*>(t + (long long)(base + i) * 32);
+            tl[i][0] = tp[0];
+            tl[i][1] = tp[1];
+        }
+        __syncthreads();
+        for (int j = 0; j < m; ++j) {
+            const uint4 ta = tl[j][0], tb = tl[j][1];
+            int d = __popc(qa.x ^ ta.x) + __popc(qa.y ^ ta.y) + __popc(qa.z ^ ta.z) +
+                    __popc(qa.w ^ ta.w) + __popc(qb.x ^ tb.x) + __popc(qb.y ^ tb.y) +
+                    __popc(qb.z ^ tb.z) + __popc(qb.w ^ tb.w);
+            if (d < b2) {
+                if (d < b1) {
+                    b2 = b1;
+                    j2 = j1;
+                    b1 = d;
+                    j1 = base + j;
+                } else {
+                    b2 = d;
+                    j2 = base + j;
+                }
+            }
+        }
+    }
+    if (qi < nq) {
+        i1[qi] = j1;
+        d1[qi] = b1;
+        i2[qi] = j2;
+        d2[qi] = b2;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_knn2_pairs(MatchArgs m) {
+    __shared__ uint4 tl[kTrainChunk][2];
+    const int pair = blockIdx.y;
+    const int qimg = 2 * pair, timg = 2 * pair + 1;
+    const int qn = m.out_n[qimg], tn = m.out_n[timg];
+    const int q0 = m.stereo_only ? m.out_mono[qimg] : 0;
+    const int t0 = m.stereo_only ? m.out_mono[timg] : 0;
+    const int nq = qn > q0 ? qn - q0 : 0, nt = tn > t0 ? tn - t0 : 0;
+    if ((int)(blockIdx.x * blockDim.x) >= nq) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) m.nq[pair] = nq;
+        return;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) m.nq[pair] = nq;
+    const uint8_t* q = m.desc + ((long long)qimg * m.out_cap + q0) * 32;
+    const uint8_t* t = m.desc + ((long long)timg * m.out_cap + t0) * 32;
+    const long long o = (long long)pair * m.out_cap;
+    knn2_core(q, nq, t, nt, blockIdx.x * blockDim.x + threadIdx.x, m.idx1 + o, m.dist1 + o,
+              m.idx2 + o, m.dist2 + o, tl);
+}
+
+__global__ __launch_bounds__(256) void k_knn2_plain(const uint8_t* q, int nq, const uint8_t* t,
+                                                    int nt, int32_t* i1, int32_t* d1, int32_t* i2,
+                                                    int32_t* d2) {
+    __shared__ uint4 tl[kTrainChunk][2];
+    knn2_core(q, nq, t, nt, blockIdx.x * blockDim.x + threadIdx.x, i1, d1, i2, d2, tl);
+}
+
+// ---------------------------------------------------------------------------------------------
+hipError_t launch_resize(const BatchArgs& a, int level, hipStream_t s) {
+    const LevelGeom& G = a.lv[level];
+    dim3 grid((G.w + 255) / 256, (G.h + 3) / 4, a.nimages);
+    hipLaunchKernelGGL(k_resize, grid, dim3(256), 0, s, a, level);
+    return hipGetLastError();
+}
+hipError_t launch_blur(const BatchArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(k_blur, dim3(a.total_tiles, a.nimages), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+hipError_t launch_fast_cells(const BatchArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(k_fast_cells, dim3(a.total_cells, a.nimages), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+hipError_t launch_octree(const BatchArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(k_octree, dim3(a.nlevels, a.nimages), dim3(512), 0, s, a);
+    return hipGetLastError();
+}
+hipError_t launch_orient_desc(const BatchArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(k_orient_desc, dim3(a.total_od_blocks, a.nimages), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+hipError_t launch_finalize(const BatchArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(k_finalize, dim3(a.nimages), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+hipError_t launch_knn2_pairs(const MatchArgs& m, int npairs, int qblocks, hipStream_t s) {
+    hipLaunchKernelGGL(k_knn2_pairs, dim3(qblocks, npairs), dim3(256), 0, s, m);
+    return hipGetLastError();
+}
+hipError_t launch_knn2_plain(const uint8_t* q, int nq, const uint8_t* t, int nt, int32_t* i1,
+                             int32_t* d1, int32_t* i2, int32_t* d2, hipStream_t s) {
+    const int blocks = (nq + 255) / 256;
+    if (blocks == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_knn2_plain, dim3(blocks), dim3(256), 0, s, q, nq, t, nt, i1, d1, i2, d2);
+    return hipGetLastError();
+}
+
+}  // namespace orbgpu

@@ -1,0 +1,102 @@
+// orb_math.h -- bit-exact scalar primitives shared by the kernels (host-callable for tests).
+//
+// Compiled with -ffp-contract=off: every float expression below is evaluated as separately
+// rounded IEEE single operations in source order, which is what the CPU reference does.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace orbgpu {
+
+// cvRound(float) = round-half-to-even (lrintf / v_rndne_f32).
+__host__ __device__ inline int cv_round(float v) { return (int)__builtin_rintf(v); }
+
+// cv::fastAtan2 (OpenCV 4.2 core mathfuncs atanImpl<float>), degrees in [0, 360).
+// Called by IC_Angle, cpp/src/ORBextractor_old.cc:104.
+__host__ __device__ inline float fast_atan2_deg(float y, float x) {
+    const float k180pi = (float)(180.0 / 3.14159265358979323846);
+    const float p1 = 0.9997878412794807f * k180pi;
+    const float p3 = -0.3258083974640975f * k180pi;
+    const float p5 = 0.1555786518463281f * k180pi;
+    const float p7 = -0.04432655554792128f * k180pi;
+    const float eps = (float)2.220446049250313080847e-16;  // (float)DBL_EPSILON
+    const float ax = __builtin_fabsf(x), ay = __builtin_fabsf(y);
+    float a, c, c2;
+    if (ax >= ay) {
+        c = ay / (ax + eps);
+        c2 = c * c;
+        a = (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    } else {
+        c = ax / (ay + eps);
+        c2 = c * c;
+        a = 90.f - (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    }
+    if (x < 0) a = 180.f - a;
+    if (y < 0) a = 360.f - a;
+    return a;
+}
+
+// FAST-9/16 Bresenham ring (OpenCV makeOffsets, patternSize 16), (dx, dy).
+__host__ __device__ inline int ring_dx(int k) {
+    const int t[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
+    return t[k];
+}
+__host__ __device__ inline int ring_dy(int k) {
+    const int t[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3};
+    return t[k];
+}
+
+// Threshold-independent FAST strength m(p) = clamp(max over the 16 cyclic 9-arcs of
+// min(v - ring) [dark] or min(ring - v) [bright], 0, 255).  With it, for any threshold t >= 0:
+//   cv::FAST corner at t      <=>  m > t
+//   cornerScore<16>(p, t)      =   m - 1                     (for corners)
+// and the 3x3 nonmax rule of FAST_t<16> becomes
+//   kept_t(p) <=> m(p) > t && m(p) >= 2 && for each 8-neighbour q in the same cell detection
+//                 region: m(q) <= t || m(p) > m(q).
+// When the 4-compass pre-test at t_min fails, S_max <= t_min and 0 is stored instead (exact
+// for every t >= t_min).  Reference call sites: cv::FAST at ORBextractor_old.cc:828,847.
+__host__ __device__ inline int fast_strength(const uint8_t* c, int stride, int t_min) {
+    const int v = c[0];
+    int d[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) d[k] = v - (int)c[ring_dx(k) + ring_dy(k) * stride];
+    // compass pre-test: any 9-arc holds two cyclically adjacent points of {0,4,8,12}
+    int dm = 0, bm = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        dm |= (d[4 * q] > t_min) << q;
+        bm |= (-d[4 * q] > t_min) << q;
+    }
+    const int dr = ((dm << 1) | (dm >> 3)) & 15, br = ((bm << 1) | (bm >> 3)) & 15;
+    if (!(dm & dr) && !(bm & br)) return 0;
+    int a2[16], b2[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const int x = d[k], y = d[(k + 1) & 15];
+        a2[k] = x < y ? x : y;
+        b2[k] = x > y ? x : y;
+    }
+    int a4[16], b4[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const int x = a2[k], y = a2[(k + 2) & 15];
+        a4[k] = x < y ? x : y;
+        const int u = b2[k], w = b2[(k + 2) & 15];
+        b4[k] = u > w ? u : w;
+    }
+    int sdark = -1024, bmin = 1024;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        int a = a4[k] < a4[(k + 4) & 15] ? a4[k] : a4[(k + 4) & 15];
+        a = a < d[(k + 8) & 15] ? a : d[(k + 8) & 15];
+        sdark = sdark > a ? sdark : a;
+        int b = b4[k] > b4[(k + 4) & 15] ? b4[k] : b4[(k + 4) & 15];
+        b = b > d[(k + 8) & 15] ? b : d[(k + 8) & 15];
+        bmin = bmin < b ? bmin : b;
+    }
+    int s = sdark > -bmin ? sdark : -bmin;
+    s = s < 0 ? 0 : s;
+    return s > 255 ? 255 : s;
+}
+
+}  // namespace orbgpu

@@ -1,0 +1,63 @@
+// orb_policy.h -- execution policies for the data-parallel algorithms in orb_octree.h.
+//
+// DevPolicy: one HIP workgroup (blockDim.x a multiple of 64), LDS scratch for the block scan.
+// SerialPolicy: a single host thread; used only by the host test harness (tests/) so the same
+// algorithm source that runs on the GPU is also checked against the oracle on the CPU.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace orbgpu {
+
+struct DevPolicy {
+    int* scratch;  // >= 16 ints of LDS
+    __device__ int tid() const { return (int)threadIdx.x; }
+    __device__ int nthreads() const { return (int)blockDim.x; }
+    __device__ void sync() { __syncthreads(); }
+    __device__ int atomic_add(int32_t* p, int v) { return atomicAdd(p, v); }
+    __device__ uint32_t atomic_max(uint32_t* p, uint32_t v) { return atomicMax(p, v); }
+    // Block-wide exclusive scan: every thread passes v, gets its exclusive prefix and the total.
+    __device__ int scan_excl(int v, int* total) {
+        const int lane = (int)(threadIdx.x & 63), wid = (int)(threadIdx.x >> 6);
+        const int nw = (int)((blockDim.x + 63) >> 6);
+        int x = v;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
+        }
+        __syncthreads();  // scratch may still be read by the previous call
+        if (lane == 63) scratch[wid] = x;
+        __syncthreads();
+        int before = 0, tot = 0;
+        for (int w = 0; w < nw; ++w) {
+            const int s = scratch[w];
+            before += (w < wid) ? s : 0;
+            tot += s;
+        }
+        *total = tot;
+        return before + x - v;
+    }
+};
+
+struct SerialPolicy {
+    __host__ __device__ int tid() const { return 0; }
+    __host__ __device__ int nthreads() const { return 1; }
+    __host__ __device__ void sync() {}
+    __host__ __device__ int atomic_add(int32_t* p, int v) {
+        const int o = *p;
+        *p = o + v;
+        return o;
+    }
+    __host__ __device__ uint32_t atomic_max(uint32_t* p, uint32_t v) {
+        const uint32_t o = *p;
+        if (v > o) *p = v;
+        return o;
+    }
+    __host__ __device__ int scan_excl(int v, int* total) {
+        *total = v;
+        return 0;
+    }
+};
+
+}  // namespace orbgpu

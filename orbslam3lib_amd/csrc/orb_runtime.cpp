@@ -1,0 +1,750 @@
+// orb_runtime.cpp -- host runtime and C ABI (include/orbgpu.h) of liborbgpu.so.
+//
+// Owns one HIP stream and every device buffer of a context (allocated once per geometry,
+// never inside a launch sequence), computes the per-level geometry and the OpenCV resize
+// tables on the host with the reference's own float/double formulas, and enqueues the kernels
+// of orb_kernels.hip.  There is no CPU compute path: every result comes from the device.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cfloat>
+#include <climits>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/orbgpu.h"
+#include "orb_kernels.h"
+
+using namespace orbgpu;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                  \
+    do {                                                                               \
+        hipError_t e_ = (expr);                                                        \
+        if (e_ != hipSuccess)                                                          \
+            return fail(ORBGPU_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+enum Stage { ST_RESIZE, ST_BLUR, ST_FAST, ST_OCTREE, ST_ORIENT, ST_FINAL, ST_KNN, ST_COUNT };
+const char* kStageNames[ST_COUNT] = {"k_resize",      "k_blur",     "k_fast_cells", "k_octree",
+                                     "k_orient_desc", "k_finalize", "k_knn2"};
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    int ensure(size_t n) {
+        if (n <= bytes) return 0;
+        if (p) hipFree(p);
+        p = nullptr;
+        bytes = 0;
+        if (hipMalloc(&p, n) != hipSuccess) return -1;
+        bytes = n;
+        return 0;
+    }
+    void release() {
+        if (p) hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    template <class T>
+    T* as() const { return reinterpret_cast<T*>(p); }
+};
+
+inline int round_up(int x, int a) { return (x + a - 1) / a * a; }
+inline long long round_up_ll(long long x, long long a) { return (x + a - 1) / a * a; }
+inline int cv_round_f(float v) { return (int)std::lrintf(v); }
+inline int cv_round_d(double v) { return (int)std::lrint(v); }
+inline int cv_floor_f(float v) { return (int)std::floor(v); }
+inline short sat_short(float v) {
+    int i = cv_round_f(v);
+    return (short)std::min(std::max(i, (int)SHRT_MIN), (int)SHRT_MAX);
+}
+
+struct Pending {
+    int stage;
+    hipEvent_t a, b;
+};
+
+}  // namespace
+
+struct orbgpu_ctx {
+    orbgpu_params prm{};
+    int device = 0;
+    hipStream_t stream = nullptr;
+    int max_w = 0, max_h = 0, max_images = 0;
+    // ORBextractor tables (ORBextractor_old.cc:416-447)
+    std::vector<float> scale, inv_scale, sigma2, inv_sigma2;
+    std::vector<int> nper;
+    // geometry of the current image size
+    int gw = -1, gh = -1;
+    BatchArgs A{};
+    std::vector<int4> rtab_host;
+    long long pyr_img = 0, blur_img = 0, cellkeys_img = 0, octws_img = 0;
+    int cellcnt_img = 0, lvlkp_img = 0, out_cap = 0;
+    // device buffers
+    DevBuf input, pyr, blur, rtab, cellkeys, cellcnt, octws, lvlkey, lvlangle, lvldesc, lvlcnt,
+        status, outkps, outdesc, outn, outmono, laps, midx1, mdist1, midx2, mdist2, mnq, scratch;
+    int input_images = 0;   // images currently sized for in `input`
+    int last_images = 0, last_w = 0, last_h = 0, last_pairs = 0;
+    // profiling
+    bool prof = false;
+    std::vector<Pending> pending;
+    std::vector<hipEvent_t> event_pool;
+    double stage_ms[ST_COUNT] = {};
+    long long stage_n[ST_COUNT] = {};
+};
+
+namespace {
+
+void build_tables(orbgpu_ctx* c) {
+    const int L = c->prm.nlevels;
+    const double scaleFactor = (double)c->prm.scale_factor;  // double member (ORBextractor_old.h:98)
+    c->scale.assign(L, 0.f);
+    c->sigma2.assign(L, 0.f);
+    c->inv_scale.assign(L, 0.f);
+    c->inv_sigma2.assign(L, 0.f);
+    c->scale[0] = 1.0f;
+    c->sigma2[0] = 1.0f;
+    for (int i = 1; i < L; i++) {
+        c->scale[i] = (float)(c->scale[i - 1] * scaleFactor);
+        c->sigma2[i] = c->scale[i] * c->scale[i];
+    }
+    for (int i = 0; i < L; i++) {
+        c->inv_scale[i] = 1.0f / c->scale[i];
+        c->inv_sigma2[i] = 1.0f / c->sigma2[i];
+    }
+    c->nper.assign(L, 0);
+    const int nfeatures = c->prm.nfeatures;
+    float factor = (float)(1.0f / scaleFactor);
+    float nDesired = nfeatures * (1 - factor) / (1 - (float)std::pow((double)factor, (double)L));
+    int sum = 0;
+    for (int l = 0; l < L - 1; l++) {
+        c->nper[l] = cv_round_f(nDesired);
+        sum += c->nper[l];
+        nDesired *= factor;
+    }
+    c->nper[L - 1] = std::max(nfeatures - sum, 0);
+}
+
+// OpenCV cv::resize INTER_LINEAR coefficient tables (resize.cpp, fixed point, ksize 2), host-side.
+// Returns true when OpenCV would take the INTER_AREA 2x path instead.
+bool resize_tables(int sw, int sh, int dw, int dh, std::vector<int4>& xt, std::vector<int4>& yt) {
+    double inv_scale_x = (double)dw / sw, inv_scale_y = (double)dh / sh;
+    double scale_x = 1. / inv_scale_x, scale_y = 1. / inv_scale_y;
+    int iscale_x = cv_round_d(scale_x), iscale_y = cv_round_d(scale_y);
+    bool area_fast = std::abs(scale_x - iscale_x) < DBL_EPSILON &&
+                     std::abs(scale_y - iscale_y) < DBL_EPSILON && iscale_x == 2 && iscale_y == 2;
+    xt.resize(dw);
+    yt.resize(dh);
+    for (int dx = 0; dx < dw; ++dx) {
+        float fx = (float)((dx + 0.5) * scale_x - 0.5);
+        int sx = cv_floor_f(fx);
+        fx -= sx;
+        if (sx < 0) fx = 0, sx = 0;
+        if (sx + 1 >= sw && sx >= sw - 1) fx = 0, sx = sw - 1;
+        const short a0 = sat_short((1.f - fx) * 2048), a1 = sat_short(fx * 2048);
+        xt[dx] = make_int4(sx, std::min(sx + 1, sw - 1), a0, a1);
+    }
+    for (int dy = 0; dy < dh; ++dy) {
+        float fy = (float)((dy + 0.5) * scale_y - 0.5);
+        int sy = cv_floor_f(fy);
+        fy -= sy;
+        const short b0 = sat_short((1.f - fy) * 2048), b1 = sat_short(fy * 2048);
+        yt[dy] = make_int4(std::min(std::max(sy, 0), sh - 1), std::min(std::max(sy + 1, 0), sh - 1),
+                           b0, b1);
+    }
+    return area_fast;
+}
+
+int simd_end(int width) {  // VResizeLinearVec_32s8u coverage (oracle pins the same rule)
+    int x = 0;
+    for (; x <= width - 16; x += 16) {}
+    for (; x <= width - 8; x += 8) {}
+    return x;
+}
+
+int alloc_all(orbgpu_ctx* c, int n_images) {
+    const size_t ni = (size_t)std::max(n_images, 1);
+    int r = 0;
+    r |= c->pyr.ensure(ni * c->pyr_img + 256);
+    r |= c->blur.ensure(ni * c->blur_img + 256);
+    r |= c->rtab.ensure(sizeof(int4) * (c->rtab_host.size() + 1));
+    r |= c->cellkeys.ensure(ni * c->cellkeys_img * 4 + 256);
+    r |= c->cellcnt.ensure(ni * c->cellcnt_img * 4 + 256);
+    r |= c->octws.ensure(ni * c->octws_img + 256);
+    r |= c->lvlkey.ensure(ni * c->lvlkp_img * 4 + 256);
+    r |= c->lvlangle.ensure(ni * c->lvlkp_img * 4 + 256);
+    r |= c->lvldesc.ensure(ni * c->lvlkp_img * 32 + 256);
+    r |= c->lvlcnt.ensure(ni * kMaxLevels * 4);
+    r |= c->status.ensure(ni * kMaxLevels * 4);
+    r |= c->outkps.ensure(ni * c->out_cap * sizeof(orbgpu_keypoint) + 256);
+    r |= c->outdesc.ensure(ni * c->out_cap * 32 + 256);
+    r |= c->outn.ensure(ni * 4);
+    r |= c->outmono.ensure(ni * 4);
+    r |= c->laps.ensure(ni * 8);
+    const size_t np = (ni + 1) / 2;
+    r |= c->midx1.ensure(np * c->out_cap * 4 + 256);
+    r |= c->mdist1.ensure(np * c->out_cap * 4 + 256);
+    r |= c->midx2.ensure(np * c->out_cap * 4 + 256);
+    r |= c->mdist2.ensure(np * c->out_cap * 4 + 256);
+    r |= c->mnq.ensure(np * 4 + 64);
+    return r ? fail(ORBGPU_ERR_HIP, "hipMalloc failed (device memory)") : 0;
+}
+
+// Level geometry for a w x h image (input row stride = w in the batch buffer).
+int set_geometry(orbgpu_ctx* c, int w, int h) {
+    if (c->gw == w && c->gh == h) return 0;
+    const int L = c->prm.nlevels;
+    BatchArgs& A = c->A;
+    A = BatchArgs{};
+    A.nlevels = L;
+    A.ini_th = c->prm.ini_th_fast;
+    A.min_th = c->prm.min_th_fast;
+    c->rtab_host.clear();
+    long long pyr_off[kMaxLevels] = {}, blur_off[kMaxLevels] = {};
+    long long pyr = 0, blr = 0, ck = 0, ows = 0;
+    int cc = 0, kpo = 0, cell_first = 0, tile_first = 0, od_first = 0;
+    for (int l = 0; l < L; ++l) {
+        LevelGeom& G = A.lv[l];
+        G.w = cv_round_f((float)w * c->inv_scale[l]);   // ComputePyramid :1336
+        G.h = cv_round_f((float)h * c->inv_scale[l]);
+        if (G.w < 2 * kEdge + 4 || G.h < 2 * kEdge + 4)
+            return fail(ORBGPU_ERR_INVALID, "pyramid level " + std::to_string(l) + " too small");
+        G.bpitch = round_up(G.w, 64);
+        if (l == 0) {
+            G.pitch = w;
+            G.img_stride = (long long)w * h;
+        } else {
+            G.pitch = G.bpitch;
+            pyr_off[l] = pyr;
+            pyr += round_up_ll((long long)G.pitch * G.h, 256);
+        }
+        blur_off[l] = blr;
+        blr += round_up_ll((long long)G.bpitch * G.h, 256);
+        // cell grid (ComputeKeyPointsOctTree :787-805)
+        G.maxBX = G.w - kEdge + 3;
+        G.maxBY = G.h - kEdge + 3;
+        const float width = (float)(G.maxBX - kMinBorder), height = (float)(G.maxBY - kMinBorder);
+        G.nCols = (int)(width / 35.f);
+        G.nRows = (int)(height / 35.f);
+        if (G.nCols < 1 || G.nRows < 1)
+            return fail(ORBGPU_ERR_INVALID, "pyramid level " + std::to_string(l) + " has no cells");
+        G.wCell = (int)std::ceil(width / G.nCols);
+        G.hCell = (int)std::ceil(height / G.nRows);
+        if (G.wCell + 6 > 80 || G.hCell + 6 > 80) return fail(ORBGPU_ERR_INVALID, "cell too large");
+        G.ncells = G.nCols * G.nRows;
+        G.cell_cap = ((G.wCell + 1) / 2) * ((G.hCell + 1) / 2);
+        G.cell_first = cell_first;
+        cell_first += G.ncells;
+        G.cellkey_off = ck;
+        G.cand_cap = G.ncells * G.cell_cap;
+        ck += round_up_ll(G.cand_cap, 64);
+        G.cellcnt_off = cc;
+        cc += round_up(G.ncells, 16);
+        // octree
+        G.N = c->nper[l];
+        G.W = G.maxBX - kMinBorder;
+        G.H = G.maxBY - kMinBorder;
+        const int nIni = std::max(1, (int)std::round((float)G.W / (float)G.H));
+        G.kp_cap = std::min(G.cand_cap, 4 * std::max(G.N, nIni)) + 8;
+        G.kp_off = kpo;
+        kpo += round_up(G.kp_cap, 16);
+        G.oct_cap = G.cand_cap + nIni + 64;
+        G.oct_off = ows;
+        ows += oct_layout(G.cand_cap, G.oct_cap).total;
+        G.scale = c->scale[l];
+        G.patch = (int)(31 * c->scale[l]);
+        G.tiles_x = (G.w + 127) / 128;
+        G.tiles_y = (G.h + 15) / 16;
+        G.tile_first = tile_first;
+        tile_first += G.tiles_x * G.tiles_y;
+        G.od_blocks = std::max(1, (G.N + 16 + 3) / 4);
+        G.od_first = od_first;
+        od_first += G.od_blocks;
+        G.area2 = 0;
+        if (l >= 1) {
+            const LevelGeom& S = A.lv[l - 1];
+            std::vector<int4> xt, yt;
+            G.area2 = resize_tables(S.w, S.h, G.w, G.h, xt, yt) ? 1 : 0;
+            G.xtab_off = (int)c->rtab_host.size();
+            c->rtab_host.insert(c->rtab_host.end(), xt.begin(), xt.end());
+            G.ytab_off = (int)c->rtab_host.size();
+            c->rtab_host.insert(c->rtab_host.end(), yt.begin(), yt.end());
+            G.simd_end = simd_end(G.w);
+        }
+    }
+    c->pyr_img = round_up_ll(pyr, 256);
+    c->blur_img = round_up_ll(blr, 256);
+    c->cellkeys_img = ck;
+    c->cellcnt_img = cc;
+    c->octws_img = round_up_ll(ows, 256);
+    c->lvlkp_img = kpo;
+    c->out_cap = kpo;
+    A.total_cells = cell_first;
+    A.total_tiles = tile_first;
+    A.total_od_blocks = od_first;
+    for (int l = 0; l < L; ++l) {
+        if (l > 0) A.lv[l].img_stride = c->pyr_img;
+        A.lv[l].bimg_stride = c->blur_img;
+    }
+    int r = alloc_all(c, c->max_images);
+    if (r) return r;
+    HIP_TRY(hipMemcpy(c->rtab.p, c->rtab_host.data(), sizeof(int4) * c->rtab_host.size(),
+                      hipMemcpyHostToDevice));
+    for (int l = 0; l < L; ++l) {
+        A.lvl_base[l] = l == 0 ? nullptr : c->pyr.as<uint8_t>() + pyr_off[l];
+        A.blur_base[l] = c->blur.as<uint8_t>() + blur_off[l];
+    }
+    A.rtab = c->rtab.as<int4>();
+    A.cellkeys = c->cellkeys.as<uint32_t>();
+    A.cellkeys_img_stride = c->cellkeys_img;
+    A.cellcnt = c->cellcnt.as<int32_t>();
+    A.cellcnt_img_stride = c->cellcnt_img;
+    A.octws = c->octws.as<uint8_t>();
+    A.octws_img_stride = c->octws_img;
+    A.lvlkey = c->lvlkey.as<uint32_t>();
+    A.lvlangle = c->lvlangle.as<float>();
+    A.lvldesc = c->lvldesc.as<uint8_t>();
+    A.lvlkp_img_stride = c->lvlkp_img;
+    A.lvlcnt = c->lvlcnt.as<int32_t>();
+    A.status = c->status.as<int32_t>();
+    A.out_kps = c->outkps.p;
+    A.out_desc = c->outdesc.as<uint8_t>();
+    A.out_cap = c->out_cap;
+    A.out_n = c->outn.as<int32_t>();
+    A.out_mono = c->outmono.as<int32_t>();
+    A.laps = c->laps.as<int32_t>();
+    c->gw = w;
+    c->gh = h;
+    return 0;
+}
+
+hipEvent_t take_event(orbgpu_ctx* c) {
+    if (!c->event_pool.empty()) {
+        hipEvent_t e = c->event_pool.back();
+        c->event_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e;
+    hipEventCreate(&e);
+    return e;
+}
+
+template <class F>
+int timed(orbgpu_ctx* c, int stage, hipStream_t s, F&& launch) {
+    hipEvent_t a = nullptr, b = nullptr;
+    if (c->prof) {
+        a = take_event(c);
+        b = take_event(c);
+        hipEventRecord(a, s);
+    }
+    hipError_t e = launch();
+    if (e != hipSuccess)
+        return fail(ORBGPU_ERR_HIP, std::string(kStageNames[stage]) + ": " + hipGetErrorString(e));
+    if (c->prof) {
+        hipEventRecord(b, s);
+        c->pending.push_back({stage, a, b});
+    }
+    return 0;
+}
+
+void resolve_pending(orbgpu_ctx* c) {
+    for (auto& p : c->pending) {
+        float ms = 0;
+        if (hipEventSynchronize(p.b) == hipSuccess && hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
+            c->stage_ms[p.stage] += ms;
+            c->stage_n[p.stage] += 1;
+        }
+        c->event_pool.push_back(p.a);
+        c->event_pool.push_back(p.b);
+    }
+    c->pending.clear();
+}
+
+int ensure_input(orbgpu_ctx* c, int n_images, int w, int h) {
+    if (n_images < 1 || n_images > c->max_images)
+        return fail(ORBGPU_ERR_CAPACITY, "n_images exceeds the context's max_images");
+    if (w > c->max_w || h > c->max_h) return fail(ORBGPU_ERR_CAPACITY, "image larger than context max");
+    if (c->input.ensure((size_t)c->max_images * c->max_w * c->max_h + 256))
+        return fail(ORBGPU_ERR_HIP, "hipMalloc failed (input)");
+    return 0;
+}
+
+}  // namespace
+
+// =============================================================================================
+extern "C" {
+
+const char* orbgpu_last_error(void) { return g_err.c_str(); }
+int orbgpu_abi_version(void) { return ORBGPU_ABI_VERSION; }
+int orbgpu_num_stages(void) { return ST_COUNT; }
+const char* orbgpu_stage_name(int s) { return (s >= 0 && s < ST_COUNT) ? kStageNames[s] : ""; }
+
+int orbgpu_create(const orbgpu_params* p, int device, int max_width, int max_height,
+                  int max_images, orbgpu_ctx** out) {
+    if (!p || !out) return fail(ORBGPU_ERR_INVALID, "null argument");
+    *out = nullptr;
+    if (p->nlevels < 1 || p->nlevels > kMaxLevels || p->nfeatures < 0 || !(p->scale_factor > 1.0f) ||
+        max_width <= 0 || max_height <= 0 || max_images <= 0 || max_width >= 4096 + 16 ||
+        max_height >= 4096 + 16)
+        return fail(ORBGPU_ERR_INVALID, "invalid ORB parameters or sizes");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+        return fail(ORBGPU_ERR_NO_DEVICE, "no HIP device");
+    if (device < 0 || device >= ndev) return fail(ORBGPU_ERR_NO_DEVICE, "bad device ordinal");
+    hipDeviceProp_t prop;
+    HIP_TRY(hipGetDeviceProperties(&prop, device));
+    if (std::string(prop.gcnArchName).find("gfx950") == std::string::npos)
+        return fail(ORBGPU_ERR_NO_DEVICE, std::string("device is not gfx950: ") + prop.gcnArchName);
+    HIP_TRY(hipSetDevice(device));
+    orbgpu_ctx* c = new orbgpu_ctx();
+    c->prm = *p;
+    c->device = device;
+    c->max_w = max_width;
+    c->max_h = max_height;
+    c->max_images = max_images;
+    build_tables(c);
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return fail(ORBGPU_ERR_HIP, "hipStreamCreate failed");
+    }
+    int r = ensure_input(c, 1, max_width, max_height);
+    if (!r) r = set_geometry(c, max_width, max_height);
+    if (r) {
+        orbgpu_destroy(c);
+        return r;
+    }
+    *out = c;
+    return ORBGPU_OK;
+}
+
+int orbgpu_destroy(orbgpu_ctx* c) {
+    if (!c) return ORBGPU_OK;
+    hipSetDevice(c->device);
+    if (c->stream) hipStreamSynchronize(c->stream);
+    resolve_pending(c);
+    for (auto e : c->event_pool) hipEventDestroy(e);
+    DevBuf* bufs[] = {&c->input,   &c->pyr,     &c->blur,   &c->rtab,    &c->cellkeys, &c->cellcnt,
+                      &c->octws,   &c->lvlkey,  &c->lvlangle, &c->lvldesc, &c->lvlcnt, &c->status,
+                      &c->outkps,  &c->outdesc, &c->outn,   &c->outmono, &c->laps,     &c->midx1,
+                      &c->mdist1,  &c->midx2,   &c->mdist2, &c->mnq,     &c->scratch};
+    for (DevBuf* b : bufs) b->release();
+    if (c->stream) hipStreamDestroy(c->stream);
+    delete c;
+    return ORBGPU_OK;
+}
+
+int orbgpu_get_scale_tables(const orbgpu_ctx* c, float* scale, float* inv_scale, float* sigma2,
+                            float* inv_sigma2, int32_t* fpl) {
+    if (!c) return fail(ORBGPU_ERR_INVALID, "null ctx");
+    for (int l = 0; l < c->prm.nlevels; ++l) {
+        if (scale) scale[l] = c->scale[l];
+        if (inv_scale) inv_scale[l] = c->inv_scale[l];
+        if (sigma2) sigma2[l] = c->sigma2[l];
+        if (inv_sigma2) inv_sigma2[l] = c->inv_sigma2[l];
+        if (fpl) fpl[l] = c->nper[l];
+    }
+    return ORBGPU_OK;
+}
+
+uint8_t* orbgpu_device_input(orbgpu_ctx* c) { return c ? c->input.as<uint8_t>() : nullptr; }
+
+int orbgpu_upload_images(orbgpu_ctx* c, const uint8_t* images, int n, int w, int h, int stride) {
+    if (!c || !images) return fail(ORBGPU_ERR_INVALID, "null argument");
+    if (w <= 0 || h <= 0) return fail(ORBGPU_ERR_EMPTY_IMAGE, "empty image");
+    if (stride < w) return fail(ORBGPU_ERR_INVALID, "stride < width");
+    int r = ensure_input(c, n, w, h);
+    if (r) return r;
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipMemcpy2DAsync(c->input.p, w, images, stride, w, (size_t)h * n, hipMemcpyHostToDevice,
+                             c->stream));
+    return ORBGPU_OK;
+}
+
+int orbgpu_run_batch(orbgpu_ctx* c, int n, int w, int h, const int32_t* laps, void* stream) {
+    if (!c) return fail(ORBGPU_ERR_INVALID, "null ctx");
+    if (w <= 0 || h <= 0) return fail(ORBGPU_ERR_EMPTY_IMAGE, "empty image");
+    int r = ensure_input(c, n, w, h);
+    if (r) return r;
+    HIP_TRY(hipSetDevice(c->device));
+    r = set_geometry(c, w, h);
+    if (r) return r;
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    if (laps) {
+        HIP_TRY(hipMemcpyAsync(c->laps.p, laps, (size_t)n * 8, hipMemcpyHostToDevice, s));
+    } else {
+        HIP_TRY(hipMemsetAsync(c->laps.p, 0, (size_t)n * 8, s));
+    }
+    BatchArgs A = c->A;
+    A.nimages = n;
+    A.lvl_base[0] = c->input.as<uint8_t>();
+    A.lv[0].img_stride = (long long)w * h;
+    for (int l = 1; l < A.nlevels; ++l) {
+        r = timed(c, ST_RESIZE, s, [&] { return launch_resize(A, l, s); });
+        if (r) return r;
+    }
+    if ((r = timed(c, ST_BLUR, s, [&] { return launch_blur(A, s); }))) return r;
+    if ((r = timed(c, ST_FAST, s, [&] { return launch_fast_cells(A, s); }))) return r;
+    if ((r = timed(c, ST_OCTREE, s, [&] { return launch_octree(A, s); }))) return r;
+    if ((r = timed(c, ST_ORIENT, s, [&] { return launch_orient_desc(A, s); }))) return r;
+    if ((r = timed(c, ST_FINAL, s, [&] { return launch_finalize(A, s); }))) return r;
+    c->last_images = n;
+    c->last_w = w;
+    c->last_h = h;
+    return ORBGPU_OK;
+}
+
+int orbgpu_synchronize(orbgpu_ctx* c) {
+    if (!c) return fail(ORBGPU_ERR_INVALID, "null ctx");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipDeviceSynchronize());
+    resolve_pending(c);
+    return ORBGPU_OK;
+}
+
+int orbgpu_download_counts(orbgpu_ctx* c, int n, int32_t* nk, int32_t* nm) {
+    if (!c) return fail(ORBGPU_ERR_INVALID, "null ctx");
+    if (n > c->last_images) return fail(ORBGPU_ERR_INVALID, "more images than the last batch");
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(hipDeviceSynchronize());
+    if (nk) HIP_TRY(hipMemcpy(nk, c->outn.p, (size_t)n * 4, hipMemcpyDeviceToHost));
+    if (nm) HIP_TRY(hipMemcpy(nm, c->outmono.p, (size_t)n * 4, hipMemcpyDeviceToHost));
+    return ORBGPU_OK;
+}
+
+int orbgpu_download_result(orbgpu_ctx* c, int img, orbgpu_keypoint* kps, uint8_t* desc, int cap,
+                           int* n, int* n_mono) {
+    if (!c || img < 0 || img >= c->last_images) return fail(ORBGPU_ERR_INVALID, "bad image index");
+    HIP_TRY(hipDeviceSynchronize());
+    int32_t nk = 0, nm = 0;
+    HIP_TRY(hipMemcpy(&nk, c->outn.as<int32_t>() + img, 4, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(&nm, c->outmono.as<int32_t>() + img, 4, hipMemcpyDeviceToHost));
+    if (nk == -5) return fail(ORBGPU_ERR_OVERFLOW, "device workspace overflow (octree)");
+    if (nk < 0) return fail(ORBGPU_ERR_CAPACITY, "context output capacity exceeded");
+    if (n) *n = nk;
+    if (n_mono) *n_mono = nm;
+    if (nk > cap) return fail(ORBGPU_ERR_CAPACITY, "caller capacity too small");
+    if (kps && nk)
+        HIP_TRY(hipMemcpy(kps, c->outkps.as<orbgpu_keypoint>() + (size_t)img * c->out_cap,
+                          sizeof(orbgpu_keypoint) * nk, hipMemcpyDeviceToHost));
+    if (desc && nk)
+        HIP_TRY(hipMemcpy(desc, c->outdesc.as<uint8_t>() + (size_t)img * c->out_cap * 32, 32 * (size_t)nk,
+                          hipMemcpyDeviceToHost));
+    return ORBGPU_OK;
+}
+
+int orbgpu_extract(orbgpu_ctx* c, const uint8_t* image, int w, int h, int stride, int lap0,
+                   int lap1, orbgpu_keypoint* kps, uint8_t* desc, int cap, int* n, int* n_mono) {
+    if (!c) return fail(ORBGPU_ERR_INVALID, "null ctx");
+    if (!image || w <= 0 || h <= 0) return fail(ORBGPU_ERR_EMPTY_IMAGE, "empty image");  // :1092
+    int r = orbgpu_upload_images(c, image, 1, w, h, stride);
+    if (r) return r;
+    int32_t laps[2] = {lap0, lap1};
+    r = orbgpu_run_batch(c, 1, w, h, laps, nullptr);
+    if (r) return r;
+    return orbgpu_download_result(c, 0, kps, desc, cap, n, n_mono);
+}
+
+int orbgpu_extract_stereo(orbgpu_ctx* c, const uint8_t* left, const uint8_t* right, int w, int h,
+                          int stride, const int lap_left[2], const int lap_right[2],
+                          orbgpu_keypoint* kl, uint8_t* dl, int* nl, int* ml, orbgpu_keypoint* kr,
+                          uint8_t* dr, int* nr, int* mr, int cap) {
+    if (!c) return fail(ORBGPU_ERR_INVALID, "null ctx");
+    if (!left || !right || w <= 0 || h <= 0) return fail(ORBGPU_ERR_EMPTY_IMAGE, "empty image");
+    int r = ensure_input(c, 2, w, h);
+    if (r) return r;
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipMemcpy2DAsync(c->input.p, w, left, stride, w, h, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpy2DAsync(c->input.as<uint8_t>() + (size_t)w * h, w, right, stride, w, h,
+                             hipMemcpyHostToDevice, c->stream));
+    int32_t laps[4] = {lap_left ? lap_left[0] : 0, lap_left ? lap_left[1] : 0,
+                       lap_right ? lap_right[0] : 0, lap_right ? lap_right[1] : 0};
+    r = orbgpu_run_batch(c, 2, w, h, laps, nullptr);
+    if (r) return r;
+    r = orbgpu_download_result(c, 0, kl, dl, cap, nl, ml);
+    if (r) return r;
+    return orbgpu_download_result(c, 1, kr, dr, cap, nr, mr);
+}
+
+int orbgpu_get_pyramid_level(orbgpu_ctx* c, int img, int level, int blurred, uint8_t* dst,
+                             int dst_stride, int* width, int* height) {
+    if (!c || img < 0 || img >= c->last_images || level < 0 || level >= c->prm.nlevels)
+        return fail(ORBGPU_ERR_INVALID, "bad image/level");
+    HIP_TRY(hipDeviceSynchronize());
+    const LevelGeom& G = c->A.lv[level];
+    if (width) *width = G.w;
+    if (height) *height = G.h;
+    if (!dst) return ORBGPU_OK;
+    if (dst_stride < G.w) return fail(ORBGPU_ERR_INVALID, "dst_stride < level width");
+    const uint8_t* src;
+    int pitch;
+    if (blurred) {
+        src = c->A.blur_base[level] + (size_t)img * c->blur_img;
+        pitch = G.bpitch;
+    } else if (level == 0) {
+        src = c->input.as<uint8_t>() + (size_t)img * c->last_w * c->last_h;
+        pitch = c->last_w;
+    } else {
+        src = c->A.lvl_base[level] + (size_t)img * c->pyr_img;
+        pitch = G.pitch;
+    }
+    HIP_TRY(hipMemcpy2D(dst, dst_stride, src, pitch, G.w, G.h, hipMemcpyDeviceToHost));
+    return ORBGPU_OK;
+}
+
+int orbgpu_get_level_keypoints(orbgpu_ctx* c, int img, orbgpu_keypoint* kps, uint8_t* desc, int cap,
+                               int32_t* counts) {
+    if (!c || img < 0 || img >= c->last_images) return fail(ORBGPU_ERR_INVALID, "bad image index");
+    HIP_TRY(hipDeviceSynchronize());
+    const int L = c->prm.nlevels;
+    std::vector<int32_t> cnt(kMaxLevels), st(kMaxLevels);
+    HIP_TRY(hipMemcpy(cnt.data(), c->lvlcnt.as<int32_t>() + img * kMaxLevels, 4 * kMaxLevels,
+                      hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(st.data(), c->status.as<int32_t>() + img * kMaxLevels, 4 * kMaxLevels,
+                      hipMemcpyDeviceToHost));
+    int off = 0;
+    for (int l = 0; l < L; ++l) {
+        if (st[l]) return fail(ORBGPU_ERR_OVERFLOW, "octree status " + std::to_string(st[l]));
+        const LevelGeom& G = c->A.lv[l];
+        const int m = cnt[l];
+        counts[l] = m;
+        if (off + m > cap) return fail(ORBGPU_ERR_CAPACITY, "caller capacity too small");
+        std::vector<uint32_t> keys(m);
+        std::vector<float> ang(m);
+        const size_t base = (size_t)img * c->lvlkp_img + G.kp_off;
+        if (m) {
+            HIP_TRY(hipMemcpy(keys.data(), c->lvlkey.as<uint32_t>() + base, 4 * m, hipMemcpyDeviceToHost));
+            HIP_TRY(hipMemcpy(ang.data(), c->lvlangle.as<float>() + base, 4 * m, hipMemcpyDeviceToHost));
+            if (desc)
+                HIP_TRY(hipMemcpy(desc + 32 * (size_t)off, c->lvldesc.as<uint8_t>() + base * 32, 32 * (size_t)m,
+                                  hipMemcpyDeviceToHost));
+        }
+        for (int i = 0; i < m; ++i) {
+            orbgpu_keypoint& k = kps[off + i];
+            k.x = (float)((keys[i] & 0xFFF) + kMinBorder);
+            k.y = (float)(((keys[i] >> 12) & 0xFFF) + kMinBorder);
+            k.size = (float)G.patch;
+            k.angle = ang[i];
+            k.response = (float)(keys[i] >> 24);
+            k.octave = l;
+            k.class_id = -1;
+        }
+        off += m;
+    }
+    return ORBGPU_OK;
+}
+
+int orbgpu_match_knn2(orbgpu_ctx* c, const uint8_t* q, int nq, const uint8_t* t, int nt,
+                      int32_t* i1, int32_t* d1, int32_t* i2, int32_t* d2) {
+    if (!c || nq < 0 || nt < 0 || (nq && !q) || (nt && !t)) return fail(ORBGPU_ERR_INVALID, "bad args");
+    if (nq == 0) return ORBGPU_OK;
+    HIP_TRY(hipSetDevice(c->device));
+    const size_t need = 32 * (size_t)(nq + nt) + 16 * (size_t)nq + 1024;
+    if (c->scratch.ensure(need)) return fail(ORBGPU_ERR_HIP, "hipMalloc failed (match scratch)");
+    uint8_t* dq = c->scratch.as<uint8_t>();
+    uint8_t* dt = dq + 32 * (size_t)nq;
+    int32_t* o = reinterpret_cast<int32_t*>(dt + 32 * (size_t)nt + 256 - ((32 * (size_t)(nq + nt)) & 255));
+    HIP_TRY(hipMemcpyAsync(dq, q, 32 * (size_t)nq, hipMemcpyHostToDevice, c->stream));
+    if (nt) HIP_TRY(hipMemcpyAsync(dt, t, 32 * (size_t)nt, hipMemcpyHostToDevice, c->stream));
+    int r = timed(c, ST_KNN, c->stream, [&] {
+        return launch_knn2_plain(dq, nq, dt, nt, o, o + nq, o + 2 * nq, o + 3 * nq, c->stream);
+    });
+    if (r) return r;
+    std::vector<int32_t> h(4 * (size_t)nq);
+    HIP_TRY(hipMemcpyAsync(h.data(), o, 16 * (size_t)nq, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    for (int i = 0; i < nq; ++i) {
+        if (i1) i1[i] = h[i];
+        if (d1) d1[i] = h[nq + i];
+        if (i2) i2[i] = h[2 * nq + i];
+        if (d2) d2[i] = h[3 * nq + i];
+    }
+    return ORBGPU_OK;
+}
+
+int orbgpu_match_stereo_batch(orbgpu_ctx* c, int n_pairs, int stereo_only, void* stream) {
+    if (!c || n_pairs < 1 || 2 * n_pairs > c->last_images) return fail(ORBGPU_ERR_INVALID, "bad pair count");
+    HIP_TRY(hipSetDevice(c->device));
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    MatchArgs m;
+    m.desc = c->outdesc.as<uint8_t>();
+    m.out_n = c->outn.as<int32_t>();
+    m.out_mono = c->outmono.as<int32_t>();
+    m.out_cap = c->out_cap;
+    m.stereo_only = stereo_only;
+    m.idx1 = c->midx1.as<int32_t>();
+    m.dist1 = c->mdist1.as<int32_t>();
+    m.idx2 = c->midx2.as<int32_t>();
+    m.dist2 = c->mdist2.as<int32_t>();
+    m.nq = c->mnq.as<int32_t>();
+    const int qblocks = (c->out_cap + 255) / 256;
+    int r = timed(c, ST_KNN, s, [&] { return launch_knn2_pairs(m, n_pairs, qblocks, s); });
+    if (r) return r;
+    c->last_pairs = n_pairs;
+    return ORBGPU_OK;
+}
+
+int orbgpu_download_matches(orbgpu_ctx* c, int pair, int32_t* i1, int32_t* d1, int32_t* i2,
+                            int32_t* d2, int cap, int* nq) {
+    if (!c || pair < 0 || pair >= c->last_pairs) return fail(ORBGPU_ERR_INVALID, "bad pair");
+    HIP_TRY(hipDeviceSynchronize());
+    int32_t n = 0;
+    HIP_TRY(hipMemcpy(&n, c->mnq.as<int32_t>() + pair, 4, hipMemcpyDeviceToHost));
+    if (nq) *nq = n;
+    if (n > cap) return fail(ORBGPU_ERR_CAPACITY, "caller capacity too small");
+    const size_t o = (size_t)pair * c->out_cap;
+    if (n) {
+        if (i1) HIP_TRY(hipMemcpy(i1, c->midx1.as<int32_t>() + o, 4 * (size_t)n, hipMemcpyDeviceToHost));
+        if (d1) HIP_TRY(hipMemcpy(d1, c->mdist1.as<int32_t>() + o, 4 * (size_t)n, hipMemcpyDeviceToHost));
+        if (i2) HIP_TRY(hipMemcpy(i2, c->midx2.as<int32_t>() + o, 4 * (size_t)n, hipMemcpyDeviceToHost));
+        if (d2) HIP_TRY(hipMemcpy(d2, c->mdist2.as<int32_t>() + o, 4 * (size_t)n, hipMemcpyDeviceToHost));
+    }
+    return ORBGPU_OK;
+}
+
+int orbgpu_descriptor_distance(const uint8_t* a, const uint8_t* b) {
+    int dist = 0;
+    for (int i = 0; i < 8; ++i) {
+        uint32_t pa, pb;
+        std::memcpy(&pa, a + 4 * i, 4);
+        std::memcpy(&pb, b + 4 * i, 4);
+        dist += __builtin_popcount(pa ^ pb);
+    }
+    return dist;
+}
+
+int orbgpu_set_profiling(orbgpu_ctx* c, int enable) {
+    if (!c) return fail(ORBGPU_ERR_INVALID, "null ctx");
+    c->prof = enable != 0;
+    return ORBGPU_OK;
+}
+
+int orbgpu_stage_times(orbgpu_ctx* c, double* ms, int64_t* launches, int max_stages) {
+    if (!c) return fail(ORBGPU_ERR_INVALID, "null ctx");
+    resolve_pending(c);
+    for (int s = 0; s < ST_COUNT && s < max_stages; ++s) {
+        if (ms) ms[s] = c->stage_ms[s];
+        if (launches) launches[s] = c->stage_n[s];
+    }
+    return ST_COUNT;
+}
+
+int orbgpu_reset_stage_times(orbgpu_ctx* c) {
+    if (!c) return fail(ORBGPU_ERR_INVALID, "null ctx");
+    resolve_pending(c);
+    for (int s = 0; s < ST_COUNT; ++s) c->stage_ms[s] = 0, c->stage_n[s] = 0;
+    return ORBGPU_OK;
+}
+
+}  // extern "C"

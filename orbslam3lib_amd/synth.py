@@ -1,0 +1,88 @@
+"""Deterministic synthetic stereo frames — there is no dataset on the box.
+
+Image = value-noise octaves (cells 64/16/4 px, weights .5/.3/.2, seed s) + 48 rectangles and
+24 discs of random intensity (seed s+1) + a zero-mean 3-px texture octave (weight .35, seed s+7;
+lifts the level-0 FAST candidate count at th=20 into the 5k-20k band SURVEY §8d asks for) +
+Gaussian noise sigma=2 (seed s+2), clipped to u8.
+The right eye is the clean left scene shifted by `disparity` px with its own noise (seed s+3).
+Frame k uses s = 42 + 4k.  Pure numpy, so CPU tests and the GPU bench see identical pixels.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+__all__ = ["scene", "frame", "stereo_pair", "stereo_batch"]
+
+
+def _value_noise(rng, h, w, cell):
+    gh, gw = h // cell + 2, w // cell + 2
+    grid = rng.random((gh, gw), dtype=np.float64)
+    ys = np.arange(h, dtype=np.float64) / cell
+    xs = np.arange(w, dtype=np.float64) / cell
+    y0 = np.floor(ys).astype(np.int64)
+    x0 = np.floor(xs).astype(np.int64)
+    fy = (ys - y0)[:, None]
+    fx = (xs - x0)[None, :]
+    fy = fy * fy * (3 - 2 * fy)  # smoothstep
+    fx = fx * fx * (3 - 2 * fx)
+    g00 = grid[y0][:, x0]
+    g01 = grid[y0][:, x0 + 1]
+    g10 = grid[y0 + 1][:, x0]
+    g11 = grid[y0 + 1][:, x0 + 1]
+    top = g00 * (1 - fx) + g01 * fx
+    bot = g10 * (1 - fx) + g11 * fx
+    return top * (1 - fy) + bot * fy
+
+
+def scene(h: int, w: int, seed: int, pad: int = 0) -> np.ndarray:
+    """Clean float scene of size h x (w + pad) (pad gives room for the stereo shift)."""
+    W = w + pad
+    rng = np.random.default_rng(seed)
+    img = np.zeros((h, W), dtype=np.float64)
+    for cell, wt in ((64, 0.5), (16, 0.3), (4, 0.2)):
+        img += wt * 255.0 * _value_noise(rng, h, W, cell)
+    rng2 = np.random.default_rng(seed + 1)
+    yy, xx = np.mgrid[0:h, 0:W]
+    for _ in range(48):
+        x0, y0 = rng2.integers(0, W), rng2.integers(0, h)
+        rw, rh = rng2.integers(8, max(9, W // 6)), rng2.integers(8, max(9, h // 6))
+        val = rng2.integers(0, 256)
+        img[y0:y0 + rh, x0:x0 + rw] = 0.35 * img[y0:y0 + rh, x0:x0 + rw] + 0.65 * val
+    for _ in range(24):
+        cx, cy = rng2.integers(0, W), rng2.integers(0, h)
+        r = rng2.integers(5, max(6, min(h, W) // 10))
+        val = rng2.integers(0, 256)
+        m = (xx - cx) ** 2 + (yy - cy) ** 2 <= r * r
+        img[m] = 0.3 * img[m] + 0.7 * val
+    rng3 = np.random.default_rng(seed + 7)
+    img += 0.35 * 255.0 * (_value_noise(rng3, h, W, 3) - 0.5)
+    return img
+
+
+def _finish(img: np.ndarray, seed: int) -> np.ndarray:
+    rng = np.random.default_rng(seed)
+    noisy = img + rng.normal(0.0, 2.0, size=img.shape)
+    return np.clip(np.rint(noisy), 0, 255).astype(np.uint8)
+
+
+def frame(h: int, w: int, k: int = 0) -> np.ndarray:
+    """Mono frame k (h x w, uint8)."""
+    s = 42 + 4 * k
+    return _finish(scene(h, w, s), s + 2)
+
+
+def stereo_pair(h: int, w: int, k: int = 0, disparity: int = 12):
+    """(left, right) uint8 frames of pair k; right = left scene shifted by `disparity` px."""
+    s = 42 + 4 * k
+    sc = scene(h, w, s, pad=disparity)
+    left = _finish(np.ascontiguousarray(sc[:, :w]), s + 2)
+    right = _finish(np.ascontiguousarray(sc[:, disparity:disparity + w]), s + 3)
+    return left, right
+
+
+def stereo_batch(h: int, w: int, npairs: int, first: int = 0, disparity: int = 12) -> np.ndarray:
+    """[2*npairs, h, w] uint8, images ordered L0, R0, L1, R1, ..."""
+    out = np.empty((2 * npairs, h, w), dtype=np.uint8)
+    for i in range(npairs):
+        out[2 * i], out[2 * i + 1] = stereo_pair(h, w, first + i, disparity)
+    return out

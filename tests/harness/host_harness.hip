@@ -1,0 +1,95 @@
+// host_harness.hip -- TEST INFRASTRUCTURE: runs the device algorithm headers of the product
+// (orb_octree.h, orb_fast_cell.h, orb_introsort.h, orb_math.h) on the host with SerialPolicy so
+// they can be checked against the CPU oracle without a GPU.  Not part of liborbgpu.so.
+#include <cmath>
+#include <vector>
+
+#include "../../orbslam3lib_amd/csrc/orb_fast_cell.h"
+#include "../../orbslam3lib_amd/csrc/orb_introsort.h"
+#include "../../orbslam3lib_amd/csrc/orb_math.h"
+#include "../../orbslam3lib_amd/csrc/orb_octree.h"
+#include "../../orbslam3lib_amd/csrc/orb_policy.h"
+
+using namespace orbgpu;
+
+extern "C" {
+
+int harness_octree(const uint32_t* keys, int n, int W, int H, int N, uint32_t* out, int out_cap) {
+    const int nIni = std::max(1, (int)std::round((float)W / (float)H));
+    const int cap = n + nIni + 64;
+    std::vector<int32_t> knode(n + 1), childcnt(4 * cap), childpos(4 * cap), divrank(cap),
+        rank2node(cap), rankoff(cap), expoff(cap), undivpos(cap), vA(cap), vB(cap);
+    std::vector<uint8_t> kq(n + 1);
+    std::vector<OctNode> nA(cap), nB(cap);
+    std::vector<SortElem> sb(cap);
+    std::vector<uint32_t> best(cap);
+    OctWS w;
+    w.keys = keys;
+    w.n = n;
+    w.cap = cap;
+    w.knode = knode.data();
+    w.kq = kq.data();
+    w.nodesA = nA.data();
+    w.nodesB = nB.data();
+    w.childcnt = childcnt.data();
+    w.childpos = childpos.data();
+    w.divrank = divrank.data();
+    w.rank2node = rank2node.data();
+    w.rankoff = rankoff.data();
+    w.expoff = expoff.data();
+    w.undivpos = undivpos.data();
+    w.vsizeA = vA.data();
+    w.vsizeB = vB.data();
+    w.sortbuf = sb.data();
+    w.best = best.data();
+    w.out_keys = out;
+    w.out_cap = out_cap;
+    OctShared sh;
+    SerialPolicy p;
+    return octree_distribute(p, w, &sh, W, H, N);
+}
+
+void harness_introsort(const int32_t* size, const int32_t* ulx, int n, int32_t* perm) {
+    std::vector<SortElem> a(n);
+    for (int i = 0; i < n; ++i) a[i] = SortElem{size[i], ulx[i], i};
+    introsort_like_libstdcxx(a.data(), n);
+    for (int i = 0; i < n; ++i) perm[i] = a[i].node;
+}
+
+int harness_fast_strength(const uint8_t* img, int stride, int x, int y, int tlow) {
+    return fast_strength(img + (long long)y * stride + x, stride, tlow);
+}
+
+float harness_fast_atan2(float y, float x) { return fast_atan2_deg(y, x); }
+
+// ComputeKeyPointsOctTree cell loop geometry (same formulas as orb_runtime.cpp) + fast_cell_run.
+int harness_level_candidates(const uint8_t* lvl, int w, int h, int ini, int mn, uint32_t* out,
+                             int cap) {
+    const int minB = 16, maxBX = w - 16, maxBY = h - 16;
+    const float width = (float)(maxBX - minB), height = (float)(maxBY - minB);
+    const int nCols = (int)(width / 35.f), nRows = (int)(height / 35.f);
+    const int wCell = (int)std::ceil(width / nCols), hCell = (int)std::ceil(height / nRows);
+    std::vector<uint8_t> T(kCellMax * kCellMax), M(kCellMax * kCellMax);
+    std::vector<uint32_t> tmp(kCellMax * kCellMax);
+    int total = 0, cnt = 0;
+    SerialPolicy p;
+    for (int i = 0; i < nRows; ++i)
+        for (int j = 0; j < nCols; ++j) {
+            CellGeom g;
+            g.iniY = minB + i * hCell;
+            g.iniX = minB + j * wCell;
+            g.minBorder = minB;
+            if (g.iniY >= maxBY - 3 || g.iniX >= maxBX - 6) continue;
+            g.rows = std::min(g.iniY + hCell + 6, maxBY) - g.iniY;
+            g.cols = std::min(g.iniX + wCell + 6, maxBX) - g.iniX;
+            const int m = fast_cell_run(p, lvl + (long long)g.iniY * w + g.iniX, w, g, ini, mn,
+                                        T.data(), M.data(), &cnt, tmp.data());
+            for (int k = 0; k < m; ++k) {
+                if (total < cap) out[total] = tmp[k];
+                ++total;
+            }
+        }
+    return total;
+}
+
+}  // extern "C"

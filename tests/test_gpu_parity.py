@@ -1,0 +1,163 @@
+"""GPU parity: liborbgpu.so (HIP, gfx950) vs the CPU oracle, bit-exact, through the C ABI.
+
+Bar (BASELINE.json north_star): keypoint indices/coordinates and 32-byte descriptors bit-exact;
+angles (centroid) within 1e-4 deg -- here they are required bit-exact too, since the descriptor
+sampling depends on them.
+"""
+import numpy as np
+import pytest
+
+from orbslam3lib_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+
+def _extractor(nf=2000, L=8, w=640, h=480, imgs=2, sf=1.2):
+    import orbslam3lib_amd as og
+    return og.ORBextractor(nf, sf, L, 20, 7, max_width=w, max_height=h, max_images=imgs)
+
+
+def _same_kps(a, b):
+    assert len(a) == len(b), (len(a), len(b))
+    for f in ("x", "y", "size", "angle", "response", "octave", "class_id"):
+        np.testing.assert_array_equal(a[f], b[f], err_msg=f)
+
+
+@pytest.fixture(scope="module")
+def frame0():
+    return synth.stereo_pair(480, 640, 0)
+
+
+def test_pyramid_and_blur_bit_exact(oracle, frame0):
+    L, _ = frame0
+    ex = _extractor()
+    ex(L)
+    ref = oracle.pyramid(L)
+    for l in range(8):
+        g = ex.pyramid_level(0, l)
+        np.testing.assert_array_equal(g, ref[l], err_msg="level %d" % l)
+        np.testing.assert_array_equal(ex.pyramid_level(0, l, blurred=True), oracle.blur(ref[l]),
+                                      err_msg="blur level %d" % l)
+
+
+def test_level_keypoints_and_descriptors(oracle, frame0):
+    L, _ = frame0
+    ex = _extractor()
+    ex(L)
+    got = ex.level_keypoints(0)
+    ref = oracle.extract_levels(L, nfeatures=2000)
+    for l in range(8):
+        (gk, gd), (rk, rd) = got[l], ref[l]
+        _same_kps(gk, rk)
+        np.testing.assert_array_equal(gd, rd, err_msg="desc level %d" % l)
+
+
+@pytest.mark.parametrize("lap", [(0, 0), (0, 1000), (200, 420)])
+def test_extract_matches_oracle(oracle, frame0, lap):
+    L, R = frame0
+    ex = _extractor()
+    for img in (L, R):
+        k, d, m = ex(img, None, lap)
+        rk, rd, rm = oracle.extract(img, nfeatures=2000, lap=lap)
+        assert m == rm
+        _same_kps(k, rk)
+        np.testing.assert_array_equal(d, rd)
+
+
+def test_mono_config_c1(oracle):
+    img = synth.frame(480, 640, 3)
+    ex = _extractor(nf=1000)
+    k, d, m = ex(img, None, (0, 1000))
+    rk, rd, rm = oracle.extract(img, nfeatures=1000, lap=(0, 1000))
+    assert m == rm == 0
+    _same_kps(k, rk)
+    np.testing.assert_array_equal(d, rd)
+
+
+def test_stereo_entry_point(oracle, frame0):
+    L, R = frame0
+    ex = _extractor()
+    (kl, dl, ml), (kr, dr, mr) = ex.extract_stereo(L, R, (0, 0), (100, 639))
+    for (k, d, m), img, lap in (((kl, dl, ml), L, (0, 0)), ((kr, dr, mr), R, (100, 639))):
+        rk, rd, rm = oracle.extract(img, nfeatures=2000, lap=lap)
+        assert m == rm
+        _same_kps(k, rk)
+        np.testing.assert_array_equal(d, rd)
+
+
+def test_batch_path_matches_oracle(oracle):
+    import orbslam3lib_amd as og
+    imgs = synth.stereo_batch(480, 640, 4, first=5)
+    be = og.BatchExtractor(2000, 1.2, 8, 20, 7, width=640, height=480, max_images=8)
+    be.upload(imgs)
+    laps = np.array([[0, 0], [50, 600]] * 4, np.int32)
+    be.run(laps)
+    be.match_stereo(False)
+    be.synchronize()
+    for i in range(8):
+        k, d, m = be.result(i)
+        rk, rd, rm = oracle.extract(imgs[i], nfeatures=2000, lap=tuple(laps[i]))
+        assert m == rm
+        _same_kps(k, rk)
+        np.testing.assert_array_equal(d, rd)
+    for p in range(4):
+        i1, d1, i2, d2 = be.matches(p)
+        _, ql, _ = be.result(2 * p)
+        _, tr, _ = be.result(2 * p + 1)
+        r = oracle.knn2(ql, tr)
+        for a, b in zip((i1, d1, i2, d2), r):
+            np.testing.assert_array_equal(a, b)
+
+
+def test_knn2_ties_and_edges(oracle):
+    import orbslam3lib_amd as og
+    ex = _extractor()
+    bf = og.BFMatcher(ex)
+    rng = np.random.default_rng(1)
+    base = rng.integers(0, 256, (40, 32), dtype=np.uint8)
+    t = np.concatenate([base, base, base[:7]])          # exact duplicates -> ties
+    q = np.concatenate([base[:13], rng.integers(0, 256, (1200, 32), dtype=np.uint8)])
+    for tt in (t, t[:1], t[:0], rng.integers(0, 256, (1700, 32), dtype=np.uint8)):
+        got = bf.knnMatch(q, tt, 2)
+        ref = oracle.knn2(q, tt)
+        for a, b in zip(got, ref):
+            np.testing.assert_array_equal(a, b)
+
+
+def test_euroc_size_and_other_frames(oracle):
+    ex = _extractor(w=752, h=480)
+    for k in (1, 7):
+        img = synth.frame(480, 752, k)
+        g = ex(img, None, (0, 0))
+        r = oracle.extract(img, nfeatures=2000, lap=(0, 0))
+        assert g[2] == r[2]
+        _same_kps(g[0], r[0])
+        np.testing.assert_array_equal(g[1], r[1])
+
+
+def test_c5_1080p_12_levels(oracle):
+    img = synth.frame(1080, 1920, 2)
+    ex = _extractor(nf=5000, L=12, w=1920, h=1080)
+    g = ex(img, None, (0, 0))
+    r = oracle.extract(img, nfeatures=5000, nlevels=12, lap=(0, 0))
+    assert g[2] == r[2]
+    _same_kps(g[0], r[0])
+    np.testing.assert_array_equal(g[1], r[1])
+
+
+def test_flat_and_empty_images(oracle):
+    ex = _extractor()
+    flat = np.full((480, 640), 128, np.uint8)
+    k, d, m = ex(flat)
+    rk, rd, rm = oracle.extract(flat, nfeatures=2000)
+    assert len(k) == len(rk) == 0 and m == rm == 0
+    k, d, m = ex(np.zeros((0, 0), np.uint8))
+    assert m == -1 and len(k) == 0
+
+
+def test_descriptor_distance_matches_reference(oracle):
+    import orbslam3lib_amd as og
+    rng = np.random.default_rng(3)
+    for _ in range(200):
+        a, b = rng.integers(0, 256, (2, 32), dtype=np.uint8)
+        assert og.ORBmatcher.DescriptorDistance(a, b) == oracle.descriptor_distance(a, b)
