@@ -1,0 +1,281 @@
+#!/usr/bin/env python3
+"""bench.py -- Mfeatures/s (ORB extract) + Mmatches/s (Hamming kNN2) on MI355X.
+
+Workload (BASELINE.json configs[1], C2): 640x480 stereo pairs, 8-level pyramid (scale 1.2),
+2000 features per frame, FAST 20/7; each pair's left descriptors are matched against all its
+right descriptors (2000 x 2000 kNN2, the C3 matcher step).  A "step" = one pass of the hot path
+over a device-resident batch of `--pairs` stereo pairs per GPU (inputs already in HBM).
+
+Multi-GPU: one process per GPU (torch.distributed.run); every rank extracts its own shard of
+pairs (frames are independent -> weak scaling, no data-path collective); barrier + max over
+ranks bracket the timed region.  Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12  # 256 CU x 4 SIMD32 x 32 lanes x 2.4 GHz, int32 ops
+
+
+def level_sizes(w, h, sf=1.2, L=8):
+    """ComputePyramid sizes (ORBextractor_old.cc:1336) with the float math of the ctor."""
+    scale = [np.float32(1.0)]
+    for _ in range(1, L):
+        scale.append(np.float32(np.float64(scale[-1]) * np.float64(np.float32(sf))))
+    out = []
+    for s in scale:
+        inv = np.float32(1.0) / s
+        out.append((int(np.rint(np.float32(w) * inv)), int(np.rint(np.float32(h) * inv))))
+    return out
+
+
+def algorithmic_bytes(w, h, L, nkp, sf=1.2):
+    """Per-image bytes by stage: pyramid sum(A_{l-1}+A_l), FAST sum(A_l),
+    blur 2*sum(A_l), 48 B per output keypoint (16 B keypoint + 32 B descriptor)."""
+    A = [a * b for a, b in level_sizes(w, h, sf, L)]
+    return {
+        "k_resize": sum(A[l - 1] + A[l] for l in range(1, L)),
+        "k_fast_cells": sum(A),
+        "k_blur": 2 * sum(A),
+        "k_orient_desc": 48 * nkp,
+    }
+
+
+def dist_setup():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as td
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+        td.init_process_group(backend=backend)
+        dist = td
+    return world, rank, local, dist
+
+
+def barrier(dist):
+    if dist is not None:
+        dist.barrier()
+
+
+def max_over_ranks(dist, x):
+    if dist is None:
+        return x
+    import torch
+    dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def sum_over_ranks(dist, x):
+    if dist is None:
+        return x
+    import torch
+    dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())
+
+
+def cpu_baseline(w, h, nfeatures, seconds):
+    """The oracle (scalar C++ restatement of the reference CPU ORBextractor + BFMatcher), one
+    thread, on a bounded sample of the same workload: pairs until `seconds` elapse."""
+    from oracle import oracle_py as O
+    from orbslam3lib_amd import synth
+    O.lib()
+    pairs = [synth.stereo_pair(h, w, 1000 + i) for i in range(4)]
+    nfeat = nq = 0
+    t_ex = t_bf = 0.0
+    i = 0
+    t_end = time.perf_counter() + seconds
+    while time.perf_counter() < t_end or i == 0:
+        L, R = pairs[i % len(pairs)]
+        t0 = time.perf_counter()
+        kl, dl, _ = O.extract(L, nfeatures=nfeatures, lap=(0, 0))
+        kr, dr, _ = O.extract(R, nfeatures=nfeatures, lap=(0, 0))
+        t1 = time.perf_counter()
+        O.knn2(dl, dr)
+        t2 = time.perf_counter()
+        nfeat += len(kl) + len(kr)
+        nq += len(dl)
+        t_ex += t1 - t0
+        t_bf += t2 - t1
+        i += 1
+    return {"pairs": i, "mfeat_s": nfeat / t_ex / 1e6, "mmatch_s": nq / t_bf / 1e6,
+            "mfeat_s_pipeline": nfeat / (t_ex + t_bf) / 1e6}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--pairs", type=int, default=64, help="stereo pairs per GPU per step")
+    ap.add_argument("--unique-pairs", type=int, default=16,
+                    help="distinct synthetic pairs generated per rank (tiled to --pairs)")
+    ap.add_argument("--width", type=int, default=640)
+    ap.add_argument("--height", type=int, default=480)
+    ap.add_argument("--nfeatures", type=int, default=2000)
+    ap.add_argument("--nlevels", type=int, default=8)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-profile", action="store_true",
+                    help="do not bracket launches with HIP events in the timed region")
+    args = ap.parse_args()
+
+    world, rank, local, dist = dist_setup()
+    import orbslam3lib_amd as og
+    from orbslam3lib_amd import synth
+
+    P, W, H = args.pairs, args.width, args.height
+    U = max(1, min(args.unique_pairs, P))
+    base = rank * 100000
+    uniq = [synth.stereo_pair(H, W, base + i) for i in range(U)]
+    imgs = np.empty((2 * P, H, W), np.uint8)
+    for p in range(P):
+        imgs[2 * p], imgs[2 * p + 1] = uniq[p % U]
+
+    be = og.BatchExtractor(args.nfeatures, 1.2, args.nlevels, 20, 7, device=local, width=W,
+                           height=H, max_images=2 * P)
+    be.upload(imgs)  # PCIe upload: outside the timed region (inputs resident in HBM)
+    laps = np.zeros((2 * P, 2), np.int32)
+
+    def step():
+        be.run(laps)
+        be.match_stereo(stereo_rows_only=False)
+
+    for _ in range(args.warmup):
+        step()
+    be.synchronize()
+    nk, _ = be.counts()
+    feats_per_step = int(nk.sum())
+    nq_per_step = int(sum(nk[2 * p] for p in range(P)))
+    pairs_per_step = int(sum(int(nk[2 * p]) * int(nk[2 * p + 1]) for p in range(P)))
+
+    be.set_profiling(not args.no_profile)
+    be.reset_stage_times()
+    try:
+        import torch
+        has_cuda = torch.cuda.is_available()
+    except Exception:
+        has_cuda = False
+    barrier(dist)
+    be.synchronize()
+    if has_cuda:
+        torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    be.synchronize()
+    if has_cuda:
+        torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    barrier(dist)
+    elapsed = max_over_ranks(dist, t1 - t0)
+    stages = be.stage_times()
+    be.set_profiling(False)
+
+    total_feats = sum_over_ranks(dist, feats_per_step * args.steps)
+    total_q = sum_over_ranks(dist, nq_per_step * args.steps)
+    total_pairs = sum_over_ranks(dist, pairs_per_step * args.steps)
+    mfeat = total_feats / elapsed / 1e6
+    mmatch = total_q / elapsed / 1e6
+
+    # roofline of the dominant kernel (per-launch algorithmic bytes / measured avg duration)
+    n_img = 2 * P
+    per_img = algorithmic_bytes(W, H, args.nlevels, feats_per_step / n_img)
+    stage_rows = {}
+    for name, (ms, cnt) in stages.items():
+        if cnt == 0:
+            continue
+        avg_ms = ms / cnt
+        row = {"avg_us": round(avg_ms * 1e3, 2), "launches": cnt, "total_ms": round(ms, 3)}
+        if name in per_img:
+            launches_per_step = (args.nlevels - 1) if name == "k_resize" else 1
+            bytes_launch = per_img[name] * n_img / launches_per_step
+            row["bytes_per_launch"] = int(bytes_launch)
+            row["GBps"] = round(bytes_launch / (avg_ms * 1e-3) / 1e9, 1)
+            row["frac_hbm"] = round(row["GBps"] / HBM_PEAK_GBS, 4)
+        if name == "k_knn2":
+            ops = 16.0 * pairs_per_step
+            row["Tops"] = round(ops / (avg_ms * 1e-3) / 1e12, 2)
+            row["frac_valu"] = round(row["Tops"] / VALU_PEAK_TOPS, 4)
+        stage_rows[name] = row
+    dom = max(stage_rows, key=lambda k: stage_rows[k]["total_ms"]) if stage_rows else None
+    roof = None
+    if dom is not None:
+        r = stage_rows[dom]
+        traffic = None
+        tp = os.path.join(ROOT, "profiles", "traffic_r01.json")
+        if os.path.exists(tp):
+            try:
+                traffic = json.load(open(tp)).get(dom, {}).get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        if "GBps" in r:
+            roof = {"kernel": dom, "bound": "hbm", "achieved": r["GBps"], "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": r["frac_hbm"], "traffic": traffic,
+                    "bytes_per_launch": r["bytes_per_launch"], "avg_us": r["avg_us"]}
+        elif "Tops" in r:
+            roof = {"kernel": dom, "bound": "valu", "achieved": r["Tops"], "peak": round(VALU_PEAK_TOPS, 1),
+                    "unit": "Tops/s", "frac": r["frac_valu"], "traffic": traffic, "avg_us": r["avg_us"]}
+        else:  # latency-bound kernel with no HBM-scale algorithmic bytes (e.g. the octree)
+            roof = {"kernel": dom, "bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": None, "traffic": traffic, "avg_us": r["avg_us"],
+                    "note": "control-flow bound kernel; see stages"}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cb = cpu_baseline(W, H, args.nfeatures, args.cpu_seconds)
+        cpu = {"value": round(cb["mfeat_s"], 5), "unit": "Mfeatures/s", "cores": 1, "kind": "port",
+               "sample": "%d synthetic 640x480 stereo pairs, oracle extract (both eyes, 1 thread); "
+                         "BF kNN2 %.4f Mmatches/s" % (cb["pairs"], cb["mmatch_s"]),
+               "mmatches_s": round(cb["mmatch_s"], 5)}
+
+    if rank == 0:
+        out = {
+            "metric": "Mfeatures/s extract + Mmatches/s BFMatch, 640x480 stereo 8-level pyr, 1/2/4/8 GPU",
+            "value": round(mfeat, 3),
+            "unit": "Mfeatures/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic seeded stereo frames (SURVEY §8d generator), resident in HBM",
+            "config": {"workload": "C2 640x480 stereo, 8 levels x1.2, 2000 feat/frame, FAST 20/7, "
+                                   "+ per-pair 2000x2000 Hamming kNN2 (left->right, all rows)",
+                       "pairs_per_gpu_per_step": P, "images_per_gpu_per_step": 2 * P,
+                       "parallelism": "frames sharded across %d GPU(s), replicas" % world},
+            "matches": {"value": round(mmatch, 3), "unit": "Mmatches/s",
+                        "gpairs_s": round(total_pairs / elapsed / 1e9, 3)},
+            "features_per_step_per_gpu": feats_per_step,
+            "roofline": roof,
+            "stages": stage_rows,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,121 @@
+"""CPU: the product's device algorithms (orb_fast_cell.h, orb_octree.h, orb_introsort.h,
+orb_math.h) run on the host with SerialPolicy and are compared with the oracle."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from orbslam3lib_amd import synth
+
+
+def _p(a):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def _unpack(k):
+    k = np.asarray(k, np.uint32)
+    return ((k & 0xFFF).astype(np.float32), ((k >> 12) & 0xFFF).astype(np.float32),
+            (k >> 24).astype(np.float32))
+
+
+def test_introsort_equals_libstdcxx(harness, oracle):
+    rng = np.random.default_rng(0)
+    for _ in range(300):
+        n = int(rng.integers(0, 600))
+        sz = rng.integers(2, 6, n).astype(np.int32)
+        ux = (rng.integers(0, 8, n) * 16).astype(np.int32)
+        perm = np.zeros(n, np.int32)
+        harness.harness_introsort(_p(sz), _p(ux), n, _p(perm))
+        np.testing.assert_array_equal(perm, oracle.sort_nodes(sz, ux))
+    # adversarial: all equal (every comparison a tie), sorted, reverse sorted, organ pipe
+    for arr in (np.full(300, 3), np.arange(300), np.arange(300)[::-1],
+                np.concatenate([np.arange(150), np.arange(150)[::-1]])):
+        sz = np.asarray(arr, np.int32)
+        ux = np.zeros_like(sz)
+        perm = np.zeros(len(sz), np.int32)
+        harness.harness_introsort(_p(sz), _p(ux), len(sz), _p(perm))
+        np.testing.assert_array_equal(perm, oracle.sort_nodes(sz, ux))
+
+
+def test_fast_atan2_bit_exact(harness, oracle):
+    rng = np.random.default_rng(1)
+    for y, x in rng.integers(-40000, 40000, (3000, 2)):
+        assert harness.harness_fast_atan2(float(y), float(x)) == oracle.fast_atan2(float(y), float(x))
+    for y, x in ((0, 0), (0, -5), (-5, 0), (7, 7), (-7, 7)):
+        assert harness.harness_fast_atan2(float(y), float(x)) == oracle.fast_atan2(float(y), float(x))
+
+
+def test_fast_strength_vs_corner_score(harness, oracle):
+    img = synth.frame(64, 64, 4)
+    for th in (7, 20, 40):
+        for y in range(3, 61, 3):
+            for x in range(3, 61, 2):
+                m = harness.harness_fast_strength(_p(img), 64, x, y, 0)
+                cs = oracle.corner_score(img, x, y, th)
+                # cornerScore<16>(t) == max(t, m) - 1
+                assert cs == max(th, m) - 1
+
+
+def _level_cands(harness, lvl, ini, mn):
+    lvl = np.ascontiguousarray(lvl)
+    h, w = lvl.shape
+    out = np.zeros(w * h, np.uint32)
+    n = harness.harness_level_candidates(_p(lvl), w, h, ini, mn, _p(out), w * h)
+    return out[:n]
+
+
+@pytest.mark.parametrize("frame", [0, 1])
+def test_cells_and_octree_all_levels(harness, oracle, frame):
+    img = synth.stereo_pair(480, 640, frame)[frame % 2]
+    for li, lvl in enumerate(oracle.pyramid(img)):
+        h, w = lvl.shape
+        cand = _level_cands(harness, lvl, 20, 7)
+        oc = oracle.level_candidates(lvl, 20, 7)
+        x, y, r = _unpack(cand)
+        np.testing.assert_array_equal(x, oc["x"])
+        np.testing.assert_array_equal(y, oc["y"])
+        np.testing.assert_array_equal(r, oc["response"])
+        for N in (oracle.features_per_level(2000)[li], 1, 0, 7, 5000):
+            ref = oracle.distribute_octree(oc, 16, w - 16, 16, h - 16, N)
+            out = np.zeros(len(cand) + 4 * max(N, 1) + 64, np.uint32)
+            m = harness.harness_octree(_p(cand), len(cand), w - 32, h - 32, N, _p(out), len(out))
+            assert m == len(ref), (li, N)
+            x2, y2, r2 = _unpack(out[:m])
+            np.testing.assert_array_equal(x2, ref["x"])
+            np.testing.assert_array_equal(y2, ref["y"])
+            np.testing.assert_array_equal(r2, ref["response"])
+
+
+def test_octree_edge_cases(harness, oracle):
+    # empty, single key, clustered keys, wide image (nIni = 2)
+    kd = oracle.KP_DTYPE
+    cases = []
+    cases.append((np.zeros(0, kd), 608, 448, 10))
+    one = np.zeros(1, kd); one["x"] = 5; one["y"] = 9; one["response"] = 30
+    cases.append((one, 608, 448, 10))
+    rng = np.random.default_rng(4)
+    pts = set()
+    while len(pts) < 300:
+        pts.add((int(rng.integers(100, 121)), int(rng.integers(200, 221))))
+    cl = np.zeros(len(pts), kd)
+    for i, (x, y) in enumerate(sorted(pts, key=lambda t: (t[1], t[0]))):
+        cl[i]["x"], cl[i]["y"], cl[i]["response"] = x, y, rng.integers(0, 60)
+    cases.append((cl, 608, 448, 50))
+    wide = np.zeros(2000, kd)
+    pts = set()
+    while len(pts) < 2000:
+        pts.add((int(rng.integers(3, 1885)), int(rng.integers(3, 1045))))
+    for i, (x, y) in enumerate(pts):
+        wide[i]["x"], wide[i]["y"], wide[i]["response"] = x, y, rng.integers(0, 9)
+    cases.append((wide, 1888, 1048, 939))
+    for keys, W, H, N in cases:
+        ref = oracle.distribute_octree(keys, 16, 16 + W, 16, 16 + H, N)
+        packed = (keys["x"].astype(np.uint32) | (keys["y"].astype(np.uint32) << 12) |
+                  (keys["response"].astype(np.uint32) << 24)).astype(np.uint32)
+        out = np.zeros(len(keys) + 4 * N + 64, np.uint32)
+        m = harness.harness_octree(_p(packed), len(keys), W, H, N, _p(out), len(out))
+        assert m == len(ref)
+        x2, y2, r2 = _unpack(out[:m])
+        np.testing.assert_array_equal(x2, ref["x"])
+        np.testing.assert_array_equal(y2, ref["y"])
+        np.testing.assert_array_equal(r2, ref["response"])
