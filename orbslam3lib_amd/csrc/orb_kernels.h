@@ -62,6 +62,7 @@ struct BatchArgs {
     int32_t* out_mono;               // [img]
     const int32_t* laps;             // [img][2]
     int total_cells, total_tiles, total_od_blocks;
+    unsigned long long* octdbg;      // diagnostic: [img][kMaxLevels][8] phase clocks, or null
 };
 
 struct MatchArgs {
@@ -77,10 +78,12 @@ struct MatchArgs {
     int32_t* nq;              // [pair]
 };
 
-// Octree workspace layout for one (image, level) with n_cap keys and node capacity C.
+// Octree workspace layout for one (image, level) with n_cap keys and node capacity C.  The node
+// state lives in LDS when C <= kOctLdsNodes, otherwise in the `nodemem` part of this block.
+constexpr int kOctLdsNodes = 1024;
+
 struct OctLayout {
-    long long keys, knode, kq, nodesA, nodesB, childcnt, childpos, divrank, rank2node, rankoff,
-        expoff, undivpos, vsizeA, vsizeB, sortbuf, best, total;
+    long long keys, knode, kq, nodemem, total;
 };
 
 __host__ __device__ inline long long oct_align(long long x) { return (x + 255) & ~255LL; }
@@ -89,21 +92,10 @@ __host__ __device__ inline OctLayout oct_layout(int n_cap, int C) {
     OctLayout L;
     long long o = 0;
     L.keys = o; o = oct_align(o + 4LL * n_cap);
-    L.knode = o; o = oct_align(o + 4LL * n_cap);
+    L.knode = o; o = oct_align(o + 2LL * n_cap);
     L.kq = o; o = oct_align(o + 1LL * n_cap);
-    L.nodesA = o; o = oct_align(o + 24LL * C);
-    L.nodesB = o; o = oct_align(o + 24LL * C);
-    L.childcnt = o; o = oct_align(o + 16LL * C);
-    L.childpos = o; o = oct_align(o + 16LL * C);
-    L.divrank = o; o = oct_align(o + 4LL * C);
-    L.rank2node = o; o = oct_align(o + 4LL * C);
-    L.rankoff = o; o = oct_align(o + 4LL * C);
-    L.expoff = o; o = oct_align(o + 4LL * C);
-    L.undivpos = o; o = oct_align(o + 4LL * C);
-    L.vsizeA = o; o = oct_align(o + 4LL * C);
-    L.vsizeB = o; o = oct_align(o + 4LL * C);
-    L.sortbuf = o; o = oct_align(o + 12LL * C);
-    L.best = o; o = oct_align(o + 4LL * C);
+    L.nodemem = o;
+    if (C > kOctLdsNodes) o = oct_align(o + (long long)((size_t)C * 78 + 64));
     L.total = o;
     return L;
 }

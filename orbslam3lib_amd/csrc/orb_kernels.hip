@@ -180,8 +180,10 @@ __global__ __launch_bounds__(256) void k_fast_cells(BatchArgs a) {
 
 // ---------------------------------------------------------------------------------------------
 // k_octree: one workgroup per (level, image).  Gathers the level's cell lists in cell order
-// (vToDistributeKeys, :807-871) then runs DistributeOctTree (orb_octree.h).
+// (vToDistributeKeys, :807-871) then runs DistributeOctTree (orb_octree.h) with the node
+// state in LDS (80 KB: two workgroups per CU).
 __global__ __launch_bounds__(512) void k_octree(BatchArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t nodemem_lds[kOctLdsNodes * 78 + 64];
     __shared__ int scratch[16];
     __shared__ OctShared sh;
     const int l = blockIdx.x, img = blockIdx.y;
@@ -192,8 +194,11 @@ __global__ __launch_bounds__(512) void k_octree(BatchArgs a) {
     uint8_t* ws = a.octws + (long long)img * a.octws_img_stride + G.oct_off;
     const OctLayout L = oct_layout(G.cand_cap, G.oct_cap);
     uint32_t* keys = reinterpret_cast<uint32_t*>(ws + L.keys);
-    int32_t* cell_off = reinterpret_cast<int32_t*>(ws + L.childpos);  // scratch before use
-    // exclusive scan of the cell counts
+    void* nm = G.oct_cap <= kOctLdsNodes ? (void*)nodemem_lds : (void*)(ws + L.nodemem);
+    // exclusive scan of the cell counts into LDS (the node area is free until the octree runs)
+    int32_t* cell_off = reinterpret_cast<int32_t*>(nodemem_lds);
+    const bool off_in_lds = G.ncells <= (int)(sizeof(nodemem_lds) / 4);
+    if (!off_in_lds) cell_off = reinterpret_cast<int32_t*>(ws + L.knode);  // huge levels only
     int carry = 0;
     for (int base = 0; base < G.ncells; base += blockDim.x) {
         const int i = base + threadIdx.x;
@@ -205,35 +210,27 @@ __global__ __launch_bounds__(512) void k_octree(BatchArgs a) {
     }
     const int n = carry;
     __syncthreads();
-    {
-        const int lane = threadIdx.x & 63, nw = blockDim.x >> 6;
-        for (int c = threadIdx.x >> 6; c < G.ncells; c += nw) {
-            const int m = cnt[c], o = cell_off[c];
-            for (int k = lane; k < m; k += 64) keys[o + k] = ck[(long long)c * G.cell_cap + k];
+    // gather: key k belongs to the last cell whose offset is <= k
+    for (int k = threadIdx.x; k < n; k += blockDim.x) {
+        int lo = 0, hi = G.ncells - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (cell_off[mid] <= k) lo = mid;
+            else hi = mid - 1;
         }
+        keys[k] = ck[(long long)lo * G.cell_cap + (k - cell_off[lo])];
     }
     __syncthreads();
     OctWS w;
     w.keys = keys;
     w.n = n;
-    w.cap = G.oct_cap;
-    w.knode = reinterpret_cast<int32_t*>(ws + L.knode);
+    w.knode = reinterpret_cast<uint16_t*>(ws + L.knode);
     w.kq = ws + L.kq;
-    w.nodesA = reinterpret_cast<OctNode*>(ws + L.nodesA);
-    w.nodesB = reinterpret_cast<OctNode*>(ws + L.nodesB);
-    w.childcnt = reinterpret_cast<int32_t*>(ws + L.childcnt);
-    w.childpos = reinterpret_cast<int32_t*>(ws + L.childpos);
-    w.divrank = reinterpret_cast<int32_t*>(ws + L.divrank);
-    w.rank2node = reinterpret_cast<int32_t*>(ws + L.rank2node);
-    w.rankoff = reinterpret_cast<int32_t*>(ws + L.rankoff);
-    w.expoff = reinterpret_cast<int32_t*>(ws + L.expoff);
-    w.undivpos = reinterpret_cast<int32_t*>(ws + L.undivpos);
-    w.vsizeA = reinterpret_cast<int32_t*>(ws + L.vsizeA);
-    w.vsizeB = reinterpret_cast<int32_t*>(ws + L.vsizeB);
-    w.sortbuf = reinterpret_cast<SortElem*>(ws + L.sortbuf);
-    w.best = reinterpret_cast<uint32_t*>(ws + L.best);
+    w.m = oct_nodemem_carve(nm, G.oct_cap);
+    w.cap = G.oct_cap;
     w.out_keys = a.lvlkey + (long long)img * a.lvlkp_img_stride + G.kp_off;
     w.out_cap = G.kp_cap;
+    w.dbg = a.octdbg ? a.octdbg + ((long long)img * kMaxLevels + l) * 8 : nullptr;
     int r = (n > G.cand_cap) ? -3 : 0;
     if (r == 0) r = octree_distribute(p, w, &sh, G.W, G.H, G.N);
     if (threadIdx.x == 0) {

@@ -16,6 +16,8 @@ struct DevPolicy {
     __device__ void sync() { __syncthreads(); }
     __device__ int atomic_add(int32_t* p, int v) { return atomicAdd(p, v); }
     __device__ uint32_t atomic_max(uint32_t* p, uint32_t v) { return atomicMax(p, v); }
+    __device__ int atomic_max_int(int* p, int v) { return atomicMax(p, v); }
+    __device__ unsigned long long now() const { return wall_clock64(); }  // 100 MHz
     // Block-wide exclusive scan: every thread passes v, gets its exclusive prefix and the total.
     __device__ int scan_excl(int v, int* total) {
         const int lane = (int)(threadIdx.x & 63), wid = (int)(threadIdx.x >> 6);
@@ -54,10 +56,16 @@ struct SerialPolicy {
         if (v > o) *p = v;
         return o;
     }
+    __host__ __device__ int atomic_max_int(int* p, int v) {
+        const int o = *p;
+        if (v > o) *p = v;
+        return o;
+    }
     __host__ __device__ int scan_excl(int v, int* total) {
         *total = v;
         return 0;
     }
+    __host__ __device__ unsigned long long now() const { return 0; }
 };
 
 }  // namespace orbgpu

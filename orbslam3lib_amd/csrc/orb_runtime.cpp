@@ -11,6 +11,7 @@
 #include <climits>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -94,7 +95,8 @@ struct orbgpu_ctx {
     int cellcnt_img = 0, lvlkp_img = 0, out_cap = 0;
     // device buffers
     DevBuf input, pyr, blur, rtab, cellkeys, cellcnt, octws, lvlkey, lvlangle, lvldesc, lvlcnt,
-        status, outkps, outdesc, outn, outmono, laps, midx1, mdist1, midx2, mdist2, mnq, scratch;
+        status, outkps, outdesc, outn, outmono, laps, midx1, mdist1, midx2, mdist2, mnq, scratch,
+        octdbg;
     int input_images = 0;   // images currently sized for in `input`
     int last_images = 0, last_w = 0, last_h = 0, last_pairs = 0;
     // profiling
@@ -257,10 +259,11 @@ int set_geometry(orbgpu_ctx* c, int w, int h) {
         G.W = G.maxBX - kMinBorder;
         G.H = G.maxBY - kMinBorder;
         const int nIni = std::max(1, (int)std::round((float)G.W / (float)G.H));
-        G.kp_cap = std::min(G.cand_cap, 4 * std::max(G.N, nIni)) + 8;
+        // live octree nodes never exceed max(N + 3, 4 * nIni) (orb_octree.h)
+        G.oct_cap = std::max(G.N + 3, 4 * nIni) + 8;
+        G.kp_cap = G.oct_cap;
         G.kp_off = kpo;
         kpo += round_up(G.kp_cap, 16);
-        G.oct_cap = G.cand_cap + nIni + 64;
         G.oct_off = ows;
         ows += oct_layout(G.cand_cap, G.oct_cap).total;
         G.scale = c->scale[l];
@@ -438,7 +441,7 @@ int orbgpu_destroy(orbgpu_ctx* c) {
     DevBuf* bufs[] = {&c->input,   &c->pyr,     &c->blur,   &c->rtab,    &c->cellkeys, &c->cellcnt,
                       &c->octws,   &c->lvlkey,  &c->lvlangle, &c->lvldesc, &c->lvlcnt, &c->status,
                       &c->outkps,  &c->outdesc, &c->outn,   &c->outmono, &c->laps,     &c->midx1,
-                      &c->mdist1,  &c->midx2,   &c->mdist2, &c->mnq,     &c->scratch};
+                      &c->mdist1,  &c->midx2,   &c->mdist2, &c->mnq,     &c->scratch, &c->octdbg};
     for (DevBuf* b : bufs) b->release();
     if (c->stream) hipStreamDestroy(c->stream);
     delete c;
@@ -488,6 +491,14 @@ int orbgpu_run_batch(orbgpu_ctx* c, int n, int w, int h, const int32_t* laps, vo
     }
     BatchArgs A = c->A;
     A.nimages = n;
+    A.octdbg = nullptr;
+    if (getenv("ORBGPU_OCT_STAMPS")) {  // diagnostic build of the octree phase clocks
+        const size_t bytes = (size_t)n * kMaxLevels * 8 * 8;
+        if (!c->octdbg.ensure(bytes)) {
+            hipMemsetAsync(c->octdbg.p, 0, bytes, s);
+            A.octdbg = c->octdbg.as<unsigned long long>();
+        }
+    }
     A.lvl_base[0] = c->input.as<uint8_t>();
     A.lv[0].img_stride = (long long)w * h;
     for (int l = 1; l < A.nlevels; ++l) {
@@ -510,6 +521,19 @@ int orbgpu_synchronize(orbgpu_ctx* c) {
     HIP_TRY(hipSetDevice(c->device));
     HIP_TRY(hipDeviceSynchronize());
     resolve_pending(c);
+    if (getenv("ORBGPU_OCT_STAMPS") && c->octdbg.p && c->last_images > 0) {
+        const int n = c->last_images, L = c->prm.nlevels;
+        std::vector<unsigned long long> d((size_t)n * kMaxLevels * 8);
+        HIP_TRY(hipMemcpy(d.data(), c->octdbg.p, d.size() * 8, hipMemcpyDeviceToHost));
+        for (int l = 0; l < L; ++l) {
+            double acc[8] = {};
+            for (int i = 0; i < n; ++i)
+                for (int k = 0; k < 8; ++k) acc[k] += (double)d[((size_t)i * kMaxLevels + l) * 8 + k];
+            fprintf(stderr, "octree L%d us: init %.1f choose %.1f count %.1f sort %.1f rebuild %.1f relabel %.1f best %.1f rounds %.1f\n",
+                    l, acc[0] / n / 100, acc[1] / n / 100, acc[2] / n / 100, acc[3] / n / 100,
+                    acc[4] / n / 100, acc[5] / n / 100, acc[6] / n / 100, acc[7] / n);
+        }
+    }
     return ORBGPU_OK;
 }
 

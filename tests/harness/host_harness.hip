@@ -16,34 +16,20 @@ extern "C" {
 
 int harness_octree(const uint32_t* keys, int n, int W, int H, int N, uint32_t* out, int out_cap) {
     const int nIni = std::max(1, (int)std::round((float)W / (float)H));
-    const int cap = n + nIni + 64;
-    std::vector<int32_t> knode(n + 1), childcnt(4 * cap), childpos(4 * cap), divrank(cap),
-        rank2node(cap), rankoff(cap), expoff(cap), undivpos(cap), vA(cap), vB(cap);
+    const int cap = std::max(N + 3, 4 * nIni) + 8;
+    std::vector<uint16_t> knode(n + 1);
     std::vector<uint8_t> kq(n + 1);
-    std::vector<OctNode> nA(cap), nB(cap);
-    std::vector<SortElem> sb(cap);
-    std::vector<uint32_t> best(cap);
+    std::vector<uint8_t> mem(oct_nodemem_bytes(cap) + 64);
     OctWS w;
     w.keys = keys;
     w.n = n;
-    w.cap = cap;
     w.knode = knode.data();
     w.kq = kq.data();
-    w.nodesA = nA.data();
-    w.nodesB = nB.data();
-    w.childcnt = childcnt.data();
-    w.childpos = childpos.data();
-    w.divrank = divrank.data();
-    w.rank2node = rank2node.data();
-    w.rankoff = rankoff.data();
-    w.expoff = expoff.data();
-    w.undivpos = undivpos.data();
-    w.vsizeA = vA.data();
-    w.vsizeB = vB.data();
-    w.sortbuf = sb.data();
-    w.best = best.data();
+    w.m = oct_nodemem_carve(mem.data(), cap);
+    w.cap = cap;
     w.out_keys = out;
     w.out_cap = out_cap;
+    w.dbg = nullptr;
     OctShared sh;
     SerialPolicy p;
     return octree_distribute(p, w, &sh, W, H, N);
