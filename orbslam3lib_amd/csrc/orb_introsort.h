@@ -172,4 +172,176 @@ __host__ __device__ inline void introsort_like_libstdcxx(SortElem* a, int n) {
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Data-parallel form of the same permutation (policy-templated, one workgroup).
+//
+// 1. __introsort_loop only partitions: segments > 16 elements are split with median-of-three +
+//    __unguarded_partition until depth runs out (then that segment is heap-sorted).  Segments of
+//    one recursion level are disjoint and are partitioned together.  The two-pointer Hoare scan
+//    is reproduced exactly from the original values: with L'_k the k-th "left stopper"
+//    (!(a[i] < pivot), i > f, ascending) and R'_k the k-th "right stopper" (!(pivot < a[i]),
+//    descending), the scan swaps (L'_k, R'_k) for every k with L'_k < R'_k (a prefix, K pairs)
+//    and returns cut = min(L'_K, R'_{K-1}) -- the positions it revisits after a swap never
+//    change a stop decision before the pointers cross.
+// 2. __final_insertion_sort over the whole partitioned array is a stable insertion sort (its
+//    leftmost segment holds the minimum, so the unguarded inserts are exact): it equals a stable
+//    sort of the partitioned array, done here as a parallel rank sort.
+struct SortScratch {
+    SortElem* tmp;       // [m]
+    uint16_t* lex;       // [m+1]
+    uint16_t* rex;       // [m+1]
+    uint16_t* segof;     // [m]
+    uint16_t* lpos;      // [m]
+    uint16_t* rpos;      // [m]
+    uint16_t* rank;      // [m]
+    uint16_t* segF[2];   // [S]
+    uint16_t* segL[2];   // [S]
+    uint16_t* segD[2];   // [S]
+    int32_t* segK;       // [S]
+};
+
+template <class P>
+__host__ __device__ void introsort_parallel(P& p, SortElem* a, int m, const SortScratch& s,
+                                            int* sh_nseg) {
+    const int tid = p.tid(), NT = p.nthreads();
+    if (m <= 1) return;
+    int cur = 0;
+    if (tid == 0) {
+        s.segF[0][0] = 0;
+        s.segL[0][0] = (uint16_t)m;
+        s.segD[0][0] = (uint16_t)(2 * isort_lg(m));
+        *sh_nseg = m > 16 ? 1 : 0;
+    }
+    p.sync();
+    while (true) {
+        const int nseg = *sh_nseg;
+        if (nseg == 0) break;
+        const uint16_t* F = s.segF[cur];
+        const uint16_t* L = s.segL[cur];
+        const uint16_t* D = s.segD[cur];
+        for (int g = tid; g < nseg; g += NT) {
+            const int f = F[g], l = L[g];
+            if (D[g] == 0) {
+                isort_heapsort(a + f, l - f);
+                s.segK[g] = -1;
+            } else {
+                isort_median_to_first(a, f, f + 1, f + (l - f) / 2, l - 1);
+                s.segK[g] = 0;
+            }
+        }
+        for (int i = tid; i < m; i += NT) s.segof[i] = 0xFFFF;
+        p.sync();
+        for (int g = 0; g < nseg; ++g) {
+            if (s.segK[g] < 0) continue;
+            const int f = F[g], l = L[g];
+            for (int i = f + tid; i < l; i += NT) s.segof[i] = (uint16_t)g;
+        }
+        p.sync();
+        int lc = 0, rc = 0;
+        for (int base = 0; base <= m; base += NT) {
+            const int i = base + tid;
+            int lf = 0, rf = 0;
+            if (i < m && s.segof[i] != 0xFFFF) {
+                const int f = F[s.segof[i]];
+                const SortElem pv = a[f];
+                lf = (i > f) && !node_less(a[i], pv);
+                rf = !node_less(pv, a[i]);
+            }
+            int tl, tr;
+            const int el = p.scan_excl(lf, &tl);
+            const int er = p.scan_excl(rf, &tr);
+            if (i <= m) {
+                s.lex[i] = (uint16_t)(lc + el);
+                s.rex[i] = (uint16_t)(rc + er);
+            }
+            lc += tl;
+            rc += tr;
+        }
+        p.sync();
+        for (int i = tid; i < m; i += NT) {
+            const int g = s.segof[i];
+            if (g == 0xFFFF) continue;
+            const int f = F[g], l = L[g];
+            const SortElem pv = a[f];
+            if (i > f && !node_less(a[i], pv)) s.lpos[f + (s.lex[i] - s.lex[f])] = (uint16_t)i;
+            if (!node_less(pv, a[i])) s.rpos[f + (s.rex[l] - s.rex[i] - 1)] = (uint16_t)i;
+        }
+        p.sync();
+        for (int j = tid; j < m; j += NT) {
+            const int g = s.segof[j];
+            if (g == 0xFFFF) continue;
+            const int f = F[g], l = L[g], k = j - f;
+            const int nl = s.lex[l] - s.lex[f], nr = s.rex[l] - s.rex[f];
+            if (k < nl && k < nr && s.lpos[j] < s.rpos[j]) p.atomic_add(&s.segK[g], 1);
+        }
+        p.sync();
+        for (int j = tid; j < m; j += NT) {
+            const int g = s.segof[j];
+            if (g == 0xFFFF || j - F[g] >= s.segK[g]) continue;
+            s.tmp[s.lpos[j]] = a[s.rpos[j]];
+            s.tmp[s.rpos[j]] = a[s.lpos[j]];
+        }
+        p.sync();
+        for (int j = tid; j < m; j += NT) {
+            const int g = s.segof[j];
+            if (g == 0xFFFF || j - F[g] >= s.segK[g]) continue;
+            a[s.lpos[j]] = s.tmp[s.lpos[j]];
+            a[s.rpos[j]] = s.tmp[s.rpos[j]];
+        }
+        p.sync();
+        // children segments, kept in position order (left child first)
+        int carry = 0;
+        for (int base = 0; base < nseg; base += NT) {
+            const int g = base + tid;
+            int c = 0, cut = 0, f = 0, l = 0, d = 0;
+            if (g < nseg && s.segK[g] >= 0) {
+                f = F[g];
+                l = L[g];
+                d = D[g] - 1;
+                const int K = s.segK[g];
+                const int nl = s.lex[l] - s.lex[f];
+                cut = K < nl ? s.lpos[f + K] : 0x7fffffff;
+                if (K > 0) cut = cut < s.rpos[f + K - 1] ? cut : s.rpos[f + K - 1];
+                c = (cut - f > 16) + (l - cut > 16);
+            }
+            int tot;
+            const int ex = p.scan_excl(c, &tot);
+            if (c) {
+                int o = carry + ex;
+                if (cut - f > 16) {
+                    s.segF[cur ^ 1][o] = (uint16_t)f;
+                    s.segL[cur ^ 1][o] = (uint16_t)cut;
+                    s.segD[cur ^ 1][o] = (uint16_t)d;
+                    ++o;
+                }
+                if (l - cut > 16) {
+                    s.segF[cur ^ 1][o] = (uint16_t)cut;
+                    s.segL[cur ^ 1][o] = (uint16_t)l;
+                    s.segD[cur ^ 1][o] = (uint16_t)d;
+                }
+            }
+            carry += tot;
+        }
+        p.sync();
+        if (tid == 0) *sh_nseg = carry;
+        cur ^= 1;
+        p.sync();
+    }
+    // stable sort of the partitioned array
+    for (int i = tid; i < m; i += NT) {
+        const SortElem x = a[i];
+        int r = 0;
+        for (int j = 0; j < m; ++j) {
+            const SortElem y = a[j];
+            r += node_less(y, x) || (j < i && !node_less(x, y));
+        }
+        s.rank[i] = (uint16_t)r;
+    }
+    p.sync();
+    for (int i = tid; i < m; i += NT) s.tmp[s.rank[i]] = a[i];
+    p.sync();
+    for (int i = tid; i < m; i += NT) a[i] = s.tmp[i];
+    p.sync();
+}
+
 }  // namespace orbgpu

@@ -261,7 +261,6 @@ __host__ __device__ int octree_distribute(P& p, const OctWS& ws, OctShared* sh, 
         } else {  // final phase: libstdc++-ordered sort of vPrev, divide from the back until N
             const int m = sh->nexp;
             SortElem* sb = reinterpret_cast<SortElem*>(nxt);  // nxt is free until the rebuild
-            for (int i = tid; i < size; i += NT) M.divrank[i] = -1;
             for (int j = tid; j < m; j += NT) {
                 const int v = vsz[j];
                 SortElem e;
@@ -271,7 +270,28 @@ __host__ __device__ int octree_distribute(P& p, const OctWS& ws, OctShared* sh, 
                 sb[j] = e;
             }
             p.sync();
-            if (tid == 0) introsort_like_libstdcxx(sb, m);
+            {
+                // scratch: every array below is free until step 3 / the rebuild
+                const int C = ws.cap;
+                SortScratch ss;
+                ss.tmp = reinterpret_cast<SortElem*>(cnxt);
+                ss.lex = M.childpos;
+                ss.rex = M.childpos + (C + 1);
+                ss.segof = M.childpos + 2 * (C + 1);
+                ss.lpos = M.undivpos;
+                ss.rpos = M.blockoff;
+                ss.rank = M.expoff;
+                uint16_t* seg = reinterpret_cast<uint16_t*>(M.divrank);
+                const int S = C / 16 + 4;
+                for (int b = 0; b < 2; ++b) {
+                    ss.segF[b] = seg + (3 * b + 0) * S;
+                    ss.segL[b] = seg + (3 * b + 1) * S;
+                    ss.segD[b] = seg + (3 * b + 2) * S;
+                }
+                ss.segK = reinterpret_cast<int32_t*>(seg + 6 * S + 2);
+                introsort_parallel(p, sb, m, ss, &sh->jstop);
+            }
+            for (int i = tid; i < size; i += NT) M.divrank[i] = -1;
             p.sync();
             mark(3);
             // S_j = size + sum_{j'>=j} (nc_j' - 1) is non-increasing in j; divide [jstop, m)

@@ -42,6 +42,33 @@ void harness_introsort(const int32_t* size, const int32_t* ulx, int n, int32_t* 
     for (int i = 0; i < n; ++i) perm[i] = a[i].node;
 }
 
+void harness_introsort_parallel(const int32_t* size, const int32_t* ulx, int n, int32_t* perm) {
+    std::vector<SortElem> a(n + 1), tmp(n + 1);
+    for (int i = 0; i < n; ++i) a[i] = SortElem{size[i], ulx[i], i};
+    std::vector<uint16_t> lex(n + 2), rex(n + 2), segof(n + 1), lpos(n + 1), rpos(n + 1), rank(n + 1);
+    const int S = n / 16 + 4;
+    std::vector<uint16_t> seg(6 * S);
+    std::vector<int32_t> segK(S);
+    SortScratch ss;
+    ss.tmp = tmp.data();
+    ss.lex = lex.data();
+    ss.rex = rex.data();
+    ss.segof = segof.data();
+    ss.lpos = lpos.data();
+    ss.rpos = rpos.data();
+    ss.rank = rank.data();
+    for (int b = 0; b < 2; ++b) {
+        ss.segF[b] = seg.data() + (3 * b + 0) * S;
+        ss.segL[b] = seg.data() + (3 * b + 1) * S;
+        ss.segD[b] = seg.data() + (3 * b + 2) * S;
+    }
+    ss.segK = segK.data();
+    int nseg = 0;
+    SerialPolicy p;
+    introsort_parallel(p, a.data(), n, ss, &nseg);
+    for (int i = 0; i < n; ++i) perm[i] = a[i].node;
+}
+
 int harness_fast_strength(const uint8_t* img, int stride, int x, int y, int tlow) {
     return fast_strength(img + (long long)y * stride + x, stride, tlow);
 }

@@ -37,6 +37,23 @@ def test_introsort_equals_libstdcxx(harness, oracle):
         np.testing.assert_array_equal(perm, oracle.sort_nodes(sz, ux))
 
 
+def test_parallel_introsort_equals_libstdcxx(harness, oracle):
+    rng = np.random.default_rng(10)
+    cases = []
+    for _ in range(400):
+        n = int(rng.integers(0, 1000))
+        cases.append((rng.integers(2, int(rng.integers(3, 12)), n), rng.integers(0, int(rng.integers(1, 9)), n) * 16))
+    for arr in (np.full(700, 3), np.arange(700), np.arange(700)[::-1],
+                np.concatenate([np.arange(350), np.arange(350)[::-1]]), np.tile([2, 3], 333)):
+        cases.append((arr, np.zeros(len(arr))))
+    for sz, ux in cases:
+        sz = np.asarray(sz, np.int32)
+        ux = np.asarray(ux, np.int32)
+        perm = np.zeros(len(sz), np.int32)
+        harness.harness_introsort_parallel(_p(sz), _p(ux), len(sz), _p(perm))
+        np.testing.assert_array_equal(perm, oracle.sort_nodes(sz, ux))
+
+
 def test_fast_atan2_bit_exact(harness, oracle):
     rng = np.random.default_rng(1)
     for y, x in rng.integers(-40000, 40000, (3000, 2)):
