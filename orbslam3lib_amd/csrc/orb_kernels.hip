@@ -42,53 +42,99 @@ __constant__ int c_umax[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9
 // ---------------------------------------------------------------------------------------------
 // k_resize: level l from level l-1 (canonical ComputePyramid, ORBextractor_old.cc:1342-1344 ->
 // cv::resize INTER_LINEAR).  Horizontal: D = S[sx]*a0 + S[sx1]*a1 (int); vertical: OpenCV's
-// 128-bit SIMD body for x < simd_end, FixedPtCast tail after.  Each thread writes 4 pixels.
+// 128-bit SIMD body for x < simd_end, FixedPtCast tail after.  A block makes a 256 x 16 output
+// tile: its x-table slice and the source window (dword loads) are staged in LDS first.
+constexpr int kRsTW = 256, kRsTH = 16, kRsSrcRows = 2 * kRsTH + 2, kRsSrcCols = 2 * kRsTW + 16;
+
 __global__ __launch_bounds__(256) void k_resize(BatchArgs a, int l) {
+    __shared__ int4 xt_s[kRsTW];
+    __shared__ uint32_t win[kRsSrcRows][kRsSrcCols / 4];
     const LevelGeom& G = a.lv[l];
     const LevelGeom& S = a.lv[l - 1];
     const int img = blockIdx.z;
-    const int dy = blockIdx.y * 4 + (threadIdx.x >> 6);
-    const int dx0 = (blockIdx.x * 64 + (threadIdx.x & 63)) * 4;
-    if (dy >= G.h || dx0 >= G.w) return;
+    const int tx0 = blockIdx.x * kRsTW, ty0 = blockIdx.y * kRsTH;
     const uint8_t* src = a.lvl_base[l - 1] + (long long)img * S.img_stride;
     uint8_t* dst = a.lvl_base[l] + (long long)img * G.img_stride;
     if (G.area2) {  // resize.cpp: INTER_LINEAR at exactly 2x is serviced by INTER_AREA fast
-        const uint8_t* s0 = src + (long long)(2 * dy) * S.pitch;
-        const uint8_t* s1 = s0 + S.pitch;
-        uint32_t pk = 0;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int dx = min(dx0 + k, G.w - 1);
-            const int o = (s0[2 * dx] + s0[2 * dx + 1] + s1[2 * dx] + s1[2 * dx + 1] + 2) >> 2;
-            pk |= (uint32_t)o << (8 * k);
+        for (int i = threadIdx.x; i < kRsTW / 4 * kRsTH; i += 256) {
+            const int dy = ty0 + i / (kRsTW / 4), dx0 = tx0 + 4 * (i % (kRsTW / 4));
+            if (dy >= G.h || dx0 >= G.w) continue;
+            const uint8_t* s0 = src + (long long)(2 * dy) * S.pitch;
+            const uint8_t* s1 = s0 + S.pitch;
+            uint32_t pk = 0;
+            for (int k = 0; k < 4; ++k) {
+                const int dx = min(dx0 + k, G.w - 1);
+                const int o = (s0[2 * dx] + s0[2 * dx + 1] + s1[2 * dx] + s1[2 * dx + 1] + 2) >> 2;
+                pk |= (uint32_t)o << (8 * k);
+            }
+            *reinterpret_cast<uint32_t*>(dst + (long long)dy * G.pitch + dx0) = pk;
         }
-        *reinterpret_cast<uint32_t*>(dst + (long long)dy * G.pitch + dx0) = pk;
         return;
     }
-    const int4 yt = a.rtab[G.ytab_off + dy];
-    const uint8_t* r0 = src + (long long)yt.x * S.pitch;
-    const uint8_t* r1 = src + (long long)yt.y * S.pitch;
-    const int b0 = yt.z, b1 = yt.w;
-    uint32_t packed = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const int dx = dx0 + k;
-        int o = 0;
-        if (dx < G.w) {
-            const int4 xt = a.rtab[G.xtab_off + dx];
-            const int D0 = r0[xt.x] * xt.z + r0[xt.y] * xt.w;
-            const int D1 = r1[xt.x] * xt.z + r1[xt.y] * xt.w;
-            if (dx < G.simd_end) {
-                const int s = (((D0 >> 4) * b0) >> 16) + (((D1 >> 4) * b1) >> 16);
-                o = (s + 2) >> 2;
+    const int tw = min(kRsTW, G.w - tx0), th = min(kRsTH, G.h - ty0);
+    for (int i = threadIdx.x; i < tw; i += 256) xt_s[i] = a.rtab[G.xtab_off + tx0 + i];
+    const int4 yfirst = a.rtab[G.ytab_off + ty0], ylast = a.rtab[G.ytab_off + ty0 + th - 1];
+    const int sy_lo = yfirst.x, sy_hi = ylast.y;
+    const int sx_lo = a.rtab[G.xtab_off + tx0].x & ~3;
+    const int sx_hi = a.rtab[G.xtab_off + tx0 + tw - 1].y;
+    const int nrows = sy_hi - sy_lo + 1, ndw = (sx_hi - sx_lo) / 4 + 1;
+    const bool staged = nrows <= kRsSrcRows && ndw <= kRsSrcCols / 4 && (S.pitch & 3) == 0;
+    if (staged) {
+        for (int i = threadIdx.x; i < nrows * ndw; i += 256) {
+            const int r = i / ndw, c = i % ndw;
+            const uint8_t* row = src + (long long)(sy_lo + r) * S.pitch;
+            const int x = sx_lo + 4 * c;
+            uint32_t v;
+            if (x + 4 <= S.w) {
+                v = *reinterpret_cast<const uint32_t*>(row + x);
             } else {
-                o = (D0 * b0 + D1 * b1 + (1 << 21)) >> 22;
+                v = 0;
+                for (int b = 0; b < 4; ++b)
+                    if (x + b < S.w) v |= (uint32_t)row[x + b] << (8 * b);
             }
-            o = o < 0 ? 0 : (o > 255 ? 255 : o);
+            win[r][c] = v;
         }
-        packed |= (uint32_t)o << (8 * k);
     }
-    *reinterpret_cast<uint32_t*>(dst + (long long)dy * G.pitch + dx0) = packed;
+    __syncthreads();
+    const uint8_t* wb = reinterpret_cast<const uint8_t*>(&win[0][0]);
+    const int q = threadIdx.x & 63;
+    for (int rr = threadIdx.x >> 6; rr < th; rr += 4) {
+        const int dy = ty0 + rr;
+        const int dx0 = tx0 + 4 * q;
+        if (4 * q >= tw) continue;
+        const int4 yt = a.rtab[G.ytab_off + dy];
+        const int b0 = yt.z, b1 = yt.w;
+        uint32_t packed = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int dx = dx0 + k;
+            int o = 0;
+            if (4 * q + k < tw) {
+                const int4 xt = xt_s[4 * q + k];
+                int p00, p01, p10, p11;
+                if (staged) {
+                    const uint8_t* r0 = wb + (yt.x - sy_lo) * kRsSrcCols - sx_lo;
+                    const uint8_t* r1 = wb + (yt.y - sy_lo) * kRsSrcCols - sx_lo;
+                    p00 = r0[xt.x]; p01 = r0[xt.y]; p10 = r1[xt.x]; p11 = r1[xt.y];
+                } else {
+                    const uint8_t* r0 = src + (long long)yt.x * S.pitch;
+                    const uint8_t* r1 = src + (long long)yt.y * S.pitch;
+                    p00 = r0[xt.x]; p01 = r0[xt.y]; p10 = r1[xt.x]; p11 = r1[xt.y];
+                }
+                const int D0 = p00 * xt.z + p01 * xt.w;
+                const int D1 = p10 * xt.z + p11 * xt.w;
+                if (dx < G.simd_end) {
+                    const int s = (((D0 >> 4) * b0) >> 16) + (((D1 >> 4) * b1) >> 16);
+                    o = (s + 2) >> 2;
+                } else {
+                    o = (D0 * b0 + D1 * b1 + (1 << 21)) >> 22;
+                }
+                o = o < 0 ? 0 : (o > 255 ? 255 : o);
+            }
+            packed |= (uint32_t)o << (8 * k);
+        }
+        *reinterpret_cast<uint32_t*>(dst + (long long)dy * G.pitch + dx0) = packed;
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -100,47 +146,91 @@ __device__ inline int refl101(int p, int n) {
     return p >= n ? 2 * n - p - 2 : p;
 }
 
+// Tile 128 x 32 outputs.  The (32+6) x (128+8) input window is staged in LDS with dword loads
+// (byte loads + reflection only where a dword leaves the plane); the horizontal pass writes
+// 4 adjacent u16 sums per thread-step, the vertical pass 4 columns x 4 rows per thread.
+constexpr int kBlurTW = 128, kBlurTH = 32;
+
 __global__ __launch_bounds__(256) void k_blur(BatchArgs a) {
-    constexpr int TW = 128, TH = 16, IW = TW + 6, IH = TH + 6;
-    __shared__ uint8_t tin[IH][IW + 2];
-    __shared__ uint16_t th[IH][TW + 1];
+    constexpr int IW = kBlurTW + 8, IH = kBlurTH + 6, IWD = IW / 4;  // input window, dwords/row
+    __shared__ uint32_t tin[IH][IWD];
+    __shared__ uint32_t thp[IH][kBlurTW / 2 + 1];  // packed u16 pairs, +1 pad
     const int img = blockIdx.y;
     int l = 0;
     while (l + 1 < a.nlevels && (int)blockIdx.x >= a.lv[l + 1].tile_first) ++l;
     const LevelGeom& G = a.lv[l];
     const int t = blockIdx.x - G.tile_first;
-    const int ty0 = (t / G.tiles_x) * TH, tx0 = (t % G.tiles_x) * TW;
+    const int ty0 = (t / G.tiles_x) * kBlurTH, tx0 = (t % G.tiles_x) * kBlurTW;
     const uint8_t* src = a.lvl_base[l] + (long long)img * G.img_stride;
     uint8_t* dst = a.blur_base[l] + (long long)img * G.bimg_stride;
-    for (int i = threadIdx.x; i < IH * IW; i += 256) {
-        const int r = i / IW, c = i % IW;
-        const int y = refl101(ty0 + r - 3, G.h), x = refl101(tx0 + c - 3, G.w);
-        tin[r][c] = src[(long long)y * G.pitch + x];
-    }
-    __syncthreads();
-    const int k0 = 18, k1 = 34, k2 = 48, k3 = 56;
-    for (int i = threadIdx.x; i < IH * TW; i += 256) {
-        const int r = i / TW, c = i % TW;
-        const uint8_t* p = &tin[r][c];
-        th[r][c] = (uint16_t)(k0 * (p[0] + p[6]) + k1 * (p[1] + p[5]) + k2 * (p[2] + p[4]) +
-                              k3 * p[3]);
-    }
-    __syncthreads();
-    const int r = threadIdx.x >> 4, c0 = (threadIdx.x & 15) * 8;
-    const int y = ty0 + r;
-    if (y >= G.h || tx0 + c0 >= G.w) return;
-    uint32_t lo = 0, hi = 0;
+    const bool dw_ok = (G.pitch & 3) == 0;
+    for (int i = threadIdx.x; i < IH * IWD; i += 256) {
+        const int r = i / IWD, cd = i % IWD;
+        const int y = refl101(ty0 + r - 3, G.h);
+        const int x = tx0 - 4 + 4 * cd;
+        const uint8_t* row = src + (long long)y * G.pitch;
+        uint32_t v;
+        if (dw_ok && x >= 0 && x + 4 <= G.w) {
+            v = *reinterpret_cast<const uint32_t*>(row + x);
+        } else {
+            v = 0;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        const int c = c0 + k;
-        const uint32_t s = k0 * ((uint32_t)th[r][c] + th[r + 6][c]) +
-                           k1 * ((uint32_t)th[r + 1][c] + th[r + 5][c]) +
-                           k2 * ((uint32_t)th[r + 2][c] + th[r + 4][c]) + k3 * (uint32_t)th[r + 3][c];
-        const uint32_t o = (s + (1u << 15)) >> 16;
-        if (k < 4) lo |= o << (8 * k);
-        else hi |= o << (8 * (k - 4));
+            for (int b = 0; b < 4; ++b) {
+                const int xx = x + b;
+                const uint32_t px = (xx < G.w + 3) ? row[refl101(xx, G.w)] : 0u;
+                v |= px << (8 * b);
+            }
+        }
+        tin[r][cd] = v;
     }
-    *reinterpret_cast<uint2*>(dst + (long long)y * G.bpitch + tx0 + c0) = make_uint2(lo, hi);
+    __syncthreads();
+    // horizontal: output cols c..c+3 (c = 4*cq) need window bytes c+1 .. c+10
+    const uint32_t k0 = 18, k1 = 34, k2 = 48, k3 = 56;
+    for (int i = threadIdx.x; i < IH * (kBlurTW / 4); i += 256) {
+        const int r = i / (kBlurTW / 4), cq = i % (kBlurTW / 4);
+        const uint32_t w0 = tin[r][cq], w1 = tin[r][cq + 1], w2 = tin[r][cq + 2];
+        uint32_t p[12];
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            p[b] = (w0 >> (8 * b)) & 255u;
+            p[4 + b] = (w1 >> (8 * b)) & 255u;
+            p[8 + b] = (w2 >> (8 * b)) & 255u;
+        }
+        uint32_t hs[4];
+#pragma unroll
+        for (int o = 0; o < 4; ++o) {
+            const uint32_t* q = p + 1 + o;  // window offset of column c+o-3 is c+o+1
+            hs[o] = k0 * (q[0] + q[6]) + k1 * (q[1] + q[5]) + k2 * (q[2] + q[4]) + k3 * q[3];
+        }
+        thp[r][2 * cq] = hs[0] | (hs[1] << 16);
+        thp[r][2 * cq + 1] = hs[2] | (hs[3] << 16);
+    }
+    __syncthreads();
+    // vertical: thread -> column quad cq, rows rg*4 .. rg*4+3
+    const int cq = threadIdx.x & 31, rg = threadIdx.x >> 5;
+    uint32_t col[10][4];
+#pragma unroll
+    for (int rr = 0; rr < 10; ++rr) {
+        const uint32_t lo = thp[rg * 4 + rr][2 * cq], hi = thp[rg * 4 + rr][2 * cq + 1];
+        col[rr][0] = lo & 0xFFFFu;
+        col[rr][1] = lo >> 16;
+        col[rr][2] = hi & 0xFFFFu;
+        col[rr][3] = hi >> 16;
+    }
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+        const int y = ty0 + rg * 4 + o;
+        const int x = tx0 + 4 * cq;
+        uint32_t packed = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const uint32_t s = k0 * (col[o][b] + col[o + 6][b]) + k1 * (col[o + 1][b] + col[o + 5][b]) +
+                               k2 * (col[o + 2][b] + col[o + 4][b]) + k3 * col[o + 3][b];
+            packed |= ((s + (1u << 15)) >> 16) << (8 * b);
+        }
+        if (y < G.h && x < G.w)
+            *reinterpret_cast<uint32_t*>(dst + (long long)y * G.bpitch + x) = packed;
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -149,8 +239,9 @@ __global__ __launch_bounds__(256) void k_blur(BatchArgs a) {
 // detection on [3,rows-3)x[3,cols-3) of the cell ROI, 3x3 nonmax inside the cell only, iniTh
 // then minTh if the cell yields nothing, keys emitted in row-major order.
 __global__ __launch_bounds__(256) void k_fast_cells(BatchArgs a) {
-    __shared__ uint8_t T[kCellMax * kCellMax];
-    __shared__ uint8_t M[kCellMax * kCellMax];
+    __shared__ __attribute__((aligned(16))) uint8_t T[kCellMax * kCellMax];
+    __shared__ __attribute__((aligned(16))) uint8_t M[kCellMax * kCellMax];
+    __shared__ uint16_t list[kCellList];
     __shared__ int scratch[16];
     __shared__ int s_cnt;
     const int img = blockIdx.y;
@@ -172,9 +263,13 @@ __global__ __launch_bounds__(256) void k_fast_cells(BatchArgs a) {
     }
     g.rows = min(g.iniY + G.hCell + 6, G.maxBY) - g.iniY;
     g.cols = min(g.iniX + G.wCell + 6, G.maxBX) - g.iniX;
-    const uint8_t* src = a.lvl_base[l] + (long long)img * G.img_stride + (long long)g.iniY * G.pitch + g.iniX;
+    const bool dword_ok = ((G.pitch | G.img_stride) & 3) == 0;
+    const int sh = dword_ok ? (g.iniX & 3) : 0;
+    const uint8_t* src = a.lvl_base[l] + (long long)img * G.img_stride + (long long)g.iniY * G.pitch +
+                         (g.iniX - sh);
     DevPolicy p{scratch};
-    const int n = fast_cell_run(p, src, G.pitch, g, a.ini_th, a.min_th, T, M, &s_cnt, key_out);
+    const int n = fast_cell_run(p, src, G.pitch, sh, dword_ok, g, a.ini_th, a.min_th, T, M, list,
+                                &s_cnt, key_out);
     if (threadIdx.x == 0) *cnt_out = n;
 }
 
@@ -243,7 +338,36 @@ __global__ __launch_bounds__(512) void k_octree(BatchArgs a) {
 // k_orient_desc: one wave per keypoint.  IC_Angle on the raw level (ORBextractor_old.cc:78-105)
 // then computeOrbDescriptor on the blurred level (:108-148): a = (float)cos, b = (float)sin of
 // angle*pi/180 (float), sample center[cvRound(x*b + y*a)*step + cvRound(x*a - y*b)].
+// Per wave: the 31x31 raw patch (moments) and 37x37 blurred patch (rotated samples stay within
+// radius 18.4 -> |offset| <= 18) are staged in LDS with dword loads, then read as bytes.
+constexpr int kRawRows = 31, kRawDw = 10, kBlrRows = 37, kBlrDw = 12;
+
+__device__ inline void wave_lds_fence() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+__device__ inline void stage_patch(uint32_t* dst, int rows, int dws, const uint8_t* plane, long long pitch,
+                                   int x0, int y0, bool dword_ok, int lane, int* shift) {
+    // copies rows [y0, y0+rows) x bytes [xa, xa + 4*dws) where xa = x0 & ~3 (dword path)
+    const int xa = dword_ok ? (x0 & ~3) : x0;
+    *shift = x0 - xa;
+    for (int i = lane; i < rows * dws; i += 64) {
+        const int r = i / dws, d = i % dws;
+        const uint8_t* s = plane + (long long)(y0 + r) * pitch + xa + 4 * d;
+        uint32_t v;
+        if (dword_ok) {
+            v = *reinterpret_cast<const uint32_t*>(s);
+        } else {
+            v = (uint32_t)s[0] | ((uint32_t)s[1] << 8) | ((uint32_t)s[2] << 16) | ((uint32_t)s[3] << 24);
+        }
+        dst[r * dws + d] = v;
+    }
+}
+
 __global__ __launch_bounds__(256) void k_orient_desc(BatchArgs a) {
+    __shared__ uint32_t raw_s[4][kRawRows * kRawDw];
+    __shared__ uint32_t blr_s[4][kBlrRows * kBlrDw];
     const int img = blockIdx.y;
     int l = 0;
     while (l + 1 < a.nlevels && (int)blockIdx.x >= a.lv[l + 1].od_first) ++l;
@@ -253,24 +377,27 @@ __global__ __launch_bounds__(256) void k_orient_desc(BatchArgs a) {
     const long long kbase = (long long)img * a.lvlkp_img_stride + G.kp_off;
     const uint8_t* lvl = a.lvl_base[l] + (long long)img * G.img_stride;
     const uint8_t* blr = a.blur_base[l] + (long long)img * G.bimg_stride;
+    const bool raw_dw = ((G.pitch | G.img_stride) & 3) == 0;
     const int stride_k = G.od_blocks * 4;
+    const uint8_t* rawb = reinterpret_cast<const uint8_t*>(raw_s[wave]);
+    const uint8_t* blrb = reinterpret_cast<const uint8_t*>(blr_s[wave]);
     for (int kp = (blockIdx.x - G.od_first) * 4 + wave; kp < count; kp += stride_k) {
         const uint32_t key = a.lvlkey[kbase + kp];
         const int x = key_x(key) + kMinBorder, y = key_y(key) + kMinBorder;
-        // moments over the r=15 disc: lane v in [0,31) covers row v-15
+        int sr, sb;
+        stage_patch(raw_s[wave], kRawRows, kRawDw, lvl, G.pitch, x - 15, y - 15, raw_dw, lane, &sr);
+        stage_patch(blr_s[wave], kBlrRows, kBlrDw, blr, G.bpitch, x - 18, y - 18, true, lane, &sb);
+        wave_lds_fence();
+        // IC_Angle moments over the r=15 disc (ORBextractor_old.cc:78-105), exact integers
         int m10 = 0, m01 = 0;
-        if (lane < 31) {
-            const int v = lane - 15;
-            const int d = c_umax[v < 0 ? -v : v];
-            const uint8_t* row = lvl + (long long)(y + v) * G.pitch + x;
-            int s = 0, su = 0;
-            for (int u = -d; u <= d; ++u) {
-                const int val = row[u];
-                s += val;
-                su += u * val;
+        for (int i = lane; i < kRawRows * 32; i += 64) {
+            const int r = i >> 5, c = i & 31;
+            const int v = r - 15, u = c - 15;
+            if (c < 31 && (u < 0 ? -u : u) <= c_umax[v < 0 ? -v : v]) {
+                const int val = rawb[r * (4 * kRawDw) + sr + c];
+                m10 += u * val;
+                m01 += v * val;
             }
-            m10 = su;
-            m01 = v * s;
         }
 #pragma unroll
         for (int o = 32; o >= 1; o >>= 1) {
@@ -279,27 +406,28 @@ __global__ __launch_bounds__(256) void k_orient_desc(BatchArgs a) {
         }
         const float angle = fast_atan2_deg((float)m01, (float)m10);
         if (lane == 0) a.lvlangle[kbase + kp] = angle;
-        if (lane < 32) {
-            const float factorPI = (float)(3.14159265358979323846 / 180.0);
-            const float ang = angle * factorPI;
-            const float ca = (float)cos((double)ang), sb = (float)sin((double)ang);
-            const uint8_t* center = blr + (long long)y * G.bpitch + x;
-            const int8_t* pat = c_pattern.v + lane * 32;  // byte `lane`: 8 pairs = 32 int8
-            int val = 0;
+        // computeOrbDescriptor (:108-148): lane covers pairs 4*lane .. 4*lane+3 (one nibble)
+        const float factorPI = (float)(3.14159265358979323846 / 180.0);
+        const float ang = angle * factorPI;
+        const float ca = (float)cos((double)ang), sn = (float)sin((double)ang);
+        const int8_t* pat = c_pattern.v + lane * 16;
+        const uint8_t* center = blrb + 18 * (4 * kBlrDw) + sb + 18;
+        int nib = 0;
 #pragma unroll
-            for (int bit = 0; bit < 8; ++bit) {
-                int t[2];
+        for (int b = 0; b < 4; ++b) {
+            int t[2];
 #pragma unroll
-                for (int e = 0; e < 2; ++e) {
-                    const float px = (float)pat[4 * bit + 2 * e], py = (float)pat[4 * bit + 2 * e + 1];
-                    const int ry = cv_round(px * sb + py * ca);
-                    const int rx = cv_round(px * ca - py * sb);
-                    t[e] = center[(long long)ry * G.bpitch + rx];
-                }
-                val |= (t[0] < t[1]) << bit;
+            for (int e = 0; e < 2; ++e) {
+                const float px = (float)pat[4 * b + 2 * e], py = (float)pat[4 * b + 2 * e + 1];
+                const int ry = cv_round(px * sn + py * ca);
+                const int rx = cv_round(px * ca - py * sn);
+                t[e] = center[ry * (4 * kBlrDw) + rx];
             }
-            a.lvldesc[(kbase + kp) * 32 + lane] = (uint8_t)val;
+            nib |= (t[0] < t[1]) << b;
         }
+        const int hi = __shfl_xor(nib, 1, 64);
+        if ((lane & 1) == 0) a.lvldesc[(kbase + kp) * 32 + (lane >> 1)] = (uint8_t)(nib | (hi << 4));
+        wave_lds_fence();  // the next keypoint overwrites this wave's patches
     }
 }
 
@@ -385,6 +513,13 @@ __global__ __launch_bounds__(256) void k_finalize(BatchArgs a) {
 // descriptors staged through LDS 512 at a time and read as broadcasts.
 constexpr int kTrainChunk = 512;
 
+// Top-2 by packed key (distance << 16 | train index): integer order == lexicographic
+// (distance, index) order, so the insertion rule becomes k1' = min(k1, k), k2' = med3(k1, k2, k)
+// with no branches.  Requires nt < 65536 (checked on the host).
+__device__ inline uint32_t med3_u32(uint32_t a, uint32_t b, uint32_t c) {
+    return max(min(a, b), min(max(a, b), c));  // lowers to v_med3_u32
+}
+
 __device__ inline void knn2_core(const uint8_t* q, int nq, const uint8_t* t, int nt, int qi,
                                  int32_t* i1, int32_t* d1, int32_t* i2, int32_t* d2,
                                  uint4 (*tl)[2]) {
@@ -394,7 +529,7 @@ __device__ inline void knn2_core(const uint8_t* q, int nq, const uint8_t* t, int
         qa = qp[0];
         qb = qp[1];
     }
-    int b1 = 0x7fffffff, b2 = 0x7fffffff, j1 = -1, j2 = -1;
+    uint32_t k1 = 0xFFFFFFFFu, k2 = 0xFFFFFFFFu;
     for (int base = 0; base < nt; base += kTrainChunk) {
         const int m = min(kTrainChunk, nt - base);
         __syncthreads();
@@ -404,29 +539,39 @@ __device__ inline void knn2_core(const uint8_t* q, int nq, const uint8_t* t, int
             tl[i][1] = tp[1];
         }
         __syncthreads();
-        for (int j = 0; j < m; ++j) {
-            const uint4 ta = tl[j][0], tb = tl[j][1];
-            int d = __popc(qa.x ^ ta.x) + __popc(qa.y ^ ta.y) + __popc(qa.z ^ ta.z) +
-                    __popc(qa.w ^ ta.w) + __popc(qb.x ^ tb.x) + __popc(qb.y ^ tb.y) +
-                    __popc(qb.z ^ tb.z) + __popc(qb.w ^ tb.w);
-            if (d < b2) {
-                if (d < b1) {
-                    b2 = b1;
-                    j2 = j1;
-                    b1 = d;
-                    j1 = base + j;
-                } else {
-                    b2 = d;
-                    j2 = base + j;
-                }
+        int j = 0;
+        for (; j + 2 <= m; j += 2) {
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const uint4 ta = tl[j + u][0], tb = tl[j + u][1];
+                uint32_t d = __popc(qa.x ^ ta.x);
+                d += __popc(qa.y ^ ta.y);
+                d += __popc(qa.z ^ ta.z);
+                d += __popc(qa.w ^ ta.w);
+                d += __popc(qb.x ^ tb.x);
+                d += __popc(qb.y ^ tb.y);
+                d += __popc(qb.z ^ tb.z);
+                d += __popc(qb.w ^ tb.w);
+                const uint32_t key = (d << 16) | (uint32_t)(base + j + u);
+                k2 = med3_u32(k1, k2, key);
+                k1 = min(k1, key);
             }
+        }
+        for (; j < m; ++j) {
+            const uint4 ta = tl[j][0], tb = tl[j][1];
+            uint32_t d = __popc(qa.x ^ ta.x) + __popc(qa.y ^ ta.y) + __popc(qa.z ^ ta.z) +
+                         __popc(qa.w ^ ta.w) + __popc(qb.x ^ tb.x) + __popc(qb.y ^ tb.y) +
+                         __popc(qb.z ^ tb.z) + __popc(qb.w ^ tb.w);
+            const uint32_t key = (d << 16) | (uint32_t)(base + j);
+            k2 = med3_u32(k1, k2, key);
+            k1 = min(k1, key);
         }
     }
     if (qi < nq) {
-        i1[qi] = j1;
-        d1[qi] = b1;
-        i2[qi] = j2;
-        d2[qi] = b2;
+        i1[qi] = k1 == 0xFFFFFFFFu ? -1 : (int32_t)(k1 & 0xFFFF);
+        d1[qi] = k1 == 0xFFFFFFFFu ? 0x7fffffff : (int32_t)(k1 >> 16);
+        i2[qi] = k2 == 0xFFFFFFFFu ? -1 : (int32_t)(k2 & 0xFFFF);
+        d2[qi] = k2 == 0xFFFFFFFFu ? 0x7fffffff : (int32_t)(k2 >> 16);
     }
 }
 
@@ -460,7 +605,7 @@ __global__ __launch_bounds__(256) void k_knn2_plain(const uint8_t* q, int nq, co
 // ---------------------------------------------------------------------------------------------
 hipError_t launch_resize(const BatchArgs& a, int level, hipStream_t s) {
     const LevelGeom& G = a.lv[level];
-    dim3 grid((G.w + 255) / 256, (G.h + 3) / 4, a.nimages);
+    dim3 grid((G.w + kRsTW - 1) / kRsTW, (G.h + kRsTH - 1) / kRsTH, a.nimages);
     hipLaunchKernelGGL(k_resize, grid, dim3(256), 0, s, a, level);
     return hipGetLastError();
 }

@@ -268,8 +268,8 @@ int set_geometry(orbgpu_ctx* c, int w, int h) {
         ows += oct_layout(G.cand_cap, G.oct_cap).total;
         G.scale = c->scale[l];
         G.patch = (int)(31 * c->scale[l]);
-        G.tiles_x = (G.w + 127) / 128;
-        G.tiles_y = (G.h + 15) / 16;
+        G.tiles_x = (G.w + 127) / 128;   // k_blur tile 128 x 32
+        G.tiles_y = (G.h + 31) / 32;
         G.tile_first = tile_first;
         tile_first += G.tiles_x * G.tiles_y;
         G.od_blocks = std::max(1, (G.N + 16 + 3) / 4);
@@ -672,6 +672,7 @@ int orbgpu_get_level_keypoints(orbgpu_ctx* c, int img, orbgpu_keypoint* kps, uin
 int orbgpu_match_knn2(orbgpu_ctx* c, const uint8_t* q, int nq, const uint8_t* t, int nt,
                       int32_t* i1, int32_t* d1, int32_t* i2, int32_t* d2) {
     if (!c || nq < 0 || nt < 0 || (nq && !q) || (nt && !t)) return fail(ORBGPU_ERR_INVALID, "bad args");
+    if (nt > 65535) return fail(ORBGPU_ERR_INVALID, "train set larger than 65535 rows");
     if (nq == 0) return ORBGPU_OK;
     HIP_TRY(hipSetDevice(c->device));
     const size_t need = 32 * (size_t)(nq + nt) + 16 * (size_t)nq + 1024;

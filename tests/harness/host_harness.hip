@@ -82,7 +82,10 @@ int harness_level_candidates(const uint8_t* lvl, int w, int h, int ini, int mn, 
     const float width = (float)(maxBX - minB), height = (float)(maxBY - minB);
     const int nCols = (int)(width / 35.f), nRows = (int)(height / 35.f);
     const int wCell = (int)std::ceil(width / nCols), hCell = (int)std::ceil(height / nRows);
-    std::vector<uint8_t> T(kCellMax * kCellMax), M(kCellMax * kCellMax);
+    std::vector<uint32_t> T32(kCellMax * kCellMax / 4), M32(kCellMax * kCellMax / 4);
+    uint8_t* T = reinterpret_cast<uint8_t*>(T32.data());
+    uint8_t* M = reinterpret_cast<uint8_t*>(M32.data());
+    std::vector<uint16_t> list(kCellList);
     std::vector<uint32_t> tmp(kCellMax * kCellMax);
     int total = 0, cnt = 0;
     SerialPolicy p;
@@ -95,8 +98,11 @@ int harness_level_candidates(const uint8_t* lvl, int w, int h, int ini, int mn, 
             if (g.iniY >= maxBY - 3 || g.iniX >= maxBX - 6) continue;
             g.rows = std::min(g.iniY + hCell + 6, maxBY) - g.iniY;
             g.cols = std::min(g.iniX + wCell + 6, maxBX) - g.iniX;
-            const int m = fast_cell_run(p, lvl + (long long)g.iniY * w + g.iniX, w, g, ini, mn,
-                                        T.data(), M.data(), &cnt, tmp.data());
+            // alternate the two load paths (dword-aligned window / plain bytes) across cells
+            const bool dw = ((i + j) & 1) == 0 && (w & 3) == 0;
+            const int sh = dw ? (g.iniX & 3) : 0;
+            const int m = fast_cell_run(p, lvl + (long long)g.iniY * w + g.iniX - sh, w, sh, dw, g,
+                                        ini, mn, T, M, list.data(), &cnt, tmp.data());
             for (int k = 0; k < m; ++k) {
                 if (total < cap) out[total] = tmp[k];
                 ++total;
