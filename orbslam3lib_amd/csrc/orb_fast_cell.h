@@ -5,14 +5,12 @@
 // sees only this cell's corners, iniThFAST first and minThFAST if the cell kept nothing, keys
 // emitted in row-major order relative to (minBorderX, minBorderY).
 //
-// Work is narrowed in three ordered passes so that lanes stay busy:
-//   A. compass pre-test at t_low = min(ini, min) (two cyclically adjacent points of {0,4,8,12}
-//      beyond t_low, necessary for any 9-arc),
-//   B. exact 9-contiguous-arc test at t_low on the 16-bit dark/bright masks,
-//   C. exact strength m (orb_math.h) for the survivors only.
-// Every pixel not in the final list has m <= t_low <= t, which the nonmax rule treats exactly
-// like m = 0, so NMS and compaction only visit the list.  Policy-templated like orb_octree.h so
-// the host harness runs the same code on the CPU.
+// Layout: the ROI (<= 76 x 78 bytes) is staged in LDS; "lanes" own columns and "row groups"
+// own rows (no integer division anywhere).  m = exact FAST strength (orb_math.h) is computed for
+// pixels passing the compass pre-test at t_low = min(ini, min), 0 elsewhere (exact for every
+// t >= t_low).  Keys are compacted per row (a 64-bit keep mask per row and its popcount), then
+// one scan over <= 70 row counts gives every row's output offset.  Policy-templated like
+// orb_octree.h so the host harness runs the same code on the CPU.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -22,8 +20,7 @@
 
 namespace orbgpu {
 
-constexpr int kCellMax = 80;    // wCell, hCell < 70 (nCols = floor(W/35)) plus the 6-px overlap
-constexpr int kCellList = 4900; // >= detection pixels of a cell (<= 69 x 69)
+constexpr int kCellMax = 80;  // wCell, hCell < 70 (nCols = floor(W/35)) plus the 6-px overlap
 
 struct CellGeom {
     int iniX, iniY;   // cell ROI origin in level coordinates
@@ -31,7 +28,7 @@ struct CellGeom {
     int minBorder;
 };
 
-// M holds the exact strength for listed pixels, 0 elsewhere (pitch kCellMax).
+// M holds m for pixels passing the pre-test, 0 elsewhere (pitch kCellMax).
 __host__ __device__ inline bool fast_kept(const uint8_t* M, int off, int t) {
     const uint8_t* m = &M[off];
     const int v = m[0];
@@ -59,11 +56,12 @@ __host__ __device__ inline bool arc9(uint32_t mask16) {
     const uint32_t m = mask16 | (mask16 << 16);
     uint32_t a = m & (m >> 1);
     a &= a >> 2;
-    a &= a >> 4;        // 8 consecutive from each bit
-    a &= m >> 8;        // 9 consecutive
+    a &= a >> 4;  // 8 consecutive from each bit
+    a &= m >> 8;  // 9 consecutive
     return (a & 0xFFFFu) != 0;
 }
 
+// cv::FAST segment test at threshold t (strict > / <), exact.
 __host__ __device__ inline bool fast_corner(const uint8_t* c, int t) {
     const int v = c[0];
     uint32_t dm = 0, bm = 0;
@@ -76,101 +74,132 @@ __host__ __device__ inline bool fast_corner(const uint8_t* c, int t) {
     return arc9(dm) || arc9(bm);
 }
 
-// src points at the ROI's first row, at column x_al = iniX & ~3 when dword loads are allowed
-// (`sh` = iniX - x_al), else at iniX (sh = 0).  T and M are kCellMax^2 scratch arrays, `list`
-// holds kCellList u16 (LDS on the GPU); cnt is a shared counter.  Returns the key count.
+// Per-cell scratch (LDS on the GPU).
+struct CellScratch {
+    uint8_t* T;        // [kCellMax * kCellMax], 4-byte aligned
+    uint8_t* M;        // [kCellMax * kCellMax], 4-byte aligned
+    uint16_t* list;    // [kCellList] wave-private candidate lists (LDS offsets into T/M)
+    int32_t* wcnt;     // [waves]
+};
+
+constexpr int kCellList = 4900;  // >= detection pixels of a cell (<= 69 x 69)
+
+// The detection pixels are split into one contiguous row-major range per wave, so the wave
+// lists concatenated in wave order are row-major: ordered output needs only a prefix over waves.
 template <class P>
 __host__ __device__ int fast_cell_run(P& p, const uint8_t* src, long long pitch, int sh,
                                       bool dword_ok, const CellGeom& g, int ini_th, int min_th,
-                                      uint8_t* T, uint8_t* M, uint16_t* list, int* cnt,
-                                      uint32_t* keys_out) {
+                                      const CellScratch& cs, uint32_t* keys_out) {
     const int tid = p.tid(), NT = p.nthreads();
     const int rows = g.rows, cols = g.cols;
+    uint8_t* T = cs.T;
+    uint8_t* M = cs.M;
+    constexpr int RW = kCellMax / 4;  // dwords per LDS row (constant divisors only)
     if (dword_ok) {
         const int ndw = (sh + cols + 3) >> 2;
         uint32_t* T32 = reinterpret_cast<uint32_t*>(T);
         uint32_t* M32 = reinterpret_cast<uint32_t*>(M);
-        for (int i = tid; i < rows * ndw; i += NT) {
-            const int r = i / ndw, d = i % ndw;
-            uint32_t v;
-            const uint8_t* s = src + (long long)r * pitch + 4 * d;
-            v = *reinterpret_cast<const uint32_t*>(s);
-            T32[r * (kCellMax / 4) + d] = v;
-            M32[r * (kCellMax / 4) + d] = 0;
+        for (int i = tid; i < rows * RW; i += NT) {
+            const int r = i / RW, d = i % RW;
+            if (d < ndw) {
+                T32[i] = *reinterpret_cast<const uint32_t*>(src + (long long)r * pitch + 4 * d);
+                M32[i] = 0;
+            }
         }
     } else {
-        for (int i = tid; i < rows * cols; i += NT) {
-            const int r = i / cols, c = i % cols;
-            T[r * kCellMax + c + sh] = src[(long long)r * pitch + c];
-            M[r * kCellMax + c + sh] = 0;
+        for (int i = tid; i < rows * kCellMax; i += NT) {
+            const int r = i / kCellMax, c = i % kCellMax;
+            if (c < cols) {
+                T[r * kCellMax + c + sh] = src[(long long)r * pitch + c];
+                M[r * kCellMax + c + sh] = 0;
+            }
         }
     }
-    if (tid == 0) *cnt = 0;
     p.sync();
     const int dr = rows - 6 > 0 ? rows - 6 : 0;
     const int dc = cols - 6 > 0 ? cols - 6 : 0;
     const int nd = dr * dc;
     const int tini = ini_th < 0 ? 0 : (ini_th > 255 ? 255 : ini_th);
     const int tmin = min_th < 0 ? 0 : (min_th > 255 ? 255 : min_th);
-    const int tlow = tini < tmin ? tini : tmin;
-    auto off_of = [&](int i) { return (3 + i / dc) * kCellMax + 3 + sh + i % dc; };
-    // A: compass pre-test over the whole detection region (ordered compaction)
-    int na = 0;
-    for (int base = 0; base < nd; base += NT) {
-        const int i = base + tid;
-        const bool f = i < nd && fast_compass(&T[off_of(i)], tlow);
-        int tot;
-        const int ex = p.scan_excl(f ? 1 : 0, &tot);
-        if (f) list[na + ex] = (uint16_t)i;
-        na += tot;
-    }
-    p.sync();
-    // B: exact 9-arc test at t_low, compacted in place (writes never pass the reads)
-    int nb = 0;
-    for (int base = 0; base < na; base += NT) {
-        const int j = base + tid;
-        int i = 0;
-        bool f = false;
-        if (j < na) {
-            i = list[j];
-            f = fast_corner(&T[off_of(i)], tlow);
+    const int W = p.nwaves(), w = p.wave(), L = p.wave_width(), lane = p.lane();
+    const uint64_t lt = p.lanemask_lt();
+    const int i0 = (int)((long long)w * nd / W), i1 = (int)((long long)(w + 1) * nd / W);
+    uint16_t* list = cs.list + i0;
+    const float inv_dc = dc > 0 ? 1.f / (float)dc : 0.f;
+    auto off_of = [&](int i) {
+        const int r = (int)(((float)i + 0.5f) * inv_dc);  // exact: i < 4900, dc < 70
+        return (3 + r) * kCellMax + 3 + sh + (i - r * dc);
+    };
+    // candidates -> corners at t -> exact strength; returns this wave's corner count
+    auto build = [&](int t) {
+        int na = 0;
+        for (int base = i0; base < i1; base += L) {
+            const int i = base + lane;
+            const int o = i < i1 ? off_of(i) : 0;
+            const bool f = i < i1 && fast_compass(&T[o], t);
+            const uint64_t m = p.ballot(f);
+            if (f) list[na + p.popc64(m & lt)] = (uint16_t)o;
+            na += p.popc64(m);
         }
-        int tot;
-        const int ex = p.scan_excl(f ? 1 : 0, &tot);
-        if (f) list[nb + ex] = (uint16_t)i;
-        nb += tot;
-    }
-    p.sync();
-    // C: exact strength of the corners
-    for (int j = tid; j < nb; j += NT) {
-        const int o = off_of(list[j]);
-        M[o] = (uint8_t)fast_strength(&T[o], kCellMax, -1);
-    }
-    p.sync();
-    int mine = 0;
-    for (int j = tid; j < nb; j += NT) mine += fast_kept(M, off_of(list[j]), tini);
-    if (mine) p.atomic_add(cnt, mine);
-    p.sync();
-    const int t = *cnt > 0 ? tini : tmin;
-    int carry = 0;
-    for (int base = 0; base < nb; base += NT) {
-        const int j = base + tid;
-        int i = 0;
-        bool k = false;
-        if (j < nb) {
-            i = list[j];
-            k = fast_kept(M, off_of(i), t);
+        int nb = 0;
+        for (int base = 0; base < na; base += L) {
+            const int j = base + lane;
+            const int o = j < na ? list[j] : 0;
+            const bool f = j < na && fast_corner(&T[o], t);
+            const uint64_t m = p.ballot(f);
+            if (f) list[nb + p.popc64(m & lt)] = (uint16_t)o;  // in place: never passes the reads
+            nb += p.popc64(m);
         }
-        int tot;
-        const int ex = p.scan_excl(k ? 1 : 0, &tot);
+        for (int j = lane; j < nb; j += L) {
+            const int o = list[j];
+            M[o] = (uint8_t)fast_strength(&T[o], kCellMax, -1);
+        }
+        return nb;
+    };
+    auto count_kept = [&](int nb, int t) {
+        int c = 0;
+        for (int base = 0; base < nb; base += L) {
+            const int j = base + lane;
+            const bool k = j < nb && fast_kept(M, list[j], t);
+            c += p.popc64(p.ballot(k));
+        }
+        if (lane == 0) cs.wcnt[w] = c;
+        p.sync();
+        int tot = 0, before = 0;
+        for (int v = 0; v < W; ++v) {
+            tot += cs.wcnt[v];
+            before += v < w ? cs.wcnt[v] : 0;
+        }
+        return make_int2(tot, before);
+    };
+    int nb = build(tini);
+    p.sync();  // M complete: nonmax reads neighbours owned by other waves
+    int2 cb = count_kept(nb, tini);
+    int t = tini;
+    if (cb.x == 0) {  // the cell kept nothing at iniThFAST: rerun at minThFAST (:845-861)
+        t = tmin;
+        p.sync();
+        if (tmin < tini) {
+            nb = build(tmin);
+            p.sync();
+        }
+        cb = count_kept(nb, t);
+    }
+    int run = 0;
+    for (int base = 0; base < nb; base += L) {
+        const int j = base + lane;
+        const int o = j < nb ? list[j] : 0;
+        const bool k = j < nb && fast_kept(M, o, t);
+        const uint64_t m = p.ballot(k);
         if (k) {
-            const int r = 3 + i / dc, c = 3 + i % dc;
-            const int resp = M[off_of(i)] - 1;  // cornerScore<16> = m - 1
-            keys_out[carry + ex] = make_key(g.iniX + c - g.minBorder, g.iniY + r - g.minBorder, resp);
+            const int r = o / kCellMax, c = o % kCellMax - sh;
+            const int resp = M[o] - 1;  // cornerScore<16> = m - 1
+            keys_out[cb.y + run + p.popc64(m & lt)] =
+                make_key(g.iniX + c - g.minBorder, g.iniY + r - g.minBorder, resp);
         }
-        carry += tot;
+        run += p.popc64(m);
     }
-    return carry;
+    return cb.x;
 }
 
 }  // namespace orbgpu

@@ -107,7 +107,8 @@ hipError_t launch_fast_cells(const BatchArgs& a, hipStream_t s);
 hipError_t launch_octree(const BatchArgs& a, hipStream_t s);
 hipError_t launch_orient_desc(const BatchArgs& a, hipStream_t s);
 hipError_t launch_finalize(const BatchArgs& a, hipStream_t s);
-hipError_t launch_knn2_pairs(const MatchArgs& m, int npairs, int qblocks, hipStream_t s);
+hipError_t launch_knn2_pairs(const MatchArgs& m, int npairs, int qblocks, void* scratch, hipStream_t s);
+size_t knn2_scratch_bytes(int npairs, int out_cap);
 hipError_t launch_knn2_plain(const uint8_t* q, int nq, const uint8_t* t, int nt, int32_t* i1,
                              int32_t* d1, int32_t* i2, int32_t* d2, hipStream_t s);
 

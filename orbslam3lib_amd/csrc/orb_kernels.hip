@@ -242,8 +242,8 @@ __global__ __launch_bounds__(256) void k_fast_cells(BatchArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t T[kCellMax * kCellMax];
     __shared__ __attribute__((aligned(16))) uint8_t M[kCellMax * kCellMax];
     __shared__ uint16_t list[kCellList];
+    __shared__ int32_t wcnt[4];
     __shared__ int scratch[16];
-    __shared__ int s_cnt;
     const int img = blockIdx.y;
     int l = 0;
     while (l + 1 < a.nlevels && (int)blockIdx.x >= a.lv[l + 1].cell_first) ++l;
@@ -268,8 +268,8 @@ __global__ __launch_bounds__(256) void k_fast_cells(BatchArgs a) {
     const uint8_t* src = a.lvl_base[l] + (long long)img * G.img_stride + (long long)g.iniY * G.pitch +
                          (g.iniX - sh);
     DevPolicy p{scratch};
-    const int n = fast_cell_run(p, src, G.pitch, sh, dword_ok, g, a.ini_th, a.min_th, T, M, list,
-                                &s_cnt, key_out);
+    CellScratch cs{T, M, list, wcnt};
+    const int n = fast_cell_run(p, src, G.pitch, sh, dword_ok, g, a.ini_th, a.min_th, cs, key_out);
     if (threadIdx.x == 0) *cnt_out = n;
 }
 
@@ -338,96 +338,94 @@ __global__ __launch_bounds__(512) void k_octree(BatchArgs a) {
 // k_orient_desc: one wave per keypoint.  IC_Angle on the raw level (ORBextractor_old.cc:78-105)
 // then computeOrbDescriptor on the blurred level (:108-148): a = (float)cos, b = (float)sin of
 // angle*pi/180 (float), sample center[cvRound(x*b + y*a)*step + cvRound(x*a - y*b)].
-// Per wave: the 31x31 raw patch (moments) and 37x37 blurred patch (rotated samples stay within
-// radius 18.4 -> |offset| <= 18) are staged in LDS with dword loads, then read as bytes.
-constexpr int kRawRows = 31, kRawDw = 10, kBlrRows = 37, kBlrDw = 12;
-
-__device__ inline void wave_lds_fence() {
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-}
-
-__device__ inline void stage_patch(uint32_t* dst, int rows, int dws, const uint8_t* plane, long long pitch,
-                                   int x0, int y0, bool dword_ok, int lane, int* shift) {
-    // copies rows [y0, y0+rows) x bytes [xa, xa + 4*dws) where xa = x0 & ~3 (dword path)
-    const int xa = dword_ok ? (x0 & ~3) : x0;
-    *shift = x0 - xa;
-    for (int i = lane; i < rows * dws; i += 64) {
-        const int r = i / dws, d = i % dws;
-        const uint8_t* s = plane + (long long)(y0 + r) * pitch + xa + 4 * d;
-        uint32_t v;
-        if (dword_ok) {
-            v = *reinterpret_cast<const uint32_t*>(s);
-        } else {
-            v = (uint32_t)s[0] | ((uint32_t)s[1] << 8) | ((uint32_t)s[2] << 16) | ((uint32_t)s[3] << 24);
-        }
-        dst[r * dws + d] = v;
-    }
-}
-
+// 16 lanes per keypoint (4 keypoints per wave, independent groups): every lane owns <= 2 disc
+// rows for the moments (dword row loads) and 16 of the 256 test pairs (two descriptor bytes),
+// sampled straight from the L2-resident blurred level.
 __global__ __launch_bounds__(256) void k_orient_desc(BatchArgs a) {
-    __shared__ uint32_t raw_s[4][kRawRows * kRawDw];
-    __shared__ uint32_t blr_s[4][kBlrRows * kBlrDw];
     const int img = blockIdx.y;
     int l = 0;
     while (l + 1 < a.nlevels && (int)blockIdx.x >= a.lv[l + 1].od_first) ++l;
     const LevelGeom& G = a.lv[l];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int sub = threadIdx.x & 15, grp = threadIdx.x >> 4;
     const int count = a.lvlcnt[img * kMaxLevels + l];
     const long long kbase = (long long)img * a.lvlkp_img_stride + G.kp_off;
     const uint8_t* lvl = a.lvl_base[l] + (long long)img * G.img_stride;
     const uint8_t* blr = a.blur_base[l] + (long long)img * G.bimg_stride;
     const bool raw_dw = ((G.pitch | G.img_stride) & 3) == 0;
-    const int stride_k = G.od_blocks * 4;
-    const uint8_t* rawb = reinterpret_cast<const uint8_t*>(raw_s[wave]);
-    const uint8_t* blrb = reinterpret_cast<const uint8_t*>(blr_s[wave]);
-    for (int kp = (blockIdx.x - G.od_first) * 4 + wave; kp < count; kp += stride_k) {
-        const uint32_t key = a.lvlkey[kbase + kp];
+    const int stride_k = G.od_blocks * 16;
+    // uniform trip count per wave so the 16-lane shuffles see all lanes
+    const int wave_first = (blockIdx.x - G.od_first) * 16 + (threadIdx.x >> 6) * 4;
+    for (int kb = wave_first; kb < count; kb += stride_k) {
+        const int kp = kb + (grp & 3);
+        const bool valid = kp < count;
+        const uint32_t key = valid ? a.lvlkey[kbase + kp] : a.lvlkey[kbase + kb];
         const int x = key_x(key) + kMinBorder, y = key_y(key) + kMinBorder;
-        int sr, sb;
-        stage_patch(raw_s[wave], kRawRows, kRawDw, lvl, G.pitch, x - 15, y - 15, raw_dw, lane, &sr);
-        stage_patch(blr_s[wave], kBlrRows, kBlrDw, blr, G.bpitch, x - 18, y - 18, true, lane, &sb);
-        wave_lds_fence();
-        // IC_Angle moments over the r=15 disc (ORBextractor_old.cc:78-105), exact integers
+        // IC_Angle moments (ORBextractor_old.cc:78-105): rows v = sub-15 and sub+1 (sub < 15)
         int m10 = 0, m01 = 0;
-        for (int i = lane; i < kRawRows * 32; i += 64) {
-            const int r = i >> 5, c = i & 31;
-            const int v = r - 15, u = c - 15;
-            if (c < 31 && (u < 0 ? -u : u) <= c_umax[v < 0 ? -v : v]) {
-                const int val = rawb[r * (4 * kRawDw) + sr + c];
-                m10 += u * val;
-                m01 += v * val;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int v = h == 0 ? sub - 15 : sub + 1;
+            if (h == 1 && sub == 15) break;
+            const int d = c_umax[v < 0 ? -v : v];
+            const uint8_t* row = lvl + (long long)(y + v) * G.pitch;
+            const int x0 = x - 15;
+            const int xa = raw_dw ? (x0 & ~3) : x0;
+            const int shf = x0 - xa;
+            uint32_t w[9];
+#pragma unroll
+            for (int i = 0; i < 9; ++i) {
+                if (raw_dw) {
+                    w[i] = *reinterpret_cast<const uint32_t*>(row + xa + 4 * i);
+                } else {
+                    const uint8_t* q = row + xa + 4 * i;
+                    w[i] = (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16) |
+                           ((uint32_t)q[3] << 24);
+                }
             }
+            int s = 0, su = 0;
+#pragma unroll
+            for (int c = 0; c < 31; ++c) {
+                const int u = c - 15;
+                const int b = shf + c;
+                const int val = (int)((w[b >> 2] >> (8 * (b & 3))) & 255u);
+                const bool in = (u < 0 ? -u : u) <= d;
+                s += in ? val : 0;
+                su += in ? u * val : 0;
+            }
+            m10 += su;
+            m01 += v * s;
         }
 #pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) {
-            m10 += __shfl_xor(m10, o, 64);
-            m01 += __shfl_xor(m01, o, 64);
+        for (int o = 8; o >= 1; o >>= 1) {
+            m10 += __shfl_xor(m10, o, 16);
+            m01 += __shfl_xor(m01, o, 16);
         }
         const float angle = fast_atan2_deg((float)m01, (float)m10);
-        if (lane == 0) a.lvlangle[kbase + kp] = angle;
-        // computeOrbDescriptor (:108-148): lane covers pairs 4*lane .. 4*lane+3 (one nibble)
+        // computeOrbDescriptor (:108-148): lane `sub` makes bytes 2*sub and 2*sub+1
         const float factorPI = (float)(3.14159265358979323846 / 180.0);
         const float ang = angle * factorPI;
-        const float ca = (float)cos((double)ang), sn = (float)sin((double)ang);
-        const int8_t* pat = c_pattern.v + lane * 16;
-        const uint8_t* center = blrb + 18 * (4 * kBlrDw) + sb + 18;
-        int nib = 0;
+        double sd, cd;
+        sincos((double)ang, &sd, &cd);
+        const float ca = (float)cd, sn = (float)sd;
+        const uint8_t* center = blr + (long long)y * G.bpitch + x;
+        const int8_t* pat = c_pattern.v + sub * 64;
+        uint32_t bits = 0;
 #pragma unroll
-        for (int b = 0; b < 4; ++b) {
+        for (int b = 0; b < 16; ++b) {
             int t[2];
 #pragma unroll
             for (int e = 0; e < 2; ++e) {
                 const float px = (float)pat[4 * b + 2 * e], py = (float)pat[4 * b + 2 * e + 1];
                 const int ry = cv_round(px * sn + py * ca);
                 const int rx = cv_round(px * ca - py * sn);
-                t[e] = center[ry * (4 * kBlrDw) + rx];
+                t[e] = center[(long long)ry * G.bpitch + rx];
             }
-            nib |= (t[0] < t[1]) << b;
+            bits |= (uint32_t)(t[0] < t[1]) << b;
         }
-        const int hi = __shfl_xor(nib, 1, 64);
-        if ((lane & 1) == 0) a.lvldesc[(kbase + kp) * 32 + (lane >> 1)] = (uint8_t)(nib | (hi << 4));
-        wave_lds_fence();  // the next keypoint overwrites this wave's patches
+        if (valid) {
+            if (sub == 0) a.lvlangle[kbase + kp] = angle;
+            reinterpret_cast<uint16_t*>(a.lvldesc + (kbase + kp) * 32)[sub] = (uint16_t)bits;
+        }
     }
 }
 
@@ -515,14 +513,25 @@ constexpr int kTrainChunk = 512;
 
 // Top-2 by packed key (distance << 16 | train index): integer order == lexicographic
 // (distance, index) order, so the insertion rule becomes k1' = min(k1, k), k2' = med3(k1, k2, k)
-// with no branches.  Requires nt < 65536 (checked on the host).
+// with no branches.  Requires nt < 65536 (checked on the host).  The train set is split over
+// kKnnSplit workgroups per query block (occupancy); a merge kernel folds the partial pairs.
+constexpr int kKnnSplit = 4;
+
 __device__ inline uint32_t med3_u32(uint32_t a, uint32_t b, uint32_t c) {
     return max(min(a, b), min(max(a, b), c));  // lowers to v_med3_u32
 }
 
-__device__ inline void knn2_core(const uint8_t* q, int nq, const uint8_t* t, int nt, int qi,
-                                 int32_t* i1, int32_t* d1, int32_t* i2, int32_t* d2,
-                                 uint4 (*tl)[2]) {
+__device__ inline uint32_t hamming256(const uint4& qa, const uint4& qb, const uint4& ta, const uint4& tb) {
+    const uint32_t s0 = __popc(qa.x ^ ta.x) + __popc(qa.y ^ ta.y);
+    const uint32_t s1 = __popc(qa.z ^ ta.z) + __popc(qa.w ^ ta.w);
+    const uint32_t s2 = __popc(qb.x ^ tb.x) + __popc(qb.y ^ tb.y);
+    const uint32_t s3 = __popc(qb.z ^ tb.z) + __popc(qb.w ^ tb.w);
+    return (s0 + s1) + (s2 + s3);
+}
+
+// Partial top-2 of query qi over train rows [t0, t1) -> packed keys.
+__device__ inline void knn2_partial(const uint8_t* q, int nq, const uint8_t* t, int t0, int t1, int qi,
+                                    uint4 (*tl)[2], uint32_t* k1o, uint32_t* k2o) {
     uint4 qa = make_uint4(0, 0, 0, 0), qb = qa;
     if (qi < nq) {
         const uint4* qp = reinterpret_cast<const uint4*>(q + (long long)qi * 32);
@@ -530,8 +539,8 @@ __device__ inline void knn2_core(const uint8_t* q, int nq, const uint8_t* t, int
         qb = qp[1];
     }
     uint32_t k1 = 0xFFFFFFFFu, k2 = 0xFFFFFFFFu;
-    for (int base = 0; base < nt; base += kTrainChunk) {
-        const int m = min(kTrainChunk, nt - base);
+    for (int base = t0; base < t1; base += kTrainChunk) {
+        const int m = min(kTrainChunk, t1 - base);
         __syncthreads();
         for (int i = threadIdx.x; i < m; i += blockDim.x) {
             const uint4* tp = reinterpret_cast<const uint4*>(t + (long long)(base + i) * 32);
@@ -540,66 +549,95 @@ __device__ inline void knn2_core(const uint8_t* q, int nq, const uint8_t* t, int
         }
         __syncthreads();
         int j = 0;
-        for (; j + 2 <= m; j += 2) {
+        for (; j + 4 <= m; j += 4) {
+            uint32_t kk[4];
 #pragma unroll
-            for (int u = 0; u < 2; ++u) {
-                const uint4 ta = tl[j + u][0], tb = tl[j + u][1];
-                uint32_t d = __popc(qa.x ^ ta.x);
-                d += __popc(qa.y ^ ta.y);
-                d += __popc(qa.z ^ ta.z);
-                d += __popc(qa.w ^ ta.w);
-                d += __popc(qb.x ^ tb.x);
-                d += __popc(qb.y ^ tb.y);
-                d += __popc(qb.z ^ tb.z);
-                d += __popc(qb.w ^ tb.w);
-                const uint32_t key = (d << 16) | (uint32_t)(base + j + u);
-                k2 = med3_u32(k1, k2, key);
-                k1 = min(k1, key);
+            for (int u = 0; u < 4; ++u)
+                kk[u] = (hamming256(qa, qb, tl[j + u][0], tl[j + u][1]) << 16) | (uint32_t)(base + j + u);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                k2 = med3_u32(k1, k2, kk[u]);
+                k1 = min(k1, kk[u]);
             }
         }
         for (; j < m; ++j) {
-            const uint4 ta = tl[j][0], tb = tl[j][1];
-            uint32_t d = __popc(qa.x ^ ta.x) + __popc(qa.y ^ ta.y) + __popc(qa.z ^ ta.z) +
-                         __popc(qa.w ^ ta.w) + __popc(qb.x ^ tb.x) + __popc(qb.y ^ tb.y) +
-                         __popc(qb.z ^ tb.z) + __popc(qb.w ^ tb.w);
-            const uint32_t key = (d << 16) | (uint32_t)(base + j);
+            const uint32_t key = (hamming256(qa, qb, tl[j][0], tl[j][1]) << 16) | (uint32_t)(base + j);
             k2 = med3_u32(k1, k2, key);
             k1 = min(k1, key);
         }
     }
-    if (qi < nq) {
-        i1[qi] = k1 == 0xFFFFFFFFu ? -1 : (int32_t)(k1 & 0xFFFF);
-        d1[qi] = k1 == 0xFFFFFFFFu ? 0x7fffffff : (int32_t)(k1 >> 16);
-        i2[qi] = k2 == 0xFFFFFFFFu ? -1 : (int32_t)(k2 & 0xFFFF);
-        d2[qi] = k2 == 0xFFFFFFFFu ? 0x7fffffff : (int32_t)(k2 >> 16);
-    }
+    *k1o = k1;
+    *k2o = k2;
 }
 
-__global__ __launch_bounds__(256) void k_knn2_pairs(MatchArgs m) {
+__device__ inline void knn2_store(uint32_t k1, uint32_t k2, int qi, int32_t* i1, int32_t* d1,
+                                  int32_t* i2, int32_t* d2) {
+    i1[qi] = k1 == 0xFFFFFFFFu ? -1 : (int32_t)(k1 & 0xFFFF);
+    d1[qi] = k1 == 0xFFFFFFFFu ? 0x7fffffff : (int32_t)(k1 >> 16);
+    i2[qi] = k2 == 0xFFFFFFFFu ? -1 : (int32_t)(k2 & 0xFFFF);
+    d2[qi] = k2 == 0xFFFFFFFFu ? 0x7fffffff : (int32_t)(k2 >> 16);
+}
+
+struct KnnPart {
+    uint32_t* keys;  // [pair][split][out_cap][2]
+};
+
+__global__ __launch_bounds__(256) void k_knn2_pairs(MatchArgs m, KnnPart part) {
     __shared__ uint4 tl[kTrainChunk][2];
-    const int pair = blockIdx.y;
+    const int pair = blockIdx.z, split = blockIdx.y;
     const int qimg = 2 * pair, timg = 2 * pair + 1;
     const int qn = m.out_n[qimg], tn = m.out_n[timg];
     const int q0 = m.stereo_only ? m.out_mono[qimg] : 0;
-    const int t0 = m.stereo_only ? m.out_mono[timg] : 0;
-    const int nq = qn > q0 ? qn - q0 : 0, nt = tn > t0 ? tn - t0 : 0;
-    if ((int)(blockIdx.x * blockDim.x) >= nq) {
-        if (blockIdx.x == 0 && threadIdx.x == 0) m.nq[pair] = nq;
-        return;
-    }
-    if (blockIdx.x == 0 && threadIdx.x == 0) m.nq[pair] = nq;
+    const int tq0 = m.stereo_only ? m.out_mono[timg] : 0;
+    const int nq = qn > q0 ? qn - q0 : 0, nt = tn > tq0 ? tn - tq0 : 0;
+    if ((int)(blockIdx.x * blockDim.x) >= nq) return;
+    const int per = (nt + kKnnSplit - 1) / kKnnSplit;
+    const int t0 = min(nt, split * per), t1 = min(nt, t0 + per);
     const uint8_t* q = m.desc + ((long long)qimg * m.out_cap + q0) * 32;
-    const uint8_t* t = m.desc + ((long long)timg * m.out_cap + t0) * 32;
+    const uint8_t* t = m.desc + ((long long)timg * m.out_cap + tq0) * 32;
+    const int qi = blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t k1, k2;
+    knn2_partial(q, nq, t, t0, t1, qi, tl, &k1, &k2);
+    if (qi < nq) {
+        uint2* o = reinterpret_cast<uint2*>(part.keys) + ((long long)pair * kKnnSplit + split) * m.out_cap + qi;
+        *o = make_uint2(k1, k2);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_knn2_merge(MatchArgs m, KnnPart part) {
+    const int pair = blockIdx.y;
+    const int qimg = 2 * pair, timg = 2 * pair + 1;
+    const int qn = m.out_n[qimg];
+    const int q0 = m.stereo_only ? m.out_mono[qimg] : 0;
+    const int nq = qn > q0 ? qn - q0 : 0;
+    const int tn = m.out_n[timg];
+    const int tq0 = m.stereo_only ? m.out_mono[timg] : 0;
+    const int nt = tn > tq0 ? tn - tq0 : 0;
+    if (blockIdx.x == 0 && threadIdx.x == 0) m.nq[pair] = nq;
+    const int qi = blockIdx.x * blockDim.x + threadIdx.x;
+    if (qi >= nq) return;
+    const int per = (nt + kKnnSplit - 1) / kKnnSplit;
+    uint32_t k1 = 0xFFFFFFFFu, k2 = 0xFFFFFFFFu;
+    for (int sp = 0; sp < kKnnSplit; ++sp) {
+        if (sp * per >= nt) break;
+        const uint2 v = reinterpret_cast<const uint2*>(part.keys)[((long long)pair * kKnnSplit + sp) * m.out_cap + qi];
+        k2 = med3_u32(k1, k2, v.x);
+        k1 = min(k1, v.x);
+        k2 = med3_u32(k1, k2, v.y);
+        k1 = min(k1, v.y);
+    }
     const long long o = (long long)pair * m.out_cap;
-    knn2_core(q, nq, t, nt, blockIdx.x * blockDim.x + threadIdx.x, m.idx1 + o, m.dist1 + o,
-              m.idx2 + o, m.dist2 + o, tl);
+    knn2_store(k1, k2, qi, m.idx1 + o, m.dist1 + o, m.idx2 + o, m.dist2 + o);
 }
 
 __global__ __launch_bounds__(256) void k_knn2_plain(const uint8_t* q, int nq, const uint8_t* t,
                                                     int nt, int32_t* i1, int32_t* d1, int32_t* i2,
                                                     int32_t* d2) {
     __shared__ uint4 tl[kTrainChunk][2];
-    knn2_core(q, nq, t, nt, blockIdx.x * blockDim.x + threadIdx.x, i1, d1, i2, d2, tl);
+    const int qi = blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t k1, k2;
+    knn2_partial(q, nq, t, 0, nt, qi, tl, &k1, &k2);
+    if (qi < nq) knn2_store(k1, k2, qi, i1, d1, i2, d2);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -629,10 +667,13 @@ hipError_t launch_finalize(const BatchArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_finalize, dim3(a.nimages), dim3(256), 0, s, a);
     return hipGetLastError();
 }
-hipError_t launch_knn2_pairs(const MatchArgs& m, int npairs, int qblocks, hipStream_t s) {
-    hipLaunchKernelGGL(k_knn2_pairs, dim3(qblocks, npairs), dim3(256), 0, s, m);
+hipError_t launch_knn2_pairs(const MatchArgs& m, int npairs, int qblocks, void* scratch, hipStream_t s) {
+    KnnPart part{reinterpret_cast<uint32_t*>(scratch)};
+    hipLaunchKernelGGL(k_knn2_pairs, dim3(qblocks, kKnnSplit, npairs), dim3(256), 0, s, m, part);
+    hipLaunchKernelGGL(k_knn2_merge, dim3(qblocks, npairs), dim3(256), 0, s, m, part);
     return hipGetLastError();
 }
+size_t knn2_scratch_bytes(int npairs, int out_cap) { return (size_t)npairs * kKnnSplit * out_cap * 8 + 256; }
 hipError_t launch_knn2_plain(const uint8_t* q, int nq, const uint8_t* t, int nt, int32_t* i1,
                              int32_t* d1, int32_t* i2, int32_t* d2, hipStream_t s) {
     const int blocks = (nq + 255) / 256;

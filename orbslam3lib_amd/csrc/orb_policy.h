@@ -18,6 +18,19 @@ struct DevPolicy {
     __device__ uint32_t atomic_max(uint32_t* p, uint32_t v) { return atomicMax(p, v); }
     __device__ int atomic_max_int(int* p, int v) { return atomicMax(p, v); }
     __device__ unsigned long long now() const { return wall_clock64(); }  // 100 MHz
+    __device__ int popc64(uint64_t x) const { return __popcll(x); }
+    __device__ int lane() const { return (int)(threadIdx.x & 63); }
+    __device__ int wave() const { return (int)(threadIdx.x >> 6); }
+    __device__ int nwaves() const { return (int)(blockDim.x >> 6); }
+    __device__ int wave_width() const { return 64; }
+    __device__ uint64_t ballot(bool f) const { return __ballot(f); }
+    __device__ uint64_t lanemask_lt() const { return (1ull << (threadIdx.x & 63)) - 1ull; }
+    // OR of x over the 64 lanes of the calling wave (all lanes must participate)
+    __device__ uint64_t wave_or(uint64_t x) const {
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) x |= __shfl_xor(x, o, 64);
+        return x;
+    }
     // Block-wide exclusive scan: every thread passes v, gets its exclusive prefix and the total.
     __device__ int scan_excl(int v, int* total) {
         const int lane = (int)(threadIdx.x & 63), wid = (int)(threadIdx.x >> 6);
@@ -66,6 +79,18 @@ struct SerialPolicy {
         return 0;
     }
     __host__ __device__ unsigned long long now() const { return 0; }
+    __host__ __device__ int popc64(uint64_t x) const {
+        int c = 0;
+        for (; x; x &= x - 1) ++c;
+        return c;
+    }
+    __host__ __device__ uint64_t wave_or(uint64_t x) const { return x; }
+    __host__ __device__ int lane() const { return 0; }
+    __host__ __device__ int wave() const { return 0; }
+    __host__ __device__ int nwaves() const { return 1; }
+    __host__ __device__ int wave_width() const { return 1; }
+    __host__ __device__ uint64_t ballot(bool f) const { return f ? 1ull : 0ull; }
+    __host__ __device__ uint64_t lanemask_lt() const { return 0ull; }
 };
 
 }  // namespace orbgpu

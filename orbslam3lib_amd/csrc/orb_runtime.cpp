@@ -96,7 +96,7 @@ struct orbgpu_ctx {
     // device buffers
     DevBuf input, pyr, blur, rtab, cellkeys, cellcnt, octws, lvlkey, lvlangle, lvldesc, lvlcnt,
         status, outkps, outdesc, outn, outmono, laps, midx1, mdist1, midx2, mdist2, mnq, scratch,
-        octdbg;
+        octdbg, knnpart;
     int input_images = 0;   // images currently sized for in `input`
     int last_images = 0, last_w = 0, last_h = 0, last_pairs = 0;
     // profiling
@@ -272,7 +272,7 @@ int set_geometry(orbgpu_ctx* c, int w, int h) {
         G.tiles_y = (G.h + 31) / 32;
         G.tile_first = tile_first;
         tile_first += G.tiles_x * G.tiles_y;
-        G.od_blocks = std::max(1, (G.N + 16 + 3) / 4);
+        G.od_blocks = std::max(1, (G.N + 16 + 15) / 16);  // 16 keypoints per block
         G.od_first = od_first;
         od_first += G.od_blocks;
         G.area2 = 0;
@@ -441,7 +441,8 @@ int orbgpu_destroy(orbgpu_ctx* c) {
     DevBuf* bufs[] = {&c->input,   &c->pyr,     &c->blur,   &c->rtab,    &c->cellkeys, &c->cellcnt,
                       &c->octws,   &c->lvlkey,  &c->lvlangle, &c->lvldesc, &c->lvlcnt, &c->status,
                       &c->outkps,  &c->outdesc, &c->outn,   &c->outmono, &c->laps,     &c->midx1,
-                      &c->mdist1,  &c->midx2,   &c->mdist2, &c->mnq,     &c->scratch, &c->octdbg};
+                      &c->mdist1,  &c->midx2,   &c->mdist2, &c->mnq,     &c->scratch, &c->octdbg,
+                      &c->knnpart};
     for (DevBuf* b : bufs) b->release();
     if (c->stream) hipStreamDestroy(c->stream);
     delete c;
@@ -714,7 +715,10 @@ int orbgpu_match_stereo_batch(orbgpu_ctx* c, int n_pairs, int stereo_only, void*
     m.dist2 = c->mdist2.as<int32_t>();
     m.nq = c->mnq.as<int32_t>();
     const int qblocks = (c->out_cap + 255) / 256;
-    int r = timed(c, ST_KNN, s, [&] { return launch_knn2_pairs(m, n_pairs, qblocks, s); });
+    if (c->out_cap > 65535) return fail(ORBGPU_ERR_INVALID, "matcher supports < 65536 rows per image");
+    if (c->knnpart.ensure(knn2_scratch_bytes(n_pairs, c->out_cap)))
+        return fail(ORBGPU_ERR_HIP, "hipMalloc failed (knn scratch)");
+    int r = timed(c, ST_KNN, s, [&] { return launch_knn2_pairs(m, n_pairs, qblocks, c->knnpart.p, s); });
     if (r) return r;
     c->last_pairs = n_pairs;
     return ORBGPU_OK;

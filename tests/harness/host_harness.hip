@@ -86,6 +86,7 @@ int harness_level_candidates(const uint8_t* lvl, int w, int h, int ini, int mn, 
     uint8_t* T = reinterpret_cast<uint8_t*>(T32.data());
     uint8_t* M = reinterpret_cast<uint8_t*>(M32.data());
     std::vector<uint16_t> list(kCellList);
+    std::vector<int32_t> wcnt(4);
     std::vector<uint32_t> tmp(kCellMax * kCellMax);
     int total = 0, cnt = 0;
     SerialPolicy p;
@@ -101,8 +102,9 @@ int harness_level_candidates(const uint8_t* lvl, int w, int h, int ini, int mn, 
             // alternate the two load paths (dword-aligned window / plain bytes) across cells
             const bool dw = ((i + j) & 1) == 0 && (w & 3) == 0;
             const int sh = dw ? (g.iniX & 3) : 0;
+            CellScratch cs{T, M, list.data(), wcnt.data()};
             const int m = fast_cell_run(p, lvl + (long long)g.iniY * w + g.iniX - sh, w, sh, dw, g,
-                                        ini, mn, T, M, list.data(), &cnt, tmp.data());
+                                        ini, mn, cs, tmp.data());
             for (int k = 0; k < m; ++k) {
                 if (total < cap) out[total] = tmp[k];
                 ++total;

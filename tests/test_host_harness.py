@@ -136,3 +136,22 @@ def test_octree_edge_cases(harness, oracle):
         np.testing.assert_array_equal(x2, ref["x"])
         np.testing.assert_array_equal(y2, ref["y"])
         np.testing.assert_array_equal(r2, ref["response"])
+
+
+@pytest.mark.parametrize("ini,mn", [(20, 7), (7, 20), (0, 0), (40, 3), (255, 1)])
+def test_cells_thresholds_and_fallback(harness, oracle, ini, mn):
+    # a low-texture frame (many cells fall back to minThFAST) and a textured one
+    rng = np.random.default_rng(ini * 7 + mn)
+    yy, xx = np.mgrid[0:240, 0:320]
+    smooth = (60 + 0.3 * xx + 0.2 * yy).astype(np.int32)
+    for _ in range(40):
+        x, y = rng.integers(20, 300), rng.integers(20, 220)
+        smooth[y - 2:y + 3, x - 2:x + 3] += int(rng.integers(-60, 60))
+    smooth = np.clip(smooth + rng.integers(-3, 4, smooth.shape), 0, 255).astype(np.uint8)
+    for img in (smooth, synth.frame(240, 320, 11)):
+        cand = _level_cands(harness, img, ini, mn)
+        oc = oracle.level_candidates(img, ini, mn)
+        x, y, r = _unpack(cand)
+        np.testing.assert_array_equal(x, oc["x"])
+        np.testing.assert_array_equal(y, oc["y"])
+        np.testing.assert_array_equal(r, oc["response"])
