@@ -63,6 +63,8 @@ struct BatchArgs {
     const int32_t* laps;             // [img][2]
     int total_cells, total_tiles, total_od_blocks;
     unsigned long long* octdbg;      // diagnostic: [img][kMaxLevels][8] phase clocks, or null
+    int oct_lds_nodes;               // node capacity of k_octree's dynamic LDS (0: all global)
+    int oct_lds_bytes;
 };
 
 struct MatchArgs {
@@ -95,7 +97,7 @@ __host__ __device__ inline OctLayout oct_layout(int n_cap, int C) {
     L.knode = o; o = oct_align(o + 2LL * n_cap);
     L.kq = o; o = oct_align(o + 1LL * n_cap);
     L.nodemem = o;
-    if (C > kOctLdsNodes) o = oct_align(o + (long long)((size_t)C * 78 + 64));
+    o = oct_align(o + (long long)((size_t)C * 78 + 64));  // used when C exceeds the LDS capacity
     L.total = o;
     return L;
 }

@@ -278,10 +278,10 @@ __global__ __launch_bounds__(256) void k_fast_cells(BatchArgs a) {
 // (vToDistributeKeys, :807-871) then runs DistributeOctTree (orb_octree.h) with the node
 // state in LDS (80 KB: two workgroups per CU).
 __global__ __launch_bounds__(512) void k_octree(BatchArgs a) {
-    __shared__ __attribute__((aligned(16))) uint8_t nodemem_lds[kOctLdsNodes * 78 + 64];
+    extern __shared__ __attribute__((aligned(16))) uint8_t nodemem_lds[];  // a.oct_lds_bytes
     __shared__ int scratch[16];
     __shared__ OctShared sh;
-    const int l = blockIdx.x, img = blockIdx.y;
+    const int img = blockIdx.x, l = blockIdx.y;  // level-major dispatch: the long level-0 groups go first
     const LevelGeom& G = a.lv[l];
     DevPolicy p{scratch};
     const int32_t* cnt = a.cellcnt + (long long)img * a.cellcnt_img_stride + G.cellcnt_off;
@@ -289,10 +289,10 @@ __global__ __launch_bounds__(512) void k_octree(BatchArgs a) {
     uint8_t* ws = a.octws + (long long)img * a.octws_img_stride + G.oct_off;
     const OctLayout L = oct_layout(G.cand_cap, G.oct_cap);
     uint32_t* keys = reinterpret_cast<uint32_t*>(ws + L.keys);
-    void* nm = G.oct_cap <= kOctLdsNodes ? (void*)nodemem_lds : (void*)(ws + L.nodemem);
+    void* nm = G.oct_cap <= a.oct_lds_nodes ? (void*)nodemem_lds : (void*)(ws + L.nodemem);
     // exclusive scan of the cell counts into LDS (the node area is free until the octree runs)
     int32_t* cell_off = reinterpret_cast<int32_t*>(nodemem_lds);
-    const bool off_in_lds = G.ncells <= (int)(sizeof(nodemem_lds) / 4);
+    const bool off_in_lds = G.ncells <= a.oct_lds_bytes / 4;
     if (!off_in_lds) cell_off = reinterpret_cast<int32_t*>(ws + L.knode);  // huge levels only
     int carry = 0;
     for (int base = 0; base < G.ncells; base += blockDim.x) {
@@ -656,7 +656,12 @@ hipError_t launch_fast_cells(const BatchArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 hipError_t launch_octree(const BatchArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(k_octree, dim3(a.nlevels, a.nimages), dim3(512), 0, s, a);
+    if (a.oct_lds_bytes > 65536) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k_octree),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, a.oct_lds_bytes);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(k_octree, dim3(a.nimages, a.nlevels), dim3(512), a.oct_lds_bytes, s, a);
     return hipGetLastError();
 }
 hipError_t launch_orient_desc(const BatchArgs& a, hipStream_t s) {

@@ -93,6 +93,8 @@ struct OctWS {
     unsigned long long* dbg;  // diagnostic phase clocks (8 slots) or nullptr
 };
 
+constexpr int kOctUnroll = 4;  // keys per thread per batch in the key passes
+
 struct OctShared {
     int size, prev_size, nexp, ndiv, phase, done, nchild, nundiv, status, jstop;
 };
@@ -391,16 +393,31 @@ __host__ __device__ int octree_distribute(P& p, const OctWS& ws, OctShared* sh, 
         }
         p.sync();
         mark(4);
-        // 3. relabel keys, and count the next round's candidates (fresh children with >1 key)
-        for (int k = tid; k < n; k += NT) {
-            const int v = ws.knode[k];
-            const bool dv = M.divrank[v] >= 0;
-            const int nv = dv ? M.childpos[4 * v + ws.kq[k]] : M.undivpos[v];
-            ws.knode[k] = (uint16_t)nv;
-            if (dv && nxt[nv].cnt > 1) {
-                const int q = oct_quadrant(ws.keys[k], nxt[nv]);
-                ws.kq[k] = (uint8_t)q;
-                p.atomic_add(&cnxt[4 * nv + q], 1);
+        // 3. relabel keys, and count the next round's candidates (fresh children with >1 key);
+        //    global loads of 4 keys per thread are issued together (latency-bound pass)
+        for (int base = tid; base < n; base += kOctUnroll * NT) {
+            int v[kOctUnroll], q0[kOctUnroll];
+            uint32_t key[kOctUnroll];
+#pragma unroll
+            for (int u = 0; u < kOctUnroll; ++u) {
+                const int k = base + u * NT;
+                const bool in = k < n;
+                v[u] = in ? ws.knode[k] : 0;
+                q0[u] = in ? ws.kq[k] : 0;
+                key[u] = in ? ws.keys[k] : 0;
+            }
+#pragma unroll
+            for (int u = 0; u < kOctUnroll; ++u) {
+                const int k = base + u * NT;
+                if (k >= n) continue;
+                const bool dv = M.divrank[v[u]] >= 0;
+                const int nv = dv ? M.childpos[4 * v[u] + q0[u]] : M.undivpos[v[u]];
+                ws.knode[k] = (uint16_t)nv;
+                if (dv && nxt[nv].cnt > 1) {
+                    const int q = oct_quadrant(key[u], nxt[nv]);
+                    ws.kq[k] = (uint8_t)q;
+                    p.atomic_add(&cnxt[4 * nv + q], 1);
+                }
             }
         }
         if (tid == 0) {
@@ -438,9 +455,22 @@ __host__ __device__ int octree_distribute(P& p, const OctWS& ws, OctShared* sh, 
     uint32_t* best = reinterpret_cast<uint32_t*>(cnxt);
     for (int i = tid; i < size; i += NT) best[i] = 0;
     p.sync();
-    for (int k = tid; k < n; k += NT) {
-        const uint32_t val = ((uint32_t)key_resp(ws.keys[k]) << 24) | (0xFFFFFFu - (uint32_t)k);
-        p.atomic_max(&best[ws.knode[k]], val);
+    for (int base = tid; base < n; base += kOctUnroll * NT) {
+        uint32_t key[kOctUnroll];
+        int v[kOctUnroll];
+#pragma unroll
+        for (int u = 0; u < kOctUnroll; ++u) {
+            const int k = base + u * NT;
+            key[u] = k < n ? ws.keys[k] : 0;
+            v[u] = k < n ? ws.knode[k] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < kOctUnroll; ++u) {
+            const int k = base + u * NT;
+            if (k >= n) continue;
+            const uint32_t val = ((uint32_t)key_resp(key[u]) << 24) | (0xFFFFFFu - (uint32_t)k);
+            p.atomic_max(&best[v[u]], val);
+        }
     }
     p.sync();
     for (int i = tid; i < size; i += NT) {

@@ -18,6 +18,7 @@
 
 #include "../../include/orbgpu.h"
 #include "orb_kernels.h"
+#include "orb_octree.h"
 
 using namespace orbgpu;
 
@@ -294,6 +295,16 @@ int set_geometry(orbgpu_ctx* c, int w, int h) {
     c->octws_img = round_up_ll(ows, 256);
     c->lvlkp_img = kpo;
     c->out_cap = kpo;
+    // k_octree dynamic LDS: the largest node capacity that fits kOctLdsNodes (levels above it
+    // keep their node state in the global workspace) and room for the cell offsets.
+    int lds_nodes = 0, max_cells = 0;
+    for (int l = 0; l < L; ++l) {
+        if (A.lv[l].oct_cap <= kOctLdsNodes) lds_nodes = std::max(lds_nodes, A.lv[l].oct_cap);
+        max_cells = std::max(max_cells, A.lv[l].ncells);
+    }
+    A.oct_lds_nodes = lds_nodes;
+    A.oct_lds_bytes = std::max((int)oct_nodemem_bytes(std::max(lds_nodes, 1)), std::min(4 * max_cells, 65536));
+    A.oct_lds_bytes = (A.oct_lds_bytes + 15) & ~15;
     A.total_cells = cell_first;
     A.total_tiles = tile_first;
     A.total_od_blocks = od_first;
