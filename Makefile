@@ -6,7 +6,7 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall 
 LIB := orbslam3lib_amd/liborbgpu.so
 HDRS := $(wildcard $(CSRC)/*.h) include/orbgpu.h
 
-all: $(LIB) oracle
+all: $(LIB) oracle facade_test
 
 $(LIB): $(CSRC)/orb_kernels.hip $(CSRC)/orb_runtime.cpp $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(CSRC)/orb_kernels.hip $(CSRC)/orb_runtime.cpp
@@ -14,8 +14,16 @@ $(LIB): $(CSRC)/orb_kernels.hip $(CSRC)/orb_runtime.cpp $(HDRS)
 oracle:
 	$(MAKE) -s -C oracle
 
+# C++ facade (what an ORB-SLAM3 build compiles) + its GPU test program
+FACADE_TEST := tests/cpp/build/facade_test
+facade_test: $(FACADE_TEST)
+$(FACADE_TEST): tests/cpp/facade_test.cpp orbslam3lib_amd/facade/ORBextractor.cc include/orbslam3/ORBextractor.h include/orbslam3/cv_shim.h $(LIB)
+	@mkdir -p tests/cpp/build
+	$(CXX) -O2 -std=c++17 -o $@ tests/cpp/facade_test.cpp orbslam3lib_amd/facade/ORBextractor.cc \
+		-L orbslam3lib_amd -lorbgpu -Wl,-rpath,'$$ORIGIN/../../../orbslam3lib_amd' -Wl,-rpath-link,/opt/rocm/lib -ldl
+
 clean:
 	rm -f $(LIB)
 	$(MAKE) -s -C oracle clean
 
-.PHONY: all oracle clean
+.PHONY: all oracle clean facade_test

@@ -161,3 +161,16 @@ def test_descriptor_distance_matches_reference(oracle):
     for _ in range(200):
         a, b = rng.integers(0, 256, (2, 32), dtype=np.uint8)
         assert og.ORBmatcher.DescriptorDistance(a, b) == oracle.descriptor_distance(a, b)
+
+
+def test_cpp_facade():
+    """The C++ ORB_SLAM3::ORBextractor facade (what an ORB-SLAM3 build links) vs the oracle."""
+    import os
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(root, "tests", "cpp", "build", "facade_test")
+    assert os.path.exists(exe), "run make (builds tests/cpp/build/facade_test)"
+    r = subprocess.run([exe, os.path.join(root, "oracle", "build", "liborb_oracle.so")],
+                       capture_output=True, text=True, timeout=300, cwd=root)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "FACADE OK" in r.stdout
