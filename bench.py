@@ -144,7 +144,8 @@ def main():
 
     P, W, H = args.pairs, args.width, args.height
     U = max(1, min(args.unique_pairs, P))
-    base = rank * 100000
+    from orbslam3lib_amd.dist import pair_seed_base
+    base = pair_seed_base(rank)  # each rank extracts its own shard of the stream (weak scaling)
     uniq = [synth.stereo_pair(H, W, base + i) for i in range(U)]
     imgs = np.empty((2 * P, H, W), np.uint8)
     for p in range(P):

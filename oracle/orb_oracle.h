@@ -9,6 +9,12 @@
 //
 // Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this code,
 // and only as the checker.  The product (liborbgpu.so) never links or calls it.
+//
+// Parity status: PARTIALLY PINNED.  The reference ships no tests/fixtures for this path and its
+// CPU extractor cannot be built here (OpenCV 4.2 is fetched at configure time, Android headers,
+// syntax error at ORBextractor_old.cc:477).  Pinned from the reference: the rBRIEF table (sha256),
+// umax, level sizes, per-level feature split.  The OpenCV internals are restated (unpinned
+// against OpenCV itself) and cross-checked by independent brute-force restatements in tests/.
 #pragma once
 #include <cstddef>
 #include <cstdint>

@@ -1,0 +1,56 @@
+"""CPU: the multi-process path of bench.py (gloo, world_size 2): sharding without overlap, and
+max/sum reductions of the timing and feature counts across ranks."""
+import os
+import socket
+
+import pytest
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    import torch.distributed as dist
+
+    from orbslam3lib_amd import dist as od
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    lo, hi = od.shard_range(130, rank, world)
+    t = od.reduce_scalar(dist, 1.5 + rank, "max")
+    s = od.reduce_scalar(dist, hi - lo, "sum")
+    dist.barrier()
+    q.put((rank, lo, hi, t, s, od.pair_seed_base(rank)))
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_sharding_and_reductions():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (r0, lo0, hi0, t0, s0, b0), (r1, lo1, hi1, t1, s1, b1) = res
+    assert (lo0, hi0, lo1, hi1) == (0, 65, 65, 130)
+    assert t0 == t1 == 2.5 and s0 == s1 == 130
+    assert b0 != b1
+
+
+@pytest.mark.parametrize("total,world", [(7, 3), (128, 8), (1, 4)])
+def test_shard_range_partitions(total, world):
+    from orbslam3lib_amd import dist as od
+    spans = [od.shard_range(total, r, world) for r in range(world)]
+    assert spans[0][0] == 0 and spans[-1][1] == total
+    for (a, b), (c, d) in zip(spans, spans[1:]):
+        assert b == c and b >= a

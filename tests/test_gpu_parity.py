@@ -174,3 +174,29 @@ def test_cpp_facade():
                        capture_output=True, text=True, timeout=300, cwd=root)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "FACADE OK" in r.stdout
+
+
+def test_gpu_matches_golden_fixtures():
+    """GPU output equals the committed golden vectors (no oracle call on the box)."""
+    import glob
+    import os
+
+    import orbslam3lib_amd as og
+    from tests.test_golden import CASES, load_case
+    assert CASES
+    for path in CASES:
+        img, z = load_case(path)
+        h, w = img.shape
+        ex = og.ORBextractor(int(z["nfeatures"]), 1.2, int(z["nlevels"]), 20, 7, max_width=w,
+                             max_height=h, max_images=2)
+        k, d, mono = ex(img, None, tuple(int(v) for v in z["lap"]))
+        assert mono == int(z["mono"]), path
+        _same_kps(k, z["kps"])
+        np.testing.assert_array_equal(d, z["desc"])
+    gold = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    L = np.load(os.path.join(gold, "c2_left_640x480_n2000.npz"))["desc"]
+    R = np.load(os.path.join(gold, "c2_right_640x480_n2000.npz"))["desc"]
+    g = np.load(os.path.join(gold, "c2_knn2_left_right.npz"))
+    got = og.BFMatcher(ex).knnMatch(L, R, 2)
+    for a, key in zip(got, ("idx1", "dist1", "idx2", "dist2")):
+        np.testing.assert_array_equal(a, g[key])
