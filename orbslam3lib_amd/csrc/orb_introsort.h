@@ -29,9 +29,14 @@ __host__ __device__ inline bool node_less(const SortElem& a, const SortElem& b) 
 }
 
 __host__ __device__ inline void isort_swap(SortElem* a, int i, int j) {
-    SortElem t = a[i];
-    a[i] = a[j];
-    a[j] = t;
+    // field-wise (a 12-byte struct temporary would be placed in scratch memory by hipcc)
+    const int32_t s0 = a[i].size, u0 = a[i].ulx, n0 = a[i].node;
+    a[i].size = a[j].size;
+    a[i].ulx = a[j].ulx;
+    a[i].node = a[j].node;
+    a[j].size = s0;
+    a[j].ulx = u0;
+    a[j].node = n0;
 }
 
 __host__ __device__ inline int isort_lg(int n) {
@@ -216,9 +221,13 @@ __host__ __device__ void introsort_parallel(P& p, SortElem* a, int m, const Sort
     while (true) {
         const int nseg = *sh_nseg;
         if (nseg == 0) break;
-        const uint16_t* F = s.segF[cur];
-        const uint16_t* L = s.segL[cur];
-        const uint16_t* D = s.segD[cur];
+        // (no runtime-indexed pointer arrays: they would live in scratch memory)
+        const uint16_t* F = cur ? s.segF[1] : s.segF[0];
+        const uint16_t* L = cur ? s.segL[1] : s.segL[0];
+        const uint16_t* D = cur ? s.segD[1] : s.segD[0];
+        uint16_t* NF = cur ? s.segF[0] : s.segF[1];
+        uint16_t* NL = cur ? s.segL[0] : s.segL[1];
+        uint16_t* ND = cur ? s.segD[0] : s.segD[1];
         for (int g = tid; g < nseg; g += NT) {
             const int f = F[g], l = L[g];
             if (D[g] == 0) {
@@ -309,15 +318,15 @@ __host__ __device__ void introsort_parallel(P& p, SortElem* a, int m, const Sort
             if (c) {
                 int o = carry + ex;
                 if (cut - f > 16) {
-                    s.segF[cur ^ 1][o] = (uint16_t)f;
-                    s.segL[cur ^ 1][o] = (uint16_t)cut;
-                    s.segD[cur ^ 1][o] = (uint16_t)d;
+                    NF[o] = (uint16_t)f;
+                    NL[o] = (uint16_t)cut;
+                    ND[o] = (uint16_t)d;
                     ++o;
                 }
                 if (l - cut > 16) {
-                    s.segF[cur ^ 1][o] = (uint16_t)cut;
-                    s.segL[cur ^ 1][o] = (uint16_t)l;
-                    s.segD[cur ^ 1][o] = (uint16_t)d;
+                    NF[o] = (uint16_t)cut;
+                    NL[o] = (uint16_t)l;
+                    ND[o] = (uint16_t)d;
                 }
             }
             carry += tot;

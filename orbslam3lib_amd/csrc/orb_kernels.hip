@@ -39,6 +39,32 @@ __constant__ PatternTable c_pattern = make_pattern();
 // umax[] of the ORBextractor ctor (ORBextractor_old.cc:455-470) for HALF_PATCH_SIZE = 15.
 __constant__ int c_umax[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};
 
+// Byte weights for the IC_Angle moments with v_dot4_u32_u8: for disc row |v| and dword j of the
+// 32-byte window starting at u = -16: {1 inside the disc, max(u,0) inside, max(-u,0) inside}.
+struct MomentWeights {
+    uint32_t w[16][8][3];
+};
+constexpr MomentWeights make_moment_weights() {
+    MomentWeights t{};
+    const int umax[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};
+    for (int av = 0; av < 16; ++av)
+        for (int j = 0; j < 8; ++j) {
+            uint32_t one = 0, pos = 0, neg = 0;
+            for (int b = 0; b < 4; ++b) {
+                const int u = 4 * j + b - 16;
+                const bool in = (u < 0 ? -u : u) <= umax[av];
+                one |= (uint32_t)(in ? 1 : 0) << (8 * b);
+                pos |= (uint32_t)(in && u > 0 ? u : 0) << (8 * b);
+                neg |= (uint32_t)(in && u < 0 ? -u : 0) << (8 * b);
+            }
+            t.w[av][j][0] = one;
+            t.w[av][j][1] = pos;
+            t.w[av][j][2] = neg;
+        }
+    return t;
+}
+__constant__ MomentWeights c_mw = make_moment_weights();
+
 // ---------------------------------------------------------------------------------------------
 // k_resize: level l from level l-1 (canonical ComputePyramid, ORBextractor_old.cc:1342-1344 ->
 // cv::resize INTER_LINEAR).  Horizontal: D = S[sx]*a0 + S[sx1]*a1 (int); vertical: OpenCV's
@@ -410,7 +436,8 @@ __global__ __launch_bounds__(256) void k_orient_desc(BatchArgs a) {
         const uint8_t* center = blr + (long long)y * G.bpitch + x;
         const int8_t* pat = c_pattern.v + sub * 64;
         uint32_t bits = 0;
-#pragma unroll
+        const int pitch = G.bpitch;
+#pragma unroll 4
         for (int b = 0; b < 16; ++b) {
             int t[2];
 #pragma unroll
@@ -418,7 +445,7 @@ __global__ __launch_bounds__(256) void k_orient_desc(BatchArgs a) {
                 const float px = (float)pat[4 * b + 2 * e], py = (float)pat[4 * b + 2 * e + 1];
                 const int ry = cv_round(px * sn + py * ca);
                 const int rx = cv_round(px * ca - py * sn);
-                t[e] = center[(long long)ry * G.bpitch + rx];
+                t[e] = center[ry * pitch + rx];  // |ry|,|rx| <= 18: 32-bit offset
             }
             bits |= (uint32_t)(t[0] < t[1]) << b;
         }
