@@ -131,9 +131,10 @@ int orbgpu_download_matches(orbgpu_ctx* ctx, int pair, int32_t* idx1, int32_t* d
 int orbgpu_descriptor_distance(const uint8_t* a, const uint8_t* b);
 
 /* ---- instrumentation ----------------------------------------------------------------------
- * When enabled, every kernel launch of run_batch/match_stereo_batch is bracketed by HIP events
- * on its stream; orbgpu_stage_times returns the summed milliseconds and launch counts per
- * stage since the last reset.  Stage names via orbgpu_stage_name. */
+ * enable = 1: every kernel launch of run_batch/match_stereo_batch is bracketed by HIP events on
+ * its stream; enable = (1 << 31) | mask: only the stages whose bit is set; 0: off.
+ * orbgpu_stage_times returns the summed milliseconds and launch counts per stage since the last
+ * reset.  Stage names via orbgpu_stage_name. */
 int orbgpu_set_profiling(orbgpu_ctx* ctx, int enable);
 int orbgpu_num_stages(void);
 const char* orbgpu_stage_name(int stage);

@@ -305,8 +305,17 @@ class BatchExtractor:
                                             C.byref(nq)))
         return tuple(o[:nq.value] for o in out)
 
-    def set_profiling(self, on=True):
-        _check(_lib.orbgpu_set_profiling(self.ctx.handle, int(on)))
+    def set_profiling(self, on=True, stages=None):
+        """on: bracket every stage's launches with HIP events; stages: only these stage names."""
+        if stages is not None:
+            names = [_lib.orbgpu_stage_name(i).decode() for i in range(_lib.orbgpu_num_stages())]
+            mask = 0
+            for st in stages:
+                mask |= 1 << names.index(st)
+            arg = C.c_int(((1 << 31) | mask) - (1 << 32))  # two's complement of the flag word
+        else:
+            arg = C.c_int(1 if on else 0)
+        _check(_lib.orbgpu_set_profiling(self.ctx.handle, arg))
 
     def reset_stage_times(self):
         _check(_lib.orbgpu_reset_stage_times(self.ctx.handle))

@@ -38,6 +38,7 @@ struct LevelGeom {
 
 struct BatchArgs {
     int nlevels, nimages;
+    int img0;                        // first image of this launch (sub-batches on parallel streams)
     int ini_th, min_th;
     LevelGeom lv[kMaxLevels];
     uint8_t* lvl_base[kMaxLevels];   // plane base of image 0 (level 0 = the input buffer)
@@ -78,6 +79,7 @@ struct MatchArgs {
     int32_t* idx2;
     int32_t* dist2;           // [pair][out_cap]
     int32_t* nq;              // [pair]
+    int pair0;                // first pair of this launch
 };
 
 // Octree workspace layout for one (image, level) with n_cap keys and node capacity C.  The node

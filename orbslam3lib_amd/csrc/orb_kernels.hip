@@ -77,7 +77,7 @@ __global__ __launch_bounds__(256) void k_resize(BatchArgs a, int l) {
     __shared__ uint32_t win[kRsSrcRows][kRsSrcCols / 4];
     const LevelGeom& G = a.lv[l];
     const LevelGeom& S = a.lv[l - 1];
-    const int img = blockIdx.z;
+    const int img = a.img0 + blockIdx.z;
     const int tx0 = blockIdx.x * kRsTW, ty0 = blockIdx.y * kRsTH;
     const uint8_t* src = a.lvl_base[l - 1] + (long long)img * S.img_stride;
     uint8_t* dst = a.lvl_base[l] + (long long)img * G.img_stride;
@@ -181,7 +181,7 @@ __global__ __launch_bounds__(256) void k_blur(BatchArgs a) {
     constexpr int IW = kBlurTW + 8, IH = kBlurTH + 6, IWD = IW / 4;  // input window, dwords/row
     __shared__ uint32_t tin[IH][IWD];
     __shared__ uint32_t thp[IH][kBlurTW / 2 + 1];  // packed u16 pairs, +1 pad
-    const int img = blockIdx.y;
+    const int img = a.img0 + blockIdx.y;
     int l = 0;
     while (l + 1 < a.nlevels && (int)blockIdx.x >= a.lv[l + 1].tile_first) ++l;
     const LevelGeom& G = a.lv[l];
@@ -270,7 +270,7 @@ __global__ __launch_bounds__(256) void k_fast_cells(BatchArgs a) {
     __shared__ uint16_t list[kCellList];
     __shared__ int32_t wcnt[4];
     __shared__ int scratch[16];
-    const int img = blockIdx.y;
+    const int img = a.img0 + blockIdx.y;
     int l = 0;
     while (l + 1 < a.nlevels && (int)blockIdx.x >= a.lv[l + 1].cell_first) ++l;
     const LevelGeom& G = a.lv[l];
@@ -307,7 +307,7 @@ __global__ __launch_bounds__(512) void k_octree(BatchArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t nodemem_lds[];  // a.oct_lds_bytes
     __shared__ int scratch[16];
     __shared__ OctShared sh;
-    const int img = blockIdx.x, l = blockIdx.y;  // level-major dispatch: the long level-0 groups go first
+    const int img = a.img0 + blockIdx.x, l = blockIdx.y;  // level-major dispatch: the long level-0 groups go first
     const LevelGeom& G = a.lv[l];
     DevPolicy p{scratch};
     const int32_t* cnt = a.cellcnt + (long long)img * a.cellcnt_img_stride + G.cellcnt_off;
@@ -368,7 +368,7 @@ __global__ __launch_bounds__(512) void k_octree(BatchArgs a) {
 // rows for the moments (dword row loads) and 16 of the 256 test pairs (two descriptor bytes),
 // sampled straight from the L2-resident blurred level.
 __global__ __launch_bounds__(256) void k_orient_desc(BatchArgs a) {
-    const int img = blockIdx.y;
+    const int img = a.img0 + blockIdx.y;
     int l = 0;
     while (l + 1 < a.nlevels && (int)blockIdx.x >= a.lv[l + 1].od_first) ++l;
     const LevelGeom& G = a.lv[l];
@@ -467,7 +467,7 @@ struct KP28 {
 
 __global__ __launch_bounds__(256) void k_finalize(BatchArgs a) {
     __shared__ int scratch[16];
-    const int img = blockIdx.x;
+    const int img = a.img0 + blockIdx.x;
     DevPolicy p{scratch};
     int total = 0;
     bool bad = false;
@@ -611,7 +611,7 @@ struct KnnPart {
 
 __global__ __launch_bounds__(256) void k_knn2_pairs(MatchArgs m, KnnPart part) {
     __shared__ uint4 tl[kTrainChunk][2];
-    const int pair = blockIdx.z, split = blockIdx.y;
+    const int pair = m.pair0 + blockIdx.z, split = blockIdx.y;
     const int qimg = 2 * pair, timg = 2 * pair + 1;
     const int qn = m.out_n[qimg], tn = m.out_n[timg];
     const int q0 = m.stereo_only ? m.out_mono[qimg] : 0;
@@ -632,7 +632,7 @@ __global__ __launch_bounds__(256) void k_knn2_pairs(MatchArgs m, KnnPart part) {
 }
 
 __global__ __launch_bounds__(256) void k_knn2_merge(MatchArgs m, KnnPart part) {
-    const int pair = blockIdx.y;
+    const int pair = m.pair0 + blockIdx.y;
     const int qimg = 2 * pair, timg = 2 * pair + 1;
     const int qn = m.out_n[qimg];
     const int q0 = m.stereo_only ? m.out_mono[qimg] : 0;

@@ -84,6 +84,7 @@ struct orbgpu_ctx {
     orbgpu_params prm{};
     int device = 0;
     hipStream_t stream = nullptr;
+    std::vector<hipStream_t> sub;  // sub-batch streams (sub[0] == stream)
     int max_w = 0, max_h = 0, max_images = 0;
     // ORBextractor tables (ORBextractor_old.cc:416-447)
     std::vector<float> scale, inv_scale, sigma2, inv_sigma2;
@@ -99,9 +100,12 @@ struct orbgpu_ctx {
         status, outkps, outdesc, outn, outmono, laps, midx1, mdist1, midx2, mdist2, mnq, scratch,
         octdbg, knnpart;
     int input_images = 0;   // images currently sized for in `input`
+    hipEvent_t fork = nullptr;
+    struct ChunkRec { int img0, n; hipStream_t st; };
+    std::vector<ChunkRec> last_chunks;
     int last_images = 0, last_w = 0, last_h = 0, last_pairs = 0;
-    // profiling
-    bool prof = false;
+    // profiling: bit s of prof_mask brackets stage s launches with HIP events
+    unsigned prof_mask = 0;
     std::vector<Pending> pending;
     std::vector<hipEvent_t> event_pool;
     double stage_ms[ST_COUNT] = {};
@@ -358,7 +362,8 @@ hipEvent_t take_event(orbgpu_ctx* c) {
 template <class F>
 int timed(orbgpu_ctx* c, int stage, hipStream_t s, F&& launch) {
     hipEvent_t a = nullptr, b = nullptr;
-    if (c->prof) {
+    const bool prof = (c->prof_mask >> stage) & 1u;
+    if (prof) {
         a = take_event(c);
         b = take_event(c);
         hipEventRecord(a, s);
@@ -366,7 +371,7 @@ int timed(orbgpu_ctx* c, int stage, hipStream_t s, F&& launch) {
     hipError_t e = launch();
     if (e != hipSuccess)
         return fail(ORBGPU_ERR_HIP, std::string(kStageNames[stage]) + ": " + hipGetErrorString(e));
-    if (c->prof) {
+    if (prof) {
         hipEventRecord(b, s);
         c->pending.push_back({stage, a, b});
     }
@@ -433,6 +438,17 @@ int orbgpu_create(const orbgpu_params* p, int device, int max_width, int max_hei
         delete c;
         return fail(ORBGPU_ERR_HIP, "hipStreamCreate failed");
     }
+    c->sub.push_back(c->stream);
+    {
+        const char* e = getenv("ORBGPU_STREAMS");
+        const int ns = std::max(1, std::min(8, e ? atoi(e) : 4));
+        for (int k = 1; k < ns; ++k) {
+            hipStream_t st;
+            if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) break;
+            c->sub.push_back(st);
+        }
+        if (hipEventCreateWithFlags(&c->fork, hipEventDisableTiming) != hipSuccess) c->fork = nullptr;
+    }
     int r = ensure_input(c, 1, max_width, max_height);
     if (!r) r = set_geometry(c, max_width, max_height);
     if (r) {
@@ -455,6 +471,8 @@ int orbgpu_destroy(orbgpu_ctx* c) {
                       &c->mdist1,  &c->midx2,   &c->mdist2, &c->mnq,     &c->scratch, &c->octdbg,
                       &c->knnpart};
     for (DevBuf* b : bufs) b->release();
+    for (size_t k = 1; k < c->sub.size(); ++k) hipStreamDestroy(c->sub[k]);
+    if (c->fork) hipEventDestroy(c->fork);
     if (c->stream) hipStreamDestroy(c->stream);
     delete c;
     return ORBGPU_OK;
@@ -503,6 +521,7 @@ int orbgpu_run_batch(orbgpu_ctx* c, int n, int w, int h, const int32_t* laps, vo
     }
     BatchArgs A = c->A;
     A.nimages = n;
+    A.img0 = 0;
     A.octdbg = nullptr;
     if (getenv("ORBGPU_OCT_STAMPS")) {  // diagnostic build of the octree phase clocks
         const size_t bytes = (size_t)n * kMaxLevels * 8 * 8;
@@ -513,15 +532,47 @@ int orbgpu_run_batch(orbgpu_ctx* c, int n, int w, int h, const int32_t* laps, vo
     }
     A.lvl_base[0] = c->input.as<uint8_t>();
     A.lv[0].img_stride = (long long)w * h;
+    // Sub-batches (whole stereo pairs) on parallel streams: the stages have complementary
+    // bottlenecks (octree latency, FAST VALU, blur/resize HBM), so their phases overlap.
+    struct Chunk { int img0, n; hipStream_t st; };
+    std::vector<Chunk> chunks;
+    const int K = (!stream && (n % 2) == 0) ? std::min((int)c->sub.size(), n / 2) : 1;
+    // a different sub-batch layout than last time may put an image on another stream: drain first
+    if (!c->last_chunks.empty() && ((int)c->last_chunks.size() != K || c->last_images != n))
+        HIP_TRY(hipDeviceSynchronize());
+    if (K > 1) {
+        HIP_TRY(hipEventRecord(c->fork, s));
+        for (int k = 0; k < K; ++k) {
+            const int p0 = (int)((long long)k * (n / 2) / K), p1 = (int)((long long)(k + 1) * (n / 2) / K);
+            if (p1 > p0) {
+                if (k > 0) HIP_TRY(hipStreamWaitEvent(c->sub[k], c->fork, 0));
+                chunks.push_back({2 * p0, 2 * (p1 - p0), c->sub[k]});
+            }
+        }
+    } else {
+        chunks.push_back({0, n, s});
+    }
+    auto each = [&](int stage, auto launch) -> int {
+        for (const Chunk& ch : chunks) {
+            BatchArgs B = A;
+            B.img0 = ch.img0;
+            B.nimages = ch.n;
+            int rr = timed(c, stage, ch.st, [&] { return launch(B, ch.st); });
+            if (rr) return rr;
+        }
+        return 0;
+    };
     for (int l = 1; l < A.nlevels; ++l) {
-        r = timed(c, ST_RESIZE, s, [&] { return launch_resize(A, l, s); });
+        r = each(ST_RESIZE, [&](const BatchArgs& B, hipStream_t st) { return launch_resize(B, l, st); });
         if (r) return r;
     }
-    if ((r = timed(c, ST_BLUR, s, [&] { return launch_blur(A, s); }))) return r;
-    if ((r = timed(c, ST_FAST, s, [&] { return launch_fast_cells(A, s); }))) return r;
-    if ((r = timed(c, ST_OCTREE, s, [&] { return launch_octree(A, s); }))) return r;
-    if ((r = timed(c, ST_ORIENT, s, [&] { return launch_orient_desc(A, s); }))) return r;
-    if ((r = timed(c, ST_FINAL, s, [&] { return launch_finalize(A, s); }))) return r;
+    if ((r = each(ST_BLUR, [](const BatchArgs& B, hipStream_t st) { return launch_blur(B, st); }))) return r;
+    if ((r = each(ST_FAST, [](const BatchArgs& B, hipStream_t st) { return launch_fast_cells(B, st); }))) return r;
+    if ((r = each(ST_OCTREE, [](const BatchArgs& B, hipStream_t st) { return launch_octree(B, st); }))) return r;
+    if ((r = each(ST_ORIENT, [](const BatchArgs& B, hipStream_t st) { return launch_orient_desc(B, st); }))) return r;
+    if ((r = each(ST_FINAL, [](const BatchArgs& B, hipStream_t st) { return launch_finalize(B, st); }))) return r;
+    c->last_chunks.clear();
+    for (const Chunk& ch : chunks) c->last_chunks.push_back({ch.img0, ch.n, ch.st});
     c->last_images = n;
     c->last_w = w;
     c->last_h = h;
@@ -729,8 +780,23 @@ int orbgpu_match_stereo_batch(orbgpu_ctx* c, int n_pairs, int stereo_only, void*
     if (c->out_cap > 65535) return fail(ORBGPU_ERR_INVALID, "matcher supports < 65536 rows per image");
     if (c->knnpart.ensure(knn2_scratch_bytes(n_pairs, c->out_cap)))
         return fail(ORBGPU_ERR_HIP, "hipMalloc failed (knn scratch)");
-    int r = timed(c, ST_KNN, s, [&] { return launch_knn2_pairs(m, n_pairs, qblocks, c->knnpart.p, s); });
-    if (r) return r;
+    // follow the extraction's sub-batches so each chunk matches right after it is extracted
+    bool chunked = !stream && !c->last_chunks.empty();
+    for (const auto& ch : c->last_chunks) chunked &= (ch.img0 % 2) == 0 && (ch.n % 2) == 0;
+    if (chunked) {
+        for (const auto& ch : c->last_chunks) {
+            const int p0 = ch.img0 / 2, np = std::min(ch.n / 2, n_pairs - p0);
+            if (np <= 0) continue;
+            MatchArgs mm = m;
+            mm.pair0 = p0;
+            int r = timed(c, ST_KNN, ch.st, [&] { return launch_knn2_pairs(mm, np, qblocks, c->knnpart.p, ch.st); });
+            if (r) return r;
+        }
+    } else {
+        m.pair0 = 0;
+        int r = timed(c, ST_KNN, s, [&] { return launch_knn2_pairs(m, n_pairs, qblocks, c->knnpart.p, s); });
+        if (r) return r;
+    }
     c->last_pairs = n_pairs;
     return ORBGPU_OK;
 }
@@ -766,7 +832,8 @@ int orbgpu_descriptor_distance(const uint8_t* a, const uint8_t* b) {
 
 int orbgpu_set_profiling(orbgpu_ctx* c, int enable) {
     if (!c) return fail(ORBGPU_ERR_INVALID, "null ctx");
-    c->prof = enable != 0;
+    // enable: 0 = off, 1 = every stage, otherwise (mask | 1u << 31) selects stages by bit
+    c->prof_mask = enable == 0 ? 0u : enable == 1 ? 0xFFFFFFFFu : ((unsigned)enable & 0x7FFFFFFFu);
     return ORBGPU_OK;
 }
 
