@@ -132,7 +132,9 @@ int orbgpu_descriptor_distance(const uint8_t* a, const uint8_t* b);
 
 /* ---- instrumentation ----------------------------------------------------------------------
  * enable = 1: every kernel launch of run_batch/match_stereo_batch is bracketed by HIP events on
- * its stream; enable = (1 << 31) | mask: only the stages whose bit is set; 0: off.
+ * its stream; enable = (1 << 31) | mask: only the stages whose bit is set; 0: off.  Adding
+ * (1 << 30) also launches every stage once over the whole batch (no sub-batch overlap), so each
+ * launch's duration is that kernel's alone.
  * orbgpu_stage_times returns the summed milliseconds and launch counts per stage since the last
  * reset.  Stage names via orbgpu_stage_name. */
 int orbgpu_set_profiling(orbgpu_ctx* ctx, int enable);

@@ -305,16 +305,20 @@ class BatchExtractor:
                                             C.byref(nq)))
         return tuple(o[:nq.value] for o in out)
 
-    def set_profiling(self, on=True, stages=None):
-        """on: bracket every stage's launches with HIP events; stages: only these stage names."""
-        if stages is not None:
-            names = [_lib.orbgpu_stage_name(i).decode() for i in range(_lib.orbgpu_num_stages())]
-            mask = 0
-            for st in stages:
-                mask |= 1 << names.index(st)
-            arg = C.c_int(((1 << 31) | mask) - (1 << 32))  # two's complement of the flag word
+    def set_profiling(self, on=True, stages=None, serialize=False):
+        """on: bracket every stage's launches with HIP events; stages: only these stage names;
+        serialize: launch each stage once over the whole batch (clean per-kernel durations)."""
+        names = [_lib.orbgpu_stage_name(i).decode() for i in range(_lib.orbgpu_num_stages())]
+        if not on:
+            arg = C.c_int(0)
+        elif stages is None and not serialize:
+            arg = C.c_int(1)
         else:
-            arg = C.c_int(1 if on else 0)
+            mask = 0
+            for st in (names if stages is None else stages):
+                mask |= 1 << names.index(st)
+            word = (1 << 31) | (1 << 30 if serialize else 0) | mask
+            arg = C.c_int(word - (1 << 32))  # the flag word as a signed int
         _check(_lib.orbgpu_set_profiling(self.ctx.handle, arg))
 
     def reset_stage_times(self):

@@ -5,12 +5,14 @@
 // sees only this cell's corners, iniThFAST first and minThFAST if the cell kept nothing, keys
 // emitted in row-major order relative to (minBorderX, minBorderY).
 //
-// Layout: the ROI (<= 76 x 78 bytes) is staged in LDS; "lanes" own columns and "row groups"
-// own rows (no integer division anywhere).  m = exact FAST strength (orb_math.h) is computed for
-// pixels passing the compass pre-test at t_low = min(ini, min), 0 elsewhere (exact for every
-// t >= t_low).  Keys are compacted per row (a 64-bit keep mask per row and its popcount), then
-// one scan over <= 70 row counts gives every row's output offset.  Policy-templated like
-// orb_octree.h so the host harness runs the same code on the CPU.
+// Layout: the ROI (<= 76 x 78 bytes) is staged in LDS (pitch kCellMax).  Each wave owns one
+// contiguous row-major range of detection pixels and keeps a private candidate list, so the
+// wave lists concatenated in wave order are row-major and ordered output needs only a prefix
+// over waves.  Per threshold t: (1) compass pre-test on 64 pixels at a time, evaluated as lane
+// masks (eight compares, the rest is scalar mask logic), compacted into the wave list;
+// (2) the exact segment test on the compacted list (both polarities in one word per ring
+// point, 9-arcs by OR-of-3 trees); (3) exact strength m (orb_math.h) for the corners.
+// Policy-templated like orb_octree.h so the host harness runs the same code on the CPU.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -43,35 +45,26 @@ __host__ __device__ inline bool fast_kept(const uint8_t* M, int off, int t) {
     return true;
 }
 
-__host__ __device__ inline bool fast_compass(const uint8_t* c, int t) {
-    const int v = c[0];
-    const int p0 = c[3 * kCellMax], p4 = c[3], p8 = c[-3 * kCellMax], p12 = c[-3];
-    const int dm = ((v - p0 > t) << 0) | ((v - p4 > t) << 1) | ((v - p8 > t) << 2) | ((v - p12 > t) << 3);
-    const int bm = ((p0 - v > t) << 0) | ((p4 - v > t) << 1) | ((p8 - v > t) << 2) | ((p12 - v > t) << 3);
-    const int dr = ((dm << 1) | (dm >> 3)) & 15, br = ((bm << 1) | (bm >> 3)) & 15;
-    return (dm & dr) || (bm & br);
-}
-
-__host__ __device__ inline bool arc9(uint32_t mask16) {
-    const uint32_t m = mask16 | (mask16 << 16);
-    uint32_t a = m & (m >> 1);
-    a &= a >> 2;
-    a &= a >> 4;  // 8 consecutive from each bit
-    a &= m >> 8;  // 9 consecutive
-    return (a & 0xFFFFu) != 0;
-}
-
 // cv::FAST segment test at threshold t (strict > / <), exact.
+// Per ring point one word q = C1 - 65535 p: low half p + t + 512 - v, high half v + t + 512 - p,
+// both in [257, 1022], so bit 9 clear <=> v - p > t (dark) and bit 25 clear <=> p - v > t
+// (bright).  A 9-arc of events exists iff some OR over 9 consecutive q has the bit clear.
 __host__ __device__ inline bool fast_corner(const uint8_t* c, int t) {
     const int v = c[0];
-    uint32_t dm = 0, bm = 0;
+    const int C1 = (t + 512 - v) + ((v + t + 512) << 16);
+    uint32_t q[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
         const int p = c[ring_dx(k) + ring_dy(k) * kCellMax];
-        dm |= (uint32_t)(v - p > t) << k;
-        bm |= (uint32_t)(p - v > t) << k;
+        q[k] = (uint32_t)(C1 + p * -65535);
     }
-    return arc9(dm) || arc9(bm);
+    uint32_t o3[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) o3[k] = q[k] | q[(k + 1) & 15] | q[(k + 2) & 15];
+    uint32_t r = 0xFFFFFFFFu;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) r &= o3[k] | o3[(k + 3) & 15] | o3[(k + 6) & 15];
+    return (~r & 0x02000200u) != 0;
 }
 
 // Per-cell scratch (LDS on the GPU).
@@ -123,7 +116,7 @@ __host__ __device__ int fast_cell_run(P& p, const uint8_t* src, long long pitch,
     const int tmin = min_th < 0 ? 0 : (min_th > 255 ? 255 : min_th);
     const int W = p.nwaves(), w = p.wave(), L = p.wave_width(), lane = p.lane();
     const uint64_t lt = p.lanemask_lt();
-    const int i0 = (int)((long long)w * nd / W), i1 = (int)((long long)(w + 1) * nd / W);
+    const int i0 = w * nd / W, i1 = (w + 1) * nd / W;  // nd <= 4900, W <= 16: no overflow
     uint16_t* list = cs.list + i0;
     const float inv_dc = dc > 0 ? 1.f / (float)dc : 0.f;
     auto off_of = [&](int i) {
@@ -134,11 +127,20 @@ __host__ __device__ int fast_cell_run(P& p, const uint8_t* src, long long pitch,
     auto build = [&](int t) {
         int na = 0;
         for (int base = i0; base < i1; base += L) {
-            const int i = base + lane;
-            const int o = i < i1 ? off_of(i) : 0;
-            const bool f = i < i1 && fast_compass(&T[o], t);
-            const uint64_t m = p.ballot(f);
-            if (f) list[na + p.popc64(m & lt)] = (uint16_t)o;
+            const int i = base + lane < i1 ? base + lane : i1 - 1;  // tail lanes recompute i1-1
+            const int o = off_of(i);
+            const uint8_t* c = &T[o];
+            const int v = c[0], lo = v - t, hi = v + t;
+            const int p0 = c[3 * kCellMax], p4 = c[3], p8 = c[-3 * kCellMax], p12 = c[-3];
+            // compass pre-test as lane masks: two cyclically adjacent of {0,4,8,12} beyond t
+            const uint64_t d0 = p.ballot(p0 < lo), d1 = p.ballot(p4 < lo);
+            const uint64_t d2 = p.ballot(p8 < lo), d3 = p.ballot(p12 < lo);
+            const uint64_t b0 = p.ballot(p0 > hi), b1 = p.ballot(p4 > hi);
+            const uint64_t b2 = p.ballot(p8 > hi), b3 = p.ballot(p12 > hi);
+            const int left = i1 - base;
+            const uint64_t valid = left >= 64 ? ~0ull : ((1ull << left) - 1ull);
+            const uint64_t m = (((d0 | d2) & (d1 | d3)) | ((b0 | b2) & (b1 | b3))) & valid;
+            if ((m >> lane) & 1ull) list[na + p.popc64(m & lt)] = (uint16_t)o;
             na += p.popc64(m);
         }
         int nb = 0;
@@ -152,15 +154,19 @@ __host__ __device__ int fast_cell_run(P& p, const uint8_t* src, long long pitch,
         }
         for (int j = lane; j < nb; j += L) {
             const int o = list[j];
-            M[o] = (uint8_t)fast_strength(&T[o], kCellMax, -1);
+            M[o] = (uint8_t)fast_strength_corner(&T[o], kCellMax);
         }
         return nb;
     };
+    // nonmax at t for every corner of the list; the verdict is kept in bit 15 of the entry
+    // (LDS offsets < 6400 use 13 bits) for the ordered write
     auto count_kept = [&](int nb, int t) {
         int c = 0;
         for (int base = 0; base < nb; base += L) {
             const int j = base + lane;
-            const bool k = j < nb && fast_kept(M, list[j], t);
+            const int o = j < nb ? (list[j] & 0x1FFF) : 0;
+            const bool k = j < nb && fast_kept(M, o, t);
+            if (j < nb) list[j] = (uint16_t)(o | (k ? 0x8000 : 0));
             c += p.popc64(p.ballot(k));
         }
         if (lane == 0) cs.wcnt[w] = c;
@@ -188,10 +194,11 @@ __host__ __device__ int fast_cell_run(P& p, const uint8_t* src, long long pitch,
     int run = 0;
     for (int base = 0; base < nb; base += L) {
         const int j = base + lane;
-        const int o = j < nb ? list[j] : 0;
-        const bool k = j < nb && fast_kept(M, o, t);
+        const int e = j < nb ? list[j] : 0;
+        const bool k = (e & 0x8000) != 0;
         const uint64_t m = p.ballot(k);
         if (k) {
+            const int o = e & 0x1FFF;
             const int r = o / kCellMax, c = o % kCellMax - sh;
             const int resp = M[o] - 1;  // cornerScore<16> = m - 1
             keys_out[cb.y + run + p.popc64(m & lt)] =

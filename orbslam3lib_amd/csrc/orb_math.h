@@ -55,20 +55,12 @@ __host__ __device__ inline int ring_dy(int k) {
 //                 region: m(q) <= t || m(p) > m(q).
 // When the 4-compass pre-test at t_min fails, S_max <= t_min and 0 is stored instead (exact
 // for every t >= t_min).  Reference call sites: cv::FAST at ORBextractor_old.cc:828,847.
-__host__ __device__ inline int fast_strength(const uint8_t* c, int stride, int t_min) {
+// Exact strength of a pixel already known to be a corner at some t >= 0 (no pre-test).
+__host__ __device__ inline int fast_strength_corner(const uint8_t* c, int stride) {
     const int v = c[0];
     int d[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) d[k] = v - (int)c[ring_dx(k) + ring_dy(k) * stride];
-    // compass pre-test: any 9-arc holds two cyclically adjacent points of {0,4,8,12}
-    int dm = 0, bm = 0;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        dm |= (d[4 * q] > t_min) << q;
-        bm |= (-d[4 * q] > t_min) << q;
-    }
-    const int dr = ((dm << 1) | (dm >> 3)) & 15, br = ((bm << 1) | (bm >> 3)) & 15;
-    if (!(dm & dr) && !(bm & br)) return 0;
     int a2[16], b2[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
@@ -97,6 +89,21 @@ __host__ __device__ inline int fast_strength(const uint8_t* c, int stride, int t
     int s = sdark > -bmin ? sdark : -bmin;
     s = s < 0 ? 0 : s;
     return s > 255 ? 255 : s;
+}
+
+__host__ __device__ inline int fast_strength(const uint8_t* c, int stride, int t_min) {
+    const int v = c[0];
+    // compass pre-test: any 9-arc holds two cyclically adjacent points of {0,4,8,12}
+    int dm = 0, bm = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int d = v - (int)c[ring_dx(4 * q) + ring_dy(4 * q) * stride];
+        dm |= (d > t_min) << q;
+        bm |= (-d > t_min) << q;
+    }
+    const int dr = ((dm << 1) | (dm >> 3)) & 15, br = ((bm << 1) | (bm >> 3)) & 15;
+    if (!(dm & dr) && !(bm & br)) return 0;
+    return fast_strength_corner(c, stride);
 }
 
 }  // namespace orbgpu

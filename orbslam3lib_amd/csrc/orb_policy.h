@@ -20,7 +20,9 @@ struct DevPolicy {
     __device__ unsigned long long now() const { return wall_clock64(); }  // 100 MHz
     __device__ int popc64(uint64_t x) const { return __popcll(x); }
     __device__ int lane() const { return (int)(threadIdx.x & 63); }
-    __device__ int wave() const { return (int)(threadIdx.x >> 6); }
+    // wave-uniform by construction; readfirstlane lets the compiler keep it (and every loop
+    // bound derived from it) in SGPRs
+    __device__ int wave() const { return __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)); }
     __device__ int nwaves() const { return (int)(blockDim.x >> 6); }
     __device__ int wave_width() const { return 64; }
     __device__ uint64_t ballot(bool f) const { return __ballot(f); }

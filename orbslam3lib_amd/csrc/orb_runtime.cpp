@@ -101,6 +101,11 @@ struct orbgpu_ctx {
         octdbg, knnpart;
     int input_images = 0;   // images currently sized for in `input`
     hipEvent_t fork = nullptr;
+    std::vector<hipEvent_t> join;  // one per sub stream
+    // stages launched once over the whole batch on the main stream (join before, fork after):
+    // the dominant kernel runs alone, so its per-launch duration is its own
+    unsigned isolate_mask = 1u << ST_FAST;
+    bool serialize = false;  // profiling: every stage isolated
     struct ChunkRec { int img0, n; hipStream_t st; };
     std::vector<ChunkRec> last_chunks;
     int last_images = 0, last_w = 0, last_h = 0, last_pairs = 0;
@@ -447,7 +452,18 @@ int orbgpu_create(const orbgpu_params* p, int device, int max_width, int max_hei
             if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) break;
             c->sub.push_back(st);
         }
-        if (hipEventCreateWithFlags(&c->fork, hipEventDisableTiming) != hipSuccess) c->fork = nullptr;
+        bool ok = hipEventCreateWithFlags(&c->fork, hipEventDisableTiming) == hipSuccess;
+        for (size_t k = 0; ok && k < c->sub.size(); ++k) {
+            hipEvent_t ev;
+            ok = hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess;
+            if (ok) c->join.push_back(ev);
+        }
+        if (!ok) {
+            orbgpu_destroy(c);
+            return fail(ORBGPU_ERR_HIP, "hipEventCreate failed");
+        }
+        const char* iso = getenv("ORBGPU_ISOLATE");  // stage bit mask (diagnostics)
+        if (iso) c->isolate_mask = (unsigned)strtoul(iso, nullptr, 0);
     }
     int r = ensure_input(c, 1, max_width, max_height);
     if (!r) r = set_geometry(c, max_width, max_height);
@@ -473,6 +489,7 @@ int orbgpu_destroy(orbgpu_ctx* c) {
     for (DevBuf* b : bufs) b->release();
     for (size_t k = 1; k < c->sub.size(); ++k) hipStreamDestroy(c->sub[k]);
     if (c->fork) hipEventDestroy(c->fork);
+    for (auto e : c->join) hipEventDestroy(e);
     if (c->stream) hipStreamDestroy(c->stream);
     delete c;
     return ORBGPU_OK;
@@ -553,6 +570,18 @@ int orbgpu_run_batch(orbgpu_ctx* c, int n, int w, int h, const int32_t* laps, vo
         chunks.push_back({0, n, s});
     }
     auto each = [&](int stage, auto launch) -> int {
+        if (chunks.size() > 1 && (c->serialize || ((c->isolate_mask >> stage) & 1u))) {
+            for (size_t k = 1; k < chunks.size(); ++k) {
+                HIP_TRY(hipEventRecord(c->join[k], chunks[k].st));
+                HIP_TRY(hipStreamWaitEvent(chunks[0].st, c->join[k], 0));
+            }
+            BatchArgs B = A;  // whole batch
+            int rr = timed(c, stage, chunks[0].st, [&] { return launch(B, chunks[0].st); });
+            if (rr) return rr;
+            HIP_TRY(hipEventRecord(c->fork, chunks[0].st));
+            for (size_t k = 1; k < chunks.size(); ++k) HIP_TRY(hipStreamWaitEvent(chunks[k].st, c->fork, 0));
+            return 0;
+        }
         for (const Chunk& ch : chunks) {
             BatchArgs B = A;
             B.img0 = ch.img0;
@@ -783,7 +812,20 @@ int orbgpu_match_stereo_batch(orbgpu_ctx* c, int n_pairs, int stereo_only, void*
     // follow the extraction's sub-batches so each chunk matches right after it is extracted
     bool chunked = !stream && !c->last_chunks.empty();
     for (const auto& ch : c->last_chunks) chunked &= (ch.img0 % 2) == 0 && (ch.n % 2) == 0;
-    if (chunked) {
+    if (chunked && c->last_chunks.size() > 1 &&
+        (c->serialize || ((c->isolate_mask >> ST_KNN) & 1u))) {  // one launch over all pairs
+        hipStream_t s0 = c->last_chunks[0].st;
+        for (size_t k = 1; k < c->last_chunks.size(); ++k) {
+            HIP_TRY(hipEventRecord(c->join[k], c->last_chunks[k].st));
+            HIP_TRY(hipStreamWaitEvent(s0, c->join[k], 0));
+        }
+        m.pair0 = 0;
+        int r = timed(c, ST_KNN, s0, [&] { return launch_knn2_pairs(m, n_pairs, qblocks, c->knnpart.p, s0); });
+        if (r) return r;
+        HIP_TRY(hipEventRecord(c->fork, s0));
+        for (size_t k = 1; k < c->last_chunks.size(); ++k)
+            HIP_TRY(hipStreamWaitEvent(c->last_chunks[k].st, c->fork, 0));
+    } else if (chunked) {
         for (const auto& ch : c->last_chunks) {
             const int p0 = ch.img0 / 2, np = std::min(ch.n / 2, n_pairs - p0);
             if (np <= 0) continue;
@@ -832,8 +874,11 @@ int orbgpu_descriptor_distance(const uint8_t* a, const uint8_t* b) {
 
 int orbgpu_set_profiling(orbgpu_ctx* c, int enable) {
     if (!c) return fail(ORBGPU_ERR_INVALID, "null ctx");
-    // enable: 0 = off, 1 = every stage, otherwise (mask | 1u << 31) selects stages by bit
-    c->prof_mask = enable == 0 ? 0u : enable == 1 ? 0xFFFFFFFFu : ((unsigned)enable & 0x7FFFFFFFu);
+    // enable: 0 = off, 1 = every stage, otherwise (1u << 31) | [1u << 30] | stage mask: the
+    // selected stages; bit 30 also runs every stage as one whole-batch launch (serial timing)
+    const unsigned e = (unsigned)enable;
+    c->prof_mask = e == 0 ? 0u : e == 1 ? 0xFFFFFFFFu : (e & 0x3FFFFFFFu);
+    c->serialize = e != 0 && e != 1 && (e & (1u << 30));
     return ORBGPU_OK;
 }
 
