@@ -5,10 +5,11 @@
 // sees only this cell's corners, iniThFAST first and minThFAST if the cell kept nothing, keys
 // emitted in row-major order relative to (minBorderX, minBorderY).
 //
-// Layout: the ROI (<= 76 x 78 bytes) is staged in LDS (pitch kCellMax).  Each wave owns one
-// contiguous row-major range of detection pixels and keeps a private candidate list, so the
-// wave lists concatenated in wave order are row-major and ordered output needs only a prefix
-// over waves.  Per threshold t: (1) compass pre-test on 64 pixels at a time, evaluated as lane
+// Layout: the ROI is staged in LDS with a compile-time pitch P (48 when every level's cells fit,
+// kCellMax = 80 otherwise).  On the GPU one wave runs one cell (no workgroup barriers); the
+// code also accepts several waves per cell: each wave owns one contiguous row-major range of
+// detection pixels and keeps a private candidate list, so the wave lists concatenated in wave
+// order are row-major and ordered output needs only a prefix over waves.  Per threshold t: (1) compass pre-test on 64 pixels at a time, evaluated as lane
 // masks (eight compares, the rest is scalar mask logic), compacted into the wave list;
 // (2) the exact segment test on the compacted list (both polarities in one word per ring
 // point, 9-arcs by OR-of-3 trees); (3) exact strength m (orb_math.h) for the corners.
@@ -23,6 +24,11 @@
 namespace orbgpu {
 
 constexpr int kCellMax = 80;  // wCell, hCell < 70 (nCols = floor(W/35)) plus the 6-px overlap
+constexpr int kCellPitchSmall = 48;  // every 640x480-class level: cells <= 39 x 42
+// candidate list capacity for pitch P: the detection area, (P-6)^2 for the 48-byte tile, 69^2
+// for the general one (wCell, hCell <= 69: nCols = floor(W/35) >= 1)
+template <int P>
+constexpr int cell_list_cap() { return P == kCellMax ? 69 * 69 : (P - 6) * (P - 6); }
 
 struct CellGeom {
     int iniX, iniY;   // cell ROI origin in level coordinates
@@ -30,13 +36,13 @@ struct CellGeom {
     int minBorder;
 };
 
-// M holds m for pixels passing the pre-test, 0 elsewhere (pitch kCellMax).
+// M holds m for corners, 0 elsewhere (pitch P).
+template <int P>
 __host__ __device__ inline bool fast_kept(const uint8_t* M, int off, int t) {
     const uint8_t* m = &M[off];
     const int v = m[0];
     if (v <= t || v < 2) return false;
-    const int nb[8] = {-kCellMax - 1, -kCellMax, -kCellMax + 1, -1, 1,
-                       kCellMax - 1,  kCellMax,  kCellMax + 1};
+    const int nb[8] = {-P - 1, -P, -P + 1, -1, 1, P - 1, P, P + 1};
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
         const int q = m[nb[k]];
@@ -49,13 +55,14 @@ __host__ __device__ inline bool fast_kept(const uint8_t* M, int off, int t) {
 // Per ring point one word q = C1 - 65535 p: low half p + t + 512 - v, high half v + t + 512 - p,
 // both in [257, 1022], so bit 9 clear <=> v - p > t (dark) and bit 25 clear <=> p - v > t
 // (bright).  A 9-arc of events exists iff some OR over 9 consecutive q has the bit clear.
+template <int P>
 __host__ __device__ inline bool fast_corner(const uint8_t* c, int t) {
     const int v = c[0];
     const int C1 = (t + 512 - v) + ((v + t + 512) << 16);
     uint32_t q[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
-        const int p = c[ring_dx(k) + ring_dy(k) * kCellMax];
+        const int p = c[ring_dx(k) + ring_dy(k) * P];
         q[k] = (uint32_t)(C1 + p * -65535);
     }
     uint32_t o3[16];
@@ -69,25 +76,23 @@ __host__ __device__ inline bool fast_corner(const uint8_t* c, int t) {
 
 // Per-cell scratch (LDS on the GPU).
 struct CellScratch {
-    uint8_t* T;        // [kCellMax * kCellMax], 4-byte aligned
-    uint8_t* M;        // [kCellMax * kCellMax], 4-byte aligned
-    uint16_t* list;    // [kCellList] wave-private candidate lists (LDS offsets into T/M)
+    uint8_t* T;        // [P * P], 4-byte aligned
+    uint8_t* M;        // [P * P], 4-byte aligned
+    uint16_t* list;    // [cell_list_cap<P>()] wave-private candidate lists (offsets into T/M)
     int32_t* wcnt;     // [waves]
 };
 
-constexpr int kCellList = 4900;  // >= detection pixels of a cell (<= 69 x 69)
-
 // The detection pixels are split into one contiguous row-major range per wave, so the wave
 // lists concatenated in wave order are row-major: ordered output needs only a prefix over waves.
-template <class P>
-__host__ __device__ int fast_cell_run(P& p, const uint8_t* src, long long pitch, int sh,
+template <int CP, class Pol>
+__host__ __device__ int fast_cell_run(Pol& p, const uint8_t* src, long long pitch, int sh,
                                       bool dword_ok, const CellGeom& g, int ini_th, int min_th,
                                       const CellScratch& cs, uint32_t* keys_out) {
     const int tid = p.tid(), NT = p.nthreads();
     const int rows = g.rows, cols = g.cols;
     uint8_t* T = cs.T;
     uint8_t* M = cs.M;
-    constexpr int RW = kCellMax / 4;  // dwords per LDS row (constant divisors only)
+    constexpr int RW = CP / 4;  // dwords per LDS row (constant divisors only)
     if (dword_ok) {
         const int ndw = (sh + cols + 3) >> 2;
         uint32_t* T32 = reinterpret_cast<uint32_t*>(T);
@@ -100,11 +105,11 @@ __host__ __device__ int fast_cell_run(P& p, const uint8_t* src, long long pitch,
             }
         }
     } else {
-        for (int i = tid; i < rows * kCellMax; i += NT) {
-            const int r = i / kCellMax, c = i % kCellMax;
+        for (int i = tid; i < rows * CP; i += NT) {
+            const int r = i / CP, c = i % CP;
             if (c < cols) {
-                T[r * kCellMax + c + sh] = src[(long long)r * pitch + c];
-                M[r * kCellMax + c + sh] = 0;
+                T[r * CP + c + sh] = src[(long long)r * pitch + c];
+                M[r * CP + c + sh] = 0;
             }
         }
     }
@@ -121,7 +126,7 @@ __host__ __device__ int fast_cell_run(P& p, const uint8_t* src, long long pitch,
     const float inv_dc = dc > 0 ? 1.f / (float)dc : 0.f;
     auto off_of = [&](int i) {
         const int r = (int)(((float)i + 0.5f) * inv_dc);  // exact: i < 4900, dc < 70
-        return (3 + r) * kCellMax + 3 + sh + (i - r * dc);
+        return (3 + r) * CP + 3 + sh + (i - r * dc);
     };
     // candidates -> corners at t -> exact strength; returns this wave's corner count
     auto build = [&](int t) {
@@ -131,7 +136,7 @@ __host__ __device__ int fast_cell_run(P& p, const uint8_t* src, long long pitch,
             const int o = off_of(i);
             const uint8_t* c = &T[o];
             const int v = c[0], lo = v - t, hi = v + t;
-            const int p0 = c[3 * kCellMax], p4 = c[3], p8 = c[-3 * kCellMax], p12 = c[-3];
+            const int p0 = c[3 * CP], p4 = c[3], p8 = c[-3 * CP], p12 = c[-3];
             // compass pre-test as lane masks: two cyclically adjacent of {0,4,8,12} beyond t
             const uint64_t d0 = p.ballot(p0 < lo), d1 = p.ballot(p4 < lo);
             const uint64_t d2 = p.ballot(p8 < lo), d3 = p.ballot(p12 < lo);
@@ -147,14 +152,14 @@ __host__ __device__ int fast_cell_run(P& p, const uint8_t* src, long long pitch,
         for (int base = 0; base < na; base += L) {
             const int j = base + lane;
             const int o = j < na ? list[j] : 0;
-            const bool f = j < na && fast_corner(&T[o], t);
+            const bool f = j < na && fast_corner<CP>(&T[o], t);
             const uint64_t m = p.ballot(f);
             if (f) list[nb + p.popc64(m & lt)] = (uint16_t)o;  // in place: never passes the reads
             nb += p.popc64(m);
         }
         for (int j = lane; j < nb; j += L) {
             const int o = list[j];
-            M[o] = (uint8_t)fast_strength_corner(&T[o], kCellMax);
+            M[o] = (uint8_t)fast_strength_corner(&T[o], CP);
         }
         return nb;
     };
@@ -165,7 +170,7 @@ __host__ __device__ int fast_cell_run(P& p, const uint8_t* src, long long pitch,
         for (int base = 0; base < nb; base += L) {
             const int j = base + lane;
             const int o = j < nb ? (list[j] & 0x1FFF) : 0;
-            const bool k = j < nb && fast_kept(M, o, t);
+            const bool k = j < nb && fast_kept<CP>(M, o, t);
             if (j < nb) list[j] = (uint16_t)(o | (k ? 0x8000 : 0));
             c += p.popc64(p.ballot(k));
         }
@@ -199,7 +204,7 @@ __host__ __device__ int fast_cell_run(P& p, const uint8_t* src, long long pitch,
         const uint64_t m = p.ballot(k);
         if (k) {
             const int o = e & 0x1FFF;
-            const int r = o / kCellMax, c = o % kCellMax - sh;
+            const int r = o / CP, c = o % CP - sh;
             const int resp = M[o] - 1;  // cornerScore<16> = m - 1
             keys_out[cb.y + run + p.popc64(m & lt)] =
                 make_key(g.iniX + c - g.minBorder, g.iniY + r - g.minBorder, resp);

@@ -30,7 +30,7 @@ struct LevelGeom {
     long long oct_off;         // byte offset of this level's octree workspace in an image
     float scale;               // mvScaleFactor[level]
     int patch;                 // (int)(PATCH_SIZE * scale) (:882)
-    int tiles_x, tiles_y, tile_first;  // blur tiling (128 x 16)
+    int tiles_x, tiles_y, tile_first;  // blur tiling (128 x 32)
     int xtab_off, ytab_off, simd_end;  // resize tables (levels >= 1)
     int area2;                 // exact 2x downscale: OpenCV switches to INTER_AREA (2x2 mean)
     int od_blocks, od_first;   // orientation/descriptor blocks for this level
@@ -63,6 +63,7 @@ struct BatchArgs {
     int32_t* out_mono;               // [img]
     const int32_t* laps;             // [img][2]
     int total_cells, total_tiles, total_od_blocks;
+    int fast_split;  // levels [0, fast_split) run the 48-byte FAST tile, the rest the 80-byte one
     unsigned long long* octdbg;      // diagnostic: [img][kMaxLevels][8] phase clocks, or null
     int oct_lds_nodes;               // node capacity of k_octree's dynamic LDS (0: all global)
     int oct_lds_bytes;

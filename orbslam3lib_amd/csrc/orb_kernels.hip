@@ -166,21 +166,29 @@ __global__ __launch_bounds__(256) void k_resize(BatchArgs a, int l) {
 // ---------------------------------------------------------------------------------------------
 // k_blur: cv::GaussianBlur(Size(7,7), 2, 2, BORDER_REFLECT_101) on each level
 // (ORBextractor_old.cc:1146-1147), bit-exact fixed point: kernel {18,34,48,56,48,34,18}/256,
-// horizontal sums exact in u16, vertical (sum + 2^15) >> 16.  Tile 128 x 16, LDS staged.
+// out = (sum_v w_v sum_h w_h p + 2^15) >> 16 with the horizontal sums exact (<= 65280, u16).
 __device__ inline int refl101(int p, int n) {
     p = p < 0 ? -p : p;
     return p >= n ? 2 * n - p - 2 : p;
 }
 
-// Tile 128 x 32 outputs.  The (32+6) x (128+8) input window is staged in LDS with dword loads
-// (byte loads + reflection only where a dword leaves the plane); the horizontal pass writes
-// 4 adjacent u16 sums per thread-step, the vertical pass 4 columns x 4 rows per thread.
+// Tile 128 x 32 outputs; the input window is rows ty0-4 .. ty0+35 (one spare row each side so
+// rows pair up) x cols tx0-16 .. tx0+143, staged in LDS with 16-byte loads.
+// Horizontal pass in "row-pair" u16x2 lanes: lane lo = row 2rp, lane hi = row 2rp+1 of the
+// same column (v_perm builds them from two row dwords), 7 taps by v_pk_add/v_pk_mad_u16.
+// Vertical pass: each output row is 4 v_dot2_u32_u16 over row pairs with weight pairs
+// {0,18}{34,48}{56,48}{34,18} (even rows) or {18,34}{48,56}{48,34}{18,0} (odd rows), the
+// accumulator seeded with the 2^15 rounding term.
 constexpr int kBlurTW = 128, kBlurTH = 32;
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+__device__ inline u16x2 as_u16x2(uint32_t x) { return __builtin_bit_cast(u16x2, x); }
+__device__ inline uint32_t as_u32(u16x2 x) { return __builtin_bit_cast(uint32_t, x); }
 
 __global__ __launch_bounds__(256) void k_blur(BatchArgs a) {
-    constexpr int IW = kBlurTW + 8, IH = kBlurTH + 6, IWD = IW / 4;  // input window, dwords/row
-    __shared__ uint32_t tin[IH][IWD];
-    __shared__ uint32_t thp[IH][kBlurTW / 2 + 1];  // packed u16 pairs, +1 pad
+    constexpr int IW = kBlurTW + 32, IH = kBlurTH + 8, IWQ = IW / 16, NRP = IH / 2;
+    __shared__ uint4 tin4[IH][IWQ];
+    __shared__ uint4 hp[NRP][kBlurTW / 4];  // [row pair][column quad]: 4 columns x (row0,row1)
     const int img = a.img0 + blockIdx.y;
     int l = 0;
     while (l + 1 < a.nlevels && (int)blockIdx.x >= a.lv[l + 1].tile_first) ++l;
@@ -189,73 +197,98 @@ __global__ __launch_bounds__(256) void k_blur(BatchArgs a) {
     const int ty0 = (t / G.tiles_x) * kBlurTH, tx0 = (t % G.tiles_x) * kBlurTW;
     const uint8_t* src = a.lvl_base[l] + (long long)img * G.img_stride;
     uint8_t* dst = a.blur_base[l] + (long long)img * G.bimg_stride;
-    const bool dw_ok = (G.pitch & 3) == 0;
-    for (int i = threadIdx.x; i < IH * IWD; i += 256) {
-        const int r = i / IWD, cd = i % IWD;
-        const int y = refl101(ty0 + r - 3, G.h);
-        const int x = tx0 - 4 + 4 * cd;
+    const bool vec_ok = (G.pitch & 15) == 0;
+    for (int i = threadIdx.x; i < IH * IWQ; i += 256) {
+        const int r = i / IWQ, cq = i - r * IWQ;
+        // rows beyond the reflected range feed only zero weights or unwritten outputs: clamp
+        const int y = min(max(refl101(ty0 + r - 4, G.h), 0), G.h - 1);
+        const int x = tx0 - 16 + 16 * cq;
         const uint8_t* row = src + (long long)y * G.pitch;
-        uint32_t v;
-        if (dw_ok && x >= 0 && x + 4 <= G.w) {
-            v = *reinterpret_cast<const uint32_t*>(row + x);
-        } else {
-            v = 0;
+        uint4 v;
+        if (vec_ok && x >= 0 && x + 16 <= G.w) {
+            v = *reinterpret_cast<const uint4*>(row + x);
+        } else {  // plane edge: per byte with reflection
+            uint32_t w4[4];
 #pragma unroll
-            for (int b = 0; b < 4; ++b) {
-                const int xx = x + b;
-                const uint32_t px = (xx < G.w + 3) ? row[refl101(xx, G.w)] : 0u;
-                v |= px << (8 * b);
+            for (int d = 0; d < 4; ++d) {
+                uint32_t u = 0;
+#pragma unroll
+                for (int b = 0; b < 4; ++b) {
+                    const int xx = x + 4 * d + b;
+                    const uint32_t px = (xx > -G.w && xx < G.w + 3) ? row[min(max(refl101(xx, G.w), 0), G.w - 1)] : 0u;
+                    u |= px << (8 * b);
+                }
+                w4[d] = u;
             }
+            v = make_uint4(w4[0], w4[1], w4[2], w4[3]);
         }
-        tin[r][cd] = v;
+        tin4[r][cq] = v;
     }
+    const uint32_t(*tin)[IW / 4] = reinterpret_cast<const uint32_t(*)[IW / 4]>(&tin4[0][0]);
     __syncthreads();
-    // horizontal: output cols c..c+3 (c = 4*cq) need window bytes c+1 .. c+10
-    const uint32_t k0 = 18, k1 = 34, k2 = 48, k3 = 56;
-    for (int i = threadIdx.x; i < IH * (kBlurTW / 4); i += 256) {
-        const int r = i / (kBlurTW / 4), cq = i % (kBlurTW / 4);
-        const uint32_t w0 = tin[r][cq], w1 = tin[r][cq + 1], w2 = tin[r][cq + 2];
-        uint32_t p[12];
+    // horizontal: item (row pair rp, column quad cq) -> output cols 4cq..4cq+3 need window
+    // bytes 4cq+13 .. 4cq+22 (dwords cq+3 .. cq+5)
+    for (int i = threadIdx.x; i < NRP * (kBlurTW / 4); i += 256) {
+        const int rp = i >> 5, cq = i & 31;
+        uint32_t A[3], B[3];
 #pragma unroll
-        for (int b = 0; b < 4; ++b) {
-            p[b] = (w0 >> (8 * b)) & 255u;
-            p[4 + b] = (w1 >> (8 * b)) & 255u;
-            p[8 + b] = (w2 >> (8 * b)) & 255u;
+        for (int d = 0; d < 3; ++d) {
+            A[d] = tin[2 * rp][cq + 3 + d];
+            B[d] = tin[2 * rp + 1][cq + 3 + d];
         }
-        uint32_t hs[4];
+        u16x2 P[12];
+#pragma unroll
+        for (int j = 1; j < 11; ++j) {
+            const uint32_t b = j & 3;
+            P[j] = as_u16x2(__builtin_amdgcn_perm(B[j >> 2], A[j >> 2], b | 0x0c00u | ((4 + b) << 16) | 0x0c000000u));
+        }
+        uint32_t h[4];
 #pragma unroll
         for (int o = 0; o < 4; ++o) {
-            const uint32_t* q = p + 1 + o;  // window offset of column c+o-3 is c+o+1
-            hs[o] = k0 * (q[0] + q[6]) + k1 * (q[1] + q[5]) + k2 * (q[2] + q[4]) + k3 * q[3];
+            const u16x2* q = P + 1 + o;  // q[0] = column x-3 ... q[6] = column x+3
+            u16x2 acc = (u16x2)(56) * q[3];
+            acc = (u16x2)(48) * (q[2] + q[4]) + acc;
+            acc = (u16x2)(34) * (q[1] + q[5]) + acc;
+            acc = (u16x2)(18) * (q[0] + q[6]) + acc;
+            h[o] = as_u32(acc);
         }
-        thp[r][2 * cq] = hs[0] | (hs[1] << 16);
-        thp[r][2 * cq + 1] = hs[2] | (hs[3] << 16);
+        hp[rp][cq] = make_uint4(h[0], h[1], h[2], h[3]);
     }
     __syncthreads();
-    // vertical: thread -> column quad cq, rows rg*4 .. rg*4+3
+    // vertical: thread -> column quad cq, output rows 4rg .. 4rg+3 (row pairs 2rg .. 2rg+5)
     const int cq = threadIdx.x & 31, rg = threadIdx.x >> 5;
-    uint32_t col[10][4];
+    uint32_t V[6][4];
 #pragma unroll
-    for (int rr = 0; rr < 10; ++rr) {
-        const uint32_t lo = thp[rg * 4 + rr][2 * cq], hi = thp[rg * 4 + rr][2 * cq + 1];
-        col[rr][0] = lo & 0xFFFFu;
-        col[rr][1] = lo >> 16;
-        col[rr][2] = hi & 0xFFFFu;
-        col[rr][3] = hi >> 16;
+    for (int k = 0; k < 6; ++k) {
+        const uint4 q = hp[2 * rg + k][cq];
+        V[k][0] = q.x;
+        V[k][1] = q.y;
+        V[k][2] = q.z;
+        V[k][3] = q.w;
     }
+    const u16x2 WE[4] = {as_u16x2(0u | (18u << 16)), as_u16x2(34u | (48u << 16)),
+                         as_u16x2(56u | (48u << 16)), as_u16x2(34u | (18u << 16))};
+    const u16x2 WO[4] = {as_u16x2(18u | (34u << 16)), as_u16x2(48u | (56u << 16)),
+                         as_u16x2(48u | (34u << 16)), as_u16x2(18u | (0u << 16))};
+    const int x = tx0 + 4 * cq;
 #pragma unroll
     for (int o = 0; o < 4; ++o) {
-        const int y = ty0 + rg * 4 + o;
-        const int x = tx0 + 4 * cq;
-        uint32_t packed = 0;
+        const int y = ty0 + 4 * rg + o;
+        const int k0 = (o + 1) >> 1;  // first row pair: o=0 -> 0, 1 -> 1, 2 -> 1, 3 -> 2
+        uint32_t sv[4];
 #pragma unroll
-        for (int b = 0; b < 4; ++b) {
-            const uint32_t s = k0 * (col[o][b] + col[o + 6][b]) + k1 * (col[o + 1][b] + col[o + 5][b]) +
-                               k2 * (col[o + 2][b] + col[o + 4][b]) + k3 * col[o + 3][b];
-            packed |= ((s + (1u << 15)) >> 16) << (8 * b);
+        for (int c = 0; c < 4; ++c) {
+            uint32_t acc = 1u << 15;
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                acc = __builtin_amdgcn_udot2(as_u16x2(V[k0 + k][c]), (o & 1) ? WO[k] : WE[k], acc, false);
+            sv[c] = acc;
         }
-        if (y < G.h && x < G.w)
-            *reinterpret_cast<uint32_t*>(dst + (long long)y * G.bpitch + x) = packed;
+        // byte 2 of each sum is the result (sum < 2^24)
+        const uint32_t lo = __builtin_amdgcn_perm(sv[1], sv[0], 0x0c0c0602u);
+        const uint32_t hi = __builtin_amdgcn_perm(sv[3], sv[2], 0x0c0c0602u);
+        const uint32_t packed = lo | (hi << 16);
+        if (y < G.h && x < G.w) *reinterpret_cast<uint32_t*>(dst + (long long)y * G.bpitch + x) = packed;
     }
 }
 
@@ -264,17 +297,22 @@ __global__ __launch_bounds__(256) void k_blur(BatchArgs a) {
 // ComputeKeyPointsOctTree (ORBextractor_old.cc:807-871) with cv::FAST(cell, kps, th, true):
 // detection on [3,rows-3)x[3,cols-3) of the cell ROI, 3x3 nonmax inside the cell only, iniTh
 // then minTh if the cell yields nothing, keys emitted in row-major order.
-__global__ __launch_bounds__(256) void k_fast_cells(BatchArgs a) {
-    __shared__ __attribute__((aligned(16))) uint8_t T[kCellMax * kCellMax];
-    __shared__ __attribute__((aligned(16))) uint8_t M[kCellMax * kCellMax];
-    __shared__ uint16_t list[kCellList];
-    __shared__ int32_t wcnt[4];
+constexpr int kFastThreads = 256;  // one workgroup (4 waves) per cell
+
+template <int CP>
+__global__ __launch_bounds__(kFastThreads) void k_fast_cells(BatchArgs a, int cell0) {
+    constexpr int kList = cell_list_cap<CP>();
+    __shared__ __attribute__((aligned(16))) uint8_t T[CP * CP];
+    __shared__ __attribute__((aligned(16))) uint8_t M[CP * CP];
+    __shared__ uint16_t list[kList];
+    __shared__ int32_t wcnt[kFastThreads / 64];
     __shared__ int scratch[16];
     const int img = a.img0 + blockIdx.y;
+    const int gcell = cell0 + blockIdx.x;  // flattened over the levels
     int l = 0;
-    while (l + 1 < a.nlevels && (int)blockIdx.x >= a.lv[l + 1].cell_first) ++l;
+    while (l + 1 < a.nlevels && gcell >= a.lv[l + 1].cell_first) ++l;
     const LevelGeom& G = a.lv[l];
-    const int cell = blockIdx.x - G.cell_first;
+    const int cell = gcell - G.cell_first;
     const int ci = cell / G.nCols, cj = cell % G.nCols;
     int32_t* cnt_out = a.cellcnt + (long long)img * a.cellcnt_img_stride + G.cellcnt_off + cell;
     uint32_t* key_out = a.cellkeys + (long long)img * a.cellkeys_img_stride + G.cellkey_off +
@@ -295,7 +333,7 @@ __global__ __launch_bounds__(256) void k_fast_cells(BatchArgs a) {
                          (g.iniX - sh);
     DevPolicy p{scratch};
     CellScratch cs{T, M, list, wcnt};
-    const int n = fast_cell_run(p, src, G.pitch, sh, dword_ok, g, a.ini_th, a.min_th, cs, key_out);
+    const int n = fast_cell_run<CP>(p, src, G.pitch, sh, dword_ok, g, a.ini_th, a.min_th, cs, key_out);
     if (threadIdx.x == 0) *cnt_out = n;
 }
 
@@ -378,7 +416,34 @@ __global__ __launch_bounds__(256) void k_orient_desc(BatchArgs a) {
     const uint8_t* lvl = a.lvl_base[l] + (long long)img * G.img_stride;
     const uint8_t* blr = a.blur_base[l] + (long long)img * G.bimg_stride;
     const bool raw_dw = ((G.pitch | G.img_stride) & 3) == 0;
+    // raw buffer over this image's blurred level (dword 3 = gfx9 raw-buffer format word)
+    const __amdgpu_buffer_rsrc_t brs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)blr, (short)0, G.bpitch * G.h, 0x00020000);
     const int stride_k = G.od_blocks * 16;
+    // this lane's disc rows v = sub-15 and sub+1 (none for sub = 15) and, per row, byte masks of
+    // the 32-byte window u = -15..16 restricted to |u| <= umax[|v|]
+    int vrow[2];
+    uint32_t msk[2][8];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int v = h == 0 ? sub - 15 : sub + 1;
+        const int d = (h == 1 && sub == 15) ? -1 : c_umax[v < 0 ? -v : v];
+        vrow[h] = (h == 1 && sub == 15) ? 0 : v;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            uint32_t m = 0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int u = 4 * i + j - 15;
+                m |= ((u < 0 ? -u : u) <= d ? 0xFFu : 0u) << (8 * j);
+            }
+            msk[h][i] = m;
+        }
+    }
+    // this lane's 16 test pairs (x0,y0,x1,y1 int8), packed
+    uint32_t patw[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) patw[i] = reinterpret_cast<const uint32_t*>(c_pattern.v)[sub * 16 + i];
     // uniform trip count per wave so the 16-lane shuffles see all lanes
     const int wave_first = (blockIdx.x - G.od_first) * 16 + (threadIdx.x >> 6) * 4;
     for (int kb = wave_first; kb < count; kb += stride_k) {
@@ -386,17 +451,16 @@ __global__ __launch_bounds__(256) void k_orient_desc(BatchArgs a) {
         const bool valid = kp < count;
         const uint32_t key = valid ? a.lvlkey[kbase + kp] : a.lvlkey[kbase + kb];
         const int x = key_x(key) + kMinBorder, y = key_y(key) + kMinBorder;
-        // IC_Angle moments (ORBextractor_old.cc:78-105): rows v = sub-15 and sub+1 (sub < 15)
+        // IC_Angle moments (ORBextractor_old.cc:78-105) on two disc rows per lane: the row window
+        // is byte-aligned with v_alignbyte, masked to the disc, then
+        //   s = sum of bytes (v_sad_u8), sum u*p = dot4(bytes, {4i..4i+3}) - 15 s
         int m10 = 0, m01 = 0;
+        const int x0 = x - 15;
+        const int xa = raw_dw ? (x0 & ~3) : x0;
+        const int shf = x0 - xa;
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-            const int v = h == 0 ? sub - 15 : sub + 1;
-            if (h == 1 && sub == 15) break;
-            const int d = c_umax[v < 0 ? -v : v];
-            const uint8_t* row = lvl + (long long)(y + v) * G.pitch;
-            const int x0 = x - 15;
-            const int xa = raw_dw ? (x0 & ~3) : x0;
-            const int shf = x0 - xa;
+            const uint8_t* row = lvl + (long long)(y + vrow[h]) * G.pitch;
             uint32_t w[9];
 #pragma unroll
             for (int i = 0; i < 9; ++i) {
@@ -408,18 +472,16 @@ __global__ __launch_bounds__(256) void k_orient_desc(BatchArgs a) {
                            ((uint32_t)q[3] << 24);
                 }
             }
-            int s = 0, su = 0;
+            uint32_t sacc = 0, uacc = 0;
 #pragma unroll
-            for (int c = 0; c < 31; ++c) {
-                const int u = c - 15;
-                const int b = shf + c;
-                const int val = (int)((w[b >> 2] >> (8 * (b & 3))) & 255u);
-                const bool in = (u < 0 ? -u : u) <= d;
-                s += in ? val : 0;
-                su += in ? u * val : 0;
+            for (int i = 0; i < 8; ++i) {
+                const uint32_t b = __builtin_amdgcn_alignbyte(w[i + 1], w[i], shf) & msk[h][i];
+                sacc = __builtin_amdgcn_sad_u8(b, 0u, sacc);
+                const uint32_t wu = (uint32_t)(4 * i) * 0x01010101u + 0x03020100u;
+                uacc = __builtin_amdgcn_udot4(b, wu, uacc, false);
             }
-            m10 += su;
-            m01 += v * s;
+            m10 += (int)uacc - 15 * (int)sacc;
+            m01 += vrow[h] * (int)sacc;
         }
 #pragma unroll
         for (int o = 8; o >= 1; o >>= 1) {
@@ -433,22 +495,26 @@ __global__ __launch_bounds__(256) void k_orient_desc(BatchArgs a) {
         double sd, cd;
         sincos((double)ang, &sd, &cd);
         const float ca = (float)cd, sn = (float)sd;
-        const uint8_t* center = blr + (long long)y * G.bpitch + x;
-        const int8_t* pat = c_pattern.v + sub * 64;
-        uint32_t bits = 0;
+        // all 32 samples of this lane are issued before any is used (one memory round trip);
+        // buffer loads with 32-bit offsets keep the addresses in one VGPR each
         const int pitch = G.bpitch;
-#pragma unroll 4
-        for (int b = 0; b < 16; ++b) {
-            int t[2];
+        const int cofs = y * pitch + x;
+        uint32_t t[32];
 #pragma unroll
-            for (int e = 0; e < 2; ++e) {
-                const float px = (float)pat[4 * b + 2 * e], py = (float)pat[4 * b + 2 * e + 1];
-                const int ry = cv_round(px * sn + py * ca);
-                const int rx = cv_round(px * ca - py * sn);
-                t[e] = center[ry * pitch + rx];  // |ry|,|rx| <= 18: 32-bit offset
-            }
-            bits |= (uint32_t)(t[0] < t[1]) << b;
+        for (int e = 0; e < 32; ++e) {
+            // the packed pattern word is opaque here, so its 64 float conversions are not
+            // hoisted out of the keypoint loop (that would hold 64 VGPRs across it)
+            uint32_t pw = patw[e >> 1];
+            asm volatile("" : "+v"(pw));
+            const int sh8 = 16 * (e & 1);
+            const float px = (float)(int8_t)(pw >> sh8), py = (float)(int8_t)(pw >> (sh8 + 8));
+            const int ry = cv_round(px * sn + py * ca);
+            const int rx = cv_round(px * ca - py * sn);
+            t[e] = __builtin_amdgcn_raw_buffer_load_b8(brs, cofs + ry * pitch + rx, 0, 0);
         }
+        uint32_t bits = 0;
+#pragma unroll
+        for (int b = 0; b < 16; ++b) bits |= (uint32_t)(t[2 * b] < t[2 * b + 1]) << b;
         if (valid) {
             if (sub == 0) a.lvlangle[kbase + kp] = angle;
             reinterpret_cast<uint16_t*>(a.lvldesc + (kbase + kp) * 32)[sub] = (uint16_t)bits;
@@ -679,7 +745,13 @@ hipError_t launch_blur(const BatchArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 hipError_t launch_fast_cells(const BatchArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(k_fast_cells, dim3(a.total_cells, a.nimages), dim3(256), 0, s, a);
+    // levels [0, fast_split) have cells that fit the 48-byte tile (higher occupancy); the rest
+    // (the small top levels, whose cells are taller) run the general 80-byte tile
+    const int c0 = a.fast_split < a.nlevels ? a.lv[a.fast_split].cell_first : a.total_cells;
+    if (c0 > 0)
+        hipLaunchKernelGGL(k_fast_cells<kCellPitchSmall>, dim3(c0, a.nimages), dim3(kFastThreads), 0, s, a, 0);
+    if (a.total_cells > c0)
+        hipLaunchKernelGGL(k_fast_cells<kCellMax>, dim3(a.total_cells - c0, a.nimages), dim3(kFastThreads), 0, s, a, c0);
     return hipGetLastError();
 }
 hipError_t launch_octree(const BatchArgs& a, hipStream_t s) {

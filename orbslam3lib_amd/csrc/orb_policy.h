@@ -57,6 +57,25 @@ struct DevPolicy {
     }
 };
 
+// One wave on its own (64 lanes), e.g. one FAST cell per wave: "sync" is a wave-level memory
+// ordering point (LDS ops of one wave complete in order; the fences stop compiler reordering).
+struct WavePolicy {
+    __device__ int tid() const { return (int)(threadIdx.x & 63); }
+    __device__ int nthreads() const { return 64; }
+    __device__ void sync() {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    __device__ int popc64(uint64_t x) const { return __popcll(x); }
+    __device__ int lane() const { return (int)(threadIdx.x & 63); }
+    __device__ int wave() const { return 0; }
+    __device__ int nwaves() const { return 1; }
+    __device__ int wave_width() const { return 64; }
+    __device__ uint64_t ballot(bool f) const { return __ballot(f); }
+    __device__ uint64_t lanemask_lt() const { return (1ull << (threadIdx.x & 63)) - 1ull; }
+};
+
 struct SerialPolicy {
     __host__ __device__ int tid() const { return 0; }
     __host__ __device__ int nthreads() const { return 1; }

@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "../../include/orbgpu.h"
+#include "orb_fast_cell.h"
 #include "orb_kernels.h"
 #include "orb_octree.h"
 
@@ -254,7 +255,7 @@ int set_geometry(orbgpu_ctx* c, int w, int h) {
             return fail(ORBGPU_ERR_INVALID, "pyramid level " + std::to_string(l) + " has no cells");
         G.wCell = (int)std::ceil(width / G.nCols);
         G.hCell = (int)std::ceil(height / G.nRows);
-        if (G.wCell + 6 > 80 || G.hCell + 6 > 80) return fail(ORBGPU_ERR_INVALID, "cell too large");
+        if (G.wCell > 69 || G.hCell > 69) return fail(ORBGPU_ERR_INVALID, "cell too large");
         G.ncells = G.nCols * G.nRows;
         G.cell_cap = ((G.wCell + 1) / 2) * ((G.hCell + 1) / 2);
         G.cell_first = cell_first;
@@ -315,6 +316,15 @@ int set_geometry(orbgpu_ctx* c, int w, int h) {
     A.oct_lds_bytes = std::max((int)oct_nodemem_bytes(std::max(lds_nodes, 1)), std::min(4 * max_cells, 65536));
     A.oct_lds_bytes = (A.oct_lds_bytes + 15) & ~15;
     A.total_cells = cell_first;
+    // FAST LDS tile: the 48-byte one for the leading levels whose cell ROIs (+3 alignment bytes)
+    // fit it; cells grow with the level (fewer, wider cells), so the rest use the 80-byte one
+    A.fast_split = 0;
+    while (A.fast_split < L && A.lv[A.fast_split].wCell + 9 <= kCellPitchSmall &&
+           A.lv[A.fast_split].hCell + 6 <= kCellPitchSmall)
+        ++A.fast_split;
+    if (const char* fp = getenv("ORBGPU_FAST_PITCH")) {  // diagnostics: one tile for every level
+        if (atoi(fp) == kCellMax) A.fast_split = 0;
+    }
     A.total_tiles = tile_first;
     A.total_od_blocks = od_first;
     for (int l = 0; l < L; ++l) {

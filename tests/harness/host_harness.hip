@@ -85,7 +85,7 @@ int harness_level_candidates(const uint8_t* lvl, int w, int h, int ini, int mn, 
     std::vector<uint32_t> T32(kCellMax * kCellMax / 4), M32(kCellMax * kCellMax / 4);
     uint8_t* T = reinterpret_cast<uint8_t*>(T32.data());
     uint8_t* M = reinterpret_cast<uint8_t*>(M32.data());
-    std::vector<uint16_t> list(kCellList);
+    std::vector<uint16_t> list(cell_list_cap<kCellMax>());
     std::vector<int32_t> wcnt(4);
     std::vector<uint32_t> tmp(kCellMax * kCellMax);
     int total = 0, cnt = 0;
@@ -103,8 +103,11 @@ int harness_level_candidates(const uint8_t* lvl, int w, int h, int ini, int mn, 
             const bool dw = ((i + j) & 1) == 0 && (w & 3) == 0;
             const int sh = dw ? (g.iniX & 3) : 0;
             CellScratch cs{T, M, list.data(), wcnt.data()};
-            const int m = fast_cell_run(p, lvl + (long long)g.iniY * w + g.iniX - sh, w, sh, dw, g,
-                                        ini, mn, cs, tmp.data());
+            // the small tile whenever the cells fit it (as the runtime picks it), else the general one
+            const bool small = wCell + 9 <= kCellPitchSmall && hCell + 6 <= kCellPitchSmall;
+            const uint8_t* src = lvl + (long long)g.iniY * w + g.iniX - sh;
+            const int m = small ? fast_cell_run<kCellPitchSmall>(p, src, w, sh, dw, g, ini, mn, cs, tmp.data())
+                                : fast_cell_run<kCellMax>(p, src, w, sh, dw, g, ini, mn, cs, tmp.data());
             for (int k = 0; k < m; ++k) {
                 if (total < cap) out[total] = tmp[k];
                 ++total;

@@ -200,3 +200,23 @@ def test_gpu_matches_golden_fixtures():
     got = og.BFMatcher(ex).knnMatch(L, R, 2)
     for a, key in zip(got, ("idx1", "dist1", "idx2", "dist2")):
         np.testing.assert_array_equal(a, g[key])
+
+
+def test_general_fast_tile(oracle, frame0, monkeypatch):
+    """The 80-byte-pitch FAST tile (used when a level's cells exceed the 48-byte tile) on the
+    640x480 frame, forced through ORBGPU_FAST_PITCH, and a small frame whose top levels have
+    cells wider than 39 px so the runtime picks it by itself."""
+    L, _ = frame0
+    monkeypatch.setenv("ORBGPU_FAST_PITCH", "80")
+    ex = _extractor()
+    k, d, m = ex(L)
+    rk, rd, rm = oracle.extract(L, nfeatures=2000)
+    _same_kps(k, rk)
+    np.testing.assert_array_equal(d, rd)
+    monkeypatch.delenv("ORBGPU_FAST_PITCH")
+    img = synth.frame(120, 160, 5)
+    ex = _extractor(nf=300, L=4, w=160, h=120)
+    k, d, m = ex(img)
+    rk, rd, rm = oracle.extract(img, nfeatures=300, nlevels=4)
+    _same_kps(k, rk)
+    np.testing.assert_array_equal(d, rd)
