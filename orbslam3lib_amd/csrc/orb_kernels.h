@@ -108,7 +108,8 @@ __host__ __device__ inline OctLayout oct_layout(int n_cap, int C) {
 // Kernel launchers (orb_kernels.hip).  Each returns hipGetLastError() of its launch.
 hipError_t launch_resize(const BatchArgs& a, int level, hipStream_t s);
 hipError_t launch_blur(const BatchArgs& a, hipStream_t s);
-hipError_t launch_fast_cells(const BatchArgs& a, hipStream_t s);
+// top = false: levels [0, fast_split) on the 48-byte tile; true: the other levels (80-byte tile)
+hipError_t launch_fast_cells(const BatchArgs& a, bool top, hipStream_t s);
 hipError_t launch_octree(const BatchArgs& a, hipStream_t s);
 hipError_t launch_orient_desc(const BatchArgs& a, hipStream_t s);
 hipError_t launch_finalize(const BatchArgs& a, hipStream_t s);

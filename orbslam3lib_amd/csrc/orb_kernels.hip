@@ -744,13 +744,13 @@ hipError_t launch_blur(const BatchArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_blur, dim3(a.total_tiles, a.nimages), dim3(256), 0, s, a);
     return hipGetLastError();
 }
-hipError_t launch_fast_cells(const BatchArgs& a, hipStream_t s) {
+hipError_t launch_fast_cells(const BatchArgs& a, bool top, hipStream_t s) {
     // levels [0, fast_split) have cells that fit the 48-byte tile (higher occupancy); the rest
     // (the small top levels, whose cells are taller) run the general 80-byte tile
     const int c0 = a.fast_split < a.nlevels ? a.lv[a.fast_split].cell_first : a.total_cells;
-    if (c0 > 0)
+    if (!top && c0 > 0)
         hipLaunchKernelGGL(k_fast_cells<kCellPitchSmall>, dim3(c0, a.nimages), dim3(kFastThreads), 0, s, a, 0);
-    if (a.total_cells > c0)
+    if (top && a.total_cells > c0)
         hipLaunchKernelGGL(k_fast_cells<kCellMax>, dim3(a.total_cells - c0, a.nimages), dim3(kFastThreads), 0, s, a, c0);
     return hipGetLastError();
 }

@@ -39,9 +39,10 @@ int fail(int code, const std::string& msg) {
             return fail(ORBGPU_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
     } while (0)
 
-enum Stage { ST_RESIZE, ST_BLUR, ST_FAST, ST_OCTREE, ST_ORIENT, ST_FINAL, ST_KNN, ST_COUNT };
-const char* kStageNames[ST_COUNT] = {"k_resize",      "k_blur",     "k_fast_cells", "k_octree",
-                                     "k_orient_desc", "k_finalize", "k_knn2"};
+enum Stage { ST_RESIZE, ST_BLUR, ST_FAST, ST_FAST_TOP, ST_OCTREE, ST_ORIENT, ST_FINAL, ST_KNN, ST_COUNT };
+// names as rocprofv3 shows the kernels (templates with their argument)
+const char* kStageNames[ST_COUNT] = {"k_resize",  "k_blur",        "k_fast_cells<48>", "k_fast_cells<80>",
+                                     "k_octree",  "k_orient_desc", "k_finalize",       "k_knn2"};
 
 struct DevBuf {
     void* p = nullptr;
@@ -105,7 +106,7 @@ struct orbgpu_ctx {
     std::vector<hipEvent_t> join;  // one per sub stream
     // stages launched once over the whole batch on the main stream (join before, fork after):
     // the dominant kernel runs alone, so its per-launch duration is its own
-    unsigned isolate_mask = 1u << ST_FAST;
+    unsigned isolate_mask = (1u << ST_FAST) | (1u << ST_FAST_TOP);
     bool serialize = false;  // profiling: every stage isolated
     struct ChunkRec { int img0, n; hipStream_t st; };
     std::vector<ChunkRec> last_chunks;
@@ -606,7 +607,8 @@ int orbgpu_run_batch(orbgpu_ctx* c, int n, int w, int h, const int32_t* laps, vo
         if (r) return r;
     }
     if ((r = each(ST_BLUR, [](const BatchArgs& B, hipStream_t st) { return launch_blur(B, st); }))) return r;
-    if ((r = each(ST_FAST, [](const BatchArgs& B, hipStream_t st) { return launch_fast_cells(B, st); }))) return r;
+    if ((r = each(ST_FAST, [](const BatchArgs& B, hipStream_t st) { return launch_fast_cells(B, false, st); }))) return r;
+    if ((r = each(ST_FAST_TOP, [](const BatchArgs& B, hipStream_t st) { return launch_fast_cells(B, true, st); }))) return r;
     if ((r = each(ST_OCTREE, [](const BatchArgs& B, hipStream_t st) { return launch_octree(B, st); }))) return r;
     if ((r = each(ST_ORIENT, [](const BatchArgs& B, hipStream_t st) { return launch_orient_desc(B, st); }))) return r;
     if ((r = each(ST_FINAL, [](const BatchArgs& B, hipStream_t st) { return launch_finalize(B, st); }))) return r;
