@@ -5,7 +5,7 @@
 // sees only this cell's corners, iniThFAST first and minThFAST if the cell kept nothing, keys
 // emitted in row-major order relative to (minBorderX, minBorderY).
 //
-// Layout: the ROI is staged in LDS with a compile-time pitch P (48 when every level's cells fit,
+// Layout: the ROI is staged in LDS with a compile-time pitch P (60 when every level's cells fit,
 // kCellMax = 80 otherwise).  On the GPU one wave runs one cell (no workgroup barriers); the
 // code also accepts several waves per cell: each wave owns one contiguous row-major range of
 // detection pixels and keeps a private candidate list, so the wave lists concatenated in wave
@@ -24,8 +24,8 @@
 namespace orbgpu {
 
 constexpr int kCellMax = 80;  // wCell, hCell < 70 (nCols = floor(W/35)) plus the 6-px overlap
-constexpr int kCellPitchSmall = 48;  // every 640x480-class level: cells <= 39 x 42
-// candidate list capacity for pitch P: the detection area, (P-6)^2 for the 48-byte tile, 69^2
+constexpr int kCellPitchSmall = 60;  // 640x480-class pyramids: every level's cells <= 51 x 54
+// candidate list capacity for pitch P: the detection area, (P-6)^2 for the 60-byte tile, 69^2
 // for the general one (wCell, hCell <= 69: nCols = floor(W/35) >= 1)
 template <int P>
 constexpr int cell_list_cap() { return P == kCellMax ? 69 * 69 : (P - 6) * (P - 6); }

@@ -745,7 +745,7 @@ hipError_t launch_blur(const BatchArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 hipError_t launch_fast_cells(const BatchArgs& a, bool top, hipStream_t s) {
-    // levels [0, fast_split) have cells that fit the 48-byte tile (higher occupancy); the rest
+    // levels [0, fast_split) have cells that fit the 60-byte tile (higher occupancy); the rest
     // (the small top levels, whose cells are taller) run the general 80-byte tile
     const int c0 = a.fast_split < a.nlevels ? a.lv[a.fast_split].cell_first : a.total_cells;
     if (!top && c0 > 0)

@@ -41,7 +41,7 @@ int fail(int code, const std::string& msg) {
 
 enum Stage { ST_RESIZE, ST_BLUR, ST_FAST, ST_FAST_TOP, ST_OCTREE, ST_ORIENT, ST_FINAL, ST_KNN, ST_COUNT };
 // names as rocprofv3 shows the kernels (templates with their argument)
-const char* kStageNames[ST_COUNT] = {"k_resize",  "k_blur",        "k_fast_cells<48>", "k_fast_cells<80>",
+const char* kStageNames[ST_COUNT] = {"k_resize",  "k_blur",        "k_fast_cells<60>", "k_fast_cells<80>",
                                      "k_octree",  "k_orient_desc", "k_finalize",       "k_knn2"};
 
 struct DevBuf {
@@ -317,7 +317,7 @@ int set_geometry(orbgpu_ctx* c, int w, int h) {
     A.oct_lds_bytes = std::max((int)oct_nodemem_bytes(std::max(lds_nodes, 1)), std::min(4 * max_cells, 65536));
     A.oct_lds_bytes = (A.oct_lds_bytes + 15) & ~15;
     A.total_cells = cell_first;
-    // FAST LDS tile: the 48-byte one for the leading levels whose cell ROIs (+3 alignment bytes)
+    // FAST LDS tile: the 60-byte one for the leading levels whose cell ROIs (+3 alignment bytes)
     // fit it; cells grow with the level (fewer, wider cells), so the rest use the 80-byte one
     A.fast_split = 0;
     while (A.fast_split < L && A.lv[A.fast_split].wCell + 9 <= kCellPitchSmall &&
