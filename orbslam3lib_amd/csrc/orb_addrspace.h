@@ -1,0 +1,24 @@
+// orb_addrspace.h -- address-space-qualified pointers for the policy-templated algorithms.
+//
+// asp<AS, T> is T* in address space AS (3 = LDS, 1 = global), or a plain generic T* for
+// AS = -1.  Kernels instantiate the octree/sort code with the spaces their buffers really live
+// in, so the compiler emits ds_* / global_* instead of flat_* accesses (a flat access waits on
+// both the LDS and the vector-memory counters); the host test harness uses -1.
+#pragma once
+
+namespace orbgpu {
+
+template <int AS, class T>
+struct asp_t {
+    using type = __attribute__((address_space(AS))) T*;
+};
+template <class T>
+struct asp_t<-1, T> {
+    using type = T*;
+};
+template <int AS, class T>
+using asp = typename asp_t<AS, T>::type;
+
+constexpr int kGeneric = -1, kGlobalAS = 1, kLdsAS = 3;
+
+}  // namespace orbgpu

@@ -12,6 +12,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "orb_addrspace.h"
+
 namespace orbgpu {
 
 // Element sorted by the octree: key = (size << 16 | ulx) would NOT reproduce libstdc++ on
@@ -22,13 +24,31 @@ struct SortElem {
     int32_t node;
 };
 
-__host__ __device__ inline bool node_less(const SortElem& a, const SortElem& b) {
+__host__ __device__ inline bool node_less(SortElem a, SortElem b) {
     if (a.size < b.size) return true;
     if (a.size > b.size) return false;
     return a.ulx < b.ulx;
 }
 
-__host__ __device__ inline void isort_swap(SortElem* a, int i, int j) {
+// Whole-element access that works for any address space (the implicit copy operations of a
+// struct take generic references, which an LDS-qualified lvalue cannot bind to).
+template <class EP>
+__host__ __device__ inline SortElem se_ld(EP a, int i) {
+    SortElem e;
+    e.size = a[i].size;
+    e.ulx = a[i].ulx;
+    e.node = a[i].node;
+    return e;
+}
+template <class EP>
+__host__ __device__ inline void se_st(EP a, int i, SortElem e) {
+    a[i].size = e.size;
+    a[i].ulx = e.ulx;
+    a[i].node = e.node;
+}
+
+template <class EP>
+__host__ __device__ inline void isort_swap(EP a, int i, int j) {
     // field-wise (a 12-byte struct temporary would be placed in scratch memory by hipcc)
     const int32_t s0 = a[i].size, u0 = a[i].ulx, n0 = a[i].node;
     a[i].size = a[j].size;
@@ -45,39 +65,42 @@ __host__ __device__ inline int isort_lg(int n) {
     return k;
 }
 
-__host__ __device__ inline void isort_push_heap(SortElem* a, int hole, int top, SortElem v) {
+template <class EP>
+__host__ __device__ inline void isort_push_heap(EP a, int hole, int top, SortElem v) {
     int parent = (hole - 1) / 2;
-    while (hole > top && node_less(a[parent], v)) {
-        a[hole] = a[parent];
+    while (hole > top && node_less(se_ld(a, parent), v)) {
+        se_st(a, hole, se_ld(a, parent));
         hole = parent;
         parent = (hole - 1) / 2;
     }
-    a[hole] = v;
+    se_st(a, hole, v);
 }
 
-__host__ __device__ inline void isort_adjust_heap(SortElem* a, int hole, int len, SortElem v) {
+template <class EP>
+__host__ __device__ inline void isort_adjust_heap(EP a, int hole, int len, SortElem v) {
     const int top = hole;
     int second = hole;
     while (second < (len - 1) / 2) {
         second = 2 * (second + 1);
-        if (node_less(a[second], a[second - 1])) second--;
-        a[hole] = a[second];
+        if (node_less(se_ld(a, second), se_ld(a, second - 1))) second--;
+        se_st(a, hole, se_ld(a, second));
         hole = second;
     }
     if ((len & 1) == 0 && second == (len - 2) / 2) {
         second = 2 * (second + 1);
-        a[hole] = a[second - 1];
+        se_st(a, hole, se_ld(a, second - 1));
         hole = second - 1;
     }
     isort_push_heap(a, hole, top, v);
 }
 
 // std::__partial_sort(first, last, last) == __make_heap + __sort_heap on [first, last).
-__host__ __device__ inline void isort_heapsort(SortElem* a, int n) {
+template <class EP>
+__host__ __device__ inline void isort_heapsort(EP a, int n) {
     if (n >= 2) {
         int parent = (n - 2) / 2;
         while (true) {
-            SortElem v = a[parent];
+            SortElem v = se_ld(a, parent);
             isort_adjust_heap(a, parent, n, v);
             if (parent == 0) break;
             parent--;
@@ -85,56 +108,60 @@ __host__ __device__ inline void isort_heapsort(SortElem* a, int n) {
     }
     while (n > 1) {
         --n;
-        SortElem v = a[n];
-        a[n] = a[0];
+        SortElem v = se_ld(a, n);
+        se_st(a, n, se_ld(a, 0));
         isort_adjust_heap(a, 0, n, v);
     }
 }
 
-__host__ __device__ inline void isort_median_to_first(SortElem* a, int result, int i, int j, int k) {
-    if (node_less(a[i], a[j])) {
-        if (node_less(a[j], a[k])) isort_swap(a, result, j);
-        else if (node_less(a[i], a[k])) isort_swap(a, result, k);
+template <class EP>
+__host__ __device__ inline void isort_median_to_first(EP a, int result, int i, int j, int k) {
+    if (node_less(se_ld(a, i), se_ld(a, j))) {
+        if (node_less(se_ld(a, j), se_ld(a, k))) isort_swap(a, result, j);
+        else if (node_less(se_ld(a, i), se_ld(a, k))) isort_swap(a, result, k);
         else isort_swap(a, result, i);
-    } else if (node_less(a[i], a[k])) {
+    } else if (node_less(se_ld(a, i), se_ld(a, k))) {
         isort_swap(a, result, i);
-    } else if (node_less(a[j], a[k])) {
+    } else if (node_less(se_ld(a, j), se_ld(a, k))) {
         isort_swap(a, result, k);
     } else {
         isort_swap(a, result, j);
     }
 }
 
-__host__ __device__ inline int isort_unguarded_partition(SortElem* a, int first, int last,
+template <class EP>
+__host__ __device__ inline int isort_unguarded_partition(EP a, int first, int last,
                                                          int pivot) {
     while (true) {
-        while (node_less(a[first], a[pivot])) ++first;
+        while (node_less(se_ld(a, first), se_ld(a, pivot))) ++first;
         --last;
-        while (node_less(a[pivot], a[last])) --last;
+        while (node_less(se_ld(a, pivot), se_ld(a, last))) --last;
         if (!(first < last)) return first;
         isort_swap(a, first, last);
         ++first;
     }
 }
 
-__host__ __device__ inline void isort_unguarded_linear_insert(SortElem* a, int last) {
-    SortElem v = a[last];
+template <class EP>
+__host__ __device__ inline void isort_unguarded_linear_insert(EP a, int last) {
+    SortElem v = se_ld(a, last);
     int next = last - 1;
-    while (node_less(v, a[next])) {
-        a[last] = a[next];
+    while (node_less(v, se_ld(a, next))) {
+        se_st(a, last, se_ld(a, next));
         last = next;
         --next;
     }
-    a[last] = v;
+    se_st(a, last, v);
 }
 
-__host__ __device__ inline void isort_insertion(SortElem* a, int first, int last) {
+template <class EP>
+__host__ __device__ inline void isort_insertion(EP a, int first, int last) {
     if (first == last) return;
     for (int i = first + 1; i != last; ++i) {
-        if (node_less(a[i], a[first])) {
-            SortElem v = a[i];
-            for (int k = i; k > first; --k) a[k] = a[k - 1];
-            a[first] = v;
+        if (node_less(se_ld(a, i), se_ld(a, first))) {
+            SortElem v = se_ld(a, i);
+            for (int k = i; k > first; --k) se_st(a, k, se_ld(a, k - 1));
+            se_st(a, first, v);
         } else {
             isort_unguarded_linear_insert(a, i);
         }
@@ -144,7 +171,8 @@ __host__ __device__ inline void isort_insertion(SortElem* a, int first, int last
 // Iterative form of __introsort_loop: libstdc++ recurses on the right part and loops on the
 // left; an explicit stack of (first, last, depth) frames visited in the same order is
 // equivalent because the two halves are disjoint.
-__host__ __device__ inline void introsort_like_libstdcxx(SortElem* a, int n) {
+template <class EP>
+__host__ __device__ inline void introsort_like_libstdcxx(EP a, int n) {
     if (n <= 1) return;
     const int kThreshold = 16;
     struct Frame { int first, last, depth; };
@@ -191,23 +219,25 @@ __host__ __device__ inline void introsort_like_libstdcxx(SortElem* a, int n) {
 // 2. __final_insertion_sort over the whole partitioned array is a stable insertion sort (its
 //    leftmost segment holds the minimum, so the unguarded inserts are exact): it equals a stable
 //    sort of the partitioned array, done here as a parallel rank sort.
-struct SortScratch {
-    SortElem* tmp;       // [m]
-    uint16_t* lex;       // [m+1]
-    uint16_t* rex;       // [m+1]
-    uint16_t* segof;     // [m]
-    uint16_t* lpos;      // [m]
-    uint16_t* rpos;      // [m]
-    uint16_t* rank;      // [m]
-    uint16_t* segF[2];   // [S]
-    uint16_t* segL[2];   // [S]
-    uint16_t* segD[2];   // [S]
-    int32_t* segK;       // [S]
+template <int AS>
+struct SortScratchT {
+    asp<AS, SortElem> tmp;       // [m]
+    asp<AS, uint16_t> lex;       // [m+1]
+    asp<AS, uint16_t> rex;       // [m+1]
+    asp<AS, uint16_t> segof;     // [m]
+    asp<AS, uint16_t> lpos;      // [m]
+    asp<AS, uint16_t> rpos;      // [m]
+    asp<AS, uint16_t> rank;      // [m]
+    asp<AS, uint16_t> segF[2];   // [S]
+    asp<AS, uint16_t> segL[2];   // [S]
+    asp<AS, uint16_t> segD[2];   // [S]
+    asp<AS, int32_t> segK;       // [S]
 };
+using SortScratch = SortScratchT<kGeneric>;
 
-template <class P>
-__host__ __device__ void introsort_parallel(P& p, SortElem* a, int m, const SortScratch& s,
-                                            int* sh_nseg) {
+template <int AS, class P>
+__host__ __device__ __attribute__((always_inline)) inline void introsort_parallel(P& p, asp<AS, SortElem> a, int m,
+                                            const SortScratchT<AS>& s, asp<AS, int> sh_nseg) {
     const int tid = p.tid(), NT = p.nthreads();
     if (m <= 1) return;
     int cur = 0;
@@ -222,12 +252,12 @@ __host__ __device__ void introsort_parallel(P& p, SortElem* a, int m, const Sort
         const int nseg = *sh_nseg;
         if (nseg == 0) break;
         // (no runtime-indexed pointer arrays: they would live in scratch memory)
-        const uint16_t* F = cur ? s.segF[1] : s.segF[0];
-        const uint16_t* L = cur ? s.segL[1] : s.segL[0];
-        const uint16_t* D = cur ? s.segD[1] : s.segD[0];
-        uint16_t* NF = cur ? s.segF[0] : s.segF[1];
-        uint16_t* NL = cur ? s.segL[0] : s.segL[1];
-        uint16_t* ND = cur ? s.segD[0] : s.segD[1];
+        const auto F = cur ? s.segF[1] : s.segF[0];
+        const auto L = cur ? s.segL[1] : s.segL[0];
+        const auto D = cur ? s.segD[1] : s.segD[0];
+        const auto NF = cur ? s.segF[0] : s.segF[1];
+        const auto NL = cur ? s.segL[0] : s.segL[1];
+        const auto ND = cur ? s.segD[0] : s.segD[1];
         for (int g = tid; g < nseg; g += NT) {
             const int f = F[g], l = L[g];
             if (D[g] == 0) {
@@ -252,9 +282,9 @@ __host__ __device__ void introsort_parallel(P& p, SortElem* a, int m, const Sort
             int lf = 0, rf = 0;
             if (i < m && s.segof[i] != 0xFFFF) {
                 const int f = F[s.segof[i]];
-                const SortElem pv = a[f];
-                lf = (i > f) && !node_less(a[i], pv);
-                rf = !node_less(pv, a[i]);
+                const SortElem pv = se_ld(a, f);
+                lf = (i > f) && !node_less(se_ld(a, i), pv);
+                rf = !node_less(pv, se_ld(a, i));
             }
             int tl, tr;
             const int el = p.scan_excl(lf, &tl);
@@ -271,9 +301,9 @@ __host__ __device__ void introsort_parallel(P& p, SortElem* a, int m, const Sort
             const int g = s.segof[i];
             if (g == 0xFFFF) continue;
             const int f = F[g], l = L[g];
-            const SortElem pv = a[f];
-            if (i > f && !node_less(a[i], pv)) s.lpos[f + (s.lex[i] - s.lex[f])] = (uint16_t)i;
-            if (!node_less(pv, a[i])) s.rpos[f + (s.rex[l] - s.rex[i] - 1)] = (uint16_t)i;
+            const SortElem pv = se_ld(a, f);
+            if (i > f && !node_less(se_ld(a, i), pv)) s.lpos[f + (s.lex[i] - s.lex[f])] = (uint16_t)i;
+            if (!node_less(pv, se_ld(a, i))) s.rpos[f + (s.rex[l] - s.rex[i] - 1)] = (uint16_t)i;
         }
         p.sync();
         for (int j = tid; j < m; j += NT) {
@@ -287,15 +317,15 @@ __host__ __device__ void introsort_parallel(P& p, SortElem* a, int m, const Sort
         for (int j = tid; j < m; j += NT) {
             const int g = s.segof[j];
             if (g == 0xFFFF || j - F[g] >= s.segK[g]) continue;
-            s.tmp[s.lpos[j]] = a[s.rpos[j]];
-            s.tmp[s.rpos[j]] = a[s.lpos[j]];
+            se_st(s.tmp, s.lpos[j], se_ld(a, s.rpos[j]));
+            se_st(s.tmp, s.rpos[j], se_ld(a, s.lpos[j]));
         }
         p.sync();
         for (int j = tid; j < m; j += NT) {
             const int g = s.segof[j];
             if (g == 0xFFFF || j - F[g] >= s.segK[g]) continue;
-            a[s.lpos[j]] = s.tmp[s.lpos[j]];
-            a[s.rpos[j]] = s.tmp[s.rpos[j]];
+            se_st(a, s.lpos[j], se_ld(s.tmp, s.lpos[j]));
+            se_st(a, s.rpos[j], se_ld(s.tmp, s.rpos[j]));
         }
         p.sync();
         // children segments, kept in position order (left child first)
@@ -338,18 +368,18 @@ __host__ __device__ void introsort_parallel(P& p, SortElem* a, int m, const Sort
     }
     // stable sort of the partitioned array
     for (int i = tid; i < m; i += NT) {
-        const SortElem x = a[i];
+        const SortElem x = se_ld(a, i);
         int r = 0;
         for (int j = 0; j < m; ++j) {
-            const SortElem y = a[j];
+            const SortElem y = se_ld(a, j);
             r += node_less(y, x) || (j < i && !node_less(x, y));
         }
         s.rank[i] = (uint16_t)r;
     }
     p.sync();
-    for (int i = tid; i < m; i += NT) s.tmp[s.rank[i]] = a[i];
+    for (int i = tid; i < m; i += NT) se_st(s.tmp, s.rank[i], se_ld(a, i));
     p.sync();
-    for (int i = tid; i < m; i += NT) a[i] = s.tmp[i];
+    for (int i = tid; i < m; i += NT) se_st(a, i, se_ld(s.tmp, i));
     p.sync();
 }
 

@@ -67,6 +67,7 @@ struct BatchArgs {
     unsigned long long* octdbg;      // diagnostic: [img][kMaxLevels][8] phase clocks, or null
     int oct_lds_nodes;               // node capacity of k_octree's dynamic LDS (0: all global)
     int oct_lds_bytes;
+    int oct_nq_off;                  // byte offset of the per-key labels in that LDS
 };
 
 struct MatchArgs {
@@ -87,8 +88,10 @@ struct MatchArgs {
 // state lives in LDS when C <= kOctLdsNodes, otherwise in the `nodemem` part of this block.
 constexpr int kOctLdsNodes = 1024;
 
+constexpr int kOctLdsKeys = 16384;  // per-key node labels (u16) kept in LDS up to this many keys
+
 struct OctLayout {
-    long long keys, knode, kq, nodemem, total;
+    long long keys, nq, nodemem, total;
 };
 
 __host__ __device__ inline long long oct_align(long long x) { return (x + 255) & ~255LL; }
@@ -97,8 +100,7 @@ __host__ __device__ inline OctLayout oct_layout(int n_cap, int C) {
     OctLayout L;
     long long o = 0;
     L.keys = o; o = oct_align(o + 4LL * n_cap);
-    L.knode = o; o = oct_align(o + 2LL * n_cap);
-    L.kq = o; o = oct_align(o + 1LL * n_cap);
+    L.nq = o; o = oct_align(o + 2LL * n_cap);  // used when n exceeds kOctLdsKeys
     L.nodemem = o;
     o = oct_align(o + (long long)((size_t)C * 78 + 64));  // used when C exceeds the LDS capacity
     L.total = o;

@@ -341,7 +341,7 @@ __global__ __launch_bounds__(kFastThreads) void k_fast_cells(BatchArgs a, int ce
 // k_octree: one workgroup per (level, image).  Gathers the level's cell lists in cell order
 // (vToDistributeKeys, :807-871) then runs DistributeOctTree (orb_octree.h) with the node
 // state in LDS (80 KB: two workgroups per CU).
-__global__ __launch_bounds__(512) void k_octree(BatchArgs a) {
+__global__ __launch_bounds__(512, 4) void k_octree(BatchArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t nodemem_lds[];  // a.oct_lds_bytes
     __shared__ int scratch[16];
     __shared__ OctShared sh;
@@ -354,10 +354,11 @@ __global__ __launch_bounds__(512) void k_octree(BatchArgs a) {
     const OctLayout L = oct_layout(G.cand_cap, G.oct_cap);
     uint32_t* keys = reinterpret_cast<uint32_t*>(ws + L.keys);
     void* nm = G.oct_cap <= a.oct_lds_nodes ? (void*)nodemem_lds : (void*)(ws + L.nodemem);
-    // exclusive scan of the cell counts into LDS (the node area is free until the octree runs)
+    // exclusive scan of the cell counts into LDS (the node area is free until the octree's
+    // gather has read it)
     int32_t* cell_off = reinterpret_cast<int32_t*>(nodemem_lds);
-    const bool off_in_lds = G.ncells <= a.oct_lds_bytes / 4;
-    if (!off_in_lds) cell_off = reinterpret_cast<int32_t*>(ws + L.knode);  // huge levels only
+    const bool off_in_lds = G.ncells <= a.oct_nq_off / 4;
+    if (!off_in_lds) cell_off = reinterpret_cast<int32_t*>(ws + L.nq);  // huge levels only
     int carry = 0;
     for (int base = 0; base < G.ncells; base += blockDim.x) {
         const int i = base + threadIdx.x;
@@ -369,29 +370,44 @@ __global__ __launch_bounds__(512) void k_octree(BatchArgs a) {
     }
     const int n = carry;
     __syncthreads();
-    // gather: key k belongs to the last cell whose offset is <= k
-    for (int k = threadIdx.x; k < n; k += blockDim.x) {
-        int lo = 0, hi = G.ncells - 1;
-        while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (cell_off[mid] <= k) lo = mid;
-            else hi = mid - 1;
-        }
-        keys[k] = ck[(long long)lo * G.cell_cap + (k - cell_off[lo])];
+    uint32_t* out_keys = a.lvlkey + (long long)img * a.lvlkp_img_stride + G.kp_off;
+    unsigned long long* dbg = a.octdbg ? a.octdbg + ((long long)img * kMaxLevels + l) * 8 : nullptr;
+    int r = n > G.cand_cap ? -3 : 0;
+    if (r == 0 && off_in_lds && G.oct_cap <= a.oct_lds_nodes && n <= kOctLdsKeys) {
+        // everything node- and label-sized in LDS: ds_* accesses throughout
+        OctWST<kLdsAS, kGlobalAS> w;
+        w.keys = (asp<kGlobalAS, uint32_t>)keys;
+        w.n = n;
+        w.nq = (asp<kLdsAS, uint16_t>)(nodemem_lds + a.oct_nq_off);
+        w.m = oct_nodemem_carve<kLdsAS>(nodemem_lds, G.oct_cap);
+        w.cap = G.oct_cap;
+        w.out_keys = (asp<kGlobalAS, uint32_t>)out_keys;
+        w.out_cap = G.kp_cap;
+        w.dbg = dbg;
+        w.cell_off = (asp<kLdsAS, const int32_t>)cell_off;
+        w.cellkeys = (asp<kGlobalAS, const uint32_t>)ck;
+        w.ncells = G.ncells;
+        w.cell_cap = G.cell_cap;
+        r = octree_distribute(p, w, (asp<kLdsAS, OctShared>)&sh, G.W, G.H, G.N);
+    } else if (r == 0) {
+        // huge levels: node state / labels / cell offsets in the global workspace where needed
+        OctWST<kGeneric, kGeneric> w;
+        w.keys = keys;
+        w.n = n;
+        w.nq = n <= kOctLdsKeys && off_in_lds ? reinterpret_cast<uint16_t*>(nodemem_lds + a.oct_nq_off)
+                                             : reinterpret_cast<uint16_t*>(ws + L.nq);
+        w.m = oct_nodemem_carve<kGeneric>(nm, G.oct_cap);
+        w.cap = G.oct_cap;
+        w.out_keys = out_keys;
+        w.out_cap = G.kp_cap;
+        w.dbg = dbg;
+        w.cell_off = cell_off;
+        w.cellkeys = ck;
+        w.ncells = G.ncells;
+        w.cell_cap = G.cell_cap;
+        if (!off_in_lds && n > kOctLdsKeys) r = -3;  // cell offsets occupy L.nq
+        else r = octree_distribute(p, w, &sh, G.W, G.H, G.N);
     }
-    __syncthreads();
-    OctWS w;
-    w.keys = keys;
-    w.n = n;
-    w.knode = reinterpret_cast<uint16_t*>(ws + L.knode);
-    w.kq = ws + L.kq;
-    w.m = oct_nodemem_carve(nm, G.oct_cap);
-    w.cap = G.oct_cap;
-    w.out_keys = a.lvlkey + (long long)img * a.lvlkp_img_stride + G.kp_off;
-    w.out_cap = G.kp_cap;
-    w.dbg = a.octdbg ? a.octdbg + ((long long)img * kMaxLevels + l) * 8 : nullptr;
-    int r = (n > G.cand_cap) ? -3 : 0;
-    if (r == 0) r = octree_distribute(p, w, &sh, G.W, G.H, G.N);
     if (threadIdx.x == 0) {
         a.lvlcnt[img * kMaxLevels + l] = r < 0 ? 0 : r;
         a.status[img * kMaxLevels + l] = r < 0 ? r : 0;

@@ -7,16 +7,69 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "orb_addrspace.h"
+
 namespace orbgpu {
+
+// Wave 0 of a workgroup working alone (the octree's node-level phases): block-wide ops become
+// wave-wide, so "sync" costs a counter wait instead of a workgroup barrier.
+struct WaveScanPolicy {
+    int* scratch;  // unused (interface parity with DevPolicy)
+    __device__ int tid() const { return (int)(threadIdx.x & 63); }
+    __device__ int nthreads() const { return 64; }
+    __device__ void sync() {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_s_waitcnt(0);  // LDS and global (node state may live in global memory)
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    template <class T>
+    __device__ int atomic_add(T p, int v) {
+        return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    template <class T>
+    __device__ uint32_t atomic_max(T p, uint32_t v) {
+        return __hip_atomic_fetch_max(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    template <class T>
+    __device__ int atomic_max_int(T p, int v) {
+        return __hip_atomic_fetch_max(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __device__ unsigned long long now() const { return wall_clock64(); }
+    __device__ int popc64(uint64_t x) const { return __popcll(x); }
+    __device__ int scan_excl(int v, int* total) {
+        const int lane = (int)(threadIdx.x & 63);
+        int x = v;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
+        }
+        *total = __shfl(x, 63, 64);
+        return x - v;
+    }
+};
 
 struct DevPolicy {
     int* scratch;  // >= 16 ints of LDS
+    // node-level work of the octree runs on wave 0 alone
+    __device__ bool node_worker() const { return threadIdx.x < 64; }
+    __device__ WaveScanPolicy node() const { return WaveScanPolicy{scratch}; }
     __device__ int tid() const { return (int)threadIdx.x; }
     __device__ int nthreads() const { return (int)blockDim.x; }
     __device__ void sync() { __syncthreads(); }
-    __device__ int atomic_add(int32_t* p, int v) { return atomicAdd(p, v); }
-    __device__ uint32_t atomic_max(uint32_t* p, uint32_t v) { return atomicMax(p, v); }
-    __device__ int atomic_max_int(int* p, int v) { return atomicMax(p, v); }
+    template <class T>
+    __device__ int atomic_add(T p, int v) {
+        return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    template <class T>
+    __device__ uint32_t atomic_max(T p, uint32_t v) {
+        return __hip_atomic_fetch_max(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    template <class T>
+    __device__ int atomic_max_int(T p, int v) {
+        return __hip_atomic_fetch_max(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     __device__ unsigned long long now() const { return wall_clock64(); }  // 100 MHz
     __device__ int popc64(uint64_t x) const { return __popcll(x); }
     __device__ int lane() const { return (int)(threadIdx.x & 63); }
@@ -77,20 +130,25 @@ struct WavePolicy {
 };
 
 struct SerialPolicy {
+    __host__ __device__ bool node_worker() const { return true; }
+    __host__ __device__ SerialPolicy node() const { return SerialPolicy{}; }
     __host__ __device__ int tid() const { return 0; }
     __host__ __device__ int nthreads() const { return 1; }
     __host__ __device__ void sync() {}
-    __host__ __device__ int atomic_add(int32_t* p, int v) {
+    template <class T>
+    __host__ __device__ int atomic_add(T p, int v) {
         const int o = *p;
         *p = o + v;
         return o;
     }
-    __host__ __device__ uint32_t atomic_max(uint32_t* p, uint32_t v) {
+    template <class T>
+    __host__ __device__ uint32_t atomic_max(T p, uint32_t v) {
         const uint32_t o = *p;
         if (v > o) *p = v;
         return o;
     }
-    __host__ __device__ int atomic_max_int(int* p, int v) {
+    template <class T>
+    __host__ __device__ int atomic_max_int(T p, int v) {
         const int o = *p;
         if (v > o) *p = v;
         return o;

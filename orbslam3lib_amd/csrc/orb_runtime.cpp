@@ -314,7 +314,8 @@ int set_geometry(orbgpu_ctx* c, int w, int h) {
         max_cells = std::max(max_cells, A.lv[l].ncells);
     }
     A.oct_lds_nodes = lds_nodes;
-    A.oct_lds_bytes = std::max((int)oct_nodemem_bytes(std::max(lds_nodes, 1)), std::min(4 * max_cells, 65536));
+    A.oct_nq_off = ((int)oct_nodemem_bytes(std::max(lds_nodes, 1)) + 15) & ~15;
+    A.oct_lds_bytes = std::max(A.oct_nq_off + 2 * kOctLdsKeys, std::min(4 * max_cells, 65536));
     A.oct_lds_bytes = (A.oct_lds_bytes + 15) & ~15;
     A.total_cells = cell_first;
     // FAST LDS tile: the 60-byte one for the leading levels whose cell ROIs (+3 alignment bytes)
@@ -633,7 +634,7 @@ int orbgpu_synchronize(orbgpu_ctx* c) {
             double acc[8] = {};
             for (int i = 0; i < n; ++i)
                 for (int k = 0; k < 8; ++k) acc[k] += (double)d[((size_t)i * kMaxLevels + l) * 8 + k];
-            fprintf(stderr, "octree L%d us: init %.1f choose %.1f count %.1f sort %.1f rebuild %.1f relabel %.1f best %.1f rounds %.1f\n",
+            fprintf(stderr, "octree L%d us: init %.1f choose %.1f barrier %.1f sort %.1f rebuild %.1f relabel %.1f best %.1f rounds %.1f\n",
                     l, acc[0] / n / 100, acc[1] / n / 100, acc[2] / n / 100, acc[3] / n / 100,
                     acc[4] / n / 100, acc[5] / n / 100, acc[6] / n / 100, acc[7] / n);
         }

@@ -17,15 +17,17 @@ extern "C" {
 int harness_octree(const uint32_t* keys, int n, int W, int H, int N, uint32_t* out, int out_cap) {
     const int nIni = std::max(1, (int)std::round((float)W / (float)H));
     const int cap = std::max(N + 3, 4 * nIni) + 8;
-    std::vector<uint16_t> knode(n + 1);
-    std::vector<uint8_t> kq(n + 1);
+    std::vector<uint16_t> nq(n + 1);
     std::vector<uint8_t> mem(oct_nodemem_bytes(cap) + 64);
-    OctWS w;
-    w.keys = keys;
+    OctWST<kGeneric, kGeneric> w;
+    w.keys = const_cast<uint32_t*>(keys);  // read-only without a cell gather
     w.n = n;
-    w.knode = knode.data();
-    w.kq = kq.data();
-    w.m = oct_nodemem_carve(mem.data(), cap);
+    w.nq = nq.data();
+    w.cell_off = nullptr;
+    w.cellkeys = nullptr;
+    w.ncells = 0;
+    w.cell_cap = 0;
+    w.m = oct_nodemem_carve<kGeneric>(mem.data(), cap);
     w.cap = cap;
     w.out_keys = out;
     w.out_cap = out_cap;
@@ -65,7 +67,7 @@ void harness_introsort_parallel(const int32_t* size, const int32_t* ulx, int n, 
     ss.segK = segK.data();
     int nseg = 0;
     SerialPolicy p;
-    introsort_parallel(p, a.data(), n, ss, &nseg);
+    introsort_parallel<kGeneric>(p, a.data(), n, ss, &nseg);
     for (int i = 0; i < n; ++i) perm[i] = a[i].node;
 }
 
