@@ -68,6 +68,8 @@ struct BatchArgs {
     int oct_lds_nodes;               // node capacity of k_octree's dynamic LDS (0: all global)
     int oct_lds_bytes;
     int oct_nq_off;                  // byte offset of the per-key labels in that LDS
+    int oct_may_retry;               // some level can exceed the LDS instantiation of k_octree
+    int oct_force_retry;             // diagnostics: every level through the generic instantiation
 };
 
 struct MatchArgs {

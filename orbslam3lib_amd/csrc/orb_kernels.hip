@@ -124,42 +124,42 @@ __global__ __launch_bounds__(256) void k_resize(BatchArgs a, int l) {
     __syncthreads();
     const uint8_t* wb = reinterpret_cast<const uint8_t*>(&win[0][0]);
     const int q = threadIdx.x & 63;
-    for (int rr = threadIdx.x >> 6; rr < th; rr += 4) {
-        const int dy = ty0 + rr;
-        const int dx0 = tx0 + 4 * q;
-        if (4 * q >= tw) continue;
-        const int4 yt = a.rtab[G.ytab_off + dy];
-        const int b0 = yt.z, b1 = yt.w;
-        uint32_t packed = 0;
+    // one body per source (LDS window / global plane): a merged body would take flat loads
+    auto body = [&](auto row_ptr) __attribute__((always_inline)) {
+        for (int rr = threadIdx.x >> 6; rr < th; rr += 4) {
+            const int dy = ty0 + rr;
+            const int dx0 = tx0 + 4 * q;
+            if (4 * q >= tw) continue;
+            const int4 yt = a.rtab[G.ytab_off + dy];
+            const int b0 = yt.z, b1 = yt.w;
+            const auto r0 = row_ptr(yt.x), r1 = row_ptr(yt.y);
+            uint32_t packed = 0;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int dx = dx0 + k;
-            int o = 0;
-            if (4 * q + k < tw) {
-                const int4 xt = xt_s[4 * q + k];
-                int p00, p01, p10, p11;
-                if (staged) {
-                    const uint8_t* r0 = wb + (yt.x - sy_lo) * kRsSrcCols - sx_lo;
-                    const uint8_t* r1 = wb + (yt.y - sy_lo) * kRsSrcCols - sx_lo;
-                    p00 = r0[xt.x]; p01 = r0[xt.y]; p10 = r1[xt.x]; p11 = r1[xt.y];
-                } else {
-                    const uint8_t* r0 = src + (long long)yt.x * S.pitch;
-                    const uint8_t* r1 = src + (long long)yt.y * S.pitch;
-                    p00 = r0[xt.x]; p01 = r0[xt.y]; p10 = r1[xt.x]; p11 = r1[xt.y];
+            for (int k = 0; k < 4; ++k) {
+                const int dx = dx0 + k;
+                int o = 0;
+                if (4 * q + k < tw) {
+                    const int4 xt = xt_s[4 * q + k];
+                    const int p00 = r0[xt.x], p01 = r0[xt.y], p10 = r1[xt.x], p11 = r1[xt.y];
+                    const int D0 = p00 * xt.z + p01 * xt.w;
+                    const int D1 = p10 * xt.z + p11 * xt.w;
+                    if (dx < G.simd_end) {
+                        const int s = (((D0 >> 4) * b0) >> 16) + (((D1 >> 4) * b1) >> 16);
+                        o = (s + 2) >> 2;
+                    } else {
+                        o = (D0 * b0 + D1 * b1 + (1 << 21)) >> 22;
+                    }
+                    o = o < 0 ? 0 : (o > 255 ? 255 : o);
                 }
-                const int D0 = p00 * xt.z + p01 * xt.w;
-                const int D1 = p10 * xt.z + p11 * xt.w;
-                if (dx < G.simd_end) {
-                    const int s = (((D0 >> 4) * b0) >> 16) + (((D1 >> 4) * b1) >> 16);
-                    o = (s + 2) >> 2;
-                } else {
-                    o = (D0 * b0 + D1 * b1 + (1 << 21)) >> 22;
-                }
-                o = o < 0 ? 0 : (o > 255 ? 255 : o);
+                packed |= (uint32_t)o << (8 * k);
             }
-            packed |= (uint32_t)o << (8 * k);
+            *reinterpret_cast<uint32_t*>(dst + (long long)dy * G.pitch + dx0) = packed;
         }
-        *reinterpret_cast<uint32_t*>(dst + (long long)dy * G.pitch + dx0) = packed;
+    };
+    if (staged) {
+        body([&](int sy) { return wb + (sy - sy_lo) * kRsSrcCols - sx_lo; });
+    } else {
+        body([&](int sy) { return src + (long long)sy * S.pitch; });
     }
 }
 
@@ -341,12 +341,18 @@ __global__ __launch_bounds__(kFastThreads) void k_fast_cells(BatchArgs a, int ce
 // k_octree: one workgroup per (level, image).  Gathers the level's cell lists in cell order
 // (vToDistributeKeys, :807-871) then runs DistributeOctTree (orb_octree.h) with the node
 // state in LDS (80 KB: two workgroups per CU).
+// kOctRetry: the level did not fit the LDS instantiation (node capacity, cell offsets or more
+// than kOctLdsKeys candidates); k_octree<false> then redoes it with generic pointers.
+constexpr int kOctRetry = -7;
+
+template <bool kLdsPath>
 __global__ __launch_bounds__(512, 4) void k_octree(BatchArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t nodemem_lds[];  // a.oct_lds_bytes
     __shared__ int scratch[16];
     __shared__ OctShared sh;
     const int img = a.img0 + blockIdx.x, l = blockIdx.y;  // level-major dispatch: the long level-0 groups go first
     const LevelGeom& G = a.lv[l];
+    if (!kLdsPath && a.status[img * kMaxLevels + l] != kOctRetry) return;
     DevPolicy p{scratch};
     const int32_t* cnt = a.cellcnt + (long long)img * a.cellcnt_img_stride + G.cellcnt_off;
     const uint32_t* ck = a.cellkeys + (long long)img * a.cellkeys_img_stride + G.cellkey_off;
@@ -373,7 +379,9 @@ __global__ __launch_bounds__(512, 4) void k_octree(BatchArgs a) {
     uint32_t* out_keys = a.lvlkey + (long long)img * a.lvlkp_img_stride + G.kp_off;
     unsigned long long* dbg = a.octdbg ? a.octdbg + ((long long)img * kMaxLevels + l) * 8 : nullptr;
     int r = n > G.cand_cap ? -3 : 0;
-    if (r == 0 && off_in_lds && G.oct_cap <= a.oct_lds_nodes && n <= kOctLdsKeys) {
+    const bool fits = off_in_lds && G.oct_cap <= a.oct_lds_nodes && n <= kOctLdsKeys && !a.oct_force_retry;
+    if (kLdsPath && r == 0 && !fits) r = kOctRetry;
+    if (kLdsPath && r == 0) {
         // everything node- and label-sized in LDS: ds_* accesses throughout
         OctWST<kLdsAS, kGlobalAS> w;
         w.keys = (asp<kGlobalAS, uint32_t>)keys;
@@ -389,7 +397,7 @@ __global__ __launch_bounds__(512, 4) void k_octree(BatchArgs a) {
         w.ncells = G.ncells;
         w.cell_cap = G.cell_cap;
         r = octree_distribute(p, w, (asp<kLdsAS, OctShared>)&sh, G.W, G.H, G.N);
-    } else if (r == 0) {
+    } else if (!kLdsPath && r == 0) {
         // huge levels: node state / labels / cell offsets in the global workspace where needed
         OctWST<kGeneric, kGeneric> w;
         w.keys = keys;
@@ -772,11 +780,17 @@ hipError_t launch_fast_cells(const BatchArgs& a, bool top, hipStream_t s) {
 }
 hipError_t launch_octree(const BatchArgs& a, hipStream_t s) {
     if (a.oct_lds_bytes > 65536) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k_octree),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, a.oct_lds_bytes);
-        if (e != hipSuccess) return e;
+        for (const void* f : {reinterpret_cast<const void*>(k_octree<true>),
+                              reinterpret_cast<const void*>(k_octree<false>)}) {
+            hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, a.oct_lds_bytes);
+            if (e != hipSuccess) return e;
+        }
     }
-    hipLaunchKernelGGL(k_octree, dim3(a.nimages, a.nlevels), dim3(512), a.oct_lds_bytes, s, a);
+    hipLaunchKernelGGL(k_octree<true>, dim3(a.nimages, a.nlevels), dim3(512), a.oct_lds_bytes, s, a);
+    // levels that did not fit the LDS instantiation (rare: > kOctLdsKeys candidates); every
+    // other block returns at once
+    if (a.oct_may_retry)
+        hipLaunchKernelGGL(k_octree<false>, dim3(a.nimages, a.nlevels), dim3(512), a.oct_lds_bytes, s, a);
     return hipGetLastError();
 }
 hipError_t launch_orient_desc(const BatchArgs& a, hipStream_t s) {

@@ -220,3 +220,15 @@ def test_general_fast_tile(oracle, frame0, monkeypatch):
     rk, rd, rm = oracle.extract(img, nfeatures=300, nlevels=4)
     _same_kps(k, rk)
     np.testing.assert_array_equal(d, rd)
+
+
+def test_octree_generic_instantiation(oracle, frame0, monkeypatch):
+    """Every level through k_octree<false> (generic pointers, the path taken by levels with
+    more candidates than the LDS label capacity), forced with ORBGPU_OCT_GENERIC."""
+    L, _ = frame0
+    monkeypatch.setenv("ORBGPU_OCT_GENERIC", "1")
+    ex = _extractor()
+    k, d, m = ex(L)
+    rk, rd, rm = oracle.extract(L, nfeatures=2000)
+    _same_kps(k, rk)
+    np.testing.assert_array_equal(d, rd)
