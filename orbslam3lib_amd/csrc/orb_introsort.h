@@ -235,9 +235,10 @@ struct SortScratchT {
 };
 using SortScratch = SortScratchT<kGeneric>;
 
+// Step 1 (partition phase) on policy p.
 template <int AS, class P>
-__host__ __device__ __attribute__((always_inline)) inline void introsort_parallel(P& p, asp<AS, SortElem> a, int m,
-                                            const SortScratchT<AS>& s, asp<AS, int> sh_nseg) {
+__host__ __device__ __attribute__((always_inline)) inline void introsort_partition(
+    P& p, asp<AS, SortElem> a, int m, const SortScratchT<AS>& s, asp<AS, int> sh_nseg) {
     const int tid = p.tid(), NT = p.nthreads();
     if (m <= 1) return;
     int cur = 0;
@@ -287,8 +288,8 @@ __host__ __device__ __attribute__((always_inline)) inline void introsort_paralle
                 rf = !node_less(pv, se_ld(a, i));
             }
             int tl, tr;
-            const int el = p.scan_excl(lf, &tl);
-            const int er = p.scan_excl(rf, &tr);
+            const int el = p.scan_small(lf, &tl);
+            const int er = p.scan_small(rf, &tr);
             if (i <= m) {
                 s.lex[i] = (uint16_t)(lc + el);
                 s.rex[i] = (uint16_t)(rc + er);
@@ -344,7 +345,7 @@ __host__ __device__ __attribute__((always_inline)) inline void introsort_paralle
                 c = (cut - f > 16) + (l - cut > 16);
             }
             int tot;
-            const int ex = p.scan_excl(c, &tot);
+            const int ex = p.scan_small(c, &tot);
             if (c) {
                 int o = carry + ex;
                 if (cut - f > 16) {
@@ -366,7 +367,14 @@ __host__ __device__ __attribute__((always_inline)) inline void introsort_paralle
         cur ^= 1;
         p.sync();
     }
-    // stable sort of the partitioned array
+}
+
+// Step 2: stable sort of the partitioned array (a rank sort, O(m^2 / threads)) on policy p.
+template <int AS, class P>
+__host__ __device__ __attribute__((always_inline)) inline void introsort_final(
+    P& p, asp<AS, SortElem> a, int m, const SortScratchT<AS>& s) {
+    const int tid = p.tid(), NT = p.nthreads();
+    if (m <= 1) return;
     for (int i = tid; i < m; i += NT) {
         const SortElem x = se_ld(a, i);
         int r = 0;
@@ -381,6 +389,13 @@ __host__ __device__ __attribute__((always_inline)) inline void introsort_paralle
     p.sync();
     for (int i = tid; i < m; i += NT) se_st(a, i, se_ld(s.tmp, i));
     p.sync();
+}
+
+template <int AS, class P>
+__host__ __device__ __attribute__((always_inline)) inline void introsort_parallel(
+    P& p, asp<AS, SortElem> a, int m, const SortScratchT<AS>& s, asp<AS, int> sh_nseg) {
+    introsort_partition<AS>(p, a, m, s, sh_nseg);
+    introsort_final<AS>(p, a, m, s);
 }
 
 }  // namespace orbgpu

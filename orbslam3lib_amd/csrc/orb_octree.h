@@ -104,7 +104,8 @@ struct OctWST {
     int ncells, cell_cap;
 };
 
-constexpr int kOctUnroll = 8;  // keys per thread per batch in the key passes
+constexpr int kOctUnroll = 8;         // keys per thread per batch in the key passes
+constexpr int kOctWaveSortMax = 128;  // final-phase sorts up to this size partition on one wave
 
 struct OctShared {
     int size, prev_size, nexp, ndiv, phase, done, nchild, nundiv, status, jstop;
@@ -275,7 +276,7 @@ __host__ __device__ __attribute__((always_inline)) inline int octree_distribute(
             const int i = base + ntid;
             const int v = (i < nIni && cur[i].cnt > 0) ? 1 : 0;
             int tot;
-            const int ex = np.scan_excl(v, &tot);
+            const int ex = np.scan_small(v, &tot);
             if (v) {
                 on_st(nxt, carry + ex, on_ld(cur, i));
                 M.undivpos[i] = (uint16_t)(carry + ex);
@@ -349,19 +350,34 @@ __host__ __device__ __attribute__((always_inline)) inline int octree_distribute(
     };
     while (!sh->done) {
         if (++guard > 4096) return -4;
-        if (sh->phase != 1) {  // final phase: libstdc++-ordered sort of vPrev by the whole block
+        if (sh->phase != 1) {  // final phase: libstdc++-ordered sort of vPrev
+            // partition rounds: wave 0 alone for small arrays (no workgroup barriers), the
+            // whole block for large ones (more segments and elements per round)
             const int m = sh->nexp;
             auto sb = reinterpret_cast<asp<LAS, SortElem>>(nxt);  // nxt is free until the rebuild
-            for (int j = tid; j < m; j += NT) {
-                const int v = vsz[j];
-                SortElem e;
-                e.size = cur[v].cnt;
-                e.ulx = cur[v].x0;
-                e.node = v;
-                se_st(sb, j, e);
+            auto fill = [&](auto& q) __attribute__((always_inline)) {
+                for (int j = q.tid(); j < m; j += q.nthreads()) {
+                    const int v = vsz[j];
+                    SortElem e;
+                    e.size = cur[v].cnt;
+                    e.ulx = cur[v].x0;
+                    e.node = v;
+                    se_st(sb, j, e);
+                }
+                q.sync();
+                introsort_partition<LAS>(q, sb, m, sort_scratch(cnxt), &sh->jstop);
+            };
+            if (m > kOctWaveSortMax) {
+                fill(p);
+            } else if (nw) {
+                auto np = p.node();
+                fill(np);
             }
+        }
+        if (sh->phase != 1) {  // the O(m^2) stable rank pass spreads over the whole block
             p.sync();
-            introsort_parallel<LAS>(p, sb, m, sort_scratch(cnxt), &sh->jstop);
+            introsort_final<LAS>(p, reinterpret_cast<asp<LAS, SortElem>>(nxt), sh->nexp,
+                                 sort_scratch(cnxt));
             p.sync();
             mark(3);
         }
@@ -378,7 +394,7 @@ __host__ __device__ __attribute__((always_inline)) inline int octree_distribute(
                     const int i = base + ntid;
                     const int v = (i < size && cur[i].cnt > 1) ? 1 : 0;
                     int tot;
-                    const int ex = np.scan_excl(v, &tot);
+                    const int ex = np.scan_small(v, &tot);
                     if (i < size) M.divrank[i] = v ? carry + ex : -1;
                     carry += tot;
                 }
@@ -396,8 +412,8 @@ __host__ __device__ __attribute__((always_inline)) inline int octree_distribute(
                         }
                     }
                     int t1, t2;
-                    const int e1 = np.scan_excl(nc, &t1);
-                    const int e2 = np.scan_excl(ne, &t2);
+                    const int e1 = np.scan_small(nc, &t1);
+                    const int e2 = np.scan_small(ne, &t2);
                     if (i < size && cur[i].cnt > 1) {
                         M.blockoff[i] = (uint16_t)(c1 + e1 + nc);  // inclusive; finalised below
                         M.expoff[i] = (uint16_t)(c2 + e2);
@@ -431,8 +447,11 @@ __host__ __device__ __attribute__((always_inline)) inline int octree_distribute(
                         for (int q = 0; q < 4; ++q) d += ccur[4 * v + q] > 0;
                         d -= 1;
                     }
+                    // d in [-1, 3]: scan d + 1 over the valid lanes (a prefix of the wave)
+                    const int nvalid = m - base < NNT ? m - base : NNT;
                     int tot;
-                    const int ex = np.scan_excl(d, &tot);
+                    const int ex = np.scan_small(t < m ? d + 1 : 0, &tot) - (ntid < nvalid ? ntid : nvalid);
+                    tot -= nvalid;
                     if (t < m && size + carry + ex + d >= N) np.atomic_max_int(&sh->jstop, j);
                     carry += tot;
                 }
@@ -452,8 +471,8 @@ __host__ __device__ __attribute__((always_inline)) inline int octree_distribute(
                         }
                     }
                     int t1, t2;
-                    const int e1 = np.scan_excl(nc, &t1);  // children of ranks > r (j' < j)
-                    const int e2 = np.scan_excl(ne, &t2);
+                    const int e1 = np.scan_small(nc, &t1);  // children of ranks > r (j' < j)
+                    const int e2 = np.scan_small(ne, &t2);
                     if (j < m) {
                         M.divrank[v] = m - 1 - j;
                         M.blockoff[v] = (uint16_t)(c1 + e1);
@@ -485,7 +504,7 @@ __host__ __device__ __attribute__((always_inline)) inline int octree_distribute(
                     const int i = base + ntid;
                     const int v = (i < size && M.divrank[i] < 0) ? 1 : 0;
                     int tot;
-                    const int ex = np.scan_excl(v, &tot);
+                    const int ex = np.scan_small(v, &tot);
                     if (v) {
                         const int pos = nchild + carry + ex;
                         M.undivpos[i] = (uint16_t)pos;

@@ -48,6 +48,13 @@ struct WaveScanPolicy {
         *total = __shfl(x, 63, 64);
         return x - v;
     }
+    // exclusive scan of values in [0, 7] by bit-sliced ballots (no cross-lane data movement)
+    __device__ int scan_small(int v, int* total) {
+        const uint64_t lt = (1ull << (threadIdx.x & 63)) - 1ull;
+        const uint64_t b0 = __ballot(v & 1), b1 = __ballot(v & 2), b2 = __ballot(v & 4);
+        *total = __popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2);
+        return __popcll(b0 & lt) + 2 * __popcll(b1 & lt) + 4 * __popcll(b2 & lt);
+    }
 };
 
 struct DevPolicy {
@@ -108,6 +115,26 @@ struct DevPolicy {
         *total = tot;
         return before + x - v;
     }
+    // block-wide exclusive scan of values in [0, 7]: ballots inside the wave, one LDS hop
+    __device__ int scan_small(int v, int* total) {
+        const int lane = (int)(threadIdx.x & 63), wid = (int)(threadIdx.x >> 6);
+        const int nw = (int)((blockDim.x + 63) >> 6);
+        const uint64_t lt = (1ull << lane) - 1ull;
+        const uint64_t b0 = __ballot(v & 1), b1 = __ballot(v & 2), b2 = __ballot(v & 4);
+        const int wtot = __popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2);
+        const int ex = __popcll(b0 & lt) + 2 * __popcll(b1 & lt) + 4 * __popcll(b2 & lt);
+        __syncthreads();  // scratch may still be read by the previous call
+        if (lane == 0) scratch[wid] = wtot;
+        __syncthreads();
+        int before = 0, tot = 0;
+        for (int w = 0; w < nw; ++w) {
+            const int s = scratch[w];
+            before += (w < wid) ? s : 0;
+            tot += s;
+        }
+        *total = tot;
+        return before + ex;
+    }
 };
 
 // One wave on its own (64 lanes), e.g. one FAST cell per wave: "sync" is a wave-level memory
@@ -154,6 +181,10 @@ struct SerialPolicy {
         return o;
     }
     __host__ __device__ int scan_excl(int v, int* total) {
+        *total = v;
+        return 0;
+    }
+    __host__ __device__ int scan_small(int v, int* total) {
         *total = v;
         return 0;
     }
