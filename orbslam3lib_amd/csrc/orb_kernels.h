@@ -89,6 +89,7 @@ struct MatchArgs {
 // Octree workspace layout for one (image, level) with n_cap keys and node capacity C.  The node
 // state lives in LDS when C <= kOctLdsNodes, otherwise in the `nodemem` part of this block.
 constexpr int kOctLdsNodes = 1024;
+constexpr int kOdKpBlock = 8;  // keypoints per k_orient_desc block (256 threads / 32 lanes)
 
 constexpr int kOctLdsKeys = 16384;  // per-key node labels (u16) kept in LDS up to this many keys
 

@@ -423,18 +423,31 @@ __global__ __launch_bounds__(512, 4) void k_octree(BatchArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// k_orient_desc: one wave per keypoint.  IC_Angle on the raw level (ORBextractor_old.cc:78-105)
-// then computeOrbDescriptor on the blurred level (:108-148): a = (float)cos, b = (float)sin of
+// k_orient_desc: IC_Angle on the raw level (ORBextractor_old.cc:78-105) then
+// computeOrbDescriptor on the blurred level (:108-148): a = (float)cos, b = (float)sin of
 // angle*pi/180 (float), sample center[cvRound(x*b + y*a)*step + cvRound(x*a - y*b)].
-// 16 lanes per keypoint (4 keypoints per wave, independent groups): every lane owns <= 2 disc
-// rows for the moments (dword row loads) and 16 of the 256 test pairs (two descriptor bytes),
-// sampled straight from the L2-resident blurred level.
+// kOdLanes lanes per keypoint (independent groups inside a wave): lane `sub` owns disc rows
+// v = sub - 15 + h * kOdLanes (one row at 32 lanes) for the moments and 256 / kOdLanes of the
+// test pairs, sampled from the keypoint's blurred patch staged in LDS.  The kernel waits on
+// three dependent memory round trips per keypoint (key, moment rows + patch, samples); few
+// vector-memory instructions and registers per lane keep many of them in flight.
+constexpr int kOdLanes = 32;                   // lanes per keypoint
+constexpr int kOdRows = 32 / kOdLanes;         // disc rows per lane
+constexpr int kOdPairs = 256 / kOdLanes;       // test pairs per lane
+static_assert(kOdKpBlock == 256 / kOdLanes, "orb_kernels.h kOdKpBlock");
+
+constexpr int kOdPatchR = 18;                    // |rotated pattern offset| <= 13*sqrt(2) < 19
+constexpr int kOdPatchRows = 2 * kOdPatchR + 1;  // 37
+constexpr int kOdPatchPitch = 48;                // 3 x 16 B: covers x-18..x+18 from the dword below
+
 __global__ __launch_bounds__(256) void k_orient_desc(BatchArgs a) {
+    // per keypoint group: the blurred patch around the keypoint, staged with 16-byte loads
+    __shared__ __attribute__((aligned(16))) uint8_t patch[kOdKpBlock][kOdPatchRows * kOdPatchPitch];
     const int img = a.img0 + blockIdx.y;
     int l = 0;
     while (l + 1 < a.nlevels && (int)blockIdx.x >= a.lv[l + 1].od_first) ++l;
     const LevelGeom& G = a.lv[l];
-    const int sub = threadIdx.x & 15, grp = threadIdx.x >> 4;
+    const int sub = threadIdx.x % kOdLanes, grp = threadIdx.x / kOdLanes;
     const int count = a.lvlcnt[img * kMaxLevels + l];
     const long long kbase = (long long)img * a.lvlkp_img_stride + G.kp_off;
     const uint8_t* lvl = a.lvl_base[l] + (long long)img * G.img_stride;
@@ -443,16 +456,16 @@ __global__ __launch_bounds__(256) void k_orient_desc(BatchArgs a) {
     // raw buffer over this image's blurred level (dword 3 = gfx9 raw-buffer format word)
     const __amdgpu_buffer_rsrc_t brs =
         __builtin_amdgcn_make_buffer_rsrc((void*)blr, (short)0, G.bpitch * G.h, 0x00020000);
-    const int stride_k = G.od_blocks * 16;
-    // this lane's disc rows v = sub-15 and sub+1 (none for sub = 15) and, per row, byte masks of
-    // the 32-byte window u = -15..16 restricted to |u| <= umax[|v|]
-    int vrow[2];
-    uint32_t msk[2][8];
+    const int stride_k = G.od_blocks * kOdKpBlock;
+    // this lane's disc rows and, per row, byte masks of the 32-byte window u = -15..16
+    // restricted to |u| <= umax[|v|] (rows past v = 15 are empty)
+    int vrow[kOdRows];
+    uint32_t msk[kOdRows][8];
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        const int v = h == 0 ? sub - 15 : sub + 1;
-        const int d = (h == 1 && sub == 15) ? -1 : c_umax[v < 0 ? -v : v];
-        vrow[h] = (h == 1 && sub == 15) ? 0 : v;
+    for (int h = 0; h < kOdRows; ++h) {
+        const int v = sub - 15 + h * kOdLanes;
+        const int d = v > 15 ? -1 : c_umax[v < 0 ? -v : v];
+        vrow[h] = v > 15 ? 0 : v;
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             uint32_t m = 0;
@@ -464,37 +477,44 @@ __global__ __launch_bounds__(256) void k_orient_desc(BatchArgs a) {
             msk[h][i] = m;
         }
     }
-    // this lane's 16 test pairs (x0,y0,x1,y1 int8), packed
-    uint32_t patw[16];
+    // this lane's test pairs (x0,y0,x1,y1 int8), packed
+    uint32_t patw[kOdPairs];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) patw[i] = reinterpret_cast<const uint32_t*>(c_pattern.v)[sub * 16 + i];
-    // uniform trip count per wave so the 16-lane shuffles see all lanes
-    const int wave_first = (blockIdx.x - G.od_first) * 16 + (threadIdx.x >> 6) * 4;
+    for (int i = 0; i < kOdPairs; ++i)
+        patw[i] = reinterpret_cast<const uint32_t*>(c_pattern.v)[sub * kOdPairs + i];
+    // uniform trip count per wave so the group shuffles see all lanes
+    const int wave_first = (blockIdx.x - G.od_first) * kOdKpBlock + (threadIdx.x >> 6) * (64 / kOdLanes);
     for (int kb = wave_first; kb < count; kb += stride_k) {
-        const int kp = kb + (grp & 3);
+        const int kp = kb + (grp % (64 / kOdLanes));
         const bool valid = kp < count;
         const uint32_t key = valid ? a.lvlkey[kbase + kp] : a.lvlkey[kbase + kb];
         const int x = key_x(key) + kMinBorder, y = key_y(key) + kMinBorder;
-        // IC_Angle moments (ORBextractor_old.cc:78-105) on two disc rows per lane: the row window
-        // is byte-aligned with v_alignbyte, masked to the disc, then
+        // IC_Angle moments (ORBextractor_old.cc:78-105): the row window is byte-aligned with
+        // v_alignbyte, masked to the disc, then
         //   s = sum of bytes (v_sad_u8), sum u*p = dot4(bytes, {4i..4i+3}) - 15 s
         int m10 = 0, m01 = 0;
         const int x0 = x - 15;
         const int xa = raw_dw ? (x0 & ~3) : x0;
         const int shf = x0 - xa;
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
+        for (int h = 0; h < kOdRows; ++h) {
             const uint8_t* row = lvl + (long long)(y + vrow[h]) * G.pitch;
             uint32_t w[9];
+            if (raw_dw) {  // 2 x dwordx4 + 1 dword (global loads need only dword alignment)
+                const uint4 A = *reinterpret_cast<const uint4*>(row + xa);
+                const uint4 B = *reinterpret_cast<const uint4*>(row + xa + 16);
+                w[0] = A.x; w[1] = A.y; w[2] = A.z; w[3] = A.w;
+                w[4] = B.x; w[5] = B.y; w[6] = B.z; w[7] = B.w;
+                w[8] = *reinterpret_cast<const uint32_t*>(row + xa + 32);
+            } else {
 #pragma unroll
             for (int i = 0; i < 9; ++i) {
-                if (raw_dw) {
-                    w[i] = *reinterpret_cast<const uint32_t*>(row + xa + 4 * i);
-                } else {
+                {
                     const uint8_t* q = row + xa + 4 * i;
                     w[i] = (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16) |
                            ((uint32_t)q[3] << 24);
                 }
+            }
             }
             uint32_t sacc = 0, uacc = 0;
 #pragma unroll
@@ -508,40 +528,59 @@ __global__ __launch_bounds__(256) void k_orient_desc(BatchArgs a) {
             m01 += vrow[h] * (int)sacc;
         }
 #pragma unroll
-        for (int o = 8; o >= 1; o >>= 1) {
-            m10 += __shfl_xor(m10, o, 16);
-            m01 += __shfl_xor(m01, o, 16);
+        for (int o = kOdLanes / 2; o >= 1; o >>= 1) {
+            m10 += __shfl_xor(m10, o, kOdLanes);
+            m01 += __shfl_xor(m01, o, kOdLanes);
         }
         const float angle = fast_atan2_deg((float)m01, (float)m10);
-        // computeOrbDescriptor (:108-148): lane `sub` makes bytes 2*sub and 2*sub+1
+        // computeOrbDescriptor (:108-148): lane `sub` makes bits [sub * kOdPairs, + kOdPairs)
         const float factorPI = (float)(3.14159265358979323846 / 180.0);
         const float ang = angle * factorPI;
         double sd, cd;
         sincos((double)ang, &sd, &cd);
         const float ca = (float)cd, sn = (float)sd;
-        // all 32 samples of this lane are issued before any is used (one memory round trip);
-        // buffer loads with 32-bit offsets keep the addresses in one VGPR each
+        // the 37 x 37 blurred patch (rows y-18..y+18 from the dword at or below x-18) goes to
+        // LDS with 16-byte buffer loads (out-of-range bytes read as 0 and are never sampled),
+        // then every sample is an LDS byte read: 4 vector-memory instructions per lane
+        // instead of one scattered byte load per sample
         const int pitch = G.bpitch;
-        const int cofs = y * pitch + x;
-        uint32_t t[32];
+        const int xb = (x - kOdPatchR) & ~3;
+        const int pofs = (y - kOdPatchR) * pitch + xb;
+        uint8_t* pt = patch[grp];
 #pragma unroll
-        for (int e = 0; e < 32; ++e) {
-            // the packed pattern word is opaque here, so its 64 float conversions are not
-            // hoisted out of the keypoint loop (that would hold 64 VGPRs across it)
+        for (int it = 0; it < (kOdPatchRows * 3 + kOdLanes - 1) / kOdLanes; ++it) {
+            const int c = sub + it * kOdLanes;
+            if (c < kOdPatchRows * 3) {
+                const int r = c / 3, part = c - 3 * r;
+                const auto v = __builtin_amdgcn_raw_buffer_load_b128(brs, pofs + r * pitch + 16 * part, 0, 0);
+                *reinterpret_cast<uint4*>(pt + r * kOdPatchPitch + 16 * part) = make_uint4(v[0], v[1], v[2], v[3]);
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the group's own lanes read it
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const int pc = kOdPatchR * kOdPatchPitch + (x - xb);  // patch offset of the keypoint
+        uint32_t t[2 * kOdPairs];
+#pragma unroll
+        for (int e = 0; e < 2 * kOdPairs; ++e) {
+            // the packed pattern word is opaque here, so its float conversions are not hoisted
+            // out of the keypoint loop (that would hold 4 VGPRs per pair across it)
             uint32_t pw = patw[e >> 1];
             asm volatile("" : "+v"(pw));
             const int sh8 = 16 * (e & 1);
             const float px = (float)(int8_t)(pw >> sh8), py = (float)(int8_t)(pw >> (sh8 + 8));
             const int ry = cv_round(px * sn + py * ca);
             const int rx = cv_round(px * ca - py * sn);
-            t[e] = __builtin_amdgcn_raw_buffer_load_b8(brs, cofs + ry * pitch + rx, 0, 0);
+            t[e] = pt[pc + ry * kOdPatchPitch + rx];
         }
         uint32_t bits = 0;
 #pragma unroll
-        for (int b = 0; b < 16; ++b) bits |= (uint32_t)(t[2 * b] < t[2 * b + 1]) << b;
+        for (int b = 0; b < kOdPairs; ++b) bits |= (uint32_t)(t[2 * b] < t[2 * b + 1]) << b;
         if (valid) {
             if (sub == 0) a.lvlangle[kbase + kp] = angle;
-            reinterpret_cast<uint16_t*>(a.lvldesc + (kbase + kp) * 32)[sub] = (uint16_t)bits;
+            uint8_t* dd = a.lvldesc + (kbase + kp) * 32;
+            if (kOdPairs == 8) dd[sub] = (uint8_t)bits;
+            else reinterpret_cast<uint16_t*>(dd)[sub] = (uint16_t)bits;
         }
     }
 }

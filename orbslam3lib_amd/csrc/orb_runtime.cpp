@@ -284,7 +284,7 @@ int set_geometry(orbgpu_ctx* c, int w, int h) {
         G.tiles_y = (G.h + 31) / 32;
         G.tile_first = tile_first;
         tile_first += G.tiles_x * G.tiles_y;
-        G.od_blocks = std::max(1, (G.N + 16 + 15) / 16);  // 16 keypoints per block
+        G.od_blocks = std::max(1, (G.N + 16 + kOdKpBlock - 1) / kOdKpBlock);  // k_orient_desc blocks
         G.od_first = od_first;
         od_first += G.od_blocks;
         G.area2 = 0;
