@@ -71,10 +71,11 @@ __constant__ MomentWeights c_mw = make_moment_weights();
 // 128-bit SIMD body for x < simd_end, FixedPtCast tail after.  A block makes a 256 x 16 output
 // tile: its x-table slice and the source window (dword loads) are staged in LDS first.
 constexpr int kRsTW = 256, kRsTH = 16, kRsSrcRows = 2 * kRsTH + 2, kRsSrcCols = 2 * kRsTW + 16;
+static_assert(kRsSrcCols % 16 == 0, "window rows are written in 16-byte chunks");
 
 __global__ __launch_bounds__(256) void k_resize(BatchArgs a, int l) {
     __shared__ int4 xt_s[kRsTW];
-    __shared__ uint32_t win[kRsSrcRows][kRsSrcCols / 4];
+    __shared__ __attribute__((aligned(16))) uint32_t win[kRsSrcRows][kRsSrcCols / 4];
     const LevelGeom& G = a.lv[l];
     const LevelGeom& S = a.lv[l - 1];
     const int img = a.img0 + blockIdx.z;
@@ -106,19 +107,18 @@ __global__ __launch_bounds__(256) void k_resize(BatchArgs a, int l) {
     const int nrows = sy_hi - sy_lo + 1, ndw = (sx_hi - sx_lo) / 4 + 1;
     const bool staged = nrows <= kRsSrcRows && ndw <= kRsSrcCols / 4 && (S.pitch & 3) == 0;
     if (staged) {
-        for (int i = threadIdx.x; i < nrows * ndw; i += 256) {
-            const int r = i / ndw, c = i % ndw;
-            const uint8_t* row = src + (long long)(sy_lo + r) * S.pitch;
-            const int x = sx_lo + 4 * c;
-            uint32_t v;
-            if (x + 4 <= S.w) {
-                v = *reinterpret_cast<const uint32_t*>(row + x);
-            } else {
-                v = 0;
-                for (int b = 0; b < 4; ++b)
-                    if (x + b < S.w) v |= (uint32_t)row[x + b] << (8 * b);
+        // 16-byte buffer loads (bounds-checked: bytes past the plane read as 0 and are never
+        // used); half a wave per source row, no integer division
+        const __amdgpu_buffer_rsrc_t srs = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)src, (short)0, (int)min(S.img_stride, 0x7fffffffLL), 0x00020000);
+        const int nq4 = (ndw + 3) >> 2;  // 16-byte chunks per row (<= 33)
+        const int half = threadIdx.x >> 5, hl = threadIdx.x & 31;
+        for (int r = half; r < nrows; r += 8) {
+            const int rowofs = (sy_lo + r) * S.pitch + sx_lo;
+            for (int c = hl; c < nq4; c += 32) {
+                const auto v = __builtin_amdgcn_raw_buffer_load_b128(srs, rowofs + 16 * c, 0, 0);
+                *reinterpret_cast<uint4*>(&win[r][4 * c]) = make_uint4(v[0], v[1], v[2], v[3]);
             }
-            win[r][c] = v;
         }
     }
     __syncthreads();
