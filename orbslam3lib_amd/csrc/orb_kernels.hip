@@ -12,6 +12,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "orb_kernels.h"
 #include "orb_math.h"
 #include "orb_fast_cell.h"
@@ -185,47 +187,97 @@ typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 __device__ inline u16x2 as_u16x2(uint32_t x) { return __builtin_bit_cast(u16x2, x); }
 __device__ inline uint32_t as_u32(u16x2 x) { return __builtin_bit_cast(uint32_t, x); }
 
+struct BlurTile {
+    int l, ty0, tx0;
+    const uint8_t* src;
+    uint8_t* dst;
+};
+
+__device__ inline BlurTile blur_tile(const BatchArgs& a, int t) {
+    BlurTile bt;
+    const int img = a.img0 + t / a.total_tiles;
+    int k = t % a.total_tiles;
+    int l = 0;
+    while (l + 1 < a.nlevels && k >= a.lv[l + 1].tile_first) ++l;
+    const LevelGeom& G = a.lv[l];
+    k -= G.tile_first;
+    bt.l = l;
+    bt.ty0 = (k / G.tiles_x) * kBlurTH;
+    bt.tx0 = (k % G.tiles_x) * kBlurTW;
+    bt.src = a.lvl_base[l] + (long long)img * G.img_stride;
+    bt.dst = a.blur_base[l] + (long long)img * G.bimg_stride;
+    return bt;
+}
+
+// Window chunk i (16 bytes) of tile bt: rows reflected here (REFLECT_101), columns loaded as
+// they are (bounds-checked buffer load; chunks left of the plane are zero) -- the few column
+// bytes outside the plane that the taps reach are reflected in LDS afterwards (blur_fix_cols).
+__device__ inline uint4 blur_chunk(const BatchArgs& a, const BlurTile& bt, int i, int IWQ) {
+    const LevelGeom& G = a.lv[bt.l];
+    const int r = i / IWQ, cq = i - r * IWQ;
+    // rows beyond the reflected range feed only zero weights or unwritten outputs: clamp
+    const int y = min(max(refl101(bt.ty0 + r - 4, G.h), 0), G.h - 1);
+    const int x = bt.tx0 - 16 + 16 * cq;
+    if (x < 0) return make_uint4(0, 0, 0, 0);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)bt.src, (short)0, (int)min(G.img_stride, 0x7fffffffLL), 0x00020000);
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, y * G.pitch + x, 0, 0);
+    return make_uint4(v[0], v[1], v[2], v[3]);
+}
+
+// Persistent over the tiles of the launch (images x levels x tiles): the next tile's window
+// is loaded into registers while the current one is filtered, so the global-memory round
+// trip is hidden behind the arithmetic of the previous tile.
 __global__ __launch_bounds__(256) void k_blur(BatchArgs a) {
     constexpr int IW = kBlurTW + 32, IH = kBlurTH + 8, IWQ = IW / 16, NRP = IH / 2;
+    constexpr int NCH = (IH * IWQ + 255) / 256;  // window chunks per thread
     __shared__ uint4 tin4[IH][IWQ];
     __shared__ uint4 hp[NRP][kBlurTW / 4];  // [row pair][column quad]: 4 columns x (row0,row1)
-    const int img = a.img0 + blockIdx.y;
-    int l = 0;
-    while (l + 1 < a.nlevels && (int)blockIdx.x >= a.lv[l + 1].tile_first) ++l;
-    const LevelGeom& G = a.lv[l];
-    const int t = blockIdx.x - G.tile_first;
-    const int ty0 = (t / G.tiles_x) * kBlurTH, tx0 = (t % G.tiles_x) * kBlurTW;
-    const uint8_t* src = a.lvl_base[l] + (long long)img * G.img_stride;
-    uint8_t* dst = a.blur_base[l] + (long long)img * G.bimg_stride;
-    const bool vec_ok = (G.pitch & 15) == 0;
-    for (int i = threadIdx.x; i < IH * IWQ; i += 256) {
-        const int r = i / IWQ, cq = i - r * IWQ;
-        // rows beyond the reflected range feed only zero weights or unwritten outputs: clamp
-        const int y = min(max(refl101(ty0 + r - 4, G.h), 0), G.h - 1);
-        const int x = tx0 - 16 + 16 * cq;
-        const uint8_t* row = src + (long long)y * G.pitch;
-        uint4 v;
-        if (vec_ok && x >= 0 && x + 16 <= G.w) {
-            v = *reinterpret_cast<const uint4*>(row + x);
-        } else {  // plane edge: per byte with reflection
-            uint32_t w4[4];
+    const int total = a.total_tiles * a.nimages;
+    int t = blockIdx.x;
+    if (t >= total) return;
+    BlurTile bt = blur_tile(a, t);
+    uint4 pre[NCH];
 #pragma unroll
-            for (int d = 0; d < 4; ++d) {
-                uint32_t u = 0;
-#pragma unroll
-                for (int b = 0; b < 4; ++b) {
-                    const int xx = x + 4 * d + b;
-                    const uint32_t px = (xx > -G.w && xx < G.w + 3) ? row[min(max(refl101(xx, G.w), 0), G.w - 1)] : 0u;
-                    u |= px << (8 * b);
-                }
-                w4[d] = u;
-            }
-            v = make_uint4(w4[0], w4[1], w4[2], w4[3]);
-        }
-        tin4[r][cq] = v;
+    for (int c = 0; c < NCH; ++c) {
+        const int i = threadIdx.x + 256 * c;
+        if (i < IH * IWQ) pre[c] = blur_chunk(a, bt, i, IWQ);
     }
+    for (; t < total; t += gridDim.x) {
+        const BlurTile cur = bt;
+        const LevelGeom& G = a.lv[cur.l];
+        const int ty0 = cur.ty0, tx0 = cur.tx0;
+        uint8_t* dst = cur.dst;
+        __syncthreads();  // the previous tile's passes are done with tin4 / hp
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+            const int i = threadIdx.x + 256 * c;
+            if (i < IH * IWQ) (&tin4[0][0])[i] = pre[c];
+        }
+        const int tn = t + gridDim.x;
+        if (tn < total) {  // prefetch the next window
+            bt = blur_tile(a, tn);
+#pragma unroll
+            for (int c = 0; c < NCH; ++c) {
+                const int i = threadIdx.x + 256 * c;
+                if (i < IH * IWQ) pre[c] = blur_chunk(a, bt, i, IWQ);
+            }
+        }
     const uint32_t(*tin)[IW / 4] = reinterpret_cast<const uint32_t(*)[IW / 4]>(&tin4[0][0]);
     __syncthreads();
+    if (tx0 == 0 || tx0 + kBlurTW + 3 > G.w) {  // REFLECT_101 of the 3 columns past each edge
+        uint8_t* wb = reinterpret_cast<uint8_t*>(&tin4[0][0]);
+        for (int i = threadIdx.x; i < IH * 6; i += 256) {
+            const int r = i / 6, k = i - 6 * r;
+            const int xx = k < 3 ? -1 - k : G.w + (k - 3);  // plane column to fill
+            const int wx = xx - (tx0 - 16);                  // its window column
+            if (wx >= 0 && wx < IW && (k < 3 ? tx0 == 0 : true)) {
+                const int sx = refl101(xx, G.w) - (tx0 - 16);
+                wb[r * IW + wx] = wb[r * IW + sx];
+            }
+        }
+        __syncthreads();
+    }
     // horizontal: item (row pair rp, column quad cq) -> output cols 4cq..4cq+3 need window
     // bytes 4cq+13 .. 4cq+22 (dwords cq+3 .. cq+5)
     for (int i = threadIdx.x; i < NRP * (kBlurTW / 4); i += 256) {
@@ -289,6 +341,7 @@ __global__ __launch_bounds__(256) void k_blur(BatchArgs a) {
         const uint32_t hi = __builtin_amdgcn_perm(sv[3], sv[2], 0x0c0c0602u);
         const uint32_t packed = lo | (hi << 16);
         if (y < G.h && x < G.w) *reinterpret_cast<uint32_t*>(dst + (long long)y * G.bpitch + x) = packed;
+    }
     }
 }
 
@@ -804,7 +857,9 @@ hipError_t launch_resize(const BatchArgs& a, int level, hipStream_t s) {
     return hipGetLastError();
 }
 hipError_t launch_blur(const BatchArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(k_blur, dim3(a.total_tiles, a.nimages), dim3(256), 0, s, a);
+    // persistent: 8192 workgroups (32 per CU, about 4 resident at a time) loop over the tiles
+    const int total = a.total_tiles * a.nimages;
+    hipLaunchKernelGGL(k_blur, dim3(std::min(total, 8192)), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 hipError_t launch_fast_cells(const BatchArgs& a, bool top, hipStream_t s) {
