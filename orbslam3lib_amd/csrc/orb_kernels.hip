@@ -350,7 +350,7 @@ __global__ __launch_bounds__(256) void k_blur(BatchArgs a) {
 // ComputeKeyPointsOctTree (ORBextractor_old.cc:807-871) with cv::FAST(cell, kps, th, true):
 // detection on [3,rows-3)x[3,cols-3) of the cell ROI, 3x3 nonmax inside the cell only, iniTh
 // then minTh if the cell yields nothing, keys emitted in row-major order.
-constexpr int kFastThreads = 256;  // one workgroup (4 waves) per cell
+constexpr int kFastThreads = 128;  // one workgroup (2 waves) per cell
 
 template <int CP>
 __global__ __launch_bounds__(kFastThreads) void k_fast_cells(BatchArgs a, int cell0) {
