@@ -51,29 +51,6 @@ __host__ __device__ inline bool fast_kept(const uint8_t* M, int off, int t) {
     return true;
 }
 
-// cv::FAST segment test at threshold t (strict > / <), exact.
-// Per ring point one word q = C1 - 65535 p: low half p + t + 512 - v, high half v + t + 512 - p,
-// both in [257, 1022], so bit 9 clear <=> v - p > t (dark) and bit 25 clear <=> p - v > t
-// (bright).  A 9-arc of events exists iff some OR over 9 consecutive q has the bit clear.
-template <int P>
-__host__ __device__ inline bool fast_corner(const uint8_t* c, int t) {
-    const int v = c[0];
-    const int C1 = (t + 512 - v) + ((v + t + 512) << 16);
-    uint32_t q[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        const int p = c[ring_dx(k) + ring_dy(k) * P];
-        q[k] = (uint32_t)(C1 + p * -65535);
-    }
-    uint32_t o3[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) o3[k] = q[k] | q[(k + 1) & 15] | q[(k + 2) & 15];
-    uint32_t r = 0xFFFFFFFFu;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) r &= o3[k] | o3[(k + 3) & 15] | o3[(k + 6) & 15];
-    return (~r & 0x02000200u) != 0;
-}
-
 // Per-cell scratch (LDS on the GPU).
 struct CellScratch {
     uint8_t* T;        // [P * P], 4-byte aligned
@@ -148,18 +125,19 @@ __host__ __device__ int fast_cell_run(Pol& p, const uint8_t* src, long long pitc
             if ((m >> lane) & 1ull) list[na + p.popc64(m & lt)] = (uint16_t)o;
             na += p.popc64(m);
         }
+        // exact strength of every candidate (m > t <=> corner at t), corners kept in order
         int nb = 0;
         for (int base = 0; base < na; base += L) {
             const int j = base + lane;
-            const int o = j < na ? list[j] : 0;
-            const bool f = j < na && fast_corner<CP>(&T[o], t);
+            const int o = list[j < na ? j : 0];
+            const int sm = fast_strength_packed<CP>(&T[o]);
+            const bool f = j < na && sm > t;
             const uint64_t m = p.ballot(f);
-            if (f) list[nb + p.popc64(m & lt)] = (uint16_t)o;  // in place: never passes the reads
+            if (f) {
+                list[nb + p.popc64(m & lt)] = (uint16_t)o;  // in place: never passes the reads
+                M[o] = (uint8_t)sm;
+            }
             nb += p.popc64(m);
-        }
-        for (int j = lane; j < nb; j += L) {
-            const int o = list[j];
-            M[o] = (uint8_t)fast_strength_corner(&T[o], CP);
         }
         return nb;
     };

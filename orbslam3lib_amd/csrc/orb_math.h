@@ -91,6 +91,38 @@ __host__ __device__ inline int fast_strength_corner(const uint8_t* c, int stride
     return s > 255 ? 255 : s;
 }
 
+// The same strength with both polarities in one 32-bit word per ring point: low half
+// d + 256, high half -d + 256 (d = v - p, both halves in [1, 511], so one v_mad_u32_u24
+// builds the word), then 9-arc minima and the maximum over arcs with packed u16 min/max:
+// low = sdark + 256, high = -bmin + 256.  Exact for any pixel; m > t <=> FAST corner at t.
+typedef unsigned short orb_u16x2 __attribute__((ext_vector_type(2)));
+
+template <int STRIDE>
+__host__ __device__ inline int fast_strength_packed(const uint8_t* c) {
+    const int v = c[0];
+    const uint32_t cv = (uint32_t)(v + 256) + ((uint32_t)(256 - v) << 16);
+    orb_u16x2 x[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const uint32_t p = c[ring_dx(k) + ring_dy(k) * STRIDE];
+        x[k] = __builtin_bit_cast(orb_u16x2, p * 65535u + cv);
+    }
+    orb_u16x2 a2[16], a4[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) a2[k] = __builtin_elementwise_min(x[k], x[(k + 1) & 15]);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) a4[k] = __builtin_elementwise_min(a2[k], a2[(k + 2) & 15]);
+    orb_u16x2 best = (orb_u16x2)(0);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const orb_u16x2 a8 = __builtin_elementwise_min(a4[k], a4[(k + 4) & 15]);
+        best = __builtin_elementwise_max(best, __builtin_elementwise_min(a8, x[(k + 8) & 15]));
+    }
+    int s = (int)(best.x > best.y ? best.x : best.y) - 256;
+    s = s < 0 ? 0 : s;
+    return s > 255 ? 255 : s;
+}
+
 __host__ __device__ inline int fast_strength(const uint8_t* c, int stride, int t_min) {
     const int v = c[0];
     // compass pre-test: any 9-arc holds two cyclically adjacent points of {0,4,8,12}
