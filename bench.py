@@ -40,25 +40,25 @@ def level_sizes(w, h, sf=1.2, L=8):
 
 
 def fast_split(w, h, sf=1.2, L=8):
-    """First level whose FAST cells do not fit the 60-byte LDS tile (orb_runtime.cpp rule)."""
+    """First level whose FAST cells do not fit the 64-byte LDS tile (orb_runtime.cpp rule)."""
     for l, (lw, lh) in enumerate(level_sizes(w, h, sf, L)):
         W, H = np.float32(lw - 32), np.float32(lh - 32)
         nc, nr = int(W / np.float32(35)), int(H / np.float32(35))
         wc, hc = int(np.ceil(W / np.float32(nc))), int(np.ceil(H / np.float32(nr)))
-        if wc + 9 > 60 or hc + 6 > 60:
+        if wc + 9 > 64 or hc + 6 > 64:
             return l
     return L
 
 
 def algorithmic_bytes(w, h, L, nkp, sf=1.2):
     """Per-image bytes by stage: pyramid sum(A_{l-1}+A_l), FAST sum(A_l) (split
-    between the 60- and 80-byte tile launches), blur 2*sum(A_l), 48 B per output keypoint
+    between the 64- and 80-byte tile launches), blur 2*sum(A_l), 48 B per output keypoint
     (16 B keypoint + 32 B descriptor)."""
     A = [a * b for a, b in level_sizes(w, h, sf, L)]
     k = fast_split(w, h, sf, L)
     return {
         "k_resize": sum(A[l - 1] + A[l] for l in range(1, L)),
-        "k_fast_cells<60>": sum(A[:k]),
+        "k_fast_cells<64>": sum(A[:k]),
         "k_fast_cells<80>": sum(A[k:]),
         "k_blur": 2 * sum(A),
         "k_orient_desc": 48 * nkp,

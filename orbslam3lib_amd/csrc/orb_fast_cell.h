@@ -5,7 +5,7 @@
 // sees only this cell's corners, iniThFAST first and minThFAST if the cell kept nothing, keys
 // emitted in row-major order relative to (minBorderX, minBorderY).
 //
-// Layout: the ROI is staged in LDS with a compile-time pitch P (60 when every level's cells fit,
+// Layout: the ROI is staged in LDS with a compile-time pitch P (64 when every level's cells fit,
 // kCellMax = 80 otherwise).  On the GPU one wave runs one cell (no workgroup barriers); the
 // code also accepts several waves per cell: each wave owns one contiguous row-major range of
 // detection pixels and keeps a private candidate list, so the wave lists concatenated in wave
@@ -24,8 +24,8 @@
 namespace orbgpu {
 
 constexpr int kCellMax = 80;  // wCell, hCell < 70 (nCols = floor(W/35)) plus the 6-px overlap
-constexpr int kCellPitchSmall = 60;  // 640x480-class pyramids: every level's cells <= 51 x 54
-// candidate list capacity for pitch P: the detection area, (P-6)^2 for the 60-byte tile, 69^2
+constexpr int kCellPitchSmall = 64;  // 640x480-class pyramids: every level's cells <= 55 x 58
+// candidate list capacity for pitch P: the detection area, (P-6)^2 for the 64-byte tile, 69^2
 // for the general one (wCell, hCell <= 69: nCols = floor(W/35) >= 1)
 template <int P>
 constexpr int cell_list_cap() { return P == kCellMax ? 69 * 69 : (P - 6) * (P - 6); }
@@ -61,16 +61,30 @@ struct CellScratch {
 
 // The detection pixels are split into one contiguous row-major range per wave, so the wave
 // lists concatenated in wave order are row-major: ordered output needs only a prefix over waves.
-template <int CP, class Pol>
+template <int CP, class Pol, class Ld16>
 __host__ __device__ int fast_cell_run(Pol& p, const uint8_t* src, long long pitch, int sh,
                                       bool dword_ok, const CellGeom& g, int ini_th, int min_th,
-                                      const CellScratch& cs, uint32_t* keys_out) {
+                                      const CellScratch& cs, uint32_t* keys_out, Ld16 ld16) {
     const int tid = p.tid(), NT = p.nthreads();
     const int rows = g.rows, cols = g.cols;
     uint8_t* T = cs.T;
     uint8_t* M = cs.M;
     constexpr int RW = CP / 4;  // dwords per LDS row (constant divisors only)
-    if (dword_ok) {
+    if (CP % 16 == 0 && dword_ok) {
+        // 16-byte row chunks (ld16: bounds-checked load of 16 bytes at src + offset; bytes past
+        // the ROI row are loaded but never read)
+        constexpr int RQ = CP / 16;
+        const int nq = (sh + cols + 15) >> 4;
+        uint4* T128 = reinterpret_cast<uint4*>(T);
+        uint4* M128 = reinterpret_cast<uint4*>(M);
+        for (int i = tid; i < rows * RQ; i += NT) {
+            const int r = i / RQ, q = i % RQ;
+            if (q < nq) {
+                T128[i] = ld16((long long)r * pitch + 16 * q);
+                M128[i] = make_uint4(0, 0, 0, 0);
+            }
+        }
+    } else if (dword_ok) {
         const int ndw = (sh + cols + 3) >> 2;
         uint32_t* T32 = reinterpret_cast<uint32_t*>(T);
         uint32_t* M32 = reinterpret_cast<uint32_t*>(M);

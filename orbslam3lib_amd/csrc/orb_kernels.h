@@ -63,7 +63,7 @@ struct BatchArgs {
     int32_t* out_mono;               // [img]
     const int32_t* laps;             // [img][2]
     int total_cells, total_tiles, total_od_blocks;
-    int fast_split;  // levels [0, fast_split) run the 60-byte FAST tile, the rest the 80-byte one
+    int fast_split;  // levels [0, fast_split) run the 64-byte FAST tile, the rest the 80-byte one
     unsigned long long* octdbg;      // diagnostic: [img][kMaxLevels][8] phase clocks, or null
     int oct_lds_nodes;               // node capacity of k_octree's dynamic LDS (0: all global)
     int oct_lds_bytes;
@@ -113,7 +113,7 @@ __host__ __device__ inline OctLayout oct_layout(int n_cap, int C) {
 // Kernel launchers (orb_kernels.hip).  Each returns hipGetLastError() of its launch.
 hipError_t launch_resize(const BatchArgs& a, int level, hipStream_t s);
 hipError_t launch_blur(const BatchArgs& a, hipStream_t s);
-// top = false: levels [0, fast_split) on the 60-byte tile; true: the other levels (80-byte tile)
+// top = false: levels [0, fast_split) on the 64-byte tile; true: the other levels (80-byte tile)
 hipError_t launch_fast_cells(const BatchArgs& a, bool top, hipStream_t s);
 hipError_t launch_octree(const BatchArgs& a, hipStream_t s);
 hipError_t launch_orient_desc(const BatchArgs& a, hipStream_t s);

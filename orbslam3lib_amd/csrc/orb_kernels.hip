@@ -356,7 +356,7 @@ template <int CP>
 __global__ __launch_bounds__(kFastThreads) void k_fast_cells(BatchArgs a, int cell0) {
     constexpr int kList = cell_list_cap<CP>();
     __shared__ __attribute__((aligned(16))) uint8_t T[CP * CP];
-    __shared__ __attribute__((aligned(16))) uint8_t M[CP * CP];
+    __shared__ __attribute__((aligned(16))) uint8_t M[CP * CP];  // 16-byte rows when CP % 16 == 0
     __shared__ uint16_t list[kList];
     __shared__ int32_t wcnt[kFastThreads / 64];
     __shared__ int scratch[16];
@@ -382,11 +382,18 @@ __global__ __launch_bounds__(kFastThreads) void k_fast_cells(BatchArgs a, int ce
     g.cols = min(g.iniX + G.wCell + 6, G.maxBX) - g.iniX;
     const bool dword_ok = ((G.pitch | G.img_stride) & 3) == 0;
     const int sh = dword_ok ? (g.iniX & 3) : 0;
-    const uint8_t* src = a.lvl_base[l] + (long long)img * G.img_stride + (long long)g.iniY * G.pitch +
-                         (g.iniX - sh);
+    const uint8_t* base = a.lvl_base[l] + (long long)img * G.img_stride;
+    const long long roi = (long long)g.iniY * G.pitch + (g.iniX - sh);
+    const uint8_t* src = base + roi;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)base, (short)0, (int)min(G.img_stride, 0x7fffffffLL), 0x00020000);
+    auto ld16 = [&](long long off) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(roi + off), 0, 0);
+        return make_uint4(v[0], v[1], v[2], v[3]);
+    };
     DevPolicy p{scratch};
     CellScratch cs{T, M, list, wcnt};
-    const int n = fast_cell_run<CP>(p, src, G.pitch, sh, dword_ok, g, a.ini_th, a.min_th, cs, key_out);
+    const int n = fast_cell_run<CP>(p, src, G.pitch, sh, dword_ok, g, a.ini_th, a.min_th, cs, key_out, ld16);
     if (threadIdx.x == 0) *cnt_out = n;
 }
 
@@ -863,7 +870,7 @@ hipError_t launch_blur(const BatchArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 hipError_t launch_fast_cells(const BatchArgs& a, bool top, hipStream_t s) {
-    // levels [0, fast_split) have cells that fit the 60-byte tile (higher occupancy); the rest
+    // levels [0, fast_split) have cells that fit the 64-byte tile (higher occupancy); the rest
     // (the small top levels, whose cells are taller) run the general 80-byte tile
     const int c0 = a.fast_split < a.nlevels ? a.lv[a.fast_split].cell_first : a.total_cells;
     if (!top && c0 > 0)

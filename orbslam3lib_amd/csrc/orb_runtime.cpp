@@ -41,7 +41,7 @@ int fail(int code, const std::string& msg) {
 
 enum Stage { ST_RESIZE, ST_BLUR, ST_FAST, ST_FAST_TOP, ST_OCTREE, ST_ORIENT, ST_FINAL, ST_KNN, ST_COUNT };
 // names as rocprofv3 shows the kernels (templates with their argument)
-const char* kStageNames[ST_COUNT] = {"k_resize",  "k_blur",        "k_fast_cells<60>", "k_fast_cells<80>",
+const char* kStageNames[ST_COUNT] = {"k_resize",  "k_blur",        "k_fast_cells<64>", "k_fast_cells<80>",
                                      "k_octree",  "k_orient_desc", "k_finalize",       "k_knn2"};
 
 struct DevBuf {
@@ -328,7 +328,7 @@ int set_geometry(orbgpu_ctx* c, int w, int h) {
     A.oct_force_retry = getenv("ORBGPU_OCT_GENERIC") ? 1 : 0;  // diagnostics / tests
     if (A.oct_force_retry) A.oct_may_retry = 1;
     A.total_cells = cell_first;
-    // FAST LDS tile: the 60-byte one for the leading levels whose cell ROIs (+3 alignment bytes)
+    // FAST LDS tile: the 64-byte one for the leading levels whose cell ROIs (+3 alignment bytes)
     // fit it; cells grow with the level (fewer, wider cells), so the rest use the 80-byte one
     A.fast_split = 0;
     while (A.fast_split < L && A.lv[A.fast_split].wCell + 9 <= kCellPitchSmall &&

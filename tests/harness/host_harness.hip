@@ -2,6 +2,7 @@
 // (orb_octree.h, orb_fast_cell.h, orb_introsort.h, orb_math.h) on the host with SerialPolicy so
 // they can be checked against the CPU oracle without a GPU.  Not part of liborbgpu.so.
 #include <cmath>
+#include <cstring>
 #include <vector>
 
 #include "../../orbslam3lib_amd/csrc/orb_fast_cell.h"
@@ -107,9 +108,18 @@ int harness_level_candidates(const uint8_t* lvl, int w, int h, int ini, int mn, 
             CellScratch cs{T, M, list.data(), wcnt.data()};
             // the small tile whenever the cells fit it (as the runtime picks it), else the general one
             const bool small = wCell + 9 <= kCellPitchSmall && hCell + 6 <= kCellPitchSmall;
-            const uint8_t* src = lvl + (long long)g.iniY * w + g.iniX - sh;
-            const int m = small ? fast_cell_run<kCellPitchSmall>(p, src, w, sh, dw, g, ini, mn, cs, tmp.data())
-                                : fast_cell_run<kCellMax>(p, src, w, sh, dw, g, ini, mn, cs, tmp.data());
+            const long long roi = (long long)g.iniY * w + g.iniX - sh;
+            const uint8_t* src = lvl + roi;
+            const long long size = (long long)w * h;
+            auto ld16 = [&](long long off) {  // bounds-checked like the device buffer load
+                uint8_t b[16];
+                for (int k = 0; k < 16; ++k) b[k] = roi + off + k < size ? src[off + k] : 0;
+                uint4 v;
+                std::memcpy(&v, b, 16);
+                return v;
+            };
+            const int m = small ? fast_cell_run<kCellPitchSmall>(p, src, w, sh, dw, g, ini, mn, cs, tmp.data(), ld16)
+                                : fast_cell_run<kCellMax>(p, src, w, sh, dw, g, ini, mn, cs, tmp.data(), ld16);
             for (int k = 0; k < m; ++k) {
                 if (total < cap) out[total] = tmp[k];
                 ++total;
