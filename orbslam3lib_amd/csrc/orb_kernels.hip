@@ -25,6 +25,15 @@ namespace orbgpu {
 
 static_assert(sizeof(BatchArgs) <= 4096, "kernel argument block too large");
 
+// XCD-aware block order (cdna_hip_programming.md T1, bijective form): the dispatcher places
+// block b on XCD b % 8, so a grid walked in (b % 8, b / 8) order gives every XCD one
+// contiguous range of work -- neighbouring cells / tiles of one image then share that XCD's L2
+// instead of being fetched once per XCD.  Speed only: any placement stays correct.
+__device__ inline int xcd_remap(int orig, int nwg) {
+    const int xcd = orig % 8, q = nwg / 8, r = nwg % 8;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
+}
+
 // rBRIEF pattern decoded at compile time from the hex data: 256 pairs (x0,y0,x1,y1) int8.
 struct PatternTable {
     int8_t v[1024];
@@ -80,8 +89,10 @@ __global__ __launch_bounds__(256) void k_resize(BatchArgs a, int l) {
     __shared__ __attribute__((aligned(16))) uint32_t win[kRsSrcRows][kRsSrcCols / 4];
     const LevelGeom& G = a.lv[l];
     const LevelGeom& S = a.lv[l - 1];
-    const int img = a.img0 + blockIdx.z;
-    const int tx0 = blockIdx.x * kRsTW, ty0 = blockIdx.y * kRsTH;
+    const int nxy = gridDim.x * gridDim.y;
+    const int wg = xcd_remap(blockIdx.x + blockIdx.y * gridDim.x + blockIdx.z * nxy, nxy * gridDim.z);
+    const int img = a.img0 + wg / nxy;
+    const int tx0 = (wg % nxy % gridDim.x) * kRsTW, ty0 = (wg % nxy / gridDim.x) * kRsTH;
     const uint8_t* src = a.lvl_base[l - 1] + (long long)img * S.img_stride;
     uint8_t* dst = a.lvl_base[l] + (long long)img * G.img_stride;
     if (G.area2) {  // resize.cpp: INTER_LINEAR at exactly 2x is serviced by INTER_AREA fast
@@ -234,8 +245,11 @@ __global__ __launch_bounds__(256) void k_blur(BatchArgs a) {
     __shared__ uint4 tin4[IH][IWQ];
     __shared__ uint4 hp[NRP][kBlurTW / 4];  // [row pair][column quad]: 4 columns x (row0,row1)
     const int total = a.total_tiles * a.nimages;
-    int t = blockIdx.x;
-    if (t >= total) return;
+    // a contiguous run of tiles per workgroup, runs placed XCD-contiguously (xcd_remap)
+    const int lb = xcd_remap(blockIdx.x, gridDim.x);
+    const int t_end = (int)((long long)(lb + 1) * total / gridDim.x);
+    int t = (int)((long long)lb * total / gridDim.x);
+    if (t >= t_end) return;
     BlurTile bt = blur_tile(a, t);
     uint4 pre[NCH];
 #pragma unroll
@@ -243,7 +257,7 @@ __global__ __launch_bounds__(256) void k_blur(BatchArgs a) {
         const int i = threadIdx.x + 256 * c;
         if (i < IH * IWQ) pre[c] = blur_chunk(a, bt, i, IWQ);
     }
-    for (; t < total; t += gridDim.x) {
+    for (; t < t_end; ++t) {
         const BlurTile cur = bt;
         const LevelGeom& G = a.lv[cur.l];
         const int ty0 = cur.ty0, tx0 = cur.tx0;
@@ -254,8 +268,8 @@ __global__ __launch_bounds__(256) void k_blur(BatchArgs a) {
             const int i = threadIdx.x + 256 * c;
             if (i < IH * IWQ) (&tin4[0][0])[i] = pre[c];
         }
-        const int tn = t + gridDim.x;
-        if (tn < total) {  // prefetch the next window
+        const int tn = t + 1;
+        if (tn < t_end) {  // prefetch the next window
             bt = blur_tile(a, tn);
 #pragma unroll
             for (int c = 0; c < NCH; ++c) {
@@ -360,8 +374,9 @@ __global__ __launch_bounds__(kFastThreads) void k_fast_cells(BatchArgs a, int ce
     __shared__ uint16_t list[kList];
     __shared__ int32_t wcnt[kFastThreads / 64];
     __shared__ int scratch[16];
-    const int img = a.img0 + blockIdx.y;
-    const int gcell = cell0 + blockIdx.x;  // flattened over the levels
+    const int wg = xcd_remap(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * gridDim.y);
+    const int img = a.img0 + wg / gridDim.x;
+    const int gcell = cell0 + wg % gridDim.x;  // flattened over the levels
     int l = 0;
     while (l + 1 < a.nlevels && gcell >= a.lv[l + 1].cell_first) ++l;
     const LevelGeom& G = a.lv[l];
@@ -503,9 +518,10 @@ constexpr int kOdPatchPitch = 48;                // 3 x 16 B: covers x-18..x+18 
 __global__ __launch_bounds__(256) void k_orient_desc(BatchArgs a) {
     // per keypoint group: the blurred patch around the keypoint, staged with 16-byte loads
     __shared__ __attribute__((aligned(16))) uint8_t patch[kOdKpBlock][kOdPatchRows * kOdPatchPitch];
-    const int img = a.img0 + blockIdx.y;
+    const int wg = xcd_remap(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * gridDim.y);
+    const int img = a.img0 + wg / gridDim.x, bx = wg % gridDim.x;
     int l = 0;
-    while (l + 1 < a.nlevels && (int)blockIdx.x >= a.lv[l + 1].od_first) ++l;
+    while (l + 1 < a.nlevels && bx >= a.lv[l + 1].od_first) ++l;
     const LevelGeom& G = a.lv[l];
     const int sub = threadIdx.x % kOdLanes, grp = threadIdx.x / kOdLanes;
     const int count = a.lvlcnt[img * kMaxLevels + l];
@@ -543,7 +559,7 @@ __global__ __launch_bounds__(256) void k_orient_desc(BatchArgs a) {
     for (int i = 0; i < kOdPairs; ++i)
         patw[i] = reinterpret_cast<const uint32_t*>(c_pattern.v)[sub * kOdPairs + i];
     // uniform trip count per wave so the group shuffles see all lanes
-    const int wave_first = (blockIdx.x - G.od_first) * kOdKpBlock + (threadIdx.x >> 6) * (64 / kOdLanes);
+    const int wave_first = (bx - G.od_first) * kOdKpBlock + (threadIdx.x >> 6) * (64 / kOdLanes);
     for (int kb = wave_first; kb < count; kb += stride_k) {
         const int kp = kb + (grp % (64 / kOdLanes));
         const bool valid = kp < count;
