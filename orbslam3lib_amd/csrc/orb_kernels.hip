@@ -417,17 +417,14 @@ __global__ __launch_bounds__(kFastThreads) void k_fast_cells(BatchArgs a, int ce
 // (vToDistributeKeys, :807-871) then runs DistributeOctTree (orb_octree.h) with the node
 // state in LDS (80 KB: two workgroups per CU).
 // kOctRetry: the level did not fit the LDS instantiation (node capacity, cell offsets or more
-// than kOctLdsKeys candidates); k_octree<false> then redoes it with generic pointers.
+// than kOctLdsKeys candidates); k_octree_retry then redoes it with generic pointers.
 constexpr int kOctRetry = -7;
 
 template <bool kLdsPath>
-__global__ __launch_bounds__(512, 4) void k_octree(BatchArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t nodemem_lds[];  // a.oct_lds_bytes
-    __shared__ int scratch[16];
-    __shared__ OctShared sh;
-    const int img = a.img0 + blockIdx.x, l = blockIdx.y;  // level-major dispatch: the long level-0 groups go first
+__device__ __attribute__((always_inline)) inline void octree_level(const BatchArgs& a, int img, int l,
+                                                                   uint8_t* nodemem_lds, int* scratch,
+                                                                   OctShared& sh) {
     const LevelGeom& G = a.lv[l];
-    if (!kLdsPath && a.status[img * kMaxLevels + l] != kOctRetry) return;
     DevPolicy p{scratch};
     const int32_t* cnt = a.cellcnt + (long long)img * a.cellcnt_img_stride + G.cellcnt_off;
     const uint32_t* ck = a.cellkeys + (long long)img * a.cellkeys_img_stride + G.cellkey_off;
@@ -494,6 +491,28 @@ __global__ __launch_bounds__(512, 4) void k_octree(BatchArgs a) {
     if (threadIdx.x == 0) {
         a.lvlcnt[img * kMaxLevels + l] = r < 0 ? 0 : r;
         a.status[img * kMaxLevels + l] = r < 0 ? r : 0;
+    }
+}
+
+// One workgroup per (image, level), level-major dispatch: the long level-0 groups go first.
+__global__ __launch_bounds__(512, 4) void k_octree(BatchArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t nodemem_lds[];  // a.oct_lds_bytes
+    __shared__ int scratch[16];
+    __shared__ OctShared sh;
+    octree_level<true>(a, a.img0 + blockIdx.x, blockIdx.y, nodemem_lds, scratch, sh);
+}
+
+// The levels k_octree left with kOctRetry, redone with generic pointers: a small persistent
+// grid walks all (image, level) slots, so the usual no-retry case costs one status read each.
+__global__ __launch_bounds__(512, 4) void k_octree_retry(BatchArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t nodemem_lds[];  // a.oct_lds_bytes
+    __shared__ int scratch[16];
+    __shared__ OctShared sh;
+    for (int s = blockIdx.x; s < a.nimages * a.nlevels; s += gridDim.x) {
+        const int img = a.img0 + s / a.nlevels, l = s % a.nlevels;
+        if (a.status[img * kMaxLevels + l] != kOctRetry) continue;  // uniform per workgroup
+        octree_level<false>(a, img, l, nodemem_lds, scratch, sh);
+        __syncthreads();
     }
 }
 
@@ -897,17 +916,17 @@ hipError_t launch_fast_cells(const BatchArgs& a, bool top, hipStream_t s) {
 }
 hipError_t launch_octree(const BatchArgs& a, hipStream_t s) {
     if (a.oct_lds_bytes > 65536) {
-        for (const void* f : {reinterpret_cast<const void*>(k_octree<true>),
-                              reinterpret_cast<const void*>(k_octree<false>)}) {
+        for (const void* f : {reinterpret_cast<const void*>(k_octree),
+                              reinterpret_cast<const void*>(k_octree_retry)}) {
             hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, a.oct_lds_bytes);
             if (e != hipSuccess) return e;
         }
     }
-    hipLaunchKernelGGL(k_octree<true>, dim3(a.nimages, a.nlevels), dim3(512), a.oct_lds_bytes, s, a);
-    // levels that did not fit the LDS instantiation (rare: > kOctLdsKeys candidates); every
-    // other block returns at once
+    hipLaunchKernelGGL(k_octree, dim3(a.nimages, a.nlevels), dim3(512), a.oct_lds_bytes, s, a);
+    // levels that did not fit the LDS instantiation (rare: > kOctLdsKeys candidates)
     if (a.oct_may_retry)
-        hipLaunchKernelGGL(k_octree<false>, dim3(a.nimages, a.nlevels), dim3(512), a.oct_lds_bytes, s, a);
+        hipLaunchKernelGGL(k_octree_retry, dim3(std::min(a.nimages * a.nlevels, 64)), dim3(512),
+                           a.oct_lds_bytes, s, a);
     return hipGetLastError();
 }
 hipError_t launch_orient_desc(const BatchArgs& a, hipStream_t s) {

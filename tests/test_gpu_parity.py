@@ -223,7 +223,7 @@ def test_general_fast_tile(oracle, frame0, monkeypatch):
 
 
 def test_octree_generic_instantiation(oracle, frame0, monkeypatch):
-    """Every level through k_octree<false> (generic pointers, the path taken by levels with
+    """Every level through k_octree_retry (generic pointers, the path taken by levels with
     more candidates than the LDS label capacity), forced with ORBGPU_OCT_GENERIC."""
     L, _ = frame0
     monkeypatch.setenv("ORBGPU_OCT_GENERIC", "1")
