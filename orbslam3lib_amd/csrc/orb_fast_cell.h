@@ -36,19 +36,17 @@ struct CellGeom {
     int minBorder;
 };
 
-// M holds m for corners, 0 elsewhere (pitch P).
+// M holds m for corners, 0 elsewhere (pitch P).  Nonmax at t: kept <=> m > t, m >= 2 and no
+// neighbour q with q > t and q >= m; given m > t, q >= m already implies q > t, so the
+// neighbour test is max(q) < m -- nine loads issued together, no short-circuit chain.
 template <int P>
 __host__ __device__ inline bool fast_kept(const uint8_t* M, int off, int t) {
     const uint8_t* m = &M[off];
     const int v = m[0];
-    if (v <= t || v < 2) return false;
-    const int nb[8] = {-P - 1, -P, -P + 1, -1, 1, P - 1, P, P + 1};
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        const int q = m[nb[k]];
-        if (q > t && v <= q) return false;
-    }
-    return true;
+    const int q0 = m[-P - 1], q1 = m[-P], q2 = m[-P + 1], q3 = m[-1];
+    const int q4 = m[1], q5 = m[P - 1], q6 = m[P], q7 = m[P + 1];
+    const int a = imax(imax(q0, q1), imax(q2, q3)), b = imax(imax(q4, q5), imax(q6, q7));
+    return (v > t) & (v >= 2) & (imax(a, b) < v);
 }
 
 // Per-cell scratch (LDS on the GPU).
@@ -123,20 +121,18 @@ __host__ __device__ int fast_cell_run(Pol& p, const uint8_t* src, long long pitc
     auto build = [&](int t) {
         int na = 0;
         for (int base = i0; base < i1; base += L) {
-            const int i = base + lane < i1 ? base + lane : i1 - 1;  // tail lanes recompute i1-1
+            const bool in = base + lane < i1;
+            const int i = in ? base + lane : i1 - 1;  // tail lanes recompute i1-1
             const int o = off_of(i);
             const uint8_t* c = &T[o];
             const int v = c[0], lo = v - t, hi = v + t;
             const int p0 = c[3 * CP], p4 = c[3], p8 = c[-3 * CP], p12 = c[-3];
-            // compass pre-test as lane masks: two cyclically adjacent of {0,4,8,12} beyond t
-            const uint64_t d0 = p.ballot(p0 < lo), d1 = p.ballot(p4 < lo);
-            const uint64_t d2 = p.ballot(p8 < lo), d3 = p.ballot(p12 < lo);
-            const uint64_t b0 = p.ballot(p0 > hi), b1 = p.ballot(p4 > hi);
-            const uint64_t b2 = p.ballot(p8 > hi), b3 = p.ballot(p12 > hi);
-            const int left = i1 - base;
-            const uint64_t valid = left >= 64 ? ~0ull : ((1ull << left) - 1ull);
-            const uint64_t m = (((d0 | d2) & (d1 | d3)) | ((b0 | b2) & (b1 | b3))) & valid;
-            if ((m >> lane) & 1ull) list[na + p.popc64(m & lt)] = (uint16_t)o;
+            // compass pre-test: two cyclically adjacent of {0,4,8,12} beyond t on one side <=>
+            // one of {0,8} and one of {4,12} beyond it <=> a min/max over the opposite pairs
+            const int dk = imax(imin(p0, p8), imin(p4, p12)), bk = imin(imax(p0, p8), imax(p4, p12));
+            const bool cand = in & ((dk < lo) | (bk > hi));
+            const uint64_t m = p.ballot(cand);
+            if (cand) list[na + p.popc64(m & lt)] = (uint16_t)o;
             na += p.popc64(m);
         }
         // exact strength of every candidate (m > t <=> corner at t), corners kept in order
@@ -161,9 +157,10 @@ __host__ __device__ int fast_cell_run(Pol& p, const uint8_t* src, long long pitc
         int c = 0;
         for (int base = 0; base < nb; base += L) {
             const int j = base + lane;
-            const int o = j < nb ? (list[j] & 0x1FFF) : 0;
-            const bool k = j < nb && fast_kept<CP>(M, o, t);
-            if (j < nb) list[j] = (uint16_t)(o | (k ? 0x8000 : 0));
+            const bool in = j < nb;
+            const int o = list[in ? j : nb - 1] & 0x1FFF;  // tail lanes re-test the last entry
+            const bool k = in & fast_kept<CP>(M, o, t);
+            if (in) list[j] = (uint16_t)(o | (k ? 0x8000 : 0));
             c += p.popc64(p.ballot(k));
         }
         if (lane == 0) cs.wcnt[w] = c;

@@ -504,7 +504,7 @@ __global__ __launch_bounds__(512, 4) void k_octree(BatchArgs a) {
 
 // The levels k_octree left with kOctRetry, redone with generic pointers: a small persistent
 // grid walks all (image, level) slots, so the usual no-retry case costs one status read each.
-__global__ __launch_bounds__(512, 4) void k_octree_retry(BatchArgs a) {
+__global__ __launch_bounds__(512, 1) void k_octree_retry(BatchArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t nodemem_lds[];  // a.oct_lds_bytes
     __shared__ int scratch[16];
     __shared__ OctShared sh;

@@ -8,6 +8,9 @@
 
 namespace orbgpu {
 
+__host__ __device__ inline int imin(int a, int b) { return a < b ? a : b; }
+__host__ __device__ inline int imax(int a, int b) { return a > b ? a : b; }
+
 // cvRound(float) = round-half-to-even (lrintf / v_rndne_f32).
 __host__ __device__ inline int cv_round(float v) { return (int)__builtin_rintf(v); }
 
@@ -112,12 +115,16 @@ __host__ __device__ inline int fast_strength_packed(const uint8_t* c) {
     for (int k = 0; k < 16; ++k) a2[k] = __builtin_elementwise_min(x[k], x[(k + 1) & 15]);
 #pragma unroll
     for (int k = 0; k < 16; ++k) a4[k] = __builtin_elementwise_min(a2[k], a2[(k + 2) & 15]);
-    orb_u16x2 best = (orb_u16x2)(0);
+    orb_u16x2 a9[16];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        const orb_u16x2 a8 = __builtin_elementwise_min(a4[k], a4[(k + 4) & 15]);
-        best = __builtin_elementwise_max(best, __builtin_elementwise_min(a8, x[(k + 8) & 15]));
-    }
+    for (int k = 0; k < 16; ++k)
+        a9[k] = __builtin_elementwise_min(__builtin_elementwise_min(a4[k], a4[(k + 4) & 15]), x[(k + 8) & 15]);
+    // max over the 16 arcs as a tree: independent packed ops, no dependent back-to-back chain
+#pragma unroll
+    for (int w = 8; w >= 1; w >>= 1)
+#pragma unroll
+        for (int k = 0; k < w; ++k) a9[k] = __builtin_elementwise_max(a9[k], a9[k + w]);
+    const orb_u16x2 best = a9[0];
     int s = (int)(best.x > best.y ? best.x : best.y) - 256;
     s = s < 0 ? 0 : s;
     return s > 255 ? 255 : s;
