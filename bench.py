@@ -39,27 +39,30 @@ def level_sizes(w, h, sf=1.2, L=8):
     return out
 
 
-def fast_split(w, h, sf=1.2, L=8):
-    """First level whose FAST cells do not fit the 64-byte LDS tile (orb_runtime.cpp rule)."""
+def fast_split(w, h, sf=1.2, L=8, tile=64):
+    """First level at or after which the FAST cells stop fitting the `tile`-byte LDS tile
+    (orb_runtime.cpp rule: wCell + 9 <= tile and hCell + 6 <= tile, levels taken in order)."""
     for l, (lw, lh) in enumerate(level_sizes(w, h, sf, L)):
         W, H = np.float32(lw - 32), np.float32(lh - 32)
         nc, nr = int(W / np.float32(35)), int(H / np.float32(35))
         wc, hc = int(np.ceil(W / np.float32(nc))), int(np.ceil(H / np.float32(nr)))
-        if wc + 9 > 64 or hc + 6 > 64:
+        if wc + 9 > tile or hc + 6 > tile:
             return l
     return L
 
 
 def algorithmic_bytes(w, h, L, nkp, sf=1.2):
     """Per-image bytes by stage: pyramid sum(A_{l-1}+A_l), FAST sum(A_l) (split
-    between the 64- and 80-byte tile launches), blur 2*sum(A_l), 48 B per output keypoint
+    between the 48-, 64- and 80-byte tile launches), blur 2*sum(A_l), 48 B per output keypoint
     (16 B keypoint + 32 B descriptor)."""
     A = [a * b for a, b in level_sizes(w, h, sf, L)]
-    k = fast_split(w, h, sf, L)
+    k48 = fast_split(w, h, sf, L, 48)
+    k64 = max(k48, fast_split(w, h, sf, L, 64))
     return {
         "k_resize": sum(A[l - 1] + A[l] for l in range(1, L)),
-        "k_fast_cells<64>": sum(A[:k]),
-        "k_fast_cells<80>": sum(A[k:]),
+        "k_fast_cells<48>": sum(A[:k48]),
+        "k_fast_cells<64>": sum(A[k48:k64]),
+        "k_fast_cells<80>": sum(A[k64:]),
         "k_blur": 2 * sum(A),
         "k_orient_desc": 48 * nkp,
     }
@@ -189,9 +192,9 @@ def main():
         has_cuda = False
 
     # 1. short untimed pass, every stage one whole-batch launch bracketed by HIP events -> per-stage
-    #    table and the dominant kernel; 2. the timed region (production sub-batch streams; the
-    #    dominant FAST stage is launched alone over the whole batch there too) brackets only that
-    #    kernel, so event cost stays small and its duration is its own
+    #    table and the dominant kernel; 2. the timed region (production sub-batch streams, one
+    #    launch per stream and stage) brackets only that kernel's launches, so event cost stays
+    #    small; their durations include whatever the other streams run beside them
     be.set_profiling(True, serialize=True)
     be.reset_stage_times()
     for _ in range(3):
@@ -241,7 +244,10 @@ def main():
                "source": "timed region" if name == dom_name and stages_timed.get(name, (0, 0))[1]
                else "3-step profiled pass"}
         if name in per_img:
-            launches_per_step = (args.nlevels - 1) if name == "k_resize" else 1
+            # launches per step as measured: one whole-batch launch per stage (per level for
+            # k_resize) in the serialized pass, one per sub-batch stream in the timed region
+            nsteps = args.steps if row["source"] == "timed region" else 3
+            launches_per_step = cnt / nsteps
             bytes_launch = per_img[name] * n_img / launches_per_step
             row["bytes_per_launch"] = int(bytes_launch)
             row["GBps"] = round(bytes_launch / (avg_ms * 1e-3) / 1e9, 1)

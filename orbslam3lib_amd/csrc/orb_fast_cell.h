@@ -25,6 +25,7 @@ namespace orbgpu {
 
 constexpr int kCellMax = 80;  // wCell, hCell < 70 (nCols = floor(W/35)) plus the 6-px overlap
 constexpr int kCellPitchSmall = 64;  // 640x480-class pyramids: every level's cells <= 55 x 58
+constexpr int kCellPitchTiny = 48;   // the leading levels of 640x480-class pyramids (cells <= 39 x 42)
 // candidate list capacity for pitch P: the detection area, (P-6)^2 for the 64-byte tile, 69^2
 // for the general one (wCell, hCell <= 69: nCols = floor(W/35) >= 1)
 template <int P>
@@ -57,12 +58,11 @@ struct CellScratch {
     int32_t* wcnt;     // [waves]
 };
 
-// The detection pixels are split into one contiguous row-major range per wave, so the wave
-// lists concatenated in wave order are row-major: ordered output needs only a prefix over waves.
+// Stages the cell ROI in LDS (T) and clears the strength plane (M); the caller syncs.
 template <int CP, class Pol, class Ld16>
-__host__ __device__ int fast_cell_run(Pol& p, const uint8_t* src, long long pitch, int sh,
-                                      bool dword_ok, const CellGeom& g, int ini_th, int min_th,
-                                      const CellScratch& cs, uint32_t* keys_out, Ld16 ld16) {
+__host__ __device__ void fast_cell_stage(Pol& p, const uint8_t* src, long long pitch, int sh,
+                                         bool dword_ok, const CellGeom& g, const CellScratch& cs,
+                                         Ld16 ld16) {
     const int tid = p.tid(), NT = p.nthreads();
     const int rows = g.rows, cols = g.cols;
     uint8_t* T = cs.T;
@@ -102,7 +102,17 @@ __host__ __device__ int fast_cell_run(Pol& p, const uint8_t* src, long long pitc
             }
         }
     }
-    p.sync();
+}
+
+// The detection pixels are split into one contiguous row-major range per wave, so the wave
+// lists concatenated in wave order are row-major: ordered output needs only a prefix over waves.
+// Runs on a staged ROI (fast_cell_stage + sync); returns the cell's kept count.
+template <int CP, class Pol>
+__host__ __device__ int fast_cell_detect(Pol& p, int sh, const CellGeom& g, int ini_th, int min_th,
+                                         const CellScratch& cs, uint32_t* keys_out) {
+    const int rows = g.rows, cols = g.cols;
+    uint8_t* T = cs.T;
+    uint8_t* M = cs.M;
     const int dr = rows - 6 > 0 ? rows - 6 : 0;
     const int dc = cols - 6 > 0 ? cols - 6 : 0;
     const int nd = dr * dc;
@@ -201,6 +211,15 @@ __host__ __device__ int fast_cell_run(Pol& p, const uint8_t* src, long long pitc
         run += p.popc64(m);
     }
     return cb.x;
+}
+
+template <int CP, class Pol, class Ld16>
+__host__ __device__ int fast_cell_run(Pol& p, const uint8_t* src, long long pitch, int sh,
+                                      bool dword_ok, const CellGeom& g, int ini_th, int min_th,
+                                      const CellScratch& cs, uint32_t* keys_out, Ld16 ld16) {
+    fast_cell_stage<CP>(p, src, pitch, sh, dword_ok, g, cs, ld16);
+    p.sync();
+    return fast_cell_detect<CP>(p, sh, g, ini_th, min_th, cs, keys_out);
 }
 
 }  // namespace orbgpu

@@ -63,7 +63,8 @@ struct BatchArgs {
     int32_t* out_mono;               // [img]
     const int32_t* laps;             // [img][2]
     int total_cells, total_tiles, total_od_blocks;
-    int fast_split;  // levels [0, fast_split) run the 64-byte FAST tile, the rest the 80-byte one
+    int fast_split48;  // levels [0, fast_split48) run the 48-byte FAST tile,
+    int fast_split;    // [fast_split48, fast_split) the 64-byte one, the rest the 80-byte one
     unsigned long long* octdbg;      // diagnostic: [img][kMaxLevels][8] phase clocks, or null
     int oct_lds_nodes;               // node capacity of k_octree's dynamic LDS (0: all global)
     int oct_lds_bytes;
@@ -113,8 +114,10 @@ __host__ __device__ inline OctLayout oct_layout(int n_cap, int C) {
 // Kernel launchers (orb_kernels.hip).  Each returns hipGetLastError() of its launch.
 hipError_t launch_resize(const BatchArgs& a, int level, hipStream_t s);
 hipError_t launch_blur(const BatchArgs& a, hipStream_t s);
-// top = false: levels [0, fast_split) on the 64-byte tile; true: the other levels (80-byte tile)
-hipError_t launch_fast_cells(const BatchArgs& a, bool top, hipStream_t s);
+// FAST cells of the levels that run the `tile`-byte LDS tile (48, 64 or kCellMax = 80):
+// fast_cell_range gives their flattened cell range, launch_fast_cells launches nothing if empty
+void fast_cell_range(const BatchArgs& a, int tile, int* c0, int* c1);
+hipError_t launch_fast_cells(const BatchArgs& a, int tile, hipStream_t s);
 hipError_t launch_octree(const BatchArgs& a, hipStream_t s);
 hipError_t launch_orient_desc(const BatchArgs& a, hipStream_t s);
 hipError_t launch_finalize(const BatchArgs& a, hipStream_t s);

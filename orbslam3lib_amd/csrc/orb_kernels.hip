@@ -904,14 +904,21 @@ hipError_t launch_blur(const BatchArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_blur, dim3(std::min(total, 8192)), dim3(256), 0, s, a);
     return hipGetLastError();
 }
-hipError_t launch_fast_cells(const BatchArgs& a, bool top, hipStream_t s) {
-    // levels [0, fast_split) have cells that fit the 64-byte tile (higher occupancy); the rest
-    // (the small top levels, whose cells are taller) run the general 80-byte tile
-    const int c0 = a.fast_split < a.nlevels ? a.lv[a.fast_split].cell_first : a.total_cells;
-    if (!top && c0 > 0)
-        hipLaunchKernelGGL(k_fast_cells<kCellPitchSmall>, dim3(c0, a.nimages), dim3(kFastThreads), 0, s, a, 0);
-    if (top && a.total_cells > c0)
-        hipLaunchKernelGGL(k_fast_cells<kCellMax>, dim3(a.total_cells - c0, a.nimages), dim3(kFastThreads), 0, s, a, c0);
+void fast_cell_range(const BatchArgs& a, int tile, int* c0, int* c1) {
+    auto first = [&](int l) { return l < a.nlevels ? a.lv[l].cell_first : a.total_cells; };
+    const int s48 = first(a.fast_split48), s64 = first(a.fast_split);
+    *c0 = tile == kCellPitchTiny ? 0 : tile == kCellPitchSmall ? s48 : s64;
+    *c1 = tile == kCellPitchTiny ? s48 : tile == kCellPitchSmall ? s64 : a.total_cells;
+}
+hipError_t launch_fast_cells(const BatchArgs& a, int tile, hipStream_t s) {
+    // smaller tiles = less LDS per workgroup = more cells resident per CU
+    int c0, c1;
+    fast_cell_range(a, tile, &c0, &c1);
+    if (c1 <= c0) return hipSuccess;
+    const dim3 grid(c1 - c0, a.nimages), block(kFastThreads);
+    if (tile == kCellPitchTiny) hipLaunchKernelGGL(k_fast_cells<kCellPitchTiny>, grid, block, 0, s, a, c0);
+    else if (tile == kCellPitchSmall) hipLaunchKernelGGL(k_fast_cells<kCellPitchSmall>, grid, block, 0, s, a, c0);
+    else hipLaunchKernelGGL(k_fast_cells<kCellMax>, grid, block, 0, s, a, c0);
     return hipGetLastError();
 }
 hipError_t launch_octree(const BatchArgs& a, hipStream_t s) {

@@ -39,10 +39,11 @@ int fail(int code, const std::string& msg) {
             return fail(ORBGPU_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
     } while (0)
 
-enum Stage { ST_RESIZE, ST_BLUR, ST_FAST, ST_FAST_TOP, ST_OCTREE, ST_ORIENT, ST_FINAL, ST_KNN, ST_COUNT };
+enum Stage { ST_RESIZE, ST_BLUR, ST_FAST48, ST_FAST, ST_FAST_TOP, ST_OCTREE, ST_ORIENT, ST_FINAL, ST_KNN, ST_COUNT };
 // names as rocprofv3 shows the kernels (templates with their argument)
-const char* kStageNames[ST_COUNT] = {"k_resize",  "k_blur",        "k_fast_cells<64>", "k_fast_cells<80>",
-                                     "k_octree",  "k_orient_desc", "k_finalize",       "k_knn2"};
+const char* kStageNames[ST_COUNT] = {"k_resize",         "k_blur",   "k_fast_cells<48>", "k_fast_cells<64>",
+                                     "k_fast_cells<80>", "k_octree", "k_orient_desc",    "k_finalize",
+                                     "k_knn2"};
 
 struct DevBuf {
     void* p = nullptr;
@@ -104,9 +105,10 @@ struct orbgpu_ctx {
     int input_images = 0;   // images currently sized for in `input`
     hipEvent_t fork = nullptr;
     std::vector<hipEvent_t> join;  // one per sub stream
-    // stages launched once over the whole batch on the main stream (join before, fork after):
-    // the dominant kernel runs alone, so its per-launch duration is its own
-    unsigned isolate_mask = (1u << ST_FAST) | (1u << ST_FAST_TOP);
+    // stages launched once over the whole batch on the main stream (join before, fork after), so
+    // their per-launch duration is their own; off by default: each join / fork costs ~30 us of
+    // idle GPU per step (ORBGPU_ISOLATE=<stage bit mask> turns it on)
+    unsigned isolate_mask = 0;
     bool serialize = false;  // profiling: every stage isolated
     struct ChunkRec { int img0, n; hipStream_t st; };
     std::vector<ChunkRec> last_chunks;
@@ -328,14 +330,21 @@ int set_geometry(orbgpu_ctx* c, int w, int h) {
     A.oct_force_retry = getenv("ORBGPU_OCT_GENERIC") ? 1 : 0;  // diagnostics / tests
     if (A.oct_force_retry) A.oct_may_retry = 1;
     A.total_cells = cell_first;
-    // FAST LDS tile: the 64-byte one for the leading levels whose cell ROIs (+3 alignment bytes)
-    // fit it; cells grow with the level (fewer, wider cells), so the rest use the 80-byte one
-    A.fast_split = 0;
-    while (A.fast_split < L && A.lv[A.fast_split].wCell + 9 <= kCellPitchSmall &&
-           A.lv[A.fast_split].hCell + 6 <= kCellPitchSmall)
-        ++A.fast_split;
-    if (const char* fp = getenv("ORBGPU_FAST_PITCH")) {  // diagnostics: one tile for every level
-        if (atoi(fp) == kCellMax) A.fast_split = 0;
+    // FAST LDS tiles: the 48-byte one for the leading levels whose cell ROIs (+3 alignment
+    // bytes) fit it, then the 64-byte one; cells grow with the level (fewer, wider cells), so the
+    // rest use the 80-byte one
+    auto fits = [&](int l, int P) { return A.lv[l].wCell + 9 <= P && A.lv[l].hCell + 6 <= P; };
+    A.fast_split48 = 0;
+    while (A.fast_split48 < L && fits(A.fast_split48, kCellPitchTiny)) ++A.fast_split48;
+    A.fast_split = A.fast_split48;
+    while (A.fast_split < L && fits(A.fast_split, kCellPitchSmall)) ++A.fast_split;
+    if (const char* fp = getenv("ORBGPU_FAST_PITCH")) {  // diagnostics: force one tile size
+        const int P = atoi(fp);
+        if (P == kCellMax) A.fast_split48 = A.fast_split = 0;
+        if (P == kCellPitchSmall) {
+            A.fast_split48 = A.fast_split = 0;
+            while (A.fast_split < L && fits(A.fast_split, kCellPitchSmall)) ++A.fast_split;
+        }
     }
     A.total_tiles = tile_first;
     A.total_od_blocks = od_first;
@@ -618,8 +627,41 @@ int orbgpu_run_batch(orbgpu_ctx* c, int n, int w, int h, const int32_t* laps, vo
         if (r) return r;
     }
     if ((r = each(ST_BLUR, [](const BatchArgs& B, hipStream_t st) { return launch_blur(B, st); }))) return r;
-    if ((r = each(ST_FAST, [](const BatchArgs& B, hipStream_t st) { return launch_fast_cells(B, false, st); }))) return r;
-    if ((r = each(ST_FAST_TOP, [](const BatchArgs& B, hipStream_t st) { return launch_fast_cells(B, true, st); }))) return r;
+    {   // the FAST tiles as one group: one join / fork around all of them when isolated
+        const int tiles[3] = {kCellPitchTiny, kCellPitchSmall, kCellMax};
+        const int stages[3] = {ST_FAST48, ST_FAST, ST_FAST_TOP};
+        bool any[3], iso = false;
+        for (int t = 0; t < 3; ++t) {
+            int c0, c1;
+            fast_cell_range(A, tiles[t], &c0, &c1);
+            any[t] = c1 > c0;
+            iso = iso || (any[t] && chunks.size() > 1 && (c->serialize || ((c->isolate_mask >> stages[t]) & 1u)));
+        }
+        if (iso) {
+            for (size_t k = 1; k < chunks.size(); ++k) {
+                HIP_TRY(hipEventRecord(c->join[k], chunks[k].st));
+                HIP_TRY(hipStreamWaitEvent(chunks[0].st, c->join[k], 0));
+            }
+        }
+        for (int t = 0; t < 3; ++t) {
+            if (!any[t]) continue;
+            for (const Chunk& ch : chunks) {
+                BatchArgs B = A;
+                if (!iso) {
+                    B.img0 = ch.img0;
+                    B.nimages = ch.n;
+                }
+                const hipStream_t st = ch.st;
+                const int tile = tiles[t];
+                if ((r = timed(c, stages[t], st, [&] { return launch_fast_cells(B, tile, st); }))) return r;
+                if (iso) break;  // whole batch on the main stream
+            }
+        }
+        if (iso) {
+            HIP_TRY(hipEventRecord(c->fork, chunks[0].st));
+            for (size_t k = 1; k < chunks.size(); ++k) HIP_TRY(hipStreamWaitEvent(chunks[k].st, c->fork, 0));
+        }
+    }
     if ((r = each(ST_OCTREE, [](const BatchArgs& B, hipStream_t st) { return launch_octree(B, st); }))) return r;
     if ((r = each(ST_ORIENT, [](const BatchArgs& B, hipStream_t st) { return launch_orient_desc(B, st); }))) return r;
     if ((r = each(ST_FINAL, [](const BatchArgs& B, hipStream_t st) { return launch_finalize(B, st); }))) return r;

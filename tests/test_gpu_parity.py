@@ -202,18 +202,23 @@ def test_gpu_matches_golden_fixtures():
         np.testing.assert_array_equal(a, g[key])
 
 
-def test_general_fast_tile(oracle, frame0, monkeypatch):
-    """The 80-byte-pitch FAST tile (used when a level's cells exceed the 48-byte tile) on the
-    640x480 frame, forced through ORBGPU_FAST_PITCH, and a small frame whose top levels have
-    cells wider than 39 px so the runtime picks it by itself."""
+@pytest.mark.parametrize("pitch", ["64", "80"])
+def test_forced_fast_tile(oracle, frame0, monkeypatch, pitch):
+    """The 64- and 80-byte-pitch FAST tiles (the runtime uses 48 bytes for the leading levels of
+    a 640x480 pyramid, 64 for its top levels and 80 for cells wider than 55 px) on every level
+    of the 640x480 frame, forced through ORBGPU_FAST_PITCH."""
     L, _ = frame0
-    monkeypatch.setenv("ORBGPU_FAST_PITCH", "80")
+    monkeypatch.setenv("ORBGPU_FAST_PITCH", pitch)
     ex = _extractor()
     k, d, m = ex(L)
     rk, rd, rm = oracle.extract(L, nfeatures=2000)
     _same_kps(k, rk)
     np.testing.assert_array_equal(d, rd)
-    monkeypatch.delenv("ORBGPU_FAST_PITCH")
+
+
+def test_general_fast_tile_small_frame(oracle):
+    """A small frame whose top levels have cells wider than 55 px, so the runtime picks the
+    80-byte tile by itself."""
     img = synth.frame(120, 160, 5)
     ex = _extractor(nf=300, L=4, w=160, h=120)
     k, d, m = ex(img)

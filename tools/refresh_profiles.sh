@@ -1,0 +1,18 @@
+#!/bin/bash
+# One-call refresh of the round's evidence (run on the GPU box from the repo root):
+# GPU parity log, the bench line, the rocprofv3 kernel-trace summary of the same bench
+# command, and the FETCH_SIZE/WRITE_SIZE traffic passes.  Stops at the first failing step.
+set -e
+cd "$(dirname "$0")/.."
+export TMPDIR=/tmp
+O=gpurun_out/refresh
+mkdir -p $O
+timeout -k 10 300 python -m pytest tests -m gpu -v > $O/pytest_gpu.log 2>&1
+echo pytest-done
+timeout -k 10 300 python bench.py > $O/bench.json 2> $O/bench.err
+echo bench-done
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 bench.py > $O/prof.log 2>&1
+echo prof-done
+bash tools/pmc_traffic.sh $O/pmct
+python3 tools/traffic.py $O/pmct $O/traffic.json > /dev/null
+echo all-done
