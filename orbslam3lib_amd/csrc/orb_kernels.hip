@@ -892,6 +892,142 @@ __global__ __launch_bounds__(256) void k_knn2_plain(const uint8_t* q, int nq, co
 }
 
 // ---------------------------------------------------------------------------------------------
+// k_knn2_mfma: BFMatcher(NORM_HAMMING).knnMatch(k=2) on the matrix cores.  With every descriptor
+// bit b mapped to +-64 (int8), the i8 MFMA dot of a train row t and a query q is
+// 4096 * (256 - 2 * Hamming(t, q)); the accumulator is preloaded with 4095 - (t mod 4096), so
+// acc = 4096 * (256 - 2H) + 4095 - t_local orders exactly like (H, t) ascending and the best two
+// train rows are the two largest accumulators (no popcount, no per-pair VALU beyond the top-2
+// update).  Train rows are walked in 4096-row segments (12-bit local index); each segment's
+// winners are folded into (H << 16 | t) keys, the layout of the VALU matcher.
+//   workgroup = 4 waves x 32 queries; per 32-row train tile each wave issues 8
+//   v_mfma_i32_32x32x32_i8 (K = 256 bits): A = train tile (expanded once per workgroup into
+//   LDS, double-buffered), B = the wave's queries (expanded once into registers).
+// C/D layout (cdna_hip_programming.md §3): lane l holds column l & 31 (its query) and rows
+// (reg & 3) + 8 (reg >> 2) + 4 (l >> 5) of the tile (train rows); the K order inside a
+// fragment is the same map for A and B, so any consistent bit -> element assignment is exact.
+typedef int knn_v4i __attribute__((ext_vector_type(4)));
+typedef int knn_v16i __attribute__((ext_vector_type(16)));
+constexpr int kKnnQ = 128;       // queries per workgroup
+constexpr int kKnnPitch = 272;   // bytes per expanded train row in LDS (256 + 16: no bank conflicts)
+constexpr int kKnnSeg = 4096;    // train rows per key segment
+
+// 4 descriptor bits -> 4 int8 (+64 for a set bit, -64 otherwise), bit k -> byte k
+__device__ inline uint32_t knn_expand4(uint32_t n) {
+    const uint32_t x = (n * 0x204081u) & 0x01010101u;
+    return (x << 7) ^ 0xC0C0C0C0u;
+}
+__device__ inline knn_v4i knn_expand16(uint32_t b) {  // 16 bits -> 16 int8
+    knn_v4i v;
+    v[0] = (int)knn_expand4(b & 15u);
+    v[1] = (int)knn_expand4((b >> 4) & 15u);
+    v[2] = (int)knn_expand4((b >> 8) & 15u);
+    v[3] = (int)knn_expand4((b >> 12) & 15u);
+    return v;
+}
+
+// One workgroup: queries [qb * 128, +128) of q against all nt train rows of t.
+__device__ __attribute__((always_inline)) inline void knn2_mfma_block(
+    const uint8_t* q, int nq, const uint8_t* t, int nt, int qb, int32_t* i1, int32_t* d1, int32_t* i2,
+    int32_t* d2, uint8_t* lds) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int r = lane & 31, h = lane >> 5;
+    const int qi = qb * kKnnQ + wave * 32 + r;
+    // B fragments: lane (r, h) of MFMA s holds bits 32 s + 16 h + [0, 16) of query qi
+    knn_v4i qf[8];
+    {
+        const uint4* qp = reinterpret_cast<const uint4*>(q + (long long)min(qi, max(nq - 1, 0)) * 32);
+        const uint4 qa = qp[0], qc = qp[1];
+        const uint32_t dw[8] = {qa.x, qa.y, qa.z, qa.w, qc.x, qc.y, qc.z, qc.w};
+#pragma unroll
+        for (int s = 0; s < 8; ++s) qf[s] = knn_expand16(dw[s] >> (16 * h));
+    }
+    uint32_t g1 = 0xFFFFFFFFu, g2 = 0xFFFFFFFFu;  // (H << 16 | t), lexicographic min
+    const int ntiles_all = (nt + 31) >> 5;
+    // expansion role: thread -> (row tid >> 3, dword tid & 7) of a tile
+    const int er = tid >> 3, ed = tid & 7;
+    auto load_packed = [&](int tile) __attribute__((always_inline)) {
+        const int row = min(tile * 32 + er, nt - 1);
+        return *reinterpret_cast<const uint32_t*>(t + (long long)row * 32 + 4 * ed);
+    };
+    auto store_expanded = [&](int buf, uint32_t w) __attribute__((always_inline)) {
+        uint8_t* dst = lds + buf * (32 * kKnnPitch) + er * kKnnPitch + 32 * ed;
+        const knn_v4i lo = knn_expand16(w & 0xFFFFu), hi = knn_expand16(w >> 16);
+        *reinterpret_cast<knn_v4i*>(dst) = lo;
+        *reinterpret_cast<knn_v4i*>(dst + 16) = hi;
+    };
+    if (nt > 0) store_expanded(0, load_packed(0));
+    for (int seg0 = 0; seg0 < nt; seg0 += kKnnSeg) {
+        const int tile0 = seg0 >> 5, tile1 = min(ntiles_all, (seg0 + kKnnSeg) >> 5);
+        int k1 = INT_MIN, k2 = INT_MIN;  // segment-local keys, lexicographic max
+        for (int ti = tile0; ti < tile1; ++ti) {
+            __syncthreads();  // tile ti expanded; the other buffer is free
+            const bool more = ti + 1 < ntiles_all;
+            uint32_t nw = 0;
+            if (more) nw = load_packed(ti + 1);  // in flight during the MFMAs
+            const uint8_t* ab = lds + (ti & 1) * (32 * kKnnPitch) + r * kKnnPitch + 16 * h;
+            knn_v16i acc;
+#pragma unroll
+            for (int g = 0; g < 16; ++g) {
+                const int row = (g & 3) + 8 * (g >> 2) + 4 * h;
+                const int tg = ti * 32 + row;  // global train row
+                acc[g] = tg < nt ? 4095 - (tg - seg0) : -(1 << 30);
+            }
+#pragma unroll
+            for (int s = 0; s < 8; ++s) {
+                const knn_v4i a = *reinterpret_cast<const knn_v4i*>(ab + 32 * s);
+                acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, qf[s], acc, 0, 0, 0);
+            }
+#pragma unroll
+            for (int g = 0; g < 16; ++g) {
+                const int x = acc[g];
+                k2 = max(min(k1, k2), min(max(k1, k2), x));  // v_med3_i32
+                k1 = max(k1, x);
+            }
+            if (more) store_expanded((ti + 1) & 1, nw);
+        }
+        // fold the segment's two winners into global (H << 16 | t) keys
+        auto fold = [&](int k) __attribute__((always_inline)) {
+            if (k < -(1 << 24)) return;  // padding rows only
+            const int tl = 4095 - (k & 4095), dotp = k >> 12;
+            const uint32_t key = ((uint32_t)((256 - dotp) >> 1) << 16) | (uint32_t)(seg0 + tl);
+            g2 = med3_u32(g1, g2, key);
+            g1 = min(g1, key);
+        };
+        fold(k1);
+        fold(k2);
+    }
+    // the two lane halves saw disjoint train rows of the same query
+    const uint32_t o1 = __shfl_xor(g1, 32), o2 = __shfl_xor(g2, 32);
+    g2 = med3_u32(g1, g2, o1);
+    g1 = min(g1, o1);
+    g2 = med3_u32(g1, g2, o2);
+    g1 = min(g1, o2);
+    if (h == 0 && qi < nq) knn2_store(g1, g2, qi, i1, d1, i2, d2);
+}
+
+__global__ __launch_bounds__(256) void k_knn2_mfma_pairs(MatchArgs m) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * 32 * kKnnPitch];
+    const int pair = m.pair0 + blockIdx.y;
+    const int qimg = 2 * pair, timg = 2 * pair + 1;
+    const int qn = m.out_n[qimg], tn = m.out_n[timg];
+    const int q0 = m.stereo_only ? m.out_mono[qimg] : 0;
+    const int tq0 = m.stereo_only ? m.out_mono[timg] : 0;
+    const int nq = qn > q0 ? qn - q0 : 0, nt = tn > tq0 ? tn - tq0 : 0;
+    if (blockIdx.x == 0 && threadIdx.x == 0) m.nq[pair] = nq;
+    if ((int)blockIdx.x * kKnnQ >= nq) return;
+    const uint8_t* q = m.desc + ((long long)qimg * m.out_cap + q0) * 32;
+    const uint8_t* t = m.desc + ((long long)timg * m.out_cap + tq0) * 32;
+    const long long o = (long long)pair * m.out_cap;
+    knn2_mfma_block(q, nq, t, nt, blockIdx.x, m.idx1 + o, m.dist1 + o, m.idx2 + o, m.dist2 + o, lds);
+}
+
+__global__ __launch_bounds__(256) void k_knn2_mfma_plain(const uint8_t* q, int nq, const uint8_t* t, int nt,
+                                                         int32_t* i1, int32_t* d1, int32_t* i2, int32_t* d2) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * 32 * kKnnPitch];
+    knn2_mfma_block(q, nq, t, nt, blockIdx.x, i1, d1, i2, d2, lds);
+}
+
+// ---------------------------------------------------------------------------------------------
 hipError_t launch_resize(const BatchArgs& a, int level, hipStream_t s) {
     const LevelGeom& G = a.lv[level];
     dim3 grid((G.w + kRsTW - 1) / kRsTW, (G.h + kRsTH - 1) / kRsTH, a.nimages);
@@ -944,7 +1080,15 @@ hipError_t launch_finalize(const BatchArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_finalize, dim3(a.nimages), dim3(256), 0, s, a);
     return hipGetLastError();
 }
+static bool knn_valu() {  // diagnostics: the VALU popcount matcher
+    static const bool v = getenv("ORBGPU_KNN_VALU") != nullptr;
+    return v;
+}
 hipError_t launch_knn2_pairs(const MatchArgs& m, int npairs, int qblocks, void* scratch, hipStream_t s) {
+    if (!knn_valu()) {
+        hipLaunchKernelGGL(k_knn2_mfma_pairs, dim3((m.out_cap + kKnnQ - 1) / kKnnQ, npairs), dim3(256), 0, s, m);
+        return hipGetLastError();
+    }
     KnnPart part{reinterpret_cast<uint32_t*>(scratch)};
     hipLaunchKernelGGL(k_knn2_pairs, dim3(qblocks, kKnnSplit, npairs), dim3(256), 0, s, m, part);
     hipLaunchKernelGGL(k_knn2_merge, dim3(qblocks, npairs), dim3(256), 0, s, m, part);
@@ -953,9 +1097,13 @@ hipError_t launch_knn2_pairs(const MatchArgs& m, int npairs, int qblocks, void* 
 size_t knn2_scratch_bytes(int npairs, int out_cap) { return (size_t)npairs * kKnnSplit * out_cap * 8 + 256; }
 hipError_t launch_knn2_plain(const uint8_t* q, int nq, const uint8_t* t, int nt, int32_t* i1,
                              int32_t* d1, int32_t* i2, int32_t* d2, hipStream_t s) {
-    const int blocks = (nq + 255) / 256;
-    if (blocks == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_knn2_plain, dim3(blocks), dim3(256), 0, s, q, nq, t, nt, i1, d1, i2, d2);
+    if (nq == 0) return hipSuccess;
+    if (!knn_valu()) {
+        hipLaunchKernelGGL(k_knn2_mfma_plain, dim3((nq + kKnnQ - 1) / kKnnQ), dim3(256), 0, s, q, nq, t, nt, i1,
+                           d1, i2, d2);
+        return hipGetLastError();
+    }
+    hipLaunchKernelGGL(k_knn2_plain, dim3((nq + 255) / 256), dim3(256), 0, s, q, nq, t, nt, i1, d1, i2, d2);
     return hipGetLastError();
 }
 
