@@ -3,13 +3,15 @@ HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
 CSRC := orbslam3lib_amd/csrc
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function -Wno-unused-value -Wno-unused-result
+# MFMA accumulators in VGPRs (k_knn2_mfma reads every result: no v_accvgpr copies)
+DEVFLAGS := -mllvm -amdgpu-mfma-vgpr-form
 LIB := orbslam3lib_amd/liborbgpu.so
 HDRS := $(wildcard $(CSRC)/*.h) include/orbgpu.h
 
 all: $(LIB) oracle facade_test
 
 $(LIB): $(CSRC)/orb_kernels.hip $(CSRC)/orb_runtime.cpp $(HDRS)
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(CSRC)/orb_kernels.hip $(CSRC)/orb_runtime.cpp
+	$(HIPCC) $(HIPFLAGS) $(DEVFLAGS) -shared -o $@ $(CSRC)/orb_kernels.hip $(CSRC)/orb_runtime.cpp
 
 oracle:
 	$(MAKE) -s -C oracle

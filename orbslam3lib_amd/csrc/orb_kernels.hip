@@ -913,7 +913,9 @@ constexpr int kKnnSeg = 4096;    // train rows per key segment
 
 // 4 descriptor bits -> 4 int8 (+64 for a set bit, -64 otherwise), bit k -> byte k
 __device__ inline uint32_t knn_expand4(uint32_t n) {
-    const uint32_t x = (n * 0x204081u) & 0x01010101u;
+    uint32_t x;  // n * 0x204081 (n < 16) on the full-rate 24-bit multiplier
+    asm("v_mul_u32_u24 %0, 0x204081, %1" : "=v"(x) : "v"(n));
+    x &= 0x01010101u;
     return (x << 7) ^ 0xC0C0C0C0u;
 }
 __device__ inline knn_v4i knn_expand16(uint32_t b) {  // 16 bits -> 16 int8
@@ -955,36 +957,70 @@ __device__ __attribute__((always_inline)) inline void knn2_mfma_block(
         *reinterpret_cast<knn_v4i*>(dst) = lo;
         *reinterpret_cast<knn_v4i*>(dst + 16) = hi;
     };
-    if (nt > 0) store_expanded(0, load_packed(0));
+    // packed train words run two tiles ahead of the MFMAs (one in LDS, one in flight): the word
+    // of tile u lives in pk[u & 1]; loads are unconditional (clamped rows) so waits stay counted
+    uint32_t pk0 = 0, pk1 = 0;
+    if (nt > 0) {
+        store_expanded(0, load_packed(0));
+        pk1 = load_packed(1);
+    }
+    // accumulator preload: row(g) = (g & 3) + 8 (g >> 2) + 4 h, so 4095 - local row index is
+    // (4095 - 4 h - 32 (tile - tile0)) - rowc(g) with a compile-time rowc
+    auto rowc = [](int g) { return (g & 3) + 8 * (g >> 2); };
     for (int seg0 = 0; seg0 < nt; seg0 += kKnnSeg) {
-        const int tile0 = seg0 >> 5, tile1 = min(ntiles_all, (seg0 + kKnnSeg) >> 5);
-        int k1 = INT_MIN, k2 = INT_MIN;  // segment-local keys, lexicographic max
-        for (int ti = tile0; ti < tile1; ++ti) {
-            __syncthreads();  // tile ti expanded; the other buffer is free
-            const bool more = ti + 1 < ntiles_all;
-            uint32_t nw = 0;
-            if (more) nw = load_packed(ti + 1);  // in flight during the MFMAs
-            const uint8_t* ab = lds + (ti & 1) * (32 * kKnnPitch) + r * kKnnPitch + 16 * h;
-            knn_v16i acc;
+        const int tile0 = seg0 >> 5, tile1 = min(ntiles_all, (seg0 + kKnnSeg) >> 5);  // tile0 even
+        // two independent top-2 chains (even / odd accumulator rows), segment-local keys,
+        // lexicographic max; the selection of tile ti - 1 runs while tile ti's MFMAs are in flight
+        int ka1 = INT_MIN, ka2 = INT_MIN, kb1 = INT_MIN, kb2 = INT_MIN;
+        auto select = [&](const knn_v16i& v) __attribute__((always_inline)) {
 #pragma unroll
-            for (int g = 0; g < 16; ++g) {
-                const int row = (g & 3) + 8 * (g >> 2) + 4 * h;
-                const int tg = ti * 32 + row;  // global train row
-                acc[g] = tg < nt ? 4095 - (tg - seg0) : -(1 << 30);
+            for (int g = 0; g < 16; g += 2) {
+                const int x = v[g], y = v[g + 1];
+                ka2 = max(min(ka1, ka2), min(max(ka1, ka2), x));  // v_med3_i32
+                ka1 = max(ka1, x);
+                kb2 = max(min(kb1, kb2), min(max(kb1, kb2), y));
+                kb1 = max(kb1, y);
+            }
+        };
+        // one tile: PAR = ti & 1 picks the LDS buffer, the accumulator and the packed word
+        auto body = [&](int ti, auto par, knn_v16i& acc, const knn_v16i& prev, uint32_t& pk_use,
+                        uint32_t& pk_load) __attribute__((always_inline)) {
+            constexpr int PAR = decltype(par)::value;
+            __syncthreads();  // tile ti expanded; the other buffer is free
+            pk_load = load_packed(ti + 2);  // word of tile ti + 2 (pk[ti & 1] is free)
+            const uint8_t* ab = lds + PAR * (32 * kKnnPitch) + r * kKnnPitch + 16 * h;
+            const int base = 4095 - 4 * h - 32 * (ti - tile0);
+#pragma unroll
+            for (int g = 0; g < 16; ++g) acc[g] = base - rowc(g);
+            if (ti * 32 + 32 > nt) {  // partial last tile: padding rows never win
+#pragma unroll
+                for (int g = 0; g < 16; ++g)
+                    if (ti * 32 + rowc(g) + 4 * h >= nt) acc[g] = -(1 << 30);
             }
 #pragma unroll
             for (int s = 0; s < 8; ++s) {
                 const knn_v4i a = *reinterpret_cast<const knn_v4i*>(ab + 32 * s);
                 acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, qf[s], acc, 0, 0, 0);
             }
-#pragma unroll
-            for (int g = 0; g < 16; ++g) {
-                const int x = acc[g];
-                k2 = max(min(k1, k2), min(max(k1, k2), x));  // v_med3_i32
-                k1 = max(k1, x);
-            }
-            if (more) store_expanded((ti + 1) & 1, nw);
+            if (ti > tile0) select(prev);
+            if (ti + 1 < ntiles_all) store_expanded(PAR ^ 1, pk_use);  // word of tile ti + 1
+        };
+        using P0 = std::integral_constant<int, 0>;
+        using P1 = std::integral_constant<int, 1>;
+        knn_v16i acc0, acc1;
+        int ti = tile0;
+        for (; ti + 1 < tile1; ti += 2) {
+            body(ti, P0{}, acc0, acc1, pk1, pk0);
+            body(ti + 1, P1{}, acc1, acc0, pk0, pk1);
         }
+        if (ti < tile1) {
+            body(ti, P0{}, acc0, acc1, pk1, pk0);
+            select(acc0);
+        } else if (tile1 > tile0) {
+            select(acc1);
+        }
+        int k1 = max(ka1, kb1);
+        int k2 = max(min(ka1, kb1), max(ka2, kb2));
         // fold the segment's two winners into global (H << 16 | t) keys
         auto fold = [&](int k) __attribute__((always_inline)) {
             if (k < -(1 << 24)) return;  // padding rows only
