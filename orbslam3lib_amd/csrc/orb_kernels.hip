@@ -81,11 +81,17 @@ __constant__ MomentWeights c_mw = make_moment_weights();
 // cv::resize INTER_LINEAR).  Horizontal: D = S[sx]*a0 + S[sx1]*a1 (int); vertical: OpenCV's
 // 128-bit SIMD body for x < simd_end, FixedPtCast tail after.  A block makes a 256 x 16 output
 // tile: its x-table slice and the source window (dword loads) are staged in LDS first.
-constexpr int kRsTW = 256, kRsTH = 16, kRsSrcRows = 2 * kRsTH + 2, kRsSrcCols = 2 * kRsTW + 16;
-static_assert(kRsSrcCols % 16 == 0, "window rows are written in 16-byte chunks");
+constexpr int kRsTW = 256, kRsTH = 16;
+// source window (rows, bytes) for scale factors up to 2 and, smaller (more workgroups per CU),
+// up to 1.25: tile * scale + the second tap + 2 px margin each side, rounded to 16 bytes
+constexpr int kRsSrcRows = 2 * kRsTH + 2, kRsSrcCols = 2 * kRsTW + 16;
+constexpr int kRsSrcRowsS = 24, kRsSrcColsS = 336;
+static_assert(kRsSrcCols % 16 == 0 && kRsSrcColsS % 16 == 0, "window rows are written in 16-byte chunks");
 
+template <int kRsSrcRows, int kRsSrcCols>
 __global__ __launch_bounds__(256) void k_resize(BatchArgs a, int l) {
     __shared__ int4 xt_s[kRsTW];
+    __shared__ int4 yt_s[kRsTH];
     __shared__ __attribute__((aligned(16))) uint32_t win[kRsSrcRows][kRsSrcCols / 4];
     const LevelGeom& G = a.lv[l];
     const LevelGeom& S = a.lv[l - 1];
@@ -112,19 +118,21 @@ __global__ __launch_bounds__(256) void k_resize(BatchArgs a, int l) {
         return;
     }
     const int tw = min(kRsTW, G.w - tx0), th = min(kRsTH, G.h - ty0);
+    // the tables and the source window load together: the window origin is estimated from the
+    // scale (2 px margin), the tables decide below whether the window covers the tile exactly
     for (int i = threadIdx.x; i < tw; i += 256) xt_s[i] = a.rtab[G.xtab_off + tx0 + i];
-    const int4 yfirst = a.rtab[G.ytab_off + ty0], ylast = a.rtab[G.ytab_off + ty0 + th - 1];
-    const int sy_lo = yfirst.x, sy_hi = ylast.y;
-    const int sx_lo = a.rtab[G.xtab_off + tx0].x & ~3;
-    const int sx_hi = a.rtab[G.xtab_off + tx0 + tw - 1].y;
-    const int nrows = sy_hi - sy_lo + 1, ndw = (sx_hi - sx_lo) / 4 + 1;
-    const bool staged = nrows <= kRsSrcRows && ndw <= kRsSrcCols / 4 && (S.pitch & 3) == 0;
-    if (staged) {
+    if (threadIdx.x < th) yt_s[threadIdx.x] = a.rtab[G.ytab_off + ty0 + threadIdx.x];
+    const float sxf = (float)S.w / (float)G.w, syf = (float)S.h / (float)G.h;
+    const int sx_lo = max(0, (int)floorf(((float)tx0 + 0.5f) * sxf - 0.5f) - 2) & ~3;
+    const int sy_lo = max(0, (int)floorf(((float)ty0 + 0.5f) * syf - 0.5f) - 2);
+    const int nrows = min(kRsSrcRows, S.h - sy_lo);
+    const int nq4 = min(kRsSrcCols / 16, (S.w - sx_lo + 15) >> 4);  // 16-byte chunks per row
+    const bool aligned = (S.pitch & 3) == 0;
+    if (aligned) {
         // 16-byte buffer loads (bounds-checked: bytes past the plane read as 0 and are never
         // used); half a wave per source row, no integer division
         const __amdgpu_buffer_rsrc_t srs = __builtin_amdgcn_make_buffer_rsrc(
             (void*)src, (short)0, (int)min(S.img_stride, 0x7fffffffLL), 0x00020000);
-        const int nq4 = (ndw + 3) >> 2;  // 16-byte chunks per row (<= 33)
         const int half = threadIdx.x >> 5, hl = threadIdx.x & 31;
         for (int r = half; r < nrows; r += 8) {
             const int rowofs = (sy_lo + r) * S.pitch + sx_lo;
@@ -135,6 +143,8 @@ __global__ __launch_bounds__(256) void k_resize(BatchArgs a, int l) {
         }
     }
     __syncthreads();
+    const bool staged = aligned && xt_s[0].x >= sx_lo && xt_s[tw - 1].y < sx_lo + 16 * nq4 &&
+                        yt_s[0].x >= sy_lo && yt_s[th - 1].y < sy_lo + nrows;
     const uint8_t* wb = reinterpret_cast<const uint8_t*>(&win[0][0]);
     const int q = threadIdx.x & 63;
     // one body per source (LDS window / global plane): a merged body would take flat loads
@@ -143,7 +153,7 @@ __global__ __launch_bounds__(256) void k_resize(BatchArgs a, int l) {
             const int dy = ty0 + rr;
             const int dx0 = tx0 + 4 * q;
             if (4 * q >= tw) continue;
-            const int4 yt = a.rtab[G.ytab_off + dy];
+            const int4 yt = yt_s[rr];
             const int b0 = yt.z, b1 = yt.w;
             const auto r0 = row_ptr(yt.x), r1 = row_ptr(yt.y);
             uint32_t packed = 0;
@@ -1066,8 +1076,12 @@ __global__ __launch_bounds__(256) void k_knn2_mfma_plain(const uint8_t* q, int n
 // ---------------------------------------------------------------------------------------------
 hipError_t launch_resize(const BatchArgs& a, int level, hipStream_t s) {
     const LevelGeom& G = a.lv[level];
+    const LevelGeom& S = a.lv[level - 1];
     dim3 grid((G.w + kRsTW - 1) / kRsTW, (G.h + kRsTH - 1) / kRsTH, a.nimages);
-    hipLaunchKernelGGL(k_resize, grid, dim3(256), 0, s, a, level);
+    if (4 * S.w <= 5 * G.w && 4 * S.h <= 5 * G.h)  // scale <= 1.25: the small window
+        hipLaunchKernelGGL((k_resize<kRsSrcRowsS, kRsSrcColsS>), grid, dim3(256), 0, s, a, level);
+    else
+        hipLaunchKernelGGL((k_resize<kRsSrcRows, kRsSrcCols>), grid, dim3(256), 0, s, a, level);
     return hipGetLastError();
 }
 hipError_t launch_blur(const BatchArgs& a, hipStream_t s) {
