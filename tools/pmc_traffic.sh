@@ -5,6 +5,6 @@ cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
 OUT=${1:-gpurun_out/pmct}
 mkdir -p $OUT
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/p0 -o pmc -- python3 tools/profile_batch.py > $OUT/p0.log 2>&1
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/p1 -o pmc -- python3 tools/profile_batch.py > $OUT/p1.log 2>&1
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/p0 -o pmc -- python3 tools/profile_batch.py > $OUT/p0.log 2>&1
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/p1 -o pmc -- python3 tools/profile_batch.py > $OUT/p1.log 2>&1
 echo traffic-done

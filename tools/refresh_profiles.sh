@@ -7,7 +7,7 @@ cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
 O=gpurun_out/refresh
 mkdir -p $O
-timeout -k 10 300 python -m pytest tests -m gpu -v > $O/pytest_gpu.log 2>&1
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1
 echo pytest-done
 timeout -k 10 300 python bench.py > $O/bench.json 2> $O/bench.err
 echo bench-done
