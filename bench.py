@@ -54,11 +54,12 @@ def fast_split(w, h, sf=1.2, L=8, tile=64):
 def algorithmic_bytes(w, h, L, nkp, sf=1.2):
     """Per-image bytes by stage: pyramid sum(A_{l-1}+A_l), FAST sum(A_l) (split
     between the 48-, 64- and 80-byte tile launches), blur 2*sum(A_l), 48 B per output keypoint
-    (16 B keypoint + 32 B descriptor)."""
+    (16 B keypoint + 32 B descriptor); k_pyramid = pyramid + blur in one launch."""
     A = [a * b for a, b in level_sizes(w, h, sf, L)]
     k48 = fast_split(w, h, sf, L, 48)
     k64 = max(k48, fast_split(w, h, sf, L, 64))
     return {
+        "k_pyramid": sum(A[l - 1] + A[l] for l in range(1, L)) + 2 * sum(A),
         "k_resize": sum(A[l - 1] + A[l] for l in range(1, L)),
         "k_fast_cells<48>": sum(A[:k48]),
         "k_fast_cells<64>": sum(A[k48:k64]),

@@ -71,7 +71,11 @@ struct BatchArgs {
     int oct_nq_off;                  // byte offset of the per-key labels in that LDS
     int oct_may_retry;               // some level can exceed the LDS instantiation of k_octree
     int oct_force_retry;             // diagnostics: every level through the generic instantiation
+    // k_pyramid stripe tables in rtab, one per stripe count 2^i (i < kPyrStripeKinds):
+    // entry [l * S + k] = {need_lo, need_hi, own_lo, own_hi} rows of level l for stripe k
+    int stripe_tab_off[5];
 };
+constexpr int kPyrStripeKinds = 5;  // 1, 2, 4, 8, 16 stripes per image
 
 struct MatchArgs {
     const uint8_t* desc;      // out_desc
@@ -114,6 +118,9 @@ __host__ __device__ inline OctLayout oct_layout(int n_cap, int C) {
 // Kernel launchers (orb_kernels.hip).  Each returns hipGetLastError() of its launch.
 hipError_t launch_resize(const BatchArgs& a, int level, hipStream_t s);
 hipError_t launch_blur(const BatchArgs& a, hipStream_t s);
+// the whole pyramid (levels 1..L-1) and every blurred level in one launch: one workgroup per
+// (image, row stripe), 2^stripe_log2 stripes per image
+hipError_t launch_pyramid(const BatchArgs& a, int stripe_log2, hipStream_t s);
 // FAST cells of the levels that run the `tile`-byte LDS tile (48, 64 or kCellMax = 80):
 // fast_cell_range gives their flattened cell range, launch_fast_cells launches nothing if empty
 void fast_cell_range(const BatchArgs& a, int tile, int* c0, int* c1);

@@ -88,25 +88,72 @@ constexpr int kRsSrcRows = 2 * kRsTH + 2, kRsSrcCols = 2 * kRsTW + 16;
 constexpr int kRsSrcRowsS = 24, kRsSrcColsS = 336;
 static_assert(kRsSrcCols % 16 == 0 && kRsSrcColsS % 16 == 0, "window rows are written in 16-byte chunks");
 
-template <int kRsSrcRows, int kRsSrcCols>
-__global__ __launch_bounds__(256) void k_resize(BatchArgs a, int l) {
-    __shared__ int4 xt_s[kRsTW];
-    __shared__ int4 yt_s[kRsTH];
-    __shared__ __attribute__((aligned(16))) uint32_t win[kRsSrcRows][kRsSrcCols / 4];
+// Four output pixels dx0 .. dx0+3 of one output row from source rows r0 / r1 (LDS window or
+// GlobalRow), x coefficients xt[0..3] (entries past the tile edge may be stale: their bytes are
+// padding or the next tile's, rewritten there), y coefficients b0 / b1.  Every product fits 24
+// bits (pixel <= 255, coefficients <= 2048, (D >> 4) < 2^15), so all multiplies are full-rate
+// v_mul_u32_u24 / v_mad_u32_u24.  Vertical rounding: OpenCV's SIMD body below simd_end,
+// FixedPtCast after it (only the last quads of a row take that branch).
+template <class Row>
+__device__ inline uint32_t rs_quad(const Row& r0, const Row& r1, const int4* xt, int b0, int b1, int dx0,
+                                   int simd_end) {
+    int D0[4], D1[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int4 x = xt[k];
+        D0[k] = __umul24(r0[x.x], x.z) + __umul24(r0[x.y], x.w);
+        D1[k] = __umul24(r1[x.x], x.z) + __umul24(r1[x.y], x.w);
+    }
+    uint32_t packed = 0;
+    if (dx0 + 3 < simd_end) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int sv = (__umul24(D0[k] >> 4, b0) >> 16) + (__umul24(D1[k] >> 4, b1) >> 16);
+            packed |= (uint32_t)min((sv + 2) >> 2, 255) << (8 * k);
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            int o;
+            if (dx0 + k < simd_end) {
+                const int sv = (__umul24(D0[k] >> 4, b0) >> 16) + (__umul24(D1[k] >> 4, b1) >> 16);
+                o = (sv + 2) >> 2;
+            } else {
+                o = (int)(((unsigned)D0[k] * (unsigned)b0 + (unsigned)D1[k] * (unsigned)b1 + (1u << 21)) >> 22);
+            }
+            packed |= (uint32_t)min(o, 255) << (8 * k);
+        }
+    }
+    return packed;
+}
+
+// Source bytes of a plane through bounds-checked byte loads (kAux: cache policy).
+template <int kAux>
+struct GlobalRow {
+    __amdgpu_buffer_rsrc_t rs;
+    int off;
+    __device__ int operator[](int x) const { return __builtin_amdgcn_raw_buffer_load_b8(rs, off + x, 0, kAux); }
+};
+
+// One 256 x 16 output tile of level l, output rows limited to [ty0, rhi).  xt_s / yt_s / win
+// are the caller's LDS; the caller synchronizes before the next tile reuses them.  kAux is the
+// cache policy of every source load (sc1 where the source was written by this launch).
+template <int kRsSrcRows, int kRsSrcCols, int kAux>
+__device__ inline void resize_tile(const BatchArgs& a, int img, int l, int tx0, int ty0, int rhi,
+                                   int4* xt_s, int4* yt_s, uint32_t (*win)[kRsSrcCols / 4]) {
     const LevelGeom& G = a.lv[l];
     const LevelGeom& S = a.lv[l - 1];
-    const int nxy = gridDim.x * gridDim.y;
-    const int wg = xcd_remap(blockIdx.x + blockIdx.y * gridDim.x + blockIdx.z * nxy, nxy * gridDim.z);
-    const int img = a.img0 + wg / nxy;
-    const int tx0 = (wg % nxy % gridDim.x) * kRsTW, ty0 = (wg % nxy / gridDim.x) * kRsTH;
     const uint8_t* src = a.lvl_base[l - 1] + (long long)img * S.img_stride;
     uint8_t* dst = a.lvl_base[l] + (long long)img * G.img_stride;
+    const __amdgpu_buffer_rsrc_t srs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)src, (short)0, (int)min(S.img_stride, 0x7fffffffLL), 0x00020000);
+    const int tw = min(kRsTW, G.w - tx0), th = min(min(kRsTH, G.h - ty0), rhi - ty0);
     if (G.area2) {  // resize.cpp: INTER_LINEAR at exactly 2x is serviced by INTER_AREA fast
         for (int i = threadIdx.x; i < kRsTW / 4 * kRsTH; i += 256) {
-            const int dy = ty0 + i / (kRsTW / 4), dx0 = tx0 + 4 * (i % (kRsTW / 4));
-            if (dy >= G.h || dx0 >= G.w) continue;
-            const uint8_t* s0 = src + (long long)(2 * dy) * S.pitch;
-            const uint8_t* s1 = s0 + S.pitch;
+            const int rr = i / (kRsTW / 4), dx0 = tx0 + 4 * (i % (kRsTW / 4));
+            if (rr >= th || dx0 >= G.w) continue;
+            const int dy = ty0 + rr;
+            const GlobalRow<kAux> s0{srs, 2 * dy * S.pitch}, s1{srs, (2 * dy + 1) * S.pitch};
             uint32_t pk = 0;
             for (int k = 0; k < 4; ++k) {
                 const int dx = min(dx0 + k, G.w - 1);
@@ -117,7 +164,6 @@ __global__ __launch_bounds__(256) void k_resize(BatchArgs a, int l) {
         }
         return;
     }
-    const int tw = min(kRsTW, G.w - tx0), th = min(kRsTH, G.h - ty0);
     // the tables and the source window load together: the window origin is estimated from the
     // scale (2 px margin), the tables decide below whether the window covers the tile exactly
     for (int i = threadIdx.x; i < tw; i += 256) xt_s[i] = a.rtab[G.xtab_off + tx0 + i];
@@ -131,13 +177,11 @@ __global__ __launch_bounds__(256) void k_resize(BatchArgs a, int l) {
     if (aligned) {
         // 16-byte buffer loads (bounds-checked: bytes past the plane read as 0 and are never
         // used); half a wave per source row, no integer division
-        const __amdgpu_buffer_rsrc_t srs = __builtin_amdgcn_make_buffer_rsrc(
-            (void*)src, (short)0, (int)min(S.img_stride, 0x7fffffffLL), 0x00020000);
         const int half = threadIdx.x >> 5, hl = threadIdx.x & 31;
         for (int r = half; r < nrows; r += 8) {
             const int rowofs = (sy_lo + r) * S.pitch + sx_lo;
             for (int c = hl; c < nq4; c += 32) {
-                const auto v = __builtin_amdgcn_raw_buffer_load_b128(srs, rowofs + 16 * c, 0, 0);
+                const auto v = __builtin_amdgcn_raw_buffer_load_b128(srs, rowofs + 16 * c, 0, kAux);
                 *reinterpret_cast<uint4*>(&win[r][4 * c]) = make_uint4(v[0], v[1], v[2], v[3]);
             }
         }
@@ -154,36 +198,29 @@ __global__ __launch_bounds__(256) void k_resize(BatchArgs a, int l) {
             const int dx0 = tx0 + 4 * q;
             if (4 * q >= tw) continue;
             const int4 yt = yt_s[rr];
-            const int b0 = yt.z, b1 = yt.w;
             const auto r0 = row_ptr(yt.x), r1 = row_ptr(yt.y);
-            uint32_t packed = 0;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const int dx = dx0 + k;
-                int o = 0;
-                if (4 * q + k < tw) {
-                    const int4 xt = xt_s[4 * q + k];
-                    const int p00 = r0[xt.x], p01 = r0[xt.y], p10 = r1[xt.x], p11 = r1[xt.y];
-                    const int D0 = p00 * xt.z + p01 * xt.w;
-                    const int D1 = p10 * xt.z + p11 * xt.w;
-                    if (dx < G.simd_end) {
-                        const int s = (((D0 >> 4) * b0) >> 16) + (((D1 >> 4) * b1) >> 16);
-                        o = (s + 2) >> 2;
-                    } else {
-                        o = (D0 * b0 + D1 * b1 + (1 << 21)) >> 22;
-                    }
-                    o = o < 0 ? 0 : (o > 255 ? 255 : o);
-                }
-                packed |= (uint32_t)o << (8 * k);
-            }
+            const uint32_t packed = rs_quad(r0, r1, xt_s + 4 * q, yt.z, yt.w, dx0, G.simd_end);
             *reinterpret_cast<uint32_t*>(dst + (long long)dy * G.pitch + dx0) = packed;
         }
     };
     if (staged) {
         body([&](int sy) { return wb + (sy - sy_lo) * kRsSrcCols - sx_lo; });
     } else {
-        body([&](int sy) { return src + (long long)sy * S.pitch; });
+        body([&](int sy) { return GlobalRow<kAux>{srs, sy * S.pitch}; });
     }
+}
+
+template <int kRsSrcRows, int kRsSrcCols>
+__global__ __launch_bounds__(256) void k_resize(BatchArgs a, int l) {
+    __shared__ int4 xt_s[kRsTW];
+    __shared__ int4 yt_s[kRsTH];
+    __shared__ __attribute__((aligned(16))) uint32_t win[kRsSrcRows][kRsSrcCols / 4];
+    const LevelGeom& G = a.lv[l];
+    const int nxy = gridDim.x * gridDim.y;
+    const int wg = xcd_remap(blockIdx.x + blockIdx.y * gridDim.x + blockIdx.z * nxy, nxy * gridDim.z);
+    const int img = a.img0 + wg / nxy;
+    const int tx0 = (wg % nxy % gridDim.x) * kRsTW, ty0 = (wg % nxy / gridDim.x) * kRsTH;
+    resize_tile<kRsSrcRows, kRsSrcCols, 0>(a, img, l, tx0, ty0, G.h, xt_s, yt_s, win);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -233,6 +270,7 @@ __device__ inline BlurTile blur_tile(const BatchArgs& a, int t) {
 // Window chunk i (16 bytes) of tile bt: rows reflected here (REFLECT_101), columns loaded as
 // they are (bounds-checked buffer load; chunks left of the plane are zero) -- the few column
 // bytes outside the plane that the taps reach are reflected in LDS afterwards (blur_fix_cols).
+template <int kAux = 0>
 __device__ inline uint4 blur_chunk(const BatchArgs& a, const BlurTile& bt, int i, int IWQ) {
     const LevelGeom& G = a.lv[bt.l];
     const int r = i / IWQ, cq = i - r * IWQ;
@@ -242,53 +280,18 @@ __device__ inline uint4 blur_chunk(const BatchArgs& a, const BlurTile& bt, int i
     if (x < 0) return make_uint4(0, 0, 0, 0);
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
         (void*)bt.src, (short)0, (int)min(G.img_stride, 0x7fffffffLL), 0x00020000);
-    const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, y * G.pitch + x, 0, 0);
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, y * G.pitch + x, 0, kAux);
     return make_uint4(v[0], v[1], v[2], v[3]);
 }
 
-// Persistent over the tiles of the launch (images x levels x tiles): the next tile's window
-// is loaded into registers while the current one is filtered, so the global-memory round
-// trip is hidden behind the arithmetic of the previous tile.
-__global__ __launch_bounds__(256) void k_blur(BatchArgs a) {
-    constexpr int IW = kBlurTW + 32, IH = kBlurTH + 8, IWQ = IW / 16, NRP = IH / 2;
-    constexpr int NCH = (IH * IWQ + 255) / 256;  // window chunks per thread
-    __shared__ uint4 tin4[IH][IWQ];
-    __shared__ uint4 hp[NRP][kBlurTW / 4];  // [row pair][column quad]: 4 columns x (row0,row1)
-    const int total = a.total_tiles * a.nimages;
-    // a contiguous run of tiles per workgroup, runs placed XCD-contiguously (xcd_remap)
-    const int lb = xcd_remap(blockIdx.x, gridDim.x);
-    const int t_end = (int)((long long)(lb + 1) * total / gridDim.x);
-    int t = (int)((long long)lb * total / gridDim.x);
-    if (t >= t_end) return;
-    BlurTile bt = blur_tile(a, t);
-    uint4 pre[NCH];
-#pragma unroll
-    for (int c = 0; c < NCH; ++c) {
-        const int i = threadIdx.x + 256 * c;
-        if (i < IH * IWQ) pre[c] = blur_chunk(a, bt, i, IWQ);
-    }
-    for (; t < t_end; ++t) {
-        const BlurTile cur = bt;
-        const LevelGeom& G = a.lv[cur.l];
-        const int ty0 = cur.ty0, tx0 = cur.tx0;
-        uint8_t* dst = cur.dst;
-        __syncthreads();  // the previous tile's passes are done with tin4 / hp
-#pragma unroll
-        for (int c = 0; c < NCH; ++c) {
-            const int i = threadIdx.x + 256 * c;
-            if (i < IH * IWQ) (&tin4[0][0])[i] = pre[c];
-        }
-        const int tn = t + 1;
-        if (tn < t_end) {  // prefetch the next window
-            bt = blur_tile(a, tn);
-#pragma unroll
-            for (int c = 0; c < NCH; ++c) {
-                const int i = threadIdx.x + 256 * c;
-                if (i < IH * IWQ) pre[c] = blur_chunk(a, bt, i, IWQ);
-            }
-        }
+// Filters one staged 128 x 32 tile (window in tin4: rows ty0-4 .., cols tx0-16 ..) and writes
+// its output rows inside [rlo, rhi).  The caller synchronizes after staging the window and
+// before the next tile reuses tin4 / hp.
+__device__ inline void blur_tile_compute(const LevelGeom& G, int tx0, int ty0, uint8_t* dst,
+                                         uint4 (*tin4)[(kBlurTW + 32) / 16],
+                                         uint4 (*hp)[kBlurTW / 4], int rlo, int rhi) {
+    constexpr int IW = kBlurTW + 32, IH = kBlurTH + 8, NRP = IH / 2;
     const uint32_t(*tin)[IW / 4] = reinterpret_cast<const uint32_t(*)[IW / 4]>(&tin4[0][0]);
-    __syncthreads();
     if (tx0 == 0 || tx0 + kBlurTW + 3 > G.w) {  // REFLECT_101 of the 3 columns past each edge
         uint8_t* wb = reinterpret_cast<uint8_t*>(&tin4[0][0]);
         for (int i = threadIdx.x; i < IH * 6; i += 256) {
@@ -364,8 +367,258 @@ __global__ __launch_bounds__(256) void k_blur(BatchArgs a) {
         const uint32_t lo = __builtin_amdgcn_perm(sv[1], sv[0], 0x0c0c0602u);
         const uint32_t hi = __builtin_amdgcn_perm(sv[3], sv[2], 0x0c0c0602u);
         const uint32_t packed = lo | (hi << 16);
-        if (y < G.h && x < G.w) *reinterpret_cast<uint32_t*>(dst + (long long)y * G.bpitch + x) = packed;
+        if (y >= rlo && y < rhi && y < G.h && x < G.w) *reinterpret_cast<uint32_t*>(dst + (long long)y * G.bpitch + x) = packed;
     }
+}
+
+// Persistent over the tiles of the launch (images x levels x tiles): the next tile's window
+// is loaded into registers while the current one is filtered, so the global-memory round
+// trip is hidden behind the arithmetic of the previous tile.
+__global__ __launch_bounds__(256) void k_blur(BatchArgs a) {
+    constexpr int IW = kBlurTW + 32, IH = kBlurTH + 8, IWQ = IW / 16, NRP = IH / 2;
+    constexpr int NCH = (IH * IWQ + 255) / 256;  // window chunks per thread
+    __shared__ uint4 tin4[IH][IWQ];
+    __shared__ uint4 hp[NRP][kBlurTW / 4];  // [row pair][column quad]: 4 columns x (row0,row1)
+    const int total = a.total_tiles * a.nimages;
+    // a contiguous run of tiles per workgroup, runs placed XCD-contiguously (xcd_remap)
+    const int lb = xcd_remap(blockIdx.x, gridDim.x);
+    const int t_end = (int)((long long)(lb + 1) * total / gridDim.x);
+    int t = (int)((long long)lb * total / gridDim.x);
+    if (t >= t_end) return;
+    BlurTile bt = blur_tile(a, t);
+    uint4 pre[NCH];
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+        const int i = threadIdx.x + 256 * c;
+        if (i < IH * IWQ) pre[c] = blur_chunk(a, bt, i, IWQ);
+    }
+    for (; t < t_end; ++t) {
+        const BlurTile cur = bt;
+        const LevelGeom& G = a.lv[cur.l];
+        const int ty0 = cur.ty0, tx0 = cur.tx0;
+        uint8_t* dst = cur.dst;
+        __syncthreads();  // the previous tile's passes are done with tin4 / hp
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+            const int i = threadIdx.x + 256 * c;
+            if (i < IH * IWQ) (&tin4[0][0])[i] = pre[c];
+        }
+        const int tn = t + 1;
+        if (tn < t_end) {  // prefetch the next window
+            bt = blur_tile(a, tn);
+#pragma unroll
+            for (int c = 0; c < NCH; ++c) {
+                const int i = threadIdx.x + 256 * c;
+                if (i < IH * IWQ) pre[c] = blur_chunk(a, bt, i, IWQ);
+            }
+        }
+        __syncthreads();
+        blur_tile_compute(G, tx0, ty0, dst, tin4, hp, 0, G.h);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// k_pyramid: ComputePyramid (ORBextractor_old.cc:1331-1356) and the per-level GaussianBlur
+// (:1146-1147) of one row stripe of one image in one workgroup, all levels in one launch.
+// Phase l blurs the stripe's own rows of level l and resizes the rows of level l+1 the stripe
+// needs; both only read level l.  The needed rows (host table) are the stripe's own rows, the
+// 3-row blur halo and the source-row cone of every later level, so each workgroup reads only
+// rows it wrote itself: the phases are separated by a vmcnt drain + workgroup barrier, and
+// every load of a level written in this launch is an sc1 load (from L2, never a stale L1
+// line).  Rows in the overlap of two stripes are computed by both, with identical values.
+constexpr int kSc1 = 16;  // buffer-load aux bit: sc1
+
+union PyrSmem {
+    struct {
+        int4 xt[kRsTW];
+        int4 yt[kRsTH];
+        uint32_t win[kRsSrcRows][kRsSrcCols / 4];
+    } r;
+    struct {
+        uint4 tin4[kBlurTH + 8][(kBlurTW + 32) / 16];
+        uint4 hp[(kBlurTH + 8) / 2][kBlurTW / 4];
+    } b;
+};
+
+// One resize tile of k_pyramid: columns [tx0, tx0 + tw) (balanced tiles of at most 256 columns,
+// tw a multiple of 4 except at the right edge), rows [ty0, ty0 + th), and its source window.
+struct RsTile {
+    int tx0, ty0, tw, th;
+    int sx_lo, sy_lo, nrows, nq4;
+};
+
+__device__ inline RsTile rs_tile(const LevelGeom& G, const LevelGeom& S, int j, int tw_nom, int ty0, int rhi) {
+    RsTile t;
+    t.tx0 = j * tw_nom;
+    t.tw = min(tw_nom, G.w - t.tx0);
+    t.ty0 = ty0;
+    t.th = min(min(kRsTH, G.h - ty0), rhi - ty0);
+    const float sxf = (float)S.w / (float)G.w, syf = (float)S.h / (float)G.h;
+    t.sx_lo = max(0, (int)floorf(((float)t.tx0 + 0.5f) * sxf - 0.5f) - 2) & ~3;
+    t.sy_lo = max(0, (int)floorf(((float)ty0 + 0.5f) * syf - 0.5f) - 2);
+    t.nrows = min(kRsSrcRows, S.h - t.sy_lo);
+    t.nq4 = min(kRsSrcCols / 16, (S.w - t.sx_lo + 15) >> 4);
+    return t;
+}
+
+// Output quads of a resize tile flattened over the workgroup (row = item / quads per row), so a
+// narrow level keeps every lane busy.  Source from the staged window when it covers every tap,
+// else from the plane through byte loads (cache policy kAux).
+template <int kAux>
+__device__ inline void rs_compute(const BatchArgs& a, int img, int l, const RsTile& t, bool aligned,
+                                  const int4* xt_s, const int4* yt_s, const uint32_t (*win)[kRsSrcCols / 4]) {
+    const LevelGeom& G = a.lv[l];
+    const LevelGeom& S = a.lv[l - 1];
+    const uint8_t* src = a.lvl_base[l - 1] + (long long)img * S.img_stride;
+    uint8_t* dst = a.lvl_base[l] + (long long)img * G.img_stride;
+    const __amdgpu_buffer_rsrc_t srs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)src, (short)0, (int)min(S.img_stride, 0x7fffffffLL), 0x00020000);
+    if (G.area2) {  // resize.cpp: INTER_LINEAR at exactly 2x is serviced by INTER_AREA fast
+        const int nq = (t.tw + 3) >> 2;
+        for (int it = threadIdx.x; it < t.th * nq; it += 256) {
+            const int rr = it / nq, dx0 = t.tx0 + 4 * (it - rr * nq);
+            const int dy = t.ty0 + rr;
+            const GlobalRow<kAux> s0{srs, 2 * dy * S.pitch}, s1{srs, (2 * dy + 1) * S.pitch};
+            uint32_t pk = 0;
+            for (int k = 0; k < 4; ++k) {
+                const int dx = min(dx0 + k, G.w - 1);
+                const int o = (s0[2 * dx] + s0[2 * dx + 1] + s1[2 * dx] + s1[2 * dx + 1] + 2) >> 2;
+                pk |= (uint32_t)o << (8 * k);
+            }
+            *reinterpret_cast<uint32_t*>(dst + (long long)dy * G.pitch + dx0) = pk;
+        }
+        return;
+    }
+    const bool staged = aligned && xt_s[0].x >= t.sx_lo && xt_s[t.tw - 1].y < t.sx_lo + 16 * t.nq4 &&
+                        yt_s[0].x >= t.sy_lo && yt_s[t.th - 1].y < t.sy_lo + t.nrows;
+    const uint8_t* wb = reinterpret_cast<const uint8_t*>(&win[0][0]);
+    const int nq = (t.tw + 3) >> 2;
+    const float inv_nq = 1.f / (float)nq;
+    auto body = [&](auto row_ptr) __attribute__((always_inline)) {
+        for (int it = threadIdx.x; it < t.th * nq; it += 256) {
+            const int rr = (int)(((float)it + 0.5f) * inv_nq);  // exact: it < 4096, nq <= 64
+            const int q = it - rr * nq;
+            const int dy = t.ty0 + rr, dx0 = t.tx0 + 4 * q;
+            const int4 yt = yt_s[rr];
+            const auto r0 = row_ptr(yt.x), r1 = row_ptr(yt.y);
+            const uint32_t packed = rs_quad(r0, r1, xt_s + 4 * q, yt.z, yt.w, dx0, G.simd_end);
+            *reinterpret_cast<uint32_t*>(dst + (long long)dy * G.pitch + dx0) = packed;
+        }
+    };
+    if (staged) {
+        body([&](int sy) { return wb + (sy - t.sy_lo) * kRsSrcCols - t.sx_lo; });
+    } else {
+        body([&](int sy) { return GlobalRow<kAux>{srs, sy * S.pitch}; });
+    }
+}
+
+// Phase l runs T = (blur tiles of level l) + (resize tiles of level l+1) tiles in order with a
+// one-tile software pipeline: tile t+1's window (and resize tables) is loaded into registers
+// while tile t is computed from LDS.
+__global__ __launch_bounds__(256) void k_pyramid(BatchArgs a, int S, int tab) {
+    constexpr int IWQ = (kBlurTW + 32) / 16, IH = kBlurTH + 8;
+    constexpr int kBlCh = IH * IWQ;                 // 16-byte chunks of a blur window
+    constexpr int kRsQ = kRsSrcCols / 16;
+    constexpr int kRsCh = kRsSrcRows * kRsQ;        // 16-byte chunks of a resize window
+    constexpr int kPre = (kRsCh + 255) / 256;
+    constexpr int kBlPre = (kBlCh + 255) / 256;
+    static_assert(kBlPre <= kPre, "prefetch registers");
+    __shared__ PyrSmem sm;
+    const int wg = xcd_remap(blockIdx.x, gridDim.x);  // the stripes of an image share an XCD
+    const int img = a.img0 + wg / S, k = wg % S;
+    const int tid = threadIdx.x;
+    for (int l = 0; l < a.nlevels; ++l) {
+        const LevelGeom& G = a.lv[l];
+        const int4 e = a.rtab[tab + l * S + k];  // own rows [e.z, e.w)
+        const int nbx = (G.w + kBlurTW - 1) / kBlurTW;
+        const int nb = e.w > e.z ? nbx * ((e.w - e.z + kBlurTH - 1) / kBlurTH) : 0;
+        const bool has_next = l + 1 < a.nlevels;
+        const LevelGeom& D = a.lv[has_next ? l + 1 : l];
+        const int4 n = has_next ? a.rtab[tab + (l + 1) * S + k] : make_int4(0, 0, 0, 0);  // needed rows
+        const int rtx = (D.w + kRsTW - 1) / kRsTW;
+        const int tw_nom = ((D.w + rtx - 1) / rtx + 3) & ~3;
+        const int nr = n.y > n.x ? rtx * ((n.y - n.x + kRsTH - 1) / kRsTH) : 0;
+        const int T = nb + nr;
+        const bool aligned = (G.pitch & 3) == 0;  // level l is the source of level l+1
+        BlurTile bt;
+        bt.l = l;
+        bt.src = a.lvl_base[l] + (long long)img * G.img_stride;
+        bt.dst = a.blur_base[l] + (long long)img * G.bimg_stride;
+        const __amdgpu_buffer_rsrc_t srs = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)bt.src, (short)0, (int)min(G.img_stride, 0x7fffffffLL), 0x00020000);
+        auto blur_xy = [&](int t, int& tx0, int& ty0) {
+            const int by = t / nbx;
+            ty0 = e.z + kBlurTH * by;
+            tx0 = kBlurTW * (t - by * nbx);
+        };
+        auto rs_of = [&](int t) {
+            const int r = t - nb, ry = r / rtx;
+            return rs_tile(D, G, r - ry * rtx, tw_nom, n.x + kRsTH * ry, n.y);
+        };
+        uint4 pre[kPre];
+        int4 pxt = make_int4(0, 0, 0, 0), pyt = make_int4(0, 0, 0, 0);
+        auto issue = [&](int t) {
+            if (t < nb) {
+                blur_xy(t, bt.tx0, bt.ty0);
+#pragma unroll
+                for (int c = 0; c < kBlPre; ++c) {
+                    const int i = tid + 256 * c;
+                    if (i < kBlCh) pre[c] = l == 0 ? blur_chunk<0>(a, bt, i, IWQ) : blur_chunk<kSc1>(a, bt, i, IWQ);
+                }
+            } else if (!D.area2) {
+                const RsTile rt = rs_of(t);
+#pragma unroll
+                for (int c = 0; c < kPre; ++c) {
+                    const int i = tid + 256 * c;
+                    const int row = i / kRsQ, q = i - row * kRsQ;
+                    pre[c] = make_uint4(0, 0, 0, 0);
+                    if (aligned && i < kRsCh && row < rt.nrows && q < rt.nq4) {
+                        const int off = (rt.sy_lo + row) * G.pitch + rt.sx_lo + 16 * q;
+                        const auto v = l == 0 ? __builtin_amdgcn_raw_buffer_load_b128(srs, off, 0, 0)
+                                              : __builtin_amdgcn_raw_buffer_load_b128(srs, off, 0, kSc1);
+                        pre[c] = make_uint4(v[0], v[1], v[2], v[3]);
+                    }
+                }
+                if (tid < rt.tw) pxt = a.rtab[D.xtab_off + rt.tx0 + tid];
+                if (tid < rt.th) pyt = a.rtab[D.ytab_off + rt.ty0 + tid];
+            }
+        };
+        if (T > 0) issue(0);
+        for (int t = 0; t < T; ++t) {
+            if (t < nb) {
+#pragma unroll
+                for (int c = 0; c < kBlPre; ++c) {
+                    const int i = tid + 256 * c;
+                    if (i < kBlCh) (&sm.b.tin4[0][0])[i] = pre[c];
+                }
+            } else if (!D.area2) {
+#pragma unroll
+                for (int c = 0; c < kPre; ++c) {
+                    const int i = tid + 256 * c;
+                    const int row = i / kRsQ, q = i - row * kRsQ;
+                    if (i < kRsCh) *reinterpret_cast<uint4*>(&sm.r.win[row][4 * q]) = pre[c];
+                }
+                sm.r.xt[tid] = pxt;
+                if (tid < kRsTH) sm.r.yt[tid] = pyt;
+            }
+            if (t + 1 < T) issue(t + 1);
+            __syncthreads();
+            if (t < nb) {
+                int tx0, ty0;
+                blur_xy(t, tx0, ty0);
+                blur_tile_compute(G, tx0, ty0, bt.dst, sm.b.tin4, sm.b.hp, e.z, e.w);
+            } else {
+                const RsTile rt = rs_of(t);
+                if (l == 0) rs_compute<0>(a, img, l + 1, rt, aligned, sm.r.xt, sm.r.yt, sm.r.win);
+                else rs_compute<kSc1>(a, img, l + 1, rt, aligned, sm.r.xt, sm.r.yt, sm.r.win);
+            }
+            __syncthreads();
+        }
+        if (has_next) {
+            // level l+1 complete in L2 before any wave of this workgroup reads it
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+        }
     }
 }
 
@@ -1088,6 +1341,11 @@ hipError_t launch_blur(const BatchArgs& a, hipStream_t s) {
     // persistent: 8192 workgroups (32 per CU, about 4 resident at a time) loop over the tiles
     const int total = a.total_tiles * a.nimages;
     hipLaunchKernelGGL(k_blur, dim3(std::min(total, 8192)), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+hipError_t launch_pyramid(const BatchArgs& a, int stripe_log2, hipStream_t s) {
+    const int S = 1 << stripe_log2;
+    hipLaunchKernelGGL(k_pyramid, dim3(a.nimages * S), dim3(256), 0, s, a, S, a.stripe_tab_off[stripe_log2]);
     return hipGetLastError();
 }
 void fast_cell_range(const BatchArgs& a, int tile, int* c0, int* c1) {

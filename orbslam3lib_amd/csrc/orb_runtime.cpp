@@ -39,11 +39,12 @@ int fail(int code, const std::string& msg) {
             return fail(ORBGPU_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
     } while (0)
 
-enum Stage { ST_RESIZE, ST_BLUR, ST_FAST48, ST_FAST, ST_FAST_TOP, ST_OCTREE, ST_ORIENT, ST_FINAL, ST_KNN, ST_COUNT };
+enum Stage { ST_RESIZE, ST_BLUR, ST_FAST48, ST_FAST, ST_FAST_TOP, ST_OCTREE, ST_ORIENT, ST_FINAL, ST_KNN,
+             ST_PYRAMID, ST_COUNT };
 // names as rocprofv3 shows the kernels (templates with their argument)
 const char* kStageNames[ST_COUNT] = {"k_resize",         "k_blur",   "k_fast_cells<48>", "k_fast_cells<64>",
                                      "k_fast_cells<80>", "k_octree", "k_orient_desc",    "k_finalize",
-                                     "k_knn2"};
+                                     "k_knn2",           "k_pyramid"};
 
 struct DevBuf {
     void* p = nullptr;
@@ -110,6 +111,12 @@ struct orbgpu_ctx {
     // idle GPU per step (ORBGPU_ISOLATE=<stage bit mask> turns it on)
     unsigned isolate_mask = 0;
     bool serialize = false;  // profiling: every stage isolated
+    // pyramid + blur as the per-level k_resize launches and k_blur (default) or as one k_pyramid
+    // launch (ORBGPU_PYR=1; measured slower on the 128-pair bench: 618 vs ~530 us per step, its
+    // stripes recompute the halo rows and each workgroup walks its tiles serially);
+    // ORBGPU_PYR_STRIPES=<log2> fixes the stripes per image
+    bool pyr_mode = false;
+    int pyr_stripes_log2 = -1;
     struct ChunkRec { int img0, n; hipStream_t st; };
     std::vector<ChunkRec> last_chunks;
     int last_images = 0, last_w = 0, last_h = 0, last_pairs = 0;
@@ -300,6 +307,41 @@ int set_geometry(orbgpu_ctx* c, int w, int h) {
             c->rtab_host.insert(c->rtab_host.end(), yt.begin(), yt.end());
             G.simd_end = simd_end(G.w);
         }
+    }
+    // k_pyramid stripe tables (1, 2, 4, 8, 16 stripes per image): own rows k*h/S .. (k+1)*h/S of
+    // every level; needed rows of level l = own rows +- 3 (blur halo, REFLECT_101 stays inside)
+    // joined with the source rows of the rows needed at level l+1, from the top level down
+    for (int si = 0; si < kPyrStripeKinds; ++si) {
+        const int S = 1 << si;
+        A.stripe_tab_off[si] = (int)c->rtab_host.size();
+        std::vector<int4> tab((size_t)L * S);
+        for (int k = 0; k < S; ++k) {
+            int nlo = 0, nhi = 0;
+            for (int l = L - 1; l >= 0; --l) {
+                const LevelGeom& G = A.lv[l];
+                const int own_lo = (int)((long long)k * G.h / S), own_hi = (int)((long long)(k + 1) * G.h / S);
+                int lo = std::max(0, own_lo - 3), hi = std::min(G.h, own_hi + 3);
+                if (l + 1 < L && nhi > nlo) {
+                    const LevelGeom& U = A.lv[l + 1];
+                    int slo, shi;
+                    if (U.area2) {
+                        slo = 2 * nlo;
+                        shi = 2 * nhi;
+                    } else {
+                        slo = c->rtab_host[U.ytab_off + nlo].x;
+                        shi = c->rtab_host[U.ytab_off + nhi - 1].y + 1;
+                    }
+                    lo = std::min(lo, slo);
+                    hi = std::max(hi, shi);
+                }
+                lo = std::max(lo, 0);
+                hi = std::min(hi, G.h);
+                tab[(size_t)l * S + k] = make_int4(lo, hi, own_lo, own_hi);
+                nlo = lo;
+                nhi = hi;
+            }
+        }
+        c->rtab_host.insert(c->rtab_host.end(), tab.begin(), tab.end());
     }
     c->pyr_img = round_up_ll(pyr, 256);
     c->blur_img = round_up_ll(blr, 256);
@@ -495,6 +537,10 @@ int orbgpu_create(const orbgpu_params* p, int device, int max_width, int max_hei
         }
         const char* iso = getenv("ORBGPU_ISOLATE");  // stage bit mask (diagnostics)
         if (iso) c->isolate_mask = (unsigned)strtoul(iso, nullptr, 0);
+        const char* pm = getenv("ORBGPU_PYR");
+        if (pm) c->pyr_mode = atoi(pm) != 0;
+        const char* ps = getenv("ORBGPU_PYR_STRIPES");
+        if (ps) c->pyr_stripes_log2 = std::max(0, std::min(kPyrStripeKinds - 1, atoi(ps)));
     }
     int r = ensure_input(c, 1, max_width, max_height);
     if (!r) r = set_geometry(c, max_width, max_height);
@@ -622,11 +668,24 @@ int orbgpu_run_batch(orbgpu_ctx* c, int n, int w, int h, const int32_t* laps, vo
         }
         return 0;
     };
-    for (int l = 1; l < A.nlevels; ++l) {
-        r = each(ST_RESIZE, [&](const BatchArgs& B, hipStream_t st) { return launch_resize(B, l, st); });
+    if (c->pyr_mode) {
+        // the whole pyramid + blur in one launch per chunk: 2^sl row stripes per image, enough
+        // workgroups for the batch to cover the chip (about 1024), at most 16 per image
+        int sl = 0;
+        if (c->pyr_stripes_log2 >= 0) {
+            sl = c->pyr_stripes_log2;
+        } else {
+            while (sl + 1 < kPyrStripeKinds && (n << sl) < 1024) ++sl;
+        }
+        r = each(ST_PYRAMID, [&](const BatchArgs& B, hipStream_t st) { return launch_pyramid(B, sl, st); });
         if (r) return r;
+    } else {
+        for (int l = 1; l < A.nlevels; ++l) {
+            r = each(ST_RESIZE, [&](const BatchArgs& B, hipStream_t st) { return launch_resize(B, l, st); });
+            if (r) return r;
+        }
+        if ((r = each(ST_BLUR, [](const BatchArgs& B, hipStream_t st) { return launch_blur(B, st); }))) return r;
     }
-    if ((r = each(ST_BLUR, [](const BatchArgs& B, hipStream_t st) { return launch_blur(B, st); }))) return r;
     {   // the FAST tiles as one group: one join / fork around all of them when isolated
         const int tiles[3] = {kCellPitchTiny, kCellPitchSmall, kCellMax};
         const int stages[3] = {ST_FAST48, ST_FAST, ST_FAST_TOP};

@@ -78,6 +78,14 @@ int harness_fast_strength(const uint8_t* img, int stride, int x, int y, int tlow
 
 float harness_fast_atan2(float y, float x) { return fast_atan2_deg(y, x); }
 
+// Packed (both polarities per word) strength vs the scalar corner strength on the same pixel.
+int harness_fast_strength_packed64(const uint8_t* img, int x, int y) {
+    return fast_strength_packed<64>(img + (long long)y * 64 + x);
+}
+int harness_fast_strength_corner(const uint8_t* img, int stride, int x, int y) {
+    return fast_strength_corner(img + (long long)y * stride + x, stride);
+}
+
 // ComputeKeyPointsOctTree cell loop geometry (same formulas as orb_runtime.cpp) + fast_cell_run.
 int harness_level_candidates(const uint8_t* lvl, int w, int h, int ini, int mn, uint32_t* out,
                              int cap) {

@@ -73,6 +73,20 @@ def test_fast_strength_vs_corner_score(harness, oracle):
                 assert cs == max(th, m) - 1
 
 
+def test_fast_strength_packed_equals_scalar(harness):
+    # random, two-level and near-constant rings: every (pixel, polarity) combination the
+    # paired-arc reduction of fast_strength_packed can meet
+    rng = np.random.default_rng(5)
+    imgs = [rng.integers(0, 256, (64, 64)), rng.integers(0, 2, (64, 64)) * 255,
+            120 + rng.integers(-3, 4, (64, 64)), synth.frame(64, 64, 9)]
+    for img in imgs:
+        img = np.ascontiguousarray(np.clip(img, 0, 255).astype(np.uint8))
+        for y in range(3, 61):
+            for x in range(3, 61):
+                assert (harness.harness_fast_strength_packed64(_p(img), x, y) ==
+                        harness.harness_fast_strength_corner(_p(img), 64, x, y)), (x, y)
+
+
 def _level_cands(harness, lvl, ini, mn):
     lvl = np.ascontiguousarray(lvl)
     h, w = lvl.shape
