@@ -117,6 +117,8 @@ def cpu_baseline(w, h, nfeatures, seconds):
     from orbslam3lib_amd import synth
     O.lib()
     pairs = [synth.stereo_pair(h, w, 1000 + i) for i in range(4)]
+    stereo_pyr = [(O.pyramid(L), O.pyramid(R)) for L, R in pairs]
+    t_st = [0.0]
     nfeat = nq = 0
     t_ex = t_bf = 0.0
     i = 0
@@ -129,12 +131,17 @@ def cpu_baseline(w, h, nfeatures, seconds):
         t1 = time.perf_counter()
         O.knn2(dl, dr)
         t2 = time.perf_counter()
+        if stereo_pyr is not None:
+            O.stereo_matches(kl, dl, kr, dr, stereo_pyr[i % len(pairs)][0], stereo_pyr[i % len(pairs)][1],
+                             47.9, float(np.float32(47.9) / np.float32(435.2)))
+            t_st[0] += time.perf_counter() - t2
         nfeat += len(kl) + len(kr)
         nq += len(dl)
         t_ex += t1 - t0
         t_bf += t2 - t1
         i += 1
     return {"pairs": i, "mfeat_s": nfeat / t_ex / 1e6, "mmatch_s": nq / t_bf / 1e6,
+            "stereo_mkp_s": nq / t_st[0] / 1e6 if t_st[0] > 0 else None,
             "mfeat_s_pipeline": nfeat / (t_ex + t_bf) / 1e6}
 
 
@@ -152,6 +159,7 @@ def main():
     ap.add_argument("--nlevels", type=int, default=8)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-stereo", action="store_true", help="skip the ComputeStereoMatches leg")
     ap.add_argument("--no-profile", action="store_true",
                     help="do not bracket launches with HIP events in the timed region")
     args = ap.parse_args()
@@ -282,13 +290,41 @@ def main():
                     "unit": "GB/s", "frac": None, "traffic": traffic, "avg_us": r["avg_us"],
                     "note": "control-flow bound kernel; see stages"}
 
+    # Frame::ComputeStereoMatches on the same resident batch, timed on its own
+    # (not part of the headline step): EuRoC-like rig, baseline 0.11 m, fx 435.2
+    stereo = None
+    if not args.no_stereo:
+        mbf = 47.9
+        mb = float(np.float32(mbf) / np.float32(435.2))
+        be.stereo_matches(mbf, mb)
+        be.synchronize()
+        be.set_profiling(True, stages=["k_stereo"])
+        be.reset_stage_times()
+        barrier(dist)
+        be.synchronize()
+        s0 = time.perf_counter()
+        for _ in range(args.steps):
+            be.stereo_matches(mbf, mb)
+        be.synchronize()
+        s1 = time.perf_counter()
+        st_el = max_over_ranks(dist, s1 - s0)
+        st = be.stage_times().get("k_stereo", (0.0, 0))
+        be.set_profiling(False)
+        ur, _, _ = be.stereo_result(0)
+        stereo = {"metric": "left keypoints stereo-matched per second (Frame::ComputeStereoMatches)",
+                  "value": round(sum_over_ranks(dist, nq_per_step * args.steps) / st_el / 1e6, 3),
+                  "unit": "Mkeypoints/s", "ms_per_step": round(st_el / args.steps * 1e3, 4),
+                  "kernel_ms_per_launch": round(st[0] / st[1], 4) if st[1] else None,
+                  "pairs_per_step": P, "matched_frac_pair0": round(float((ur >= 0).mean()), 3) if len(ur) else 0.0}
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cb = cpu_baseline(W, H, args.nfeatures, args.cpu_seconds)
         cpu = {"value": round(cb["mfeat_s"], 5), "unit": "Mfeatures/s", "cores": 1, "kind": "port",
                "sample": "%d synthetic 640x480 stereo pairs, oracle extract (both eyes, 1 thread); "
                          "BF kNN2 %.4f Mmatches/s" % (cb["pairs"], cb["mmatch_s"]),
-               "mmatches_s": round(cb["mmatch_s"], 5)}
+               "mmatches_s": round(cb["mmatch_s"], 5),
+               "stereo_mkeypoints_s": round(cb["stereo_mkp_s"], 5) if cb["stereo_mkp_s"] else None}
 
     if rank == 0:
         out = {
@@ -314,6 +350,7 @@ def main():
             "roofline": roof,
             "stages": stage_rows,
             "cpu_baseline": cpu,
+            "stereo_matches": stereo,
         }
         print(json.dumps(out))
     if dist is not None:

@@ -17,6 +17,7 @@
  *   - ORBmatcher::DescriptorDistance      cpp/include/ORBmatcher.h:44, cpp/src/ORBmatcher.cc:2107
  *   - cv::BFMatcher(NORM_HAMMING).knnMatch(k=2)  cpp/src/Frame.cc:45,1227
  *   - mvImagePyramid (public member)      cpp/include/ORBextractor_old.h:80
+ *   - Frame::ComputeStereoMatches         cpp/include/Frame.h:119, cpp/src/Frame.cc:827-997
  */
 #ifndef ORBGPU_H_
 #define ORBGPU_H_
@@ -126,6 +127,17 @@ int orbgpu_match_knn2(orbgpu_ctx* ctx, const uint8_t* query, int nq, const uint8
 int orbgpu_match_stereo_batch(orbgpu_ctx* ctx, int n_pairs, int stereo_rows_only, void* stream);
 int orbgpu_download_matches(orbgpu_ctx* ctx, int pair, int32_t* idx1, int32_t* dist1,
                             int32_t* idx2, int32_t* dist2, int cap, int* nq);
+
+/* ---- stereo matching ----------------------------------------------------------------------
+ * Frame::ComputeStereoMatches (cpp/src/Frame.cc:827-997, called from the stereo Frame ctor
+ * :161 and FrameAHB.cc:129) on the device-resident results of the last orbgpu_run_batch:
+ * pair p = left image 2p (mvKeys), right image 2p+1 (mvKeysRight), rectified pinhole stereo.
+ * mbf = baseline * fx, mb = baseline (Frame::mbf, Frame::mb).  Per left keypoint: mvuRight and
+ * mvDepth (-1 = no stereo match), and the accepted SAD distance (-1 = none; also set for
+ * matches the median rule rejects).  Results stay in HBM; fetch with orbgpu_download_stereo. */
+int orbgpu_stereo_matches_batch(orbgpu_ctx* ctx, int n_pairs, float mbf, float mb, void* stream);
+int orbgpu_download_stereo(orbgpu_ctx* ctx, int pair, float* u_right, float* depth, int32_t* sad,
+                           int cap, int* n);
 
 /* ORBmatcher::DescriptorDistance on two 32-byte descriptors (host, no device work). */
 int orbgpu_descriptor_distance(const uint8_t* a, const uint8_t* b);

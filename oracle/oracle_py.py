@@ -212,3 +212,28 @@ def sort_nodes(size, ulx):
     perm = np.zeros(len(size), np.int32)
     lib().oracle_sort_nodes(_p(size), _p(ulx), len(size), _p(perm))
     return perm
+
+
+def stereo_matches(kps_l, desc_l, kps_r, desc_r, pyr_l, pyr_r, mbf, mb, scale_factor=1.2):
+    """Frame::ComputeStereoMatches (Frame.cc:827-997) -> (mvuRight, mvDepth, sad) float32/int32.
+    pyr_l / pyr_r: the unblurred pyramids (lists of levels, as pyramid() returns)."""
+    nlevels = len(pyr_l)
+    kl = np.ascontiguousarray(kps_l, dtype=KP_DTYPE)
+    kr = np.ascontiguousarray(kps_r, dtype=KP_DTYPE)
+    dl = np.ascontiguousarray(desc_l, dtype=np.uint8).reshape(-1, 32)
+    dr = np.ascontiguousarray(desc_r, dtype=np.uint8).reshape(-1, 32)
+    pl = [np.ascontiguousarray(p, dtype=np.uint8) for p in pyr_l]
+    pr = [np.ascontiguousarray(p, dtype=np.uint8) for p in pyr_r]
+    PL = (C.c_void_p * nlevels)(*[p.ctypes.data for p in pl])
+    PR = (C.c_void_p * nlevels)(*[p.ctypes.data for p in pr])
+    lw = np.array([p.shape[1] for p in pl], np.int32)
+    lh = np.array([p.shape[0] for p in pl], np.int32)
+    scale, inv_scale, _, _ = scale_factors(scale_factor, nlevels)
+    n = len(kl)
+    ur = np.zeros(n, np.float32)
+    dep = np.zeros(n, np.float32)
+    sad = np.zeros(n, np.int32)
+    lib().oracle_stereo_matches(_p(kl), n, _p(dl), _p(kr), len(kr), _p(dr), PL, PR, _p(lw), _p(lh),
+                                nlevels, _p(scale), _p(inv_scale), C.c_float(mbf), C.c_float(mb),
+                                _p(ur), _p(dep), _p(sad))
+    return ur, dep, sad

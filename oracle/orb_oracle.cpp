@@ -944,3 +944,131 @@ void oracle_sort_nodes(const int32_t* size, const int32_t* ulx, int n, int32_t* 
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------------------------
+// Frame::ComputeStereoMatches (cpp/src/Frame.cc:827-997), restated line by line for one rectified
+// stereo frame.  kpsL/kpsR are the extractor outputs (mvKeys / mvKeysRight, level-0 coordinates),
+// descL/descR their descriptors, pyrL/pyrR the UNBLURRED pyramids (mvImagePyramid, level l at
+// pyr[l], lw[l] x lh[l], pitch lw[l]), scale/inv_scale = mvScaleFactors / mvInvScaleFactors.
+// Writes mvuRight / mvDepth (-1 = no stereo match) and, for tests, the SAD distance of each
+// accepted match in sad[] (-1 otherwise; entries later rejected by the median rule keep theirs).
+// Float expressions are evaluated in source order without contraction (-ffp-contract=off).
+void oracle_stereo_matches(const oracle_kp* kpsL, int nL, const uint8_t* descL, const oracle_kp* kpsR,
+                           int nR, const uint8_t* descR, const uint8_t* const* pyrL,
+                           const uint8_t* const* pyrR, const int* lw, const int* lh, int nlevels,
+                           const float* scale, const float* inv_scale, float mbf, float mb,
+                           float* uRight, float* depth, int32_t* sad) {
+    (void)nlevels;
+    for (int i = 0; i < nL; ++i) uRight[i] = -1.0f, depth[i] = -1.0f, sad[i] = -1;
+    const int TH_HIGH = 100, TH_LOW = 50;       // ORBmatcher.cc:36-37
+    const int thOrbDist = (TH_HIGH + TH_LOW) / 2;
+    const int nRows = lh[0];
+    // :842-855 row table (rows outside the image are dropped: the reference writes past the
+    // table there, which our keypoints never reach)
+    std::vector<std::vector<size_t>> vRowIndices(nRows);
+    for (int iR = 0; iR < nR; iR++) {
+        const oracle_kp& kp = kpsR[iR];
+        const float& kpY = kp.y;
+        const float r = 2.0f * scale[kp.octave];
+        const int maxr = (int)std::ceil(kpY + r);
+        const int minr = (int)std::floor(kpY - r);
+        for (int yi = minr; yi <= maxr; yi++)
+            if (yi >= 0 && yi < nRows) vRowIndices[yi].push_back(iR);
+    }
+    const float minZ = mb;
+    const float minD = 0;
+    const float maxD = mbf / minZ;
+    std::vector<std::pair<int, int>> vDistIdx;
+    for (int iL = 0; iL < nL; iL++) {
+        const oracle_kp& kpL = kpsL[iL];
+        const int& levelL = kpL.octave;
+        const float& vL = kpL.y;
+        const float& uL = kpL.x;
+        const size_t row = (size_t)vL;
+        if (row >= (size_t)nRows) continue;
+        const std::vector<size_t>& vCandidates = vRowIndices[row];
+        if (vCandidates.empty()) continue;
+        const float minU = uL - maxD;
+        const float maxU = uL - minD;
+        if (maxU < 0) continue;
+        int bestDist = TH_HIGH;
+        size_t bestIdxR = 0;
+        const uint8_t* dL = descL + 32 * (size_t)iL;
+        for (size_t iC = 0; iC < vCandidates.size(); iC++) {
+            const size_t iR = vCandidates[iC];
+            const oracle_kp& kpR = kpsR[iR];
+            if (kpR.octave < levelL - 1 || kpR.octave > levelL + 1) continue;
+            const float& uR = kpR.x;
+            if (uR >= minU && uR <= maxU) {
+                const int dist = oracle_descriptor_distance(dL, descR + 32 * iR);
+                if (dist < bestDist) {
+                    bestDist = dist;
+                    bestIdxR = iR;
+                }
+            }
+        }
+        if (bestDist < thOrbDist) {
+            const float uR0 = kpsR[bestIdxR].x;
+            const float scaleFactor = inv_scale[kpL.octave];
+            const float scaleduL = std::round(kpL.x * scaleFactor);
+            const float scaledvL = std::round(kpL.y * scaleFactor);
+            const float scaleduR0 = std::round(uR0 * scaleFactor);
+            const int w = 5;
+            const int lvl = kpL.octave, W = lw[lvl], H = lh[lvl];
+            const int r0 = (int)scaledvL - w, c0 = (int)scaleduL - w;
+            int sadBest = INT_MAX;
+            int bestincR = 0;
+            const int L = 5;
+            float vDists[2 * L + 1];
+            const float iniu = scaleduR0 + L - w;
+            const float endu = scaleduR0 + L + w + 1;
+            if (iniu < 0 || endu >= W) continue;
+            // cv::Mat rowRange/colRange would assert outside the level; never reached here
+            if (r0 < 0 || r0 + 2 * w + 1 > H || c0 < 0 || c0 + 2 * w + 1 > W || (int)scaleduR0 - L - w < 0) continue;
+            for (int incR = -L; incR <= +L; incR++) {
+                const int cr = (int)scaleduR0 + incR - w;
+                int s = 0;  // cv::norm(IL, IR, NORM_L1): exact integer sum, returned as double
+                for (int y = 0; y < 2 * w + 1; ++y)
+                    for (int x = 0; x < 2 * w + 1; ++x)
+                        s += std::abs((int)pyrL[lvl][(size_t)(r0 + y) * W + c0 + x] -
+                                      (int)pyrR[lvl][(size_t)(r0 + y) * W + cr + x]);
+                const float dist = (float)(double)s;
+                if (dist < sadBest) {
+                    sadBest = (int)dist;
+                    bestincR = incR;
+                }
+                vDists[L + incR] = dist;
+            }
+            if (bestincR == -L || bestincR == L) continue;
+            const float dist1 = vDists[L + bestincR - 1];
+            const float dist2 = vDists[L + bestincR];
+            const float dist3 = vDists[L + bestincR + 1];
+            const float deltaR = (dist1 - dist3) / (2.0f * (dist1 + dist3 - 2.0f * dist2));
+            if (deltaR < -1 || deltaR > 1) continue;
+            float bestuR = scale[kpL.octave] * ((float)scaleduR0 + (float)bestincR + deltaR);
+            float disparity = (uL - bestuR);
+            if (disparity >= minD && disparity < maxD) {
+                if (disparity <= 0) {
+                    disparity = 0.01;
+                    bestuR = uL - 0.01;
+                }
+                depth[iL] = mbf / disparity;
+                uRight[iL] = bestuR;
+                sad[iL] = sadBest;
+                vDistIdx.push_back(std::pair<int, int>(sadBest, iL));
+            }
+        }
+    }
+    if (vDistIdx.empty()) return;  // the reference reads vDistIdx[0] of an empty vector here
+    std::sort(vDistIdx.begin(), vDistIdx.end());
+    const float median = vDistIdx[vDistIdx.size() / 2].first;
+    const float thDist = 1.5f * 1.4f * median;
+    for (int i = (int)vDistIdx.size() - 1; i >= 0; i--) {
+        if (vDistIdx[i].first < thDist)
+            break;
+        else {
+            uRight[vDistIdx[i].second] = -1;
+            depth[vDistIdx[i].second] = -1;
+        }
+    }
+}

@@ -87,4 +87,14 @@ void oracle_knn2(const uint8_t* q, int nq, const uint8_t* t, int nt, int32_t* id
 // (size, ULx) pairs; writes the permutation of input indices.
 void oracle_sort_nodes(const int32_t* size, const int32_t* ulx, int n, int32_t* perm);
 
+// Frame::ComputeStereoMatches (Frame.cc:827-997) on one rectified stereo frame: row-band Hamming
+// search (TH_HIGH / (TH_HIGH+TH_LOW)/2), 11x11 SAD over +-5 px on the unblurred pyramid level of
+// the left keypoint, parabola sub-pixel fit, median-SAD outlier rejection.  Outputs mvuRight and
+// mvDepth (-1 = unmatched) and the accepted SAD distances (-1 = none).
+void oracle_stereo_matches(const oracle_kp* kpsL, int nL, const uint8_t* descL, const oracle_kp* kpsR,
+                           int nR, const uint8_t* descR, const uint8_t* const* pyrL,
+                           const uint8_t* const* pyrR, const int* lw, const int* lh, int nlevels,
+                           const float* scale, const float* inv_scale, float mbf, float mb,
+                           float* uRight, float* depth, int32_t* sad);
+
 }  // extern "C"

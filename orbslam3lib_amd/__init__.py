@@ -34,6 +34,7 @@ EXPORTED = [
     "orbgpu_download_result", "orbgpu_download_counts", "orbgpu_synchronize",
     "orbgpu_get_pyramid_level", "orbgpu_get_level_keypoints", "orbgpu_match_knn2",
     "orbgpu_match_stereo_batch", "orbgpu_download_matches", "orbgpu_descriptor_distance",
+    "orbgpu_stereo_matches_batch", "orbgpu_download_stereo",
     "orbgpu_set_profiling", "orbgpu_num_stages", "orbgpu_stage_name", "orbgpu_stage_times",
     "orbgpu_reset_stage_times", "orbgpu_last_error", "orbgpu_abi_version",
 ]
@@ -304,6 +305,22 @@ class BatchExtractor:
         _check(_lib.orbgpu_download_matches(self.ctx.handle, pair, *[_p(o) for o in out], cap,
                                             C.byref(nq)))
         return tuple(o[:nq.value] for o in out)
+
+    def stereo_matches(self, mbf, mb, stream=None):
+        """Frame::ComputeStereoMatches (Frame.cc:827-997) for every pair 2p / 2p+1 of the last
+        run(); results stay in HBM (stereo_result)."""
+        _check(_lib.orbgpu_stereo_matches_batch(self.ctx.handle, self.n // 2, C.c_float(mbf),
+                                                C.c_float(mb), C.c_void_p(stream) if stream else None))
+
+    def stereo_result(self, pair, cap=65536):
+        """(mvuRight, mvDepth, sad) of pair `pair`: float32, float32, int32 per left keypoint."""
+        ur = np.zeros(cap, np.float32)
+        dp = np.zeros(cap, np.float32)
+        sad = np.zeros(cap, np.int32)
+        n = C.c_int(0)
+        _check(_lib.orbgpu_download_stereo(self.ctx.handle, pair, _p(ur), _p(dp), _p(sad), cap,
+                                           C.byref(n)))
+        return ur[:n.value], dp[:n.value], sad[:n.value]
 
     def set_profiling(self, on=True, stages=None, serialize=False):
         """on: bracket every stage's launches with HIP events; stages: only these stage names;

@@ -91,6 +91,26 @@ struct MatchArgs {
     int pair0;                // first pair of this launch
 };
 
+// Frame::ComputeStereoMatches over a batch's device-resident results (orb_stereo.hip).
+struct StereoArgs {
+    const void* kps;                 // out_kps: orbgpu_keypoint [img][out_cap]
+    const uint8_t* desc;             // out_desc: [img][out_cap][32]
+    const int32_t* out_n;            // [img]
+    int out_cap;
+    int nlevels, H0;                 // levels, rows of level 0
+    const uint8_t* lvl_base[kMaxLevels];  // unblurred pyramid (mvImagePyramid), image 0
+    long long limg_stride[kMaxLevels];
+    int lw[kMaxLevels], lh[kMaxLevels], lpitch[kMaxLevels];
+    float scale[kMaxLevels], inv_scale[kMaxLevels];  // mvScaleFactors / mvInvScaleFactors
+    float mbf, mb;                   // Frame::mbf, Frame::mb
+    int32_t* row_start;              // [pair][H0 + 1] right keypoints by row (CSR)
+    int32_t* row_idx;                // [pair][out_cap]
+    float* u_right;                  // [pair][out_cap] mvuRight
+    float* depth;                    // [pair][out_cap] mvDepth
+    int32_t* sad;                    // [pair][out_cap] accepted SAD distance, -1 if none
+    int pair0;                       // first pair of this launch
+};
+
 // Octree workspace layout for one (image, level) with n_cap keys and node capacity C.  The node
 // state lives in LDS when C <= kOctLdsNodes, otherwise in the `nodemem` part of this block.
 constexpr int kOctLdsNodes = 1024;
@@ -130,6 +150,7 @@ hipError_t launch_orient_desc(const BatchArgs& a, hipStream_t s);
 hipError_t launch_finalize(const BatchArgs& a, hipStream_t s);
 hipError_t launch_knn2_pairs(const MatchArgs& m, int npairs, int qblocks, void* scratch, hipStream_t s);
 size_t knn2_scratch_bytes(int npairs, int out_cap);
+hipError_t launch_stereo(const StereoArgs& s, int npairs, hipStream_t st);  // orb_stereo.hip
 hipError_t launch_knn2_plain(const uint8_t* q, int nq, const uint8_t* t, int nt, int32_t* i1,
                              int32_t* d1, int32_t* i2, int32_t* d2, hipStream_t s);
 

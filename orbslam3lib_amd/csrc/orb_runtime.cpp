@@ -40,11 +40,11 @@ int fail(int code, const std::string& msg) {
     } while (0)
 
 enum Stage { ST_RESIZE, ST_BLUR, ST_FAST48, ST_FAST, ST_FAST_TOP, ST_OCTREE, ST_ORIENT, ST_FINAL, ST_KNN,
-             ST_PYRAMID, ST_COUNT };
+             ST_PYRAMID, ST_STEREO, ST_COUNT };
 // names as rocprofv3 shows the kernels (templates with their argument)
 const char* kStageNames[ST_COUNT] = {"k_resize",         "k_blur",   "k_fast_cells<48>", "k_fast_cells<64>",
                                      "k_fast_cells<80>", "k_octree", "k_orient_desc",    "k_finalize",
-                                     "k_knn2",           "k_pyramid"};
+                                     "k_knn2",           "k_pyramid", "k_stereo"};
 
 struct DevBuf {
     void* p = nullptr;
@@ -102,7 +102,8 @@ struct orbgpu_ctx {
     // device buffers
     DevBuf input, pyr, blur, rtab, cellkeys, cellcnt, octws, lvlkey, lvlangle, lvldesc, lvlcnt,
         status, outkps, outdesc, outn, outmono, laps, midx1, mdist1, midx2, mdist2, mnq, scratch,
-        octdbg, knnpart;
+        octdbg, knnpart, strow, stidx, stur, stdepth, stsad;
+    int stereo_pairs = 0;  // pairs of the last orbgpu_stereo_matches_batch
     int input_images = 0;   // images currently sized for in `input`
     hipEvent_t fork = nullptr;
     std::vector<hipEvent_t> join;  // one per sub stream
@@ -562,7 +563,7 @@ int orbgpu_destroy(orbgpu_ctx* c) {
                       &c->octws,   &c->lvlkey,  &c->lvlangle, &c->lvldesc, &c->lvlcnt, &c->status,
                       &c->outkps,  &c->outdesc, &c->outn,   &c->outmono, &c->laps,     &c->midx1,
                       &c->mdist1,  &c->midx2,   &c->mdist2, &c->mnq,     &c->scratch, &c->octdbg,
-                      &c->knnpart};
+                      &c->knnpart, &c->strow,  &c->stidx, &c->stur,    &c->stdepth,  &c->stsad};
     for (DevBuf* b : bufs) b->release();
     for (size_t k = 1; k < c->sub.size(); ++k) hipStreamDestroy(c->sub[k]);
     if (c->fork) hipEventDestroy(c->fork);
@@ -981,6 +982,80 @@ int orbgpu_download_matches(orbgpu_ctx* c, int pair, int32_t* i1, int32_t* d1, i
         if (d1) HIP_TRY(hipMemcpy(d1, c->mdist1.as<int32_t>() + o, 4 * (size_t)n, hipMemcpyDeviceToHost));
         if (i2) HIP_TRY(hipMemcpy(i2, c->midx2.as<int32_t>() + o, 4 * (size_t)n, hipMemcpyDeviceToHost));
         if (d2) HIP_TRY(hipMemcpy(d2, c->mdist2.as<int32_t>() + o, 4 * (size_t)n, hipMemcpyDeviceToHost));
+    }
+    return ORBGPU_OK;
+}
+
+int orbgpu_stereo_matches_batch(orbgpu_ctx* c, int n_pairs, float mbf, float mb, void* stream) {
+    if (!c || n_pairs < 1 || 2 * n_pairs > c->last_images) return fail(ORBGPU_ERR_INVALID, "bad pair count");
+    if (!(mb > 0.f) || !(mbf > 0.f)) return fail(ORBGPU_ERR_INVALID, "mbf and mb must be positive");
+    HIP_TRY(hipSetDevice(c->device));
+    const BatchArgs& A = c->A;
+    const int H0 = A.lv[0].h;
+    const size_t np = (size_t)n_pairs;
+    if (c->strow.ensure(np * (H0 + 1) * 4 + 256) || c->stidx.ensure(np * c->out_cap * 4 + 256) ||
+        c->stur.ensure(np * c->out_cap * 4 + 256) || c->stdepth.ensure(np * c->out_cap * 4 + 256) ||
+        c->stsad.ensure(np * c->out_cap * 4 + 256))
+        return fail(ORBGPU_ERR_HIP, "hipMalloc failed (stereo buffers)");
+    StereoArgs S{};
+    S.kps = c->outkps.p;
+    S.desc = c->outdesc.as<uint8_t>();
+    S.out_n = c->outn.as<int32_t>();
+    S.out_cap = c->out_cap;
+    S.nlevels = A.nlevels;
+    S.H0 = H0;
+    for (int l = 0; l < A.nlevels; ++l) {
+        S.lvl_base[l] = l == 0 ? c->input.as<uint8_t>() : A.lvl_base[l];
+        S.limg_stride[l] = l == 0 ? (long long)A.lv[0].w * A.lv[0].h : A.lv[l].img_stride;
+        S.lw[l] = A.lv[l].w;
+        S.lh[l] = A.lv[l].h;
+        S.lpitch[l] = l == 0 ? A.lv[0].w : A.lv[l].pitch;
+        S.scale[l] = c->scale[l];
+        S.inv_scale[l] = c->inv_scale[l];
+    }
+    S.mbf = mbf;
+    S.mb = mb;
+    S.row_start = c->strow.as<int32_t>();
+    S.row_idx = c->stidx.as<int32_t>();
+    S.u_right = c->stur.as<float>();
+    S.depth = c->stdepth.as<float>();
+    S.sad = c->stsad.as<int32_t>();
+    // follow the extraction's sub-batches (each chunk's pairs right after their extraction)
+    bool chunked = !stream && !c->last_chunks.empty();
+    for (const auto& ch : c->last_chunks) chunked &= (ch.img0 % 2) == 0 && (ch.n % 2) == 0;
+    if (chunked) {
+        for (const auto& ch : c->last_chunks) {
+            const int p0 = ch.img0 / 2, npp = std::min(ch.n / 2, n_pairs - p0);
+            if (npp <= 0) continue;
+            StereoArgs SS = S;
+            SS.pair0 = p0;
+            int r = timed(c, ST_STEREO, ch.st, [&] { return launch_stereo(SS, npp, ch.st); });
+            if (r) return r;
+        }
+    } else {
+        hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+        S.pair0 = 0;
+        int r = timed(c, ST_STEREO, s, [&] { return launch_stereo(S, n_pairs, s); });
+        if (r) return r;
+    }
+    c->stereo_pairs = n_pairs;
+    return ORBGPU_OK;
+}
+
+int orbgpu_download_stereo(orbgpu_ctx* c, int pair, float* u_right, float* depth, int32_t* sad, int cap,
+                           int* n) {
+    if (!c || pair < 0 || pair >= c->stereo_pairs) return fail(ORBGPU_ERR_INVALID, "bad pair");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipDeviceSynchronize());
+    int32_t nl = 0;
+    HIP_TRY(hipMemcpy(&nl, c->outn.as<int32_t>() + 2 * pair, 4, hipMemcpyDeviceToHost));
+    if (n) *n = nl;
+    if (nl > cap) return fail(ORBGPU_ERR_CAPACITY, "caller capacity too small");
+    const size_t o = (size_t)pair * c->out_cap;
+    if (nl) {
+        if (u_right) HIP_TRY(hipMemcpy(u_right, c->stur.as<float>() + o, 4 * (size_t)nl, hipMemcpyDeviceToHost));
+        if (depth) HIP_TRY(hipMemcpy(depth, c->stdepth.as<float>() + o, 4 * (size_t)nl, hipMemcpyDeviceToHost));
+        if (sad) HIP_TRY(hipMemcpy(sad, c->stsad.as<int32_t>() + o, 4 * (size_t)nl, hipMemcpyDeviceToHost));
     }
     return ORBGPU_OK;
 }
