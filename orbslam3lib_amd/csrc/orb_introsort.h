@@ -248,6 +248,10 @@ __host__ __device__ __attribute__((always_inline)) inline void introsort_partiti
         s.segD[0][0] = (uint16_t)(2 * isort_lg(m));
         *sh_nseg = m > 16 ? 1 : 0;
     }
+    // s.rank[i] = first index of the final segment holding i (a segment of <= 16 elements is
+    // never partitioned again), 0xFFFF inside a heap-sorted segment (step 2 reads it)
+    if (m <= 16)
+        for (int i = tid; i < m; i += NT) s.rank[i] = 0;
     p.sync();
     while (true) {
         const int nseg = *sh_nseg;
@@ -264,6 +268,7 @@ __host__ __device__ __attribute__((always_inline)) inline void introsort_partiti
             if (D[g] == 0) {
                 isort_heapsort(a + f, l - f);
                 s.segK[g] = -1;
+                for (int i = f; i < l; ++i) s.rank[i] = 0xFFFF;
             } else {
                 isort_median_to_first(a, f, f + 1, f + (l - f) / 2, l - 1);
                 s.segK[g] = 0;
@@ -343,6 +348,10 @@ __host__ __device__ __attribute__((always_inline)) inline void introsort_partiti
                 cut = K < nl ? s.lpos[f + K] : 0x7fffffff;
                 if (K > 0) cut = cut < s.rpos[f + K - 1] ? cut : s.rpos[f + K - 1];
                 c = (cut - f > 16) + (l - cut > 16);
+                if (cut - f <= 16)
+                    for (int i = f; i < cut; ++i) s.rank[i] = (uint16_t)f;
+                if (l - cut <= 16)
+                    for (int i = cut; i < l; ++i) s.rank[i] = (uint16_t)cut;
             }
             int tot;
             const int ex = p.scan_small(c, &tot);
@@ -369,7 +378,10 @@ __host__ __device__ __attribute__((always_inline)) inline void introsort_partiti
     }
 }
 
-// Step 2: stable sort of the partitioned array (a rank sort, O(m^2 / threads)) on policy p.
+// Step 2: stable sort of the partitioned array on policy p.  Partitioning leaves every element
+// of a segment <= every element of the segments to its right, so the stable sort of the whole
+// array is the stable sort of each final segment (<= 16 elements: a rank among them; a
+// heap-sorted segment is already in order and keeps its positions).
 template <int AS, class P>
 __host__ __device__ __attribute__((always_inline)) inline void introsort_final(
     P& p, asp<AS, SortElem> a, int m, const SortScratchT<AS>& s) {
@@ -377,15 +389,17 @@ __host__ __device__ __attribute__((always_inline)) inline void introsort_final(
     if (m <= 1) return;
     for (int i = tid; i < m; i += NT) {
         const SortElem x = se_ld(a, i);
-        int r = 0;
-        for (int j = 0; j < m; ++j) {
-            const SortElem y = se_ld(a, j);
-            r += node_less(y, x) || (j < i && !node_less(x, y));
+        const int s0 = s.rank[i];
+        int r = i;
+        if (s0 != 0xFFFF) {
+            r = s0;
+            for (int j = s0; j < m && s.rank[j] == s0; ++j) {
+                const SortElem y = se_ld(a, j);
+                r += node_less(y, x) || (j < i && !node_less(x, y));
+            }
         }
-        s.rank[i] = (uint16_t)r;
+        se_st(s.tmp, r, x);
     }
-    p.sync();
-    for (int i = tid; i < m; i += NT) se_st(s.tmp, s.rank[i], se_ld(a, i));
     p.sync();
     for (int i = tid; i < m; i += NT) se_st(a, i, se_ld(s.tmp, i));
     p.sync();

@@ -261,10 +261,8 @@ __host__ __device__ __attribute__((always_inline)) inline int octree_distribute(
             const int k = base + u * NT + tid;
             int idx = (int)((float)key_x(key[u]) / hX);
             if (idx >= nIni) idx = nIni - 1;  // unreachable for in-range keys; keeps memory safe
-            if (k < n) {
-                nq[k] = (uint16_t)(idx << 2);
-                p.atomic_add(&cur[idx].cnt, 1);
-            }
+            if (k < n) nq[k] = (uint16_t)(idx << 2);
+            p.run_add(&cur[idx].cnt, idx, k < n);
         }
     });
     p.sync();
@@ -312,14 +310,10 @@ __host__ __device__ __attribute__((always_inline)) inline int octree_distribute(
 #pragma unroll
         for (int u = 0; u < kOctUnroll; ++u) {
             const int k = base + u * NT + tid;
-            if (k < n) {
-                int q = 0;
-                if (nd[u].cnt > 1) {
-                    q = oct_quadrant(key[u], nd[u]);
-                    p.atomic_add(&ccur[4 * v[u] + q], 1);
-                }
-                nq[k] = (uint16_t)((v[u] << 2) | q);
-            }
+            const bool split = k < n && nd[u].cnt > 1;
+            const int q = split ? oct_quadrant(key[u], nd[u]) : 0;
+            p.run_add(&ccur[4 * v[u] + q], 4 * v[u] + q, split);
+            if (k < n) nq[k] = (uint16_t)((v[u] << 2) | q);
         }
     });
     p.sync();
@@ -574,14 +568,10 @@ __host__ __device__ __attribute__((always_inline)) inline int octree_distribute(
 #pragma unroll
             for (int u = 0; u < kOctUnroll; ++u) {
                 const int k = base + u * NT + tid;
-                if (k < n) {
-                    int q = 0;
-                    if (dv[u] && nd[u].cnt > 1) {
-                        q = oct_quadrant(key[u], nd[u]);
-                        p.atomic_add(&cnxt[4 * nv[u] + q], 1);
-                    }
-                    nq[k] = (uint16_t)((nv[u] << 2) | q);
-                }
+                const bool split = k < n && dv[u] && nd[u].cnt > 1;
+                const int q = split ? oct_quadrant(key[u], nd[u]) : 0;
+                p.run_add(&cnxt[4 * nv[u] + q], 4 * nv[u] + q, split);
+                if (k < n) nq[k] = (uint16_t)((nv[u] << 2) | q);
             }
         });
         {

@@ -78,6 +78,21 @@ struct DevPolicy {
         return __hip_atomic_fetch_max(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __device__ unsigned long long now() const { return wall_clock64(); }  // 100 MHz
+    // +1 on the counter `ptr` of every valid lane, where lanes naming the same counter `key` in a
+    // run of neighbouring lanes add once (the run's first lane adds the run length).  The key
+    // passes of the octree visit keys in cell order, so a wave's lanes mostly hit a few counters:
+    // per-lane LDS atomics on one address serialize lane by lane.  All lanes must call it.
+    template <class T>
+    __device__ void run_add(T ptr, int key, bool valid) {
+        const int lane = (int)(threadIdx.x & 63);
+        const int k = valid ? key : -1 - lane;  // invalid lanes end runs
+        const int prev = __shfl_up(k, 1, 64);
+        const bool head = valid && (lane == 0 || prev != k);
+        const uint64_t bound = __ballot(head || !valid);
+        const uint64_t above = lane == 63 ? 0ull : (bound & (~0ull << (lane + 1)));
+        const int next = above ? (int)__builtin_ctzll(above) : 64;
+        if (head) __hip_atomic_fetch_add(ptr, next - lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     __device__ int popc64(uint64_t x) const { return __popcll(x); }
     __device__ int lane() const { return (int)(threadIdx.x & 63); }
     // wave-uniform by construction; readfirstlane lets the compiler keep it (and every loop
@@ -183,6 +198,10 @@ struct SerialPolicy {
     __host__ __device__ int scan_excl(int v, int* total) {
         *total = v;
         return 0;
+    }
+    template <class T>
+    __host__ __device__ void run_add(T ptr, int, bool valid) {
+        if (valid) *ptr += 1;
     }
     __host__ __device__ int scan_small(int v, int* total) {
         *total = v;

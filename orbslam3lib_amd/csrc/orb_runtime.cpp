@@ -112,6 +112,10 @@ struct orbgpu_ctx {
     // idle GPU per step (ORBGPU_ISOLATE=<stage bit mask> turns it on)
     unsigned isolate_mask = 0;
     bool serialize = false;  // profiling: every stage isolated
+    std::vector<int32_t> laps_host;  // lapping areas currently in `laps` (device), per image
+    bool need_fork = true;           // the main stream holds work the sub streams must wait for
+    bool stagger = true;             // ORBGPU_STAGGER=0: the chunks start every layout in lockstep
+    std::vector<hipEvent_t> stagger_ev;
     // pyramid + blur as the per-level k_resize launches and k_blur (default) or as one k_pyramid
     // launch (ORBGPU_PYR=1; measured slower on the 128-pair bench: 618 vs ~530 us per step, its
     // stripes recompute the halo rows and each workgroup walks its tiles serially);
@@ -457,6 +461,16 @@ int timed(orbgpu_ctx* c, int stage, hipStream_t s, F&& launch) {
     return 0;
 }
 
+// Makes stream s wait for everything already enqueued on the context's other streams.
+int join_all(orbgpu_ctx* c, hipStream_t s) {
+    for (size_t k = 0; k < c->sub.size() && k < c->join.size(); ++k) {
+        if (c->sub[k] == s) continue;
+        HIP_TRY(hipEventRecord(c->join[k], c->sub[k]));
+        HIP_TRY(hipStreamWaitEvent(s, c->join[k], 0));
+    }
+    return 0;
+}
+
 void resolve_pending(orbgpu_ctx* c) {
     for (auto& p : c->pending) {
         float ms = 0;
@@ -538,6 +552,8 @@ int orbgpu_create(const orbgpu_params* p, int device, int max_width, int max_hei
         }
         const char* iso = getenv("ORBGPU_ISOLATE");  // stage bit mask (diagnostics)
         if (iso) c->isolate_mask = (unsigned)strtoul(iso, nullptr, 0);
+        const char* sg = getenv("ORBGPU_STAGGER");
+        if (sg) c->stagger = atoi(sg) != 0;
         const char* pm = getenv("ORBGPU_PYR");
         if (pm) c->pyr_mode = atoi(pm) != 0;
         const char* ps = getenv("ORBGPU_PYR_STRIPES");
@@ -567,6 +583,7 @@ int orbgpu_destroy(orbgpu_ctx* c) {
     for (DevBuf* b : bufs) b->release();
     for (size_t k = 1; k < c->sub.size(); ++k) hipStreamDestroy(c->sub[k]);
     if (c->fork) hipEventDestroy(c->fork);
+    for (hipEvent_t e : c->stagger_ev) hipEventDestroy(e);
     for (auto e : c->join) hipEventDestroy(e);
     if (c->stream) hipStreamDestroy(c->stream);
     delete c;
@@ -595,8 +612,11 @@ int orbgpu_upload_images(orbgpu_ctx* c, const uint8_t* images, int n, int w, int
     int r = ensure_input(c, n, w, h);
     if (r) return r;
     HIP_TRY(hipSetDevice(c->device));
+    r = join_all(c, c->stream);  // sub streams may still read the previous images
+    if (r) return r;
     HIP_TRY(hipMemcpy2DAsync(c->input.p, w, images, stride, w, (size_t)h * n, hipMemcpyHostToDevice,
                              c->stream));
+    c->need_fork = true;
     return ORBGPU_OK;
 }
 
@@ -609,10 +629,19 @@ int orbgpu_run_batch(orbgpu_ctx* c, int n, int w, int h, const int32_t* laps, vo
     r = set_geometry(c, w, h);
     if (r) return r;
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
-    if (laps) {
-        HIP_TRY(hipMemcpyAsync(c->laps.p, laps, (size_t)n * 8, hipMemcpyHostToDevice, s));
-    } else {
-        HIP_TRY(hipMemsetAsync(c->laps.p, 0, (size_t)n * 8, s));
+    // the lapping areas change rarely (per camera): upload them only when they differ from the
+    // copy already on the device, after every stream has finished reading the old one
+    {
+        std::vector<int32_t> want((size_t)n * 2, 0);
+        if (laps) std::memcpy(want.data(), laps, (size_t)n * 8);
+        if (want != c->laps_host) {
+            r = join_all(c, s);
+            if (r) return r;
+            HIP_TRY(hipMemcpyAsync(c->laps.p, want.data(), (size_t)n * 8, hipMemcpyHostToDevice, s));
+            HIP_TRY(hipStreamSynchronize(s));  // `want` is pageable host memory
+            c->laps_host.swap(want);
+            c->need_fork = true;
+        }
     }
     BatchArgs A = c->A;
     A.nimages = n;
@@ -635,17 +664,32 @@ int orbgpu_run_batch(orbgpu_ctx* c, int n, int w, int h, const int32_t* laps, vo
     // a different sub-batch layout than last time may put an image on another stream: drain first
     if (!c->last_chunks.empty() && ((int)c->last_chunks.size() != K || c->last_images != n))
         HIP_TRY(hipDeviceSynchronize());
+    const bool relayout = c->last_chunks.empty() || (int)c->last_chunks.size() != K || c->last_images != n;
     if (K > 1) {
-        HIP_TRY(hipEventRecord(c->fork, s));
+        // sub stream k > 0 waits for the main stream only when the main stream holds work it
+        // depends on (a new layout, uploaded images, new lapping areas): in the steady state
+        // every chunk's chain of steps stays on its own stream, so the streams keep the offset
+        // they were given at the first step (stagger below) instead of restarting in lockstep
+        const bool fork = relayout || c->need_fork;
+        if (fork) HIP_TRY(hipEventRecord(c->fork, s));
         for (int k = 0; k < K; ++k) {
             const int p0 = (int)((long long)k * (n / 2) / K), p1 = (int)((long long)(k + 1) * (n / 2) / K);
             if (p1 > p0) {
-                if (k > 0) HIP_TRY(hipStreamWaitEvent(c->sub[k], c->fork, 0));
+                if (k > 0 && fork) HIP_TRY(hipStreamWaitEvent(c->sub[k], c->fork, 0));
                 chunks.push_back({2 * p0, 2 * (p1 - p0), c->sub[k]});
             }
         }
+        c->need_fork = false;
     } else {
         chunks.push_back({0, n, s});
+    }
+    // first step of a layout: chunk k starts after chunk k-1 finished its pyramid + blur, so the
+    // chunks run different stages (memory-, VALU- and latency-bound ones) at the same time
+    const bool stagger = relayout && c->stagger && chunks.size() > 1 && !c->serialize;
+    while (stagger && c->stagger_ev.size() < chunks.size()) {
+        hipEvent_t ev;
+        HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        c->stagger_ev.push_back(ev);
     }
     auto each = [&](int stage, auto launch) -> int {
         if (chunks.size() > 1 && (c->serialize || ((c->isolate_mask >> stage) & 1u))) {
@@ -669,15 +713,32 @@ int orbgpu_run_batch(orbgpu_ctx* c, int n, int w, int h, const int32_t* laps, vo
         }
         return 0;
     };
-    if (c->pyr_mode) {
-        // the whole pyramid + blur in one launch per chunk: 2^sl row stripes per image, enough
-        // workgroups for the batch to cover the chip (about 1024), at most 16 per image
-        int sl = 0;
-        if (c->pyr_stripes_log2 >= 0) {
-            sl = c->pyr_stripes_log2;
-        } else {
-            while (sl + 1 < kPyrStripeKinds && (n << sl) < 1024) ++sl;
+    // the whole pyramid + blur in one k_pyramid launch per chunk: 2^sl row stripes per image,
+    // enough workgroups for the batch to cover the chip (about 1024), at most 16 per image
+    int sl = 0;
+    if (c->pyr_stripes_log2 >= 0) {
+        sl = c->pyr_stripes_log2;
+    } else {
+        while (sl + 1 < kPyrStripeKinds && (n << sl) < 1024) ++sl;
+    }
+    if (stagger) {
+        // chunk-major: chunk k's first kernel waits for chunk k-1's pyramid + blur
+        for (size_t k = 0; k < chunks.size(); ++k) {
+            const Chunk& ch = chunks[k];
+            BatchArgs B = A;
+            B.img0 = ch.img0;
+            B.nimages = ch.n;
+            if (k > 0) HIP_TRY(hipStreamWaitEvent(ch.st, c->stagger_ev[k - 1], 0));
+            if (c->pyr_mode) {
+                if ((r = timed(c, ST_PYRAMID, ch.st, [&] { return launch_pyramid(B, sl, ch.st); }))) return r;
+            } else {
+                for (int l = 1; l < A.nlevels; ++l)
+                    if ((r = timed(c, ST_RESIZE, ch.st, [&] { return launch_resize(B, l, ch.st); }))) return r;
+                if ((r = timed(c, ST_BLUR, ch.st, [&] { return launch_blur(B, ch.st); }))) return r;
+            }
+            HIP_TRY(hipEventRecord(c->stagger_ev[k], ch.st));
         }
+    } else if (c->pyr_mode) {
         r = each(ST_PYRAMID, [&](const BatchArgs& B, hipStream_t st) { return launch_pyramid(B, sl, st); });
         if (r) return r;
     } else {
