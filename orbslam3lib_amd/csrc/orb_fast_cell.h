@@ -50,6 +50,41 @@ __host__ __device__ inline bool fast_kept(const uint8_t* M, int off, int t) {
     return (v > t) & (v >= 2) & (imax(a, b) < v);
 }
 
+typedef unsigned short fw_u16x2 __attribute__((ext_vector_type(2)));
+
+__device__ inline fw_u16x2 fw_as16(uint32_t x) { return __builtin_bit_cast(fw_u16x2, x); }
+__device__ inline uint32_t fw_as32(fw_u16x2 x) { return __builtin_bit_cast(uint32_t, x); }
+
+// Compass pre-test of the 4 pixels of LDS dword C (Cm / Cp: the dwords left and right of it,
+// U / D: the dwords 3 rows up / down), device only: bit k set when pixel k has two cyclically
+// adjacent compass points of {0, 4, 8, 12} beyond threshold t (tt = t in both u16 halves) on the
+// same side -- one of {0,8} and one of {4,12} darker than v-t, or both brighter than v+t.  The
+// pixels go through packed u16 arithmetic in pairs (0, 2) and (1, 3) built with v_perm.
+__device__ inline uint32_t fw_compass4(uint32_t C, uint32_t Cm, uint32_t Cp, uint32_t U, uint32_t D,
+                                       uint32_t tt) {
+    const uint32_t Lf = __builtin_amdgcn_alignbyte(C, Cm, 1);  // pixels x-3 (ring 12)
+    const uint32_t Rt = __builtin_amdgcn_alignbyte(Cp, C, 3);  // pixels x+3 (ring 4)
+    const fw_u16x2 T2 = fw_as16(tt);
+    auto test = [&](uint32_t sel) {
+        const fw_u16x2 v = fw_as16(__builtin_amdgcn_perm(0u, C, sel));
+        const fw_u16x2 p0 = fw_as16(__builtin_amdgcn_perm(0u, D, sel));    // ring 0: (0, +3)
+        const fw_u16x2 p8 = fw_as16(__builtin_amdgcn_perm(0u, U, sel));    // ring 8: (0, -3)
+        const fw_u16x2 p4 = fw_as16(__builtin_amdgcn_perm(0u, Rt, sel));   // ring 4: (+3, 0)
+        const fw_u16x2 p12 = fw_as16(__builtin_amdgcn_perm(0u, Lf, sel));  // ring 12: (-3, 0)
+        const fw_u16x2 lo = __builtin_elementwise_sub_sat(v, T2), hi = v + T2;
+        const fw_u16x2 dk = __builtin_elementwise_max(__builtin_elementwise_min(p0, p8),
+                                                      __builtin_elementwise_min(p4, p12));
+        const fw_u16x2 bk = __builtin_elementwise_min(__builtin_elementwise_max(p0, p8),
+                                                      __builtin_elementwise_max(p4, p12));
+        // dk < v - t  <=>  sat(lo - dk) > 0;   bk > v + t  <=>  sat(bk - hi) > 0
+        const fw_u16x2 r = __builtin_elementwise_sub_sat(lo, dk) | __builtin_elementwise_sub_sat(bk, hi);
+        return fw_as32(__builtin_elementwise_min(r, (fw_u16x2)(1)));
+    };
+    const uint32_t e = test(0x0c020c00u), o = test(0x0c030c01u);  // pixels (0, 2) and (1, 3)
+    const uint32_t comb = e | (o << 1);                           // halves: p0 | p1 << 1, p2 | p3 << 1
+    return (comb & 3u) | ((comb >> 14) & 0xCu);
+}
+
 // Per-cell scratch (LDS on the GPU).
 struct CellScratch {
     uint8_t* T;        // [P * P], 4-byte aligned
@@ -116,20 +151,76 @@ __host__ __device__ int fast_cell_detect(Pol& p, int sh, const CellGeom& g, int 
     const int dr = rows - 6 > 0 ? rows - 6 : 0;
     const int dc = cols - 6 > 0 ? cols - 6 : 0;
     const int nd = dr * dc;
+    (void)nd;
     const int tini = ini_th < 0 ? 0 : (ini_th > 255 ? 255 : ini_th);
     const int tmin = min_th < 0 ? 0 : (min_th > 255 ? 255 : min_th);
     const int W = p.nwaves(), w = p.wave(), L = p.wave_width(), lane = p.lane();
     const uint64_t lt = p.lanemask_lt();
+#if defined(__HIP_DEVICE_COMPILE__)
+    // device: the pre-test takes 4 pixels per lane (fw_compass4); a wave owns a contiguous
+    // row-major range of (row, dword group) items, and its list starts after the detection
+    // pixels of the items before it
+    const int xs = 3 + sh, xe = 3 + sh + dc;
+    const int g0 = xs >> 2;
+    const int ng = dc > 0 ? ((xe - 1) >> 2) - g0 + 1 : 0;
+    const int items = dr * ng;
+    const int j0 = w * items / W, j1 = (w + 1) * items / W;
+    const float inv_ng = ng > 0 ? 1.f / (float)ng : 0.f;
+    auto pix_before = [&](int j) {  // detection pixels of the items before item j
+        if (ng == 0) return 0;
+        const int r = (int)(((float)j + 0.5f) * inv_ng), q = j - r * ng;
+        const int c = 4 * (g0 + q) - xs;
+        return r * dc + (c < 0 ? 0 : (c > dc ? dc : c));
+    };
+    const int i0 = pix_before(j0);
+    (void)lane;
+#else
     const int i0 = w * nd / W, i1 = (w + 1) * nd / W;  // nd <= 4900, W <= 16: no overflow
+#endif
     uint16_t* list = cs.list + i0;
+#if !defined(__HIP_DEVICE_COMPILE__)
     const float inv_dc = dc > 0 ? 1.f / (float)dc : 0.f;
     auto off_of = [&](int i) {
         const int r = (int)(((float)i + 0.5f) * inv_dc);  // exact: i < 4900, dc < 70
         return (3 + r) * CP + 3 + sh + (i - r * dc);
     };
+#endif
     // candidates -> corners at t -> exact strength; returns this wave's corner count
     auto build = [&](int t) {
         int na = 0;
+#if defined(__HIP_DEVICE_COMPILE__)
+        {
+            constexpr int RW = CP / 4;
+            const uint32_t* T32 = reinterpret_cast<const uint32_t*>(T);
+            const uint32_t tt = (uint32_t)t * 0x00010001u;
+            for (int base = j0; base < j1; base += L) {
+                const int i = base + lane;
+                uint32_t m4 = 0;
+                int o = 0;
+                if (i < j1) {
+                    const int r = (int)(((float)i + 0.5f) * inv_ng);  // exact: i < 69 * 19
+                    const int gg = g0 + (i - r * ng);
+                    const int dw = (r + 3) * RW + gg;
+                    m4 = fw_compass4(T32[dw], T32[dw - 1], T32[dw + 1], T32[dw - 3 * RW], T32[dw + 3 * RW], tt);
+                    const int x0 = 4 * gg;
+                    const int lo_cut = xs - x0 > 0 ? xs - x0 : 0;
+                    const int hi_cut = xe - x0 < 4 ? xe - x0 : 4;
+                    m4 &= ((1u << hi_cut) - 1u) & ~((1u << lo_cut) - 1u);
+                    o = (r + 3) * CP + x0;
+                }
+                const int c = __builtin_popcount(m4);
+                const uint64_t b0 = p.ballot(c & 1), b1 = p.ballot(c & 2), b2 = p.ballot(c & 4);
+                int pos = na + p.popc64(b0 & lt) + 2 * p.popc64(b1 & lt) + 4 * p.popc64(b2 & lt);
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if ((m4 >> k) & 1u) list[pos++] = (uint16_t)(o + k);
+                na += p.popc64(b0) + 2 * p.popc64(b1) + 4 * p.popc64(b2);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the list is read by other lanes
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+#else
         for (int base = i0; base < i1; base += L) {
             const bool in = base + lane < i1;
             const int i = in ? base + lane : i1 - 1;  // tail lanes recompute i1-1
@@ -145,6 +236,7 @@ __host__ __device__ int fast_cell_detect(Pol& p, int sh, const CellGeom& g, int 
             if (cand) list[na + p.popc64(m & lt)] = (uint16_t)o;
             na += p.popc64(m);
         }
+#endif
         // exact strength of every candidate (m > t <=> corner at t), corners kept in order
         int nb = 0;
         for (int base = 0; base < na; base += L) {

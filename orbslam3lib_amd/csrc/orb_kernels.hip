@@ -17,6 +17,7 @@
 #include "orb_kernels.h"
 #include "orb_math.h"
 #include "orb_fast_cell.h"
+#include "orb_fast_wave.h"
 #include "orb_octree.h"
 #include "orb_pattern_data.h"
 #include "orb_policy.h"
@@ -673,6 +674,81 @@ __global__ __launch_bounds__(kFastThreads) void k_fast_cells(BatchArgs a, int ce
     CellScratch cs{T, M, list, wcnt};
     const int n = fast_cell_run<CP>(p, src, G.pitch, sh, dword_ok, g, a.ini_th, a.min_th, cs, key_out, ld16);
     if (threadIdx.x == 0) *cnt_out = n;
+}
+
+// k_fast_wave: the same cells, one wave per cell (orb_fast_wave.h: 4 pixels per lane in the
+// compass pre-test), kFastWaveCells<CP> cells per workgroup, each wave with its own LDS tile, so
+// the waves never wait for each other.  Work item = (image, cell of the tile's levels), walked in
+// XCD order so neighbouring cells of one image share an L2.
+template <int CP>
+constexpr int kFastWaveCells = CP == kCellPitchTiny ? 2 : 1;  // LDS: 8 KB per 48-byte-tile cell
+
+template <int CP>
+__global__ __launch_bounds__(64 * kFastWaveCells<CP>) void k_fast_wave(BatchArgs a, int cell0, int ncell) {
+    constexpr int NW = kFastWaveCells<CP>;
+    constexpr int kList = cell_list_cap<CP>();
+    constexpr int RQ = CP / 16;
+    static_assert(CP % 16 == 0, "16-byte LDS rows");
+    __shared__ __attribute__((aligned(16))) uint8_t Ts[NW][CP * CP];
+    __shared__ __attribute__((aligned(16))) uint8_t Ms[NW][CP * CP];
+    __shared__ uint16_t Ls[NW][kList];
+    const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int lane = (int)(threadIdx.x & 63);
+    const int item = xcd_remap(blockIdx.x, gridDim.x) * NW + w;
+    if (item >= ncell * a.nimages) return;  // wave-uniform; no barrier in this kernel
+    const int img = a.img0 + item / ncell;
+    const int gcell = cell0 + item % ncell;  // flattened over the levels
+    int l = 0;
+    while (l + 1 < a.nlevels && gcell >= a.lv[l + 1].cell_first) ++l;
+    const LevelGeom& G = a.lv[l];
+    const int cell = gcell - G.cell_first;
+    const int ci = cell / G.nCols, cj = cell % G.nCols;
+    int32_t* cnt_out = a.cellcnt + (long long)img * a.cellcnt_img_stride + G.cellcnt_off + cell;
+    uint32_t* key_out = a.cellkeys + (long long)img * a.cellkeys_img_stride + G.cellkey_off +
+                        (long long)cell * G.cell_cap;
+    CellGeom g;
+    g.iniY = kMinBorder + ci * G.hCell;
+    g.iniX = kMinBorder + cj * G.wCell;
+    g.minBorder = kMinBorder;
+    if (g.iniY >= G.maxBY - 3 || g.iniX >= G.maxBX - 6) {  // :812, :821
+        if (lane == 0) *cnt_out = 0;
+        return;
+    }
+    g.rows = min(g.iniY + G.hCell + 6, G.maxBY) - g.iniY;
+    g.cols = min(g.iniX + G.wCell + 6, G.maxBX) - g.iniX;
+    const bool dword_ok = ((G.pitch | G.img_stride) & 3) == 0;
+    const int sh = dword_ok ? (g.iniX & 3) : 0;
+    const uint8_t* base = a.lvl_base[l] + (long long)img * G.img_stride;
+    const long long roi = (long long)g.iniY * G.pitch + (g.iniX - sh);
+    uint8_t* T = Ts[w];
+    uint8_t* M = Ms[w];
+    uint4* T128 = reinterpret_cast<uint4*>(T);
+    uint4* M128 = reinterpret_cast<uint4*>(M);
+    // stage the ROI (16-byte bounds-checked buffer loads) and clear the strength plane
+    const int rows = g.rows;
+    if (dword_ok) {
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)base, (short)0, (int)min(G.img_stride, 0x7fffffffLL), 0x00020000);
+        const int nq = (sh + g.cols + 15) >> 4;
+        for (int i = lane; i < rows * RQ; i += 64) {
+            const int r = i / RQ, q = i - r * RQ;
+            if (q < nq) {
+                const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(roi + (long long)r * G.pitch + 16 * q), 0, 0);
+                T128[i] = make_uint4(v[0], v[1], v[2], v[3]);
+            }
+            M128[i] = make_uint4(0, 0, 0, 0);
+        }
+    } else {  // rows not dword aligned (odd input widths): byte path, sh = 0
+        const uint8_t* src = base + roi;
+        for (int i = lane; i < rows * CP; i += 64) {
+            const int r = i / CP, c = i - r * CP;
+            if (c < g.cols) T[i] = src[(long long)r * G.pitch + c];
+        }
+        for (int i = lane; i < rows * RQ; i += 64) M128[i] = make_uint4(0, 0, 0, 0);
+    }
+    fw_wave_sync();
+    const int n = fast_cell_wave<CP>(T, M, Ls[w], sh, g, a.ini_th, a.min_th, key_out);
+    if (lane == 0) *cnt_out = n;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1359,6 +1435,21 @@ hipError_t launch_fast_cells(const BatchArgs& a, int tile, hipStream_t s) {
     int c0, c1;
     fast_cell_range(a, tile, &c0, &c1);
     if (c1 <= c0) return hipSuccess;
+    static const bool one_wave = getenv("ORBGPU_FAST_WAVE") != nullptr;  // one wave per cell
+    if (one_wave) {
+        const long long items = (long long)(c1 - c0) * a.nimages;
+        auto wgs = [&](int nw) { return dim3((unsigned)((items + nw - 1) / nw)); };
+        if (tile == kCellPitchTiny)
+            hipLaunchKernelGGL(k_fast_wave<kCellPitchTiny>, wgs(kFastWaveCells<kCellPitchTiny>),
+                               dim3(64 * kFastWaveCells<kCellPitchTiny>), 0, s, a, c0, c1 - c0);
+        else if (tile == kCellPitchSmall)
+            hipLaunchKernelGGL(k_fast_wave<kCellPitchSmall>, wgs(kFastWaveCells<kCellPitchSmall>),
+                               dim3(64 * kFastWaveCells<kCellPitchSmall>), 0, s, a, c0, c1 - c0);
+        else
+            hipLaunchKernelGGL(k_fast_wave<kCellMax>, wgs(kFastWaveCells<kCellMax>),
+                               dim3(64 * kFastWaveCells<kCellMax>), 0, s, a, c0, c1 - c0);
+        return hipGetLastError();
+    }
     const dim3 grid(c1 - c0, a.nimages), block(kFastThreads);
     if (tile == kCellPitchTiny) hipLaunchKernelGGL(k_fast_cells<kCellPitchTiny>, grid, block, 0, s, a, c0);
     else if (tile == kCellPitchSmall) hipLaunchKernelGGL(k_fast_cells<kCellPitchSmall>, grid, block, 0, s, a, c0);

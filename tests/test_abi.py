@@ -27,7 +27,7 @@ def test_all_declared_symbols_exported():
 def test_library_has_gfx950_code_object():
     data = open(os.path.join(ROOT, "orbslam3lib_amd", "liborbgpu.so"), "rb").read()
     assert b"gfx950" in data
-    for k in (b"k_fast_cells", b"k_octree", b"k_orient_desc", b"k_knn2_pairs", b"k_resize", b"k_blur"):
+    for k in (b"k_fast_wave", b"k_fast_cells", b"k_octree", b"k_orient_desc", b"k_knn2_pairs", b"k_resize", b"k_blur"):
         assert k in data, k
 
 
