@@ -51,10 +51,11 @@ def fast_split(w, h, sf=1.2, L=8, tile=64):
     return L
 
 
-def algorithmic_bytes(w, h, L, nkp, sf=1.2):
+def algorithmic_bytes(w, h, L, nkp, sf=1.2, ncand=0.0):
     """Per-image bytes by stage: pyramid sum(A_{l-1}+A_l), FAST sum(A_l) (split
     between the 48-, 64- and 80-byte tile launches), blur 2*sum(A_l), 48 B per output keypoint
-    (16 B keypoint + 32 B descriptor); k_pyramid = pyramid + blur in one launch."""
+    (16 B keypoint + 32 B descriptor); k_pyramid = pyramid + blur in one launch; the octree reads
+    its 4-byte candidate keys and writes 4 bytes per kept keypoint."""
     A = [a * b for a, b in level_sizes(w, h, sf, L)]
     k48 = fast_split(w, h, sf, L, 48)
     k64 = max(k48, fast_split(w, h, sf, L, 64))
@@ -66,7 +67,14 @@ def algorithmic_bytes(w, h, L, nkp, sf=1.2):
         "k_fast_cells<80>": sum(A[k64:]),
         "k_blur": 2 * sum(A),
         "k_orient_desc": 48 * nkp,
+        "k_octree": 4 * ncand + 4 * nkp,
     }
+
+
+def fast_pyramid_bytes(w, h, L, sf=1.2):
+    """B_fp per image: pyramid sum_{l>=1}(A_{l-1}+A_l) + FAST sum_l A_l."""
+    A = [a * b for a, b in level_sizes(w, h, sf, L)]
+    return sum(A[l - 1] + A[l] for l in range(1, L)) + sum(A)
 
 
 def dist_setup():
@@ -190,6 +198,7 @@ def main():
         step()
     be.synchronize()
     nk, _ = be.counts()
+    cand_per_img = float(be.candidate_counts().mean())
     feats_per_step = int(nk.sum())
     nq_per_step = int(sum(nk[2 * p] for p in range(P)))
     pairs_per_step = int(sum(int(nk[2 * p]) * int(nk[2 * p + 1]) for p in range(P)))
@@ -243,7 +252,7 @@ def main():
 
     # roofline of the dominant kernel (per-launch algorithmic bytes / measured avg duration)
     n_img = 2 * P
-    per_img = algorithmic_bytes(W, H, args.nlevels, feats_per_step / n_img)
+    per_img = algorithmic_bytes(W, H, args.nlevels, feats_per_step / n_img, ncand=cand_per_img)
     stage_rows = {}
     for name, (ms, cnt) in stages.items():
         if cnt == 0:
@@ -285,10 +294,24 @@ def main():
         elif "Tops" in r:
             roof = {"kernel": dom, "bound": "valu", "achieved": r["Tops"], "peak": round(VALU_PEAK_TOPS, 1),
                     "unit": "Tops/s", "frac": r["frac_valu"], "traffic": traffic, "avg_us": r["avg_us"]}
-        else:  # latency-bound kernel with no HBM-scale algorithmic bytes (e.g. the octree)
+        else:
             roof = {"kernel": dom, "bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": None, "traffic": traffic, "avg_us": r["avg_us"],
-                    "note": "control-flow bound kernel; see stages"}
+                    "unit": "GB/s", "frac": None, "traffic": traffic, "avg_us": r["avg_us"]}
+        if dom == "k_octree":
+            roof["note"] = ("DistributeOctTree is barrier/LDS-latency bound (serial list rounds per "
+                            "(image, level)); its HBM bytes are the 4-B keys in and out")
+
+    # the north_star's named pair, FAST + pyramid, as one figure: B_fp per image over
+    # the summed per-step time of the k_resize and k_fast_cells launches of the serialized pass
+    fp_names = [k for k in stages_all if k == "k_resize" or k.startswith("k_fast_cells")]
+    fp_ms = sum(stages_all[k][0] for k in fp_names) / 3.0  # 3 serialized steps
+    roof_fp = None
+    if fp_ms > 0:
+        fp_bytes = fast_pyramid_bytes(W, H, args.nlevels) * n_img
+        ach = fp_bytes / (fp_ms * 1e-3) / 1e9
+        roof_fp = {"kernels": fp_names, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                   "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "bytes_per_step": int(fp_bytes),
+                   "us_per_step": round(fp_ms * 1e3, 1)}
 
     # Frame::ComputeStereoMatches on the same resident batch, timed on its own
     # (not part of the headline step): EuRoC-like rig, baseline 0.11 m, fx 435.2
@@ -316,6 +339,27 @@ def main():
                   "unit": "Mkeypoints/s", "ms_per_step": round(st_el / args.steps * 1e3, 4),
                   "kernel_ms_per_launch": round(st[0] / st[1], 4) if st[1] else None,
                   "pairs_per_step": P, "matched_frac_pair0": round(float((ur >= 0).mean()), 3) if len(ur) else 0.0}
+
+    # C5's exchange step when several GPUs run: every rank contributes its camera
+    # (pair 0's left eye), one RCCL all_gather moves the descriptors, each rank matches its own
+    # against all others on its GPU.  Reported beside the headline, never part of it.
+    cross = None
+    if world > 1:
+        try:
+            from orbslam3lib_amd.dist import cross_camera_match
+            kl0, dl0, _ = be.result(0)
+            bfm = og.BFMatcher.__new__(og.BFMatcher)
+            bfm._ctx = be.ctx
+            barrier(dist)
+            c0 = time.perf_counter()
+            res = cross_camera_match(dist, dl0, lambda q, t: bfm.knnMatch(q, t, 2))
+            c1 = time.perf_counter()
+            cel = max_over_ranks(dist, c1 - c0)
+            nqm = sum_over_ranks(dist, len(dl0) * len(res))
+            cross = {"cameras": world, "queries_per_camera": len(dl0), "ms": round(cel * 1e3, 3),
+                     "mmatches_s": round(nqm / cel / 1e6, 3), "exchange": "all_gather (RCCL)"}
+        except Exception as e:  # reported, never fatal to the headline line
+            cross = {"error": repr(e)[:200]}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -348,9 +392,11 @@ def main():
                         "gpairs_s": round(total_pairs / elapsed / 1e9, 3)},
             "features_per_step_per_gpu": feats_per_step,
             "roofline": roof,
+            "roofline_fast_pyramid": roof_fp,
             "stages": stage_rows,
             "cpu_baseline": cpu,
             "stereo_matches": stereo,
+            "cross_camera": cross,
         }
         print(json.dumps(out))
     if dist is not None:

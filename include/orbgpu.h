@@ -102,6 +102,9 @@ int orbgpu_download_result(orbgpu_ctx* ctx, int image, orbgpu_keypoint* kps, uin
                            int cap, int* n, int* n_mono);
 /* Per-image keypoint counts and mono counts of the last batch (host arrays of n_images). */
 int orbgpu_download_counts(orbgpu_ctx* ctx, int n_images, int32_t* n, int32_t* n_mono);
+/* Per-image number of cell keypoints that entered DistributeOctTree (vToDistributeKeys summed
+ * over the levels) in the last batch: the octree's input size, for instrumentation. */
+int orbgpu_candidate_counts(orbgpu_ctx* ctx, int n_images, int32_t* counts);
 int orbgpu_synchronize(orbgpu_ctx* ctx);
 
 /* Pyramid level `level` of batch image `image` (mvImagePyramid[level]), optionally blurred

@@ -34,7 +34,7 @@ EXPORTED = [
     "orbgpu_download_result", "orbgpu_download_counts", "orbgpu_synchronize",
     "orbgpu_get_pyramid_level", "orbgpu_get_level_keypoints", "orbgpu_match_knn2",
     "orbgpu_match_stereo_batch", "orbgpu_download_matches", "orbgpu_descriptor_distance",
-    "orbgpu_stereo_matches_batch", "orbgpu_download_stereo",
+    "orbgpu_stereo_matches_batch", "orbgpu_download_stereo", "orbgpu_candidate_counts",
     "orbgpu_set_profiling", "orbgpu_num_stages", "orbgpu_stage_name", "orbgpu_stage_times",
     "orbgpu_reset_stage_times", "orbgpu_last_error", "orbgpu_abi_version",
 ]
@@ -290,6 +290,12 @@ class BatchExtractor:
         m = np.zeros(self.n, np.int32)
         _check(_lib.orbgpu_download_counts(self.ctx.handle, self.n, _p(n), _p(m)))
         return n, m
+
+    def candidate_counts(self):
+        """Keys that entered DistributeOctTree per image (all levels) in the last run()."""
+        c = np.zeros(self.n, np.int32)
+        _check(_lib.orbgpu_candidate_counts(self.ctx.handle, self.n, _p(c)))
+        return c
 
     def result(self, i, cap=65536):
         kps = np.zeros(cap, KEYPOINT_DTYPE)

@@ -825,6 +825,24 @@ int orbgpu_download_counts(orbgpu_ctx* c, int n, int32_t* nk, int32_t* nm) {
     return ORBGPU_OK;
 }
 
+int orbgpu_candidate_counts(orbgpu_ctx* c, int n, int32_t* counts) {
+    if (!c || !counts) return fail(ORBGPU_ERR_INVALID, "null argument");
+    if (n > c->last_images) return fail(ORBGPU_ERR_INVALID, "more images than the last batch");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipDeviceSynchronize());
+    std::vector<int32_t> cc((size_t)n * c->cellcnt_img);
+    if (!cc.empty())
+        HIP_TRY(hipMemcpy(cc.data(), c->cellcnt.p, cc.size() * 4, hipMemcpyDeviceToHost));
+    const BatchArgs& A = c->A;
+    for (int i = 0; i < n; ++i) {
+        long long s = 0;
+        for (int l = 0; l < A.nlevels; ++l)
+            for (int k = 0; k < A.lv[l].ncells; ++k) s += cc[(size_t)i * c->cellcnt_img + A.lv[l].cellcnt_off + k];
+        counts[i] = (int32_t)s;
+    }
+    return ORBGPU_OK;
+}
+
 int orbgpu_download_result(orbgpu_ctx* c, int img, orbgpu_keypoint* kps, uint8_t* desc, int cap,
                            int* n, int* n_mono) {
     if (!c || img < 0 || img >= c->last_images) return fail(ORBGPU_ERR_INVALID, "bad image index");

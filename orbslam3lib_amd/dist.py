@@ -1,7 +1,8 @@
 """Multi-GPU plumbing for the batch path: one process per GPU (torch.distributed, RCCL on the
 GPU box, gloo on CPU).  Stereo pairs are independent, so the hot path shards them with no
 data-path collective; only the timing barrier and the max/sum reductions of bench.py cross
-ranks ("replicas only")."""
+ranks ("replicas only").  The one real exchange step of §8e, the cross-camera
+BFMatch of C5 (one camera per GPU), is cross_camera_match."""
 from __future__ import annotations
 
 
@@ -15,6 +16,28 @@ def shard_range(total: int, rank: int, world: int):
 def pair_seed_base(rank: int) -> int:
     """Synthetic frame index offset of a rank's shard (ranks never share frames)."""
     return rank * 100000
+
+
+def cross_camera_match(dist, desc, matcher, device=None):
+    """C5 cross-camera BFMatch: each rank holds one camera's descriptors (uint8
+    [n, 32]); one exchange step -- an all_gather of the counts, then of the rows padded to the
+    largest count (RCCL over xGMI on the GPU box, gloo on the CPU) -- after which every rank
+    matches its own rows against every other camera's rows with matcher(query, train) ->
+    (idx1, dist1, idx2, dist2).  Returns {rank: matcher result} for the other ranks."""
+    import numpy as np
+    import torch
+    world, rank = dist.get_world_size(), dist.get_rank()
+    dev = device or ("cuda" if dist.get_backend() == "nccl" else "cpu")
+    desc = np.ascontiguousarray(desc, dtype=np.uint8).reshape(-1, 32)
+    n = torch.tensor([desc.shape[0]], dtype=torch.int64, device=dev)
+    counts = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(counts, n)
+    counts = [int(c.item()) for c in counts]
+    buf = torch.zeros((max(max(counts), 1), 32), dtype=torch.uint8, device=dev)
+    buf[:desc.shape[0]] = torch.from_numpy(desc).to(dev)
+    rows = [torch.empty_like(buf) for _ in range(world)]
+    dist.all_gather(rows, buf)
+    return {r: matcher(desc, rows[r][:counts[r]].cpu().numpy()) for r in range(world) if r != rank}
 
 
 def reduce_scalar(dist, x: float, op: str = "max") -> float:

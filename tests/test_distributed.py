@@ -47,6 +47,44 @@ def test_gloo_world2_sharding_and_reductions():
     assert b0 != b1
 
 
+def _cross_worker(rank, world, port, q):
+    import numpy as np
+    import torch.distributed as dist
+
+    from oracle import oracle_py as O
+    from orbslam3lib_amd import dist as od
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    cams = [np.random.default_rng(50 + r).integers(0, 256, (37 + 11 * r, 32), dtype=np.uint8)
+            for r in range(world)]
+    got = od.cross_camera_match(dist, cams[rank], O.knn2)
+    ok = sorted(got) == [r for r in range(world) if r != rank]
+    for r, res in got.items():
+        ref = O.knn2(cams[rank], cams[r])
+        ok &= all(np.array_equal(a, b) for a, b in zip(res, ref))
+    dist.barrier()
+    q.put((rank, bool(ok)))
+    dist.destroy_process_group()
+
+
+def test_gloo_cross_camera_match_world3():
+    """C5's exchange step: each rank's camera descriptors (ragged counts) reach every other rank
+    intact and are matched there (the oracle kNN2 stands in for the GPU matcher on the CPU)."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_cross_worker, args=(r, 3, port, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(ok for _, ok in res)
+
+
 @pytest.mark.parametrize("total,world", [(7, 3), (128, 8), (1, 4)])
 def test_shard_range_partitions(total, world):
     from orbslam3lib_amd import dist as od

@@ -276,3 +276,18 @@ def test_pyramid_exact_2x_area_path(oracle, monkeypatch, pyr):
     rk, rd, rm = oracle.extract(img, nfeatures=500, scale_factor=2.0, nlevels=3)
     _same_kps(k, rk)
     np.testing.assert_array_equal(d, rd)
+
+
+@pytest.mark.parametrize("pitch", [None, "80"])
+def test_one_wave_fast_cells(oracle, frame0, monkeypatch, pitch):
+    """The one-wave-per-cell FAST kernel (ORBGPU_FAST_WAVE=1, k_fast_wave) on the 640x480 frame,
+    with the runtime's tiles and with every level forced through the 80-byte tile."""
+    L, _ = frame0
+    monkeypatch.setenv("ORBGPU_FAST_WAVE", "1")
+    if pitch:
+        monkeypatch.setenv("ORBGPU_FAST_PITCH", pitch)
+    ex = _extractor()
+    k, d, m = ex(L)
+    rk, rd, rm = oracle.extract(L, nfeatures=2000)
+    _same_kps(k, rk)
+    np.testing.assert_array_equal(d, rd)
