@@ -10,8 +10,8 @@ HDRS := $(wildcard $(CSRC)/*.h) include/orbgpu.h
 
 all: $(LIB) oracle facade_test
 
-$(LIB): $(CSRC)/orb_kernels.hip $(CSRC)/orb_stereo.hip $(CSRC)/orb_runtime.cpp $(HDRS)
-	$(HIPCC) $(HIPFLAGS) $(DEVFLAGS) -shared -o $@ $(CSRC)/orb_kernels.hip $(CSRC)/orb_stereo.hip $(CSRC)/orb_runtime.cpp
+$(LIB): $(CSRC)/orb_kernels.hip $(CSRC)/orb_stereo.hip $(CSRC)/orb_frame.hip $(CSRC)/orb_runtime.cpp $(HDRS)
+	$(HIPCC) $(HIPFLAGS) $(DEVFLAGS) -shared -o $@ $(CSRC)/orb_kernels.hip $(CSRC)/orb_stereo.hip $(CSRC)/orb_frame.hip $(CSRC)/orb_runtime.cpp
 
 oracle:
 	$(MAKE) -s -C oracle

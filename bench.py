@@ -118,6 +118,10 @@ def sum_over_ranks(dist, x):
     return float(t.item())
 
 
+EUROC_K = (458.654, 457.296, 367.215, 248.375)  # EuRoC cam0 fx fy cx cy
+EUROC_D = (-0.28340811, 0.07395907, 0.00019359, 1.76187114e-05)
+
+
 def cpu_baseline(w, h, nfeatures, seconds):
     """The oracle (scalar C++ restatement of the reference CPU ORBextractor + BFMatcher), one
     thread, on a bounded sample of the same workload: pairs until `seconds` elapse."""
@@ -127,6 +131,7 @@ def cpu_baseline(w, h, nfeatures, seconds):
     pairs = [synth.stereo_pair(h, w, 1000 + i) for i in range(4)]
     stereo_pyr = [(O.pyramid(L), O.pyramid(R)) for L, R in pairs]
     t_st = [0.0]
+    t_gr = 0.0
     nfeat = nq = 0
     t_ex = t_bf = 0.0
     i = 0
@@ -143,6 +148,10 @@ def cpu_baseline(w, h, nfeatures, seconds):
             O.stereo_matches(kl, dl, kr, dr, stereo_pyr[i % len(pairs)][0], stereo_pyr[i % len(pairs)][1],
                              47.9, float(np.float32(47.9) / np.float32(435.2)))
             t_st[0] += time.perf_counter() - t2
+        t3 = time.perf_counter()
+        O.undistort_grid(kl, EUROC_K, EUROC_D, w, h)
+        O.undistort_grid(kr, EUROC_K, EUROC_D, w, h)
+        t_gr += time.perf_counter() - t3
         nfeat += len(kl) + len(kr)
         nq += len(dl)
         t_ex += t1 - t0
@@ -150,6 +159,7 @@ def cpu_baseline(w, h, nfeatures, seconds):
         i += 1
     return {"pairs": i, "mfeat_s": nfeat / t_ex / 1e6, "mmatch_s": nq / t_bf / 1e6,
             "stereo_mkp_s": nq / t_st[0] / 1e6 if t_st[0] > 0 else None,
+            "grid_mkp_s": nfeat / t_gr / 1e6 if t_gr > 0 else None,
             "mfeat_s_pipeline": nfeat / (t_ex + t_bf) / 1e6}
 
 
@@ -168,6 +178,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-stereo", action="store_true", help="skip the ComputeStereoMatches leg")
+    ap.add_argument("--no-grid", action="store_true", help="skip the UndistortKeyPoints + grid leg")
     ap.add_argument("--no-profile", action="store_true",
                     help="do not bracket launches with HIP events in the timed region")
     args = ap.parse_args()
@@ -340,6 +351,31 @@ def main():
                   "kernel_ms_per_launch": round(st[0] / st[1], 4) if st[1] else None,
                   "pairs_per_step": P, "matched_frac_pair0": round(float((ur >= 0).mean()), 3) if len(ur) else 0.0}
 
+    # Frame::UndistortKeyPoints + AssignFeaturesToGrid over every image of the
+    # resident batch, timed on its own: EuRoC cam0 calibration (k1 k2 p1 p2)
+    grid = None
+    if not args.no_grid:
+        be.undistort_grid(EUROC_K, EUROC_D)
+        be.synchronize()
+        be.set_profiling(True, stages=["k_undistort_grid"])
+        be.reset_stage_times()
+        barrier(dist)
+        be.synchronize()
+        g0 = time.perf_counter()
+        for _ in range(args.steps):
+            be.undistort_grid(EUROC_K, EUROC_D)
+        be.synchronize()
+        g1 = time.perf_counter()
+        g_el = max_over_ranks(dist, g1 - g0)
+        gt = be.stage_times().get("k_undistort_grid", (0.0, 0))
+        be.set_profiling(False)
+        grid = {"metric": "keypoints undistorted + gridded per second (Frame::UndistortKeyPoints + "
+                          "AssignFeaturesToGrid)",
+                "value": round(sum_over_ranks(dist, feats_per_step * args.steps) / g_el / 1e6, 3),
+                "unit": "Mkeypoints/s", "ms_per_step": round(g_el / args.steps * 1e3, 4),
+                "kernel_ms_per_launch": round(gt[0] / gt[1], 4) if gt[1] else None,
+                "images_per_step": 2 * P}
+
     # C5's exchange step when several GPUs run: every rank contributes its camera
     # (pair 0's left eye), one RCCL all_gather moves the descriptors, each rank matches its own
     # against all others on its GPU.  Reported beside the headline, never part of it.
@@ -368,7 +404,8 @@ def main():
                "sample": "%d synthetic 640x480 stereo pairs, oracle extract (both eyes, 1 thread); "
                          "BF kNN2 %.4f Mmatches/s" % (cb["pairs"], cb["mmatch_s"]),
                "mmatches_s": round(cb["mmatch_s"], 5),
-               "stereo_mkeypoints_s": round(cb["stereo_mkp_s"], 5) if cb["stereo_mkp_s"] else None}
+               "stereo_mkeypoints_s": round(cb["stereo_mkp_s"], 5) if cb["stereo_mkp_s"] else None,
+               "undistort_grid_mkeypoints_s": round(cb["grid_mkp_s"], 5) if cb["grid_mkp_s"] else None}
 
     if rank == 0:
         out = {
@@ -396,6 +433,7 @@ def main():
             "stages": stage_rows,
             "cpu_baseline": cpu,
             "stereo_matches": stereo,
+            "undistort_grid": grid,
             "cross_camera": cross,
         }
         print(json.dumps(out))

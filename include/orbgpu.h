@@ -18,6 +18,8 @@
  *   - cv::BFMatcher(NORM_HAMMING).knnMatch(k=2)  cpp/src/Frame.cc:45,1227
  *   - mvImagePyramid (public member)      cpp/include/ORBextractor_old.h:80
  *   - Frame::ComputeStereoMatches         cpp/include/Frame.h:119, cpp/src/Frame.cc:827-997
+ *   - Frame::UndistortKeyPoints / ComputeImageBounds / AssignFeaturesToGrid
+ *                                         cpp/src/Frame.cc:405-436, 741-825
  */
 #ifndef ORBGPU_H_
 #define ORBGPU_H_
@@ -141,6 +143,22 @@ int orbgpu_download_matches(orbgpu_ctx* ctx, int pair, int32_t* idx1, int32_t* d
 int orbgpu_stereo_matches_batch(orbgpu_ctx* ctx, int n_pairs, float mbf, float mb, void* stream);
 int orbgpu_download_stereo(orbgpu_ctx* ctx, int pair, float* u_right, float* depth, int32_t* sad,
                            int cap, int* n);
+
+/* ---- Frame post-processing ----------------------------------------------------------------
+ * Frame::UndistortKeyPoints (cpp/src/Frame.cc:763-796; cv::undistortPoints with P = K, 5
+ * iterations in double) and Frame::AssignFeaturesToGrid + PosInGrid (:405-436, 741-751; 64 x 48
+ * cells, Frame.h:46-47) for the first n_images images of the last orbgpu_run_batch.
+ * K = {fx, fy, cx, cy}; dist = {k1, k2, p1, p2[, k3]} (ndist 0, 4 or 5; k1 == 0: no undistortion,
+ * as :765).  The grid spans Frame::ComputeImageBounds (:798-825) of the batch image size, which
+ * orbgpu_image_bounds returns ({mnMinX, mnMaxX, mnMinY, mnMaxY}, host computation).
+ * Per image: undistorted positions (mvKeysUn.pt), the cell of each keypoint (posX * 48 + posY,
+ * -1 outside the grid) and the cells as CSR lists (cell_start[64*48 + 1], cell_idx: keypoint
+ * indices ascending within a cell = mGrid[posX][posY]). */
+int orbgpu_image_bounds(int cols, int rows, const float K[4], const float* dist, int ndist, float bounds[4]);
+int orbgpu_undistort_grid_batch(orbgpu_ctx* ctx, int n_images, const float K[4], const float* dist,
+                                int ndist, void* stream);
+int orbgpu_download_grid(orbgpu_ctx* ctx, int image, float* xy_un, int32_t* cell, int32_t* cell_start,
+                         int32_t* cell_idx, int cap, int* n);
 
 /* ORBmatcher::DescriptorDistance on two 32-byte descriptors (host, no device work). */
 int orbgpu_descriptor_distance(const uint8_t* a, const uint8_t* b);

@@ -237,3 +237,22 @@ def stereo_matches(kps_l, desc_l, kps_r, desc_r, pyr_l, pyr_r, mbf, mb, scale_fa
                                 nlevels, _p(scale), _p(inv_scale), C.c_float(mbf), C.c_float(mb),
                                 _p(ur), _p(dep), _p(sad))
     return ur, dep, sad
+
+
+def undistort_grid(kps, K, dist, cols, rows):
+    """Frame::UndistortKeyPoints + ComputeImageBounds + AssignFeaturesToGrid (Frame.cc:405-436,
+    741-825) -> (xy_un [n,2] f32, bounds [4] f32, cell [n] i32, cell_start [3073], cell_idx)."""
+    kps = np.ascontiguousarray(kps, dtype=KP_DTYPE)
+    n = len(kps)
+    xy = np.ascontiguousarray(np.stack([kps["x"], kps["y"]], 1).astype(np.float32))
+    Kf = np.ascontiguousarray(K, dtype=np.float32)
+    d = np.ascontiguousarray(dist, dtype=np.float32)
+    out = np.zeros((n, 2), np.float32)
+    lib().oracle_undistort_points(_p(xy), n, _p(Kf), _p(d), len(d), _p(out))
+    bounds = np.zeros(4, np.float32)
+    lib().oracle_image_bounds(int(cols), int(rows), _p(Kf), _p(d), len(d), _p(bounds))
+    cell = np.zeros(n, np.int32)
+    cs = np.zeros(64 * 48 + 1, np.int32)
+    ci = np.zeros(max(n, 1), np.int32)
+    lib().oracle_assign_grid(_p(out), n, _p(bounds), _p(cell), _p(cs), _p(ci))
+    return out, bounds, cell, cs, ci[:cs[-1]]

@@ -1072,3 +1072,100 @@ void oracle_stereo_matches(const oracle_kp* kpsL, int nL, const uint8_t* descL, 
         }
     }
 }
+
+// ---------------------------------------------------------------------------------------------
+// Frame::UndistortKeyPoints (cpp/src/Frame.cc:763-796) -> cv::undistortPoints(src, dst, K, D,
+// noArray(), K) [EXT: OpenCV 4.2 cvUndistortPointsInternal, TermCriteria(COUNT, 5, 0.01)], in
+// double with the operation order of that function (identity tilt and rectification folded: the
+// products with 1 / 0 they add are exact), no FMA contraction.  dist = k1 k2 p1 p2 [k3].
+static void undistort_point(float px, float py, const float K[4], const double k[14], float* ox, float* oy) {
+    const double fx = K[0], fy = K[1], cx = K[2], cy = K[3];
+    const double ifx = 1. / fx, ify = 1. / fy;
+    double x = px, y = py;
+    const double u = x, v = y;
+    x = (x - cx) * ifx;
+    y = (y - cy) * ify;
+    const double x0 = x, y0 = y;
+    for (int j = 0; j < 5; j++) {
+        const double r2 = x * x + y * y;
+        const double icdist = (1 + ((k[7] * r2 + k[6]) * r2 + k[5]) * r2) / (1 + ((k[4] * r2 + k[1]) * r2 + k[0]) * r2);
+        if (icdist < 0) {  // undistortPoints.regression_14583
+            x = (u - cx) * ifx;
+            y = (v - cy) * ify;
+            break;
+        }
+        const double deltaX = 2 * k[2] * x * y + k[3] * (r2 + 2 * x * x) + k[8] * r2 + k[9] * r2 * r2;
+        const double deltaY = k[2] * (r2 + 2 * y * y) + 2 * k[3] * x * y + k[10] * r2 + k[11] * r2 * r2;
+        x = (x0 - deltaX) * icdist;
+        y = (y0 - deltaY) * icdist;
+    }
+    // P = K, R = I: xx = fx*x + 0*y + cx, ww = 1/(0*x + 0*y + 1) = 1
+    const double xx = fx * x + 0. * y + cx;
+    const double yy = 0. * x + fy * y + cy;
+    const double ww = 1. / (0. * x + 0. * y + 1.);
+    *ox = (float)(xx * ww);
+    *oy = (float)(yy * ww);
+}
+
+static void dist_table(const float* dist, int ndist, double k[14]) {
+    for (int i = 0; i < 14; ++i) k[i] = 0;
+    for (int i = 0; i < ndist && i < 5; ++i) k[i] = dist[i];
+}
+
+void oracle_undistort_points(const float* xy, int n, const float K[4], const float* dist, int ndist, float* out) {
+    double k[14];
+    dist_table(dist, ndist, k);
+    for (int i = 0; i < n; ++i) {
+        if (ndist == 0 || dist[0] == 0.0f) {  // Frame.cc:765-769: mvKeysUn = mvKeys
+            out[2 * i] = xy[2 * i];
+            out[2 * i + 1] = xy[2 * i + 1];
+        } else {
+            undistort_point(xy[2 * i], xy[2 * i + 1], K, k, &out[2 * i], &out[2 * i + 1]);
+        }
+    }
+}
+
+// Frame::ComputeImageBounds (Frame.cc:798-825): the undistorted image corners.
+void oracle_image_bounds(int cols, int rows, const float K[4], const float* dist, int ndist, float bounds[4]) {
+    if (ndist > 0 && dist[0] != 0.0f) {
+        const float c[8] = {0.0f, 0.0f, (float)cols, 0.0f, 0.0f, (float)rows, (float)cols, (float)rows};
+        float u[8];
+        oracle_undistort_points(c, 4, K, dist, ndist, u);
+        bounds[0] = std::min(u[0], u[4]);  // mnMinX
+        bounds[1] = std::max(u[2], u[6]);  // mnMaxX
+        bounds[2] = std::min(u[1], u[3]);  // mnMinY
+        bounds[3] = std::max(u[5], u[7]);  // mnMaxY
+    } else {
+        bounds[0] = 0.0f;
+        bounds[1] = (float)cols;
+        bounds[2] = 0.0f;
+        bounds[3] = (float)rows;
+    }
+}
+
+// Frame::AssignFeaturesToGrid + PosInGrid (Frame.cc:405-436, 741-751), FRAME_GRID_COLS x ROWS =
+// 64 x 48 (Frame.h:46-47), on undistorted points: cell[i] = posX * 48 + posY or -1;
+// cell_start[64*48 + 1] / cell_idx: the mGrid[posX][posY] vectors, indices ascending.
+void oracle_assign_grid(const float* xy_un, int n, const float bounds[4], int32_t* cell, int32_t* cell_start,
+                        int32_t* cell_idx) {
+    const int GC = 64, GR = 48;
+    const float wInv = static_cast<float>(GC) / (bounds[1] - bounds[0]);
+    const float hInv = static_cast<float>(GR) / (bounds[3] - bounds[2]);
+    std::vector<std::vector<int>> grid((size_t)GC * GR);
+    for (int i = 0; i < n; ++i) {
+        const int posX = (int)std::round((xy_un[2 * i] - bounds[0]) * wInv);
+        const int posY = (int)std::round((xy_un[2 * i + 1] - bounds[2]) * hInv);
+        if (posX < 0 || posX >= GC || posY < 0 || posY >= GR) {
+            cell[i] = -1;
+            continue;
+        }
+        cell[i] = posX * GR + posY;
+        grid[(size_t)posX * GR + posY].push_back(i);
+    }
+    int o = 0;
+    for (int c = 0; c < GC * GR; ++c) {
+        cell_start[c] = o;
+        for (int i : grid[c]) cell_idx[o++] = i;
+    }
+    cell_start[GC * GR] = o;
+}

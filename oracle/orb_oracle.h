@@ -97,4 +97,12 @@ void oracle_stereo_matches(const oracle_kp* kpsL, int nL, const uint8_t* descL, 
                            const float* scale, const float* inv_scale, float mbf, float mb,
                            float* uRight, float* depth, int32_t* sad);
 
+// Frame::UndistortKeyPoints (Frame.cc:763-796; cv::undistortPoints, 5 fixed-point iterations in
+// double, P = K), Frame::ComputeImageBounds (:798-825) and Frame::AssignFeaturesToGrid +
+// PosInGrid (:405-436, 741-751) on a 64 x 48 grid.  K = fx fy cx cy, dist = k1 k2 p1 p2 [k3].
+void oracle_undistort_points(const float* xy, int n, const float K[4], const float* dist, int ndist, float* out);
+void oracle_image_bounds(int cols, int rows, const float K[4], const float* dist, int ndist, float bounds[4]);
+void oracle_assign_grid(const float* xy_un, int n, const float bounds[4], int32_t* cell, int32_t* cell_start,
+                        int32_t* cell_idx);
+
 }  // extern "C"

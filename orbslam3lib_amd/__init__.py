@@ -35,6 +35,7 @@ EXPORTED = [
     "orbgpu_get_pyramid_level", "orbgpu_get_level_keypoints", "orbgpu_match_knn2",
     "orbgpu_match_stereo_batch", "orbgpu_download_matches", "orbgpu_descriptor_distance",
     "orbgpu_stereo_matches_batch", "orbgpu_download_stereo", "orbgpu_candidate_counts",
+    "orbgpu_image_bounds", "orbgpu_undistort_grid_batch", "orbgpu_download_grid",
     "orbgpu_set_profiling", "orbgpu_num_stages", "orbgpu_stage_name", "orbgpu_stage_times",
     "orbgpu_reset_stage_times", "orbgpu_last_error", "orbgpu_abi_version",
 ]
@@ -327,6 +328,25 @@ class BatchExtractor:
         _check(_lib.orbgpu_download_stereo(self.ctx.handle, pair, _p(ur), _p(dp), _p(sad), cap,
                                            C.byref(n)))
         return ur[:n.value], dp[:n.value], sad[:n.value]
+
+    def undistort_grid(self, K, dist=(), stream=None):
+        """Frame::UndistortKeyPoints + AssignFeaturesToGrid (Frame.cc:405-436, 741-825) for every
+        image of the last run(); K = (fx, fy, cx, cy), dist = (k1, k2, p1, p2[, k3])."""
+        Kf = np.ascontiguousarray(K, dtype=np.float32)
+        d = np.ascontiguousarray(dist, dtype=np.float32)
+        _check(_lib.orbgpu_undistort_grid_batch(self.ctx.handle, self.n, _p(Kf), _p(d) if len(d) else None,
+                                                len(d), C.c_void_p(stream) if stream else None))
+
+    def grid_result(self, image, cap=65536):
+        """(xy_un [n,2], cell [n], cell_start [3073], cell_idx) of image `image`."""
+        xy = np.zeros((cap, 2), np.float32)
+        cell = np.zeros(cap, np.int32)
+        cs = np.zeros(64 * 48 + 1, np.int32)
+        ci = np.zeros(cap, np.int32)
+        n = C.c_int(0)
+        _check(_lib.orbgpu_download_grid(self.ctx.handle, image, _p(xy), _p(cell), _p(cs), _p(ci), cap,
+                                         C.byref(n)))
+        return xy[:n.value], cell[:n.value], cs, ci[:cs[-1]]
 
     def set_profiling(self, on=True, stages=None, serialize=False):
         """on: bracket every stage's launches with HIP events; stages: only these stage names;

@@ -111,6 +111,24 @@ struct StereoArgs {
     int pair0;                       // first pair of this launch
 };
 
+// Frame::UndistortKeyPoints + AssignFeaturesToGrid over a batch's keypoints (orb_frame.hip).
+constexpr int kGridCols = 64, kGridRows = 48;  // FRAME_GRID_COLS / ROWS (Frame.h:46-47)
+struct GridArgs {
+    const void* kps;       // out_kps: orbgpu_keypoint [img][out_cap]
+    const int32_t* out_n;  // [img]
+    int out_cap;
+    int undistort;         // mDistCoef(0) != 0 (Frame.cc:765)
+    float K[4];            // fx fy cx cy
+    double k[14];          // OpenCV distortion vector (k1 k2 p1 p2 k3, rest 0)
+    float bounds[4];       // mnMinX mnMaxX mnMinY mnMaxY
+    float grid_inv[2];     // mfGridElementWidthInv / HeightInv
+    float* xy_un;          // [img][out_cap][2] mvKeysUn positions
+    int32_t* cell;         // [img][out_cap] posX * 48 + posY or -1
+    int32_t* cell_start;   // [img][64 * 48 + 1]
+    int32_t* cell_idx;     // [img][out_cap]
+    int img0;
+};
+
 // Octree workspace layout for one (image, level) with n_cap keys and node capacity C.  The node
 // state lives in LDS when C <= kOctLdsNodes, otherwise in the `nodemem` part of this block.
 constexpr int kOctLdsNodes = 1024;
@@ -151,6 +169,9 @@ hipError_t launch_finalize(const BatchArgs& a, hipStream_t s);
 hipError_t launch_knn2_pairs(const MatchArgs& m, int npairs, int qblocks, void* scratch, hipStream_t s);
 size_t knn2_scratch_bytes(int npairs, int out_cap);
 hipError_t launch_stereo(const StereoArgs& s, int npairs, hipStream_t st);  // orb_stereo.hip
+hipError_t launch_undistort_grid(const GridArgs& g, int nimages, hipStream_t st);  // orb_frame.hip
+void grid_dist_table(const float* dist, int ndist, double k[14]);
+void image_bounds_host(int cols, int rows, const float K[4], const float* dist, int ndist, float bounds[4]);
 hipError_t launch_knn2_plain(const uint8_t* q, int nq, const uint8_t* t, int nt, int32_t* i1,
                              int32_t* d1, int32_t* i2, int32_t* d2, hipStream_t s);
 

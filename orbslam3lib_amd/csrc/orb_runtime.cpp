@@ -40,11 +40,11 @@ int fail(int code, const std::string& msg) {
     } while (0)
 
 enum Stage { ST_RESIZE, ST_BLUR, ST_FAST48, ST_FAST, ST_FAST_TOP, ST_OCTREE, ST_ORIENT, ST_FINAL, ST_KNN,
-             ST_PYRAMID, ST_STEREO, ST_COUNT };
+             ST_PYRAMID, ST_STEREO, ST_GRID, ST_COUNT };
 // names as rocprofv3 shows the kernels (templates with their argument)
 const char* kStageNames[ST_COUNT] = {"k_resize",         "k_blur",   "k_fast_cells<48>", "k_fast_cells<64>",
                                      "k_fast_cells<80>", "k_octree", "k_orient_desc",    "k_finalize",
-                                     "k_knn2",           "k_pyramid", "k_stereo"};
+                                     "k_knn2",           "k_pyramid", "k_stereo",         "k_undistort_grid"};
 
 struct DevBuf {
     void* p = nullptr;
@@ -102,7 +102,8 @@ struct orbgpu_ctx {
     // device buffers
     DevBuf input, pyr, blur, rtab, cellkeys, cellcnt, octws, lvlkey, lvlangle, lvldesc, lvlcnt,
         status, outkps, outdesc, outn, outmono, laps, midx1, mdist1, midx2, mdist2, mnq, scratch,
-        octdbg, knnpart, strow, stidx, stur, stdepth, stsad;
+        octdbg, knnpart, strow, stidx, stur, stdepth, stsad, gxy, gcell, gstart, gidx;
+    int grid_images = 0;   // images of the last orbgpu_undistort_grid_batch
     int stereo_pairs = 0;  // pairs of the last orbgpu_stereo_matches_batch
     int input_images = 0;   // images currently sized for in `input`
     hipEvent_t fork = nullptr;
@@ -579,7 +580,8 @@ int orbgpu_destroy(orbgpu_ctx* c) {
                       &c->octws,   &c->lvlkey,  &c->lvlangle, &c->lvldesc, &c->lvlcnt, &c->status,
                       &c->outkps,  &c->outdesc, &c->outn,   &c->outmono, &c->laps,     &c->midx1,
                       &c->mdist1,  &c->midx2,   &c->mdist2, &c->mnq,     &c->scratch, &c->octdbg,
-                      &c->knnpart, &c->strow,  &c->stidx, &c->stur,    &c->stdepth,  &c->stsad};
+                      &c->knnpart, &c->strow,  &c->stidx, &c->stur,    &c->stdepth,  &c->stsad,
+                      &c->gxy,     &c->gcell,  &c->gstart, &c->gidx};
     for (DevBuf* b : bufs) b->release();
     for (size_t k = 1; k < c->sub.size(); ++k) hipStreamDestroy(c->sub[k]);
     if (c->fork) hipEventDestroy(c->fork);
@@ -1136,6 +1138,75 @@ int orbgpu_download_stereo(orbgpu_ctx* c, int pair, float* u_right, float* depth
         if (depth) HIP_TRY(hipMemcpy(depth, c->stdepth.as<float>() + o, 4 * (size_t)nl, hipMemcpyDeviceToHost));
         if (sad) HIP_TRY(hipMemcpy(sad, c->stsad.as<int32_t>() + o, 4 * (size_t)nl, hipMemcpyDeviceToHost));
     }
+    return ORBGPU_OK;
+}
+
+int orbgpu_image_bounds(int cols, int rows, const float K[4], const float* dist, int ndist, float bounds[4]) {
+    if (!K || !bounds || (ndist > 0 && !dist) || ndist < 0) return fail(ORBGPU_ERR_INVALID, "null argument");
+    image_bounds_host(cols, rows, K, dist, ndist, bounds);
+    return ORBGPU_OK;
+}
+
+int orbgpu_undistort_grid_batch(orbgpu_ctx* c, int n, const float K[4], const float* dist, int ndist,
+                                void* stream) {
+    if (!c || !K || (ndist > 0 && !dist) || ndist < 0) return fail(ORBGPU_ERR_INVALID, "null argument");
+    if (n < 1 || n > c->last_images) return fail(ORBGPU_ERR_INVALID, "bad image count");
+    if (!(K[0] != 0.f) || !(K[1] != 0.f)) return fail(ORBGPU_ERR_INVALID, "fx and fy must be nonzero");
+    HIP_TRY(hipSetDevice(c->device));
+    const size_t ni = (size_t)n, cap = (size_t)c->out_cap;
+    if (c->gxy.ensure(ni * cap * 8 + 256) || c->gcell.ensure(ni * cap * 4 + 256) ||
+        c->gstart.ensure(ni * (kGridCols * kGridRows + 1) * 4 + 256) || c->gidx.ensure(ni * cap * 4 + 256))
+        return fail(ORBGPU_ERR_HIP, "hipMalloc failed (grid buffers)");
+    GridArgs g{};
+    g.kps = c->outkps.p;
+    g.out_n = c->outn.as<int32_t>();
+    g.out_cap = c->out_cap;
+    g.undistort = ndist > 0 && dist[0] != 0.0f;
+    for (int i = 0; i < 4; ++i) g.K[i] = K[i];
+    grid_dist_table(dist, ndist, g.k);
+    image_bounds_host(c->A.lv[0].w, c->A.lv[0].h, K, dist, ndist, g.bounds);
+    g.grid_inv[0] = static_cast<float>(kGridCols) / (g.bounds[1] - g.bounds[0]);  // Frame.cc:107-108
+    g.grid_inv[1] = static_cast<float>(kGridRows) / (g.bounds[3] - g.bounds[2]);
+    g.xy_un = c->gxy.as<float>();
+    g.cell = c->gcell.as<int32_t>();
+    g.cell_start = c->gstart.as<int32_t>();
+    g.cell_idx = c->gidx.as<int32_t>();
+    bool chunked = !stream && !c->last_chunks.empty();
+    if (chunked) {
+        for (const auto& ch : c->last_chunks) {
+            const int nn = std::min(ch.n, n - ch.img0);
+            if (nn <= 0) continue;
+            GridArgs gg = g;
+            gg.img0 = ch.img0;
+            int r = timed(c, ST_GRID, ch.st, [&] { return launch_undistort_grid(gg, nn, ch.st); });
+            if (r) return r;
+        }
+    } else {
+        hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+        g.img0 = 0;
+        int r = timed(c, ST_GRID, s, [&] { return launch_undistort_grid(g, n, s); });
+        if (r) return r;
+    }
+    c->grid_images = n;
+    return ORBGPU_OK;
+}
+
+int orbgpu_download_grid(orbgpu_ctx* c, int image, float* xy_un, int32_t* cell, int32_t* cell_start,
+                         int32_t* cell_idx, int cap, int* n) {
+    if (!c || image < 0 || image >= c->grid_images) return fail(ORBGPU_ERR_INVALID, "bad image");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipDeviceSynchronize());
+    int32_t nk = 0;
+    HIP_TRY(hipMemcpy(&nk, c->outn.as<int32_t>() + image, 4, hipMemcpyDeviceToHost));
+    nk = std::max(nk, 0);
+    if (n) *n = nk;
+    if (nk > cap) return fail(ORBGPU_ERR_CAPACITY, "caller capacity too small");
+    const size_t o = (size_t)image * c->out_cap;
+    const size_t G = kGridCols * kGridRows + 1;
+    if (xy_un && nk) HIP_TRY(hipMemcpy(xy_un, c->gxy.as<float>() + 2 * o, 8 * (size_t)nk, hipMemcpyDeviceToHost));
+    if (cell && nk) HIP_TRY(hipMemcpy(cell, c->gcell.as<int32_t>() + o, 4 * (size_t)nk, hipMemcpyDeviceToHost));
+    if (cell_start) HIP_TRY(hipMemcpy(cell_start, c->gstart.as<int32_t>() + (size_t)image * G, 4 * G, hipMemcpyDeviceToHost));
+    if (cell_idx && nk) HIP_TRY(hipMemcpy(cell_idx, c->gidx.as<int32_t>() + o, 4 * (size_t)nk, hipMemcpyDeviceToHost));
     return ORBGPU_OK;
 }
 
