@@ -10,8 +10,18 @@ HDRS := $(wildcard $(CSRC)/*.h) include/orbgpu.h
 
 all: $(LIB) oracle facade_test
 
-$(LIB): $(CSRC)/orb_kernels.hip $(CSRC)/orb_stereo.hip $(CSRC)/orb_frame.hip $(CSRC)/orb_runtime.cpp $(HDRS)
-	$(HIPCC) $(HIPFLAGS) $(DEVFLAGS) -shared -o $@ $(CSRC)/orb_kernels.hip $(CSRC)/orb_stereo.hip $(CSRC)/orb_frame.hip $(CSRC)/orb_runtime.cpp
+# one object per translation unit (each launcher sits beside its kernels: no relocatable device
+# code needed), so `make -j` compiles them in parallel
+LIBSRC := orb_kernels.hip orb_stereo.hip orb_frame.hip orb_io.hip orb_runtime.cpp
+OBJDIR := $(CSRC)/build
+LIBOBJ := $(patsubst %,$(OBJDIR)/%.o,$(LIBSRC))
+
+$(OBJDIR)/%.o: $(CSRC)/% $(HDRS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) $(DEVFLAGS) -c -o $@ $<
+
+$(LIB): $(LIBOBJ)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(LIBOBJ)
 
 oracle:
 	$(MAKE) -s -C oracle
@@ -25,7 +35,7 @@ $(FACADE_TEST): tests/cpp/facade_test.cpp orbslam3lib_amd/facade/ORBextractor.cc
 		-L orbslam3lib_amd -lorbgpu -Wl,-rpath,'$$ORIGIN/../../../orbslam3lib_amd' -Wl,-rpath-link,/opt/rocm/lib -ldl
 
 clean:
-	rm -f $(LIB)
+	rm -f $(LIB) $(LIBOBJ)
 	$(MAKE) -s -C oracle clean
 
 .PHONY: all oracle clean facade_test

@@ -13,6 +13,7 @@ ranks bracket the timed region.  Prints ONE JSON line on rank 0.
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -85,9 +86,12 @@ def dist_setup():
     if world > 1:
         import torch
         import torch.distributed as td
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        # ORBGPU_BENCH_BACKEND=gloo + ORBGPU_BENCH_DEVICE=0 rehearse several ranks on one GPU
+        backend = os.environ.get("ORBGPU_BENCH_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
         if backend == "nccl":
             torch.cuda.set_device(local)
+        else:
+            local = int(os.environ.get("ORBGPU_BENCH_DEVICE", local))
         td.init_process_group(backend=backend)
         dist = td
     return world, rank, local, dist
@@ -179,6 +183,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-stereo", action="store_true", help="skip the ComputeStereoMatches leg")
     ap.add_argument("--no-grid", action="store_true", help="skip the UndistortKeyPoints + grid leg")
+    ap.add_argument("--no-wire", action="store_true", help="skip the side-by-side ingest / SoA egress leg")
     ap.add_argument("--no-profile", action="store_true",
                     help="do not bracket launches with HIP events in the timed region")
     args = ap.parse_args()
@@ -376,6 +381,45 @@ def main():
                 "kernel_ms_per_launch": round(gt[0] / gt[1], 4) if gt[1] else None,
                 "images_per_step": 2 * P}
 
+    # Wire formats: the P side-by-side frames of a step split from the device
+    # staging buffer into the batch layout, and the step's results packed to the IDL SoA layout.
+    # Timed on their own (HBM-bound copies; 4 B/px moved by the split, 2 x 28 B read + 16 B
+    # written per keypoint and 3 x (4 + 2) B per match by the pack).
+    wire = None
+    if not args.no_wire:
+        lib = og.load_library()
+        dptr = lib.orbgpu_device_sbs_input(be.ctx.handle)
+        if dptr and be.ctx.max_images >= 2:
+            # fill the staging buffer from the resident batch (device to device, untimed)
+            hip = ctypes.CDLL("libamdhip64.so.7")  # the runtime liborbgpu.so loaded
+            vp, sz = ctypes.c_void_p, ctypes.c_size_t
+            hip.hipMemcpy2D.argtypes = [vp, sz, vp, sz, sz, sz, ctypes.c_int]
+            src = lib.orbgpu_device_input(be.ctx.handle)
+            for p in range(P):
+                for e in range(2):
+                    hip.hipMemcpy2D(dptr + p * H * 2 * W + e * W, 2 * W, src + (2 * p + e) * H * W, W, W, H, 3)
+            be.ingest_sbs(dptr, P, 2 * W)
+            be.run()
+            be.match_stereo(stereo_rows_only=False)
+            be.pack_soa()
+            be.synchronize()
+            be.set_profiling(True, stages=["k_sbs_split", "k_pack_soa"])
+            be.reset_stage_times()
+            for _ in range(args.steps):
+                be.ingest_sbs(dptr, P, 2 * W)
+                be.pack_soa()
+            be.synchronize()
+            wt = be.stage_times()
+            be.set_profiling(False)
+            sp, pk = wt.get("k_sbs_split", (0.0, 0)), wt.get("k_pack_soa", (0.0, 0))
+            split_b = 4.0 * H * W * P
+            pack_b = 72.0 * feats_per_step + 18.0 * nq_per_step
+            wire = {"sbs_split_us": round(sp[0] / sp[1] * 1e3, 2) if sp[1] else None,
+                    "sbs_split_GBps": round(split_b / (sp[0] / sp[1] * 1e-3) / 1e9, 1) if sp[1] else None,
+                    "pack_soa_us": round(pk[0] / pk[1] * 1e3, 2) if pk[1] else None,
+                    "pack_soa_GBps": round(pack_b / (pk[0] / pk[1] * 1e-3) / 1e9, 1) if pk[1] else None,
+                    "frames_per_step": P, "hbm_peak_GBps": HBM_PEAK_GBS}
+
     # C5's exchange step when several GPUs run: every rank contributes its camera
     # (pair 0's left eye), one RCCL all_gather moves the descriptors, each rank matches its own
     # against all others on its GPU.  Reported beside the headline, never part of it.
@@ -393,7 +437,7 @@ def main():
             cel = max_over_ranks(dist, c1 - c0)
             nqm = sum_over_ranks(dist, len(dl0) * len(res))
             cross = {"cameras": world, "queries_per_camera": len(dl0), "ms": round(cel * 1e3, 3),
-                     "mmatches_s": round(nqm / cel / 1e6, 3), "exchange": "all_gather (RCCL)"}
+                     "mmatches_s": round(nqm / cel / 1e6, 3), "exchange": "all_gather (%s)" % ("RCCL" if dist.get_backend() == "nccl" else dist.get_backend())}
         except Exception as e:  # reported, never fatal to the headline line
             cross = {"error": repr(e)[:200]}
 
@@ -434,6 +478,7 @@ def main():
             "cpu_baseline": cpu,
             "stereo_matches": stereo,
             "undistort_grid": grid,
+            "wire": wire,
             "cross_camera": cross,
         }
         print(json.dumps(out))

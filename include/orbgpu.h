@@ -144,6 +144,48 @@ int orbgpu_stereo_matches_batch(orbgpu_ctx* ctx, int n_pairs, float mbf, float m
 int orbgpu_download_stereo(orbgpu_ctx* ctx, int pair, float* u_right, float* depth, int32_t* sad,
                            int cap, int* n);
 
+/* ---- wire formats ---------------------------------------------------------------------------
+ * Ingest of side-by-side stereo Y8 frames (the headset's 2W x H AHardwareBuffer,
+ * ORBextractor.cc:131-143; DSP split orbslam_dsp.cpp:643-648): frame f's left half (columns
+ * [0, W)) becomes batch image 2f, its right half (columns [W, 2W)) image 2f + 1.  Frames are
+ * height rows of `stride` bytes (stride >= 2W), height * stride bytes apart.
+ *   orbgpu_upload_sbs: host frames (PCIe into a staging buffer, then the split kernel);
+ *   orbgpu_ingest_sbs: frames already in device memory (e.g. the staging buffer returned by
+ *   orbgpu_device_sbs_input, sized for max_images / 2 frames of stride 2 * max_width), on
+ *   `stream` -- the zero-copy path. */
+uint8_t* orbgpu_device_sbs_input(orbgpu_ctx* ctx);
+int orbgpu_upload_sbs(orbgpu_ctx* ctx, const uint8_t* frames, int n_frames, int width, int height,
+                      int stride);
+int orbgpu_ingest_sbs(orbgpu_ctx* ctx, const uint8_t* device_frames, int n_frames, int width,
+                      int height, int stride, void* stream);
+
+/* Egress in the FastRPC result layout (cpp/inc/orbslam3.idl:15-19): per image int32 X, Y (the
+ * level-0 coordinates truncated to int), angle ((cos8 & 0xFF) | (sin8 & 0xFF) << 8 with
+ * cos8/sin8 = rint(64 cos / 64 sin) of the keypoint angle: what LynxHardwareAccelerator.cpp:
+ * 174-178 decodes), level (octave) and the N x 32 B descriptors; per stereo pair the kNN result
+ * as int16 indices / distances1 / distances2 (distances clamped to 32767; absent = -1 / 32767).
+ * orbgpu_pack_soa converts the first n_images images and n_pairs pairs of the last batch on the
+ * device (device-resident SoA), the download functions copy one image / pair out. */
+int orbgpu_pack_soa(orbgpu_ctx* ctx, int n_images, int n_pairs, void* stream);
+int orbgpu_download_soa(orbgpu_ctx* ctx, int image, int32_t* x, int32_t* y, int32_t* angle,
+                        int32_t* level, uint8_t* orb, int cap, int* count, int* mono);
+int orbgpu_download_matches16(orbgpu_ctx* ctx, int pair, int16_t* indices, int16_t* dist1,
+                              int16_t* dist2, int cap, int* n_queries);
+
+/* orbslam3_extractFeatures (orbslam3.idl:15-19, impl orbslam_dsp.cpp:1003-1087) in one call: one
+ * side-by-side frame in, both eyes extracted (lapping areas {l0, l1} / {r0, r1}), the stereo
+ * rows ([mono, n) of each eye, Frame.cc:1142-1148) kNN2-matched left -> right, everything out in
+ * the SoA layout above.  `threshold` is accepted and ignored, as the DSP does; the context's
+ * FAST thresholds apply.  *count_* is the exact keypoint count (the DSP's host wrapper subtracts
+ * one from its count, LynxHardwareAccelerator.cpp:158-159; a caller of this ABI must not). */
+int orbgpu_extract_features(orbgpu_ctx* ctx, const uint8_t* image, int image_len, int width,
+                            int height, int stride, int threshold, int lap_l0, int lap_l1,
+                            int lap_r0, int lap_r1, int* count_l, int32_t* x_l, int32_t* y_l,
+                            int32_t* angle_l, int32_t* level_l, uint8_t* orb_l, int* count_r,
+                            int32_t* x_r, int32_t* y_r, int32_t* angle_r, int32_t* level_r,
+                            uint8_t* orb_r, int kp_cap, int* mono_l, int* mono_r, int16_t* indices,
+                            int16_t* dist1, int16_t* dist2, int match_cap);
+
 /* ---- Frame post-processing ----------------------------------------------------------------
  * Frame::UndistortKeyPoints (cpp/src/Frame.cc:763-796; cv::undistortPoints with P = K, 5
  * iterations in double) and Frame::AssignFeaturesToGrid + PosInGrid (:405-436, 741-751; 64 x 48

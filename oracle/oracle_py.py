@@ -256,3 +256,20 @@ def undistort_grid(kps, K, dist, cols, rows):
     ci = np.zeros(max(n, 1), np.int32)
     lib().oracle_assign_grid(_p(out), n, _p(bounds), _p(cell), _p(cs), _p(ci))
     return out, bounds, cell, cs, ci[:cs[-1]]
+
+
+def pack_soa(kps):
+    """orbslam3.idl SoA of keypoints: dict of int32 x, y, angle (cos8 | sin8 << 8), level."""
+    kps = np.ascontiguousarray(kps, dtype=KP_DTYPE)
+    n = len(kps)
+    out = {k: np.zeros(max(n, 1), np.int32) for k in ("x", "y", "angle", "level")}
+    lib().oracle_pack_soa(_p(kps), n, _p(out["x"]), _p(out["y"]), _p(out["angle"]), _p(out["level"]))
+    return {k: v[:n] for k, v in out.items()}
+
+
+def decode_angle(enc):
+    """LynxHardwareAccelerator.cpp:174-178: int8 cos / sin -> degrees."""
+    enc = np.asarray(enc, np.int32)
+    c = (enc & 0xFF).astype(np.uint8).view(np.int8).astype(np.float32)
+    s = ((enc >> 8) & 0xFF).astype(np.uint8).view(np.int8).astype(np.float32)
+    return np.degrees(np.arctan2(s / 64.0, c / 64.0))

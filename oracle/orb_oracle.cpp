@@ -1169,3 +1169,16 @@ void oracle_assign_grid(const float* xy_un, int n, const float bounds[4], int32_
     }
     cell_start[GC * GR] = o;
 }
+
+// IDL SoA egress (see the header): the host-side restatement of what the device packs.
+void oracle_pack_soa(const oracle_kp* kps, int n, int32_t* x, int32_t* y, int32_t* angle, int32_t* level) {
+    for (int i = 0; i < n; ++i) {
+        const float rad = (float)kps[i].angle * factorPI;
+        const float a = (float)std::cos((double)rad), b = (float)std::sin((double)rad);
+        const int c8 = (int)std::nearbyint(64.0f * a), s8 = (int)std::nearbyint(64.0f * b);
+        x[i] = (int32_t)kps[i].x;
+        y[i] = (int32_t)kps[i].y;
+        angle[i] = (c8 & 0xFF) | ((s8 & 0xFF) << 8);
+        level[i] = kps[i].octave;
+    }
+}

@@ -105,4 +105,10 @@ void oracle_image_bounds(int cols, int rows, const float K[4], const float* dist
 void oracle_assign_grid(const float* xy_un, int n, const float bounds[4], int32_t* cell, int32_t* cell_start,
                         int32_t* cell_idx);
 
+// The orbslam3.idl:15-19 result layout of n keypoints: X/Y = (int) of the coordinates (the DSP's
+// truncation, orbslam_dsp.cpp:447-453), angle = (cos8 & 0xFF) | (sin8 & 0xFF) << 8 with
+// cos8/sin8 = rint(64 * the descriptor rotation's (float)cos/sin((double)(angle * factorPI)))
+// (decoded by LynxHardwareAccelerator.cpp:174-178), level = octave.
+void oracle_pack_soa(const oracle_kp* kps, int n, int32_t* x, int32_t* y, int32_t* angle, int32_t* level);
+
 }  // extern "C"

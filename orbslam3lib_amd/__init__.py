@@ -36,6 +36,8 @@ EXPORTED = [
     "orbgpu_match_stereo_batch", "orbgpu_download_matches", "orbgpu_descriptor_distance",
     "orbgpu_stereo_matches_batch", "orbgpu_download_stereo", "orbgpu_candidate_counts",
     "orbgpu_image_bounds", "orbgpu_undistort_grid_batch", "orbgpu_download_grid",
+    "orbgpu_device_sbs_input", "orbgpu_upload_sbs", "orbgpu_ingest_sbs", "orbgpu_pack_soa",
+    "orbgpu_download_soa", "orbgpu_download_matches16", "orbgpu_extract_features",
     "orbgpu_set_profiling", "orbgpu_num_stages", "orbgpu_stage_name", "orbgpu_stage_times",
     "orbgpu_reset_stage_times", "orbgpu_last_error", "orbgpu_abi_version",
 ]
@@ -67,6 +69,8 @@ def load_library(path: str = LIB_PATH):
     lib.orbgpu_stage_name.restype = C.c_char_p
     lib.orbgpu_device_input.restype = C.c_void_p
     lib.orbgpu_device_input.argtypes = [C.c_void_p]
+    lib.orbgpu_device_sbs_input.restype = C.c_void_p
+    lib.orbgpu_device_sbs_input.argtypes = [C.c_void_p]
     for name in ("orbgpu_destroy", "orbgpu_synchronize", "orbgpu_set_profiling",
                  "orbgpu_reset_stage_times"):
         getattr(lib, name).argtypes = [C.c_void_p] + ([C.c_int] if name == "orbgpu_set_profiling" else [])
@@ -328,6 +332,46 @@ class BatchExtractor:
         _check(_lib.orbgpu_download_stereo(self.ctx.handle, pair, _p(ur), _p(dp), _p(sad), cap,
                                            C.byref(n)))
         return ur[:n.value], dp[:n.value], sad[:n.value]
+
+    def upload_sbs(self, frames, width=None):
+        """Side-by-side stereo Y8 frames [n, H, S] (row stride S >= 2W; W = S // 2 by default) ->
+        images 2f (left half) and 2f + 1 (right half) of the batch (ORBextractor.cc:131-143)."""
+        frames = np.ascontiguousarray(frames, dtype=np.uint8)
+        n, h, stride = frames.shape
+        w = stride // 2 if width is None else int(width)
+        _check(_lib.orbgpu_upload_sbs(self.ctx.handle, _p(frames), n, w, h, stride))
+        self.n, self.height, self.width = 2 * n, h, w
+
+    def ingest_sbs(self, device_ptr, n_frames, stride, stream=None):
+        """Split side-by-side frames already in device memory (zero-copy ingest)."""
+        _check(_lib.orbgpu_ingest_sbs(self.ctx.handle, C.c_void_p(device_ptr), int(n_frames), self.width,
+                                      self.height, int(stride), C.c_void_p(stream) if stream else None))
+        self.n = 2 * int(n_frames)
+
+    def pack_soa(self, n_pairs=None, stream=None):
+        """The orbslam3.idl SoA layout for every image (and n_pairs stereo pairs' matches)."""
+        npairs = self.n // 2 if n_pairs is None else int(n_pairs)
+        _check(_lib.orbgpu_pack_soa(self.ctx.handle, self.n, npairs, C.c_void_p(stream) if stream else None))
+
+    def soa_result(self, image, cap=65536):
+        """dict(x, y, angle, level: int32 [n], orb: uint8 [n, 32], mono: int)."""
+        a = {k: np.zeros(cap, np.int32) for k in ("x", "y", "angle", "level")}
+        orb = np.zeros((cap, 32), np.uint8)
+        n, m = C.c_int(0), C.c_int(0)
+        _check(_lib.orbgpu_download_soa(self.ctx.handle, image, _p(a["x"]), _p(a["y"]), _p(a["angle"]),
+                                        _p(a["level"]), _p(orb), cap, C.byref(n), C.byref(m)))
+        out = {k: v[:n.value] for k, v in a.items()}
+        out["orb"] = orb[:n.value]
+        out["mono"] = m.value
+        return out
+
+    def matches16(self, pair, cap=65536):
+        """(indices, distances1, distances2) int16 of stereo pair `pair` after pack_soa."""
+        r = [np.zeros(cap, np.int16) for _ in range(3)]
+        n = C.c_int(0)
+        _check(_lib.orbgpu_download_matches16(self.ctx.handle, pair, _p(r[0]), _p(r[1]), _p(r[2]), cap,
+                                              C.byref(n)))
+        return tuple(a[:n.value] for a in r)
 
     def undistort_grid(self, K, dist=(), stream=None):
         """Frame::UndistortKeyPoints + AssignFeaturesToGrid (Frame.cc:405-436, 741-825) for every

@@ -172,6 +172,24 @@ hipError_t launch_stereo(const StereoArgs& s, int npairs, hipStream_t st);  // o
 hipError_t launch_undistort_grid(const GridArgs& g, int nimages, hipStream_t st);  // orb_frame.hip
 void grid_dist_table(const float* dist, int ndist, double k[14]);
 void image_bounds_host(int cols, int rows, const float K[4], const float* dist, int ndist, float bounds[4]);
+
+// Wire formats (orb_io.hip): side-by-side Y8 ingest and the IDL SoA egress.
+struct SbsArgs {
+    const uint8_t* src;     // nframes frames of h rows x stride bytes, frame_bytes apart
+    long long frame_bytes;
+    int stride, w, h, nframes;  // w = one eye's width (the frame is 2w wide)
+    uint8_t* dst;           // batch input: image 2f = left, 2f + 1 = right, [h][w] each
+};
+struct SoaArgs {
+    const void* kps;        // out_kps [img][out_cap] (28 B)
+    const int32_t* out_n;
+    int out_cap, nimages, img0;
+    int32_t *x, *y, *angle, *level;  // [img][out_cap]
+    const int32_t *nq, *idx1, *dist1, *dist2;  // kNN results [pair][out_cap]
+    int16_t *idx16, *d1_16, *d2_16;
+};
+hipError_t launch_sbs_split(const SbsArgs& a, hipStream_t st);
+hipError_t launch_pack_soa(const SoaArgs& a, int npairs, hipStream_t st);
 hipError_t launch_knn2_plain(const uint8_t* q, int nq, const uint8_t* t, int nt, int32_t* i1,
                              int32_t* d1, int32_t* i2, int32_t* d2, hipStream_t s);
 

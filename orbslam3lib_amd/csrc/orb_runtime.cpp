@@ -40,11 +40,12 @@ int fail(int code, const std::string& msg) {
     } while (0)
 
 enum Stage { ST_RESIZE, ST_BLUR, ST_FAST48, ST_FAST, ST_FAST_TOP, ST_OCTREE, ST_ORIENT, ST_FINAL, ST_KNN,
-             ST_PYRAMID, ST_STEREO, ST_GRID, ST_COUNT };
+             ST_PYRAMID, ST_STEREO, ST_GRID, ST_SBS, ST_SOA, ST_COUNT };
 // names as rocprofv3 shows the kernels (templates with their argument)
 const char* kStageNames[ST_COUNT] = {"k_resize",         "k_blur",   "k_fast_cells<48>", "k_fast_cells<64>",
                                      "k_fast_cells<80>", "k_octree", "k_orient_desc",    "k_finalize",
-                                     "k_knn2",           "k_pyramid", "k_stereo",         "k_undistort_grid"};
+                                     "k_knn2",           "k_pyramid", "k_stereo",         "k_undistort_grid",
+                                     "k_sbs_split",      "k_pack_soa"};
 
 struct DevBuf {
     void* p = nullptr;
@@ -102,7 +103,8 @@ struct orbgpu_ctx {
     // device buffers
     DevBuf input, pyr, blur, rtab, cellkeys, cellcnt, octws, lvlkey, lvlangle, lvldesc, lvlcnt,
         status, outkps, outdesc, outn, outmono, laps, midx1, mdist1, midx2, mdist2, mnq, scratch,
-        octdbg, knnpart, strow, stidx, stur, stdepth, stsad, gxy, gcell, gstart, gidx;
+        octdbg, knnpart, strow, stidx, stur, stdepth, stsad, gxy, gcell, gstart, gidx, sbs, soa, m16;
+    int soa_images = 0, soa_pairs = 0;  // coverage of the last orbgpu_pack_soa
     int grid_images = 0;   // images of the last orbgpu_undistort_grid_batch
     int stereo_pairs = 0;  // pairs of the last orbgpu_stereo_matches_batch
     int input_images = 0;   // images currently sized for in `input`
@@ -581,7 +583,8 @@ int orbgpu_destroy(orbgpu_ctx* c) {
                       &c->outkps,  &c->outdesc, &c->outn,   &c->outmono, &c->laps,     &c->midx1,
                       &c->mdist1,  &c->midx2,   &c->mdist2, &c->mnq,     &c->scratch, &c->octdbg,
                       &c->knnpart, &c->strow,  &c->stidx, &c->stur,    &c->stdepth,  &c->stsad,
-                      &c->gxy,     &c->gcell,  &c->gstart, &c->gidx};
+                      &c->gxy,     &c->gcell,  &c->gstart, &c->gidx,    &c->sbs,      &c->soa,
+                      &c->m16};
     for (DevBuf* b : bufs) b->release();
     for (size_t k = 1; k < c->sub.size(); ++k) hipStreamDestroy(c->sub[k]);
     if (c->fork) hipEventDestroy(c->fork);
@@ -1139,6 +1142,152 @@ int orbgpu_download_stereo(orbgpu_ctx* c, int pair, float* u_right, float* depth
         if (sad) HIP_TRY(hipMemcpy(sad, c->stsad.as<int32_t>() + o, 4 * (size_t)nl, hipMemcpyDeviceToHost));
     }
     return ORBGPU_OK;
+}
+
+// ---- wire formats (orb_io.hip) ---------------------------------------------------------------
+uint8_t* orbgpu_device_sbs_input(orbgpu_ctx* c) {
+    if (!c) return nullptr;
+    if (hipSetDevice(c->device) != hipSuccess) return nullptr;
+    const size_t frames = (size_t)(c->max_images / 2 > 0 ? c->max_images / 2 : 1);
+    if (c->sbs.ensure(frames * c->max_h * 2 * (size_t)c->max_w + 256)) {
+        fail(ORBGPU_ERR_HIP, "hipMalloc failed (sbs staging)");
+        return nullptr;
+    }
+    return c->sbs.as<uint8_t>();
+}
+
+static int check_sbs(orbgpu_ctx* c, int n, int w, int h, int stride) {
+    if (w <= 0 || h <= 0) return fail(ORBGPU_ERR_EMPTY_IMAGE, "empty image");
+    if (stride < 2 * w) return fail(ORBGPU_ERR_INVALID, "stride < 2 * width (side-by-side frame)");
+    if (n < 1) return fail(ORBGPU_ERR_INVALID, "bad frame count");
+    return ensure_input(c, 2 * n, w, h);
+}
+
+int orbgpu_ingest_sbs(orbgpu_ctx* c, const uint8_t* frames, int n, int w, int h, int stride, void* stream) {
+    if (!c || !frames) return fail(ORBGPU_ERR_INVALID, "null argument");
+    int r = check_sbs(c, n, w, h, stride);
+    if (r) return r;
+    HIP_TRY(hipSetDevice(c->device));
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    r = join_all(c, s);  // sub streams may still read the previous images
+    if (r) return r;
+    SbsArgs a{frames, (long long)h * stride, stride, w, h, n, c->input.as<uint8_t>()};
+    r = timed(c, ST_SBS, s, [&] { return launch_sbs_split(a, s); });
+    if (r) return r;
+    c->need_fork = true;
+    return ORBGPU_OK;
+}
+
+int orbgpu_upload_sbs(orbgpu_ctx* c, const uint8_t* frames, int n, int w, int h, int stride) {
+    if (!c || !frames) return fail(ORBGPU_ERR_INVALID, "null argument");
+    int r = check_sbs(c, n, w, h, stride);
+    if (r) return r;
+    HIP_TRY(hipSetDevice(c->device));
+    const size_t bytes = (size_t)n * h * stride;
+    if (c->sbs.ensure(bytes + 256)) return fail(ORBGPU_ERR_HIP, "hipMalloc failed (sbs staging)");
+    r = join_all(c, c->stream);
+    if (r) return r;
+    HIP_TRY(hipMemcpyAsync(c->sbs.p, frames, bytes, hipMemcpyHostToDevice, c->stream));
+    return orbgpu_ingest_sbs(c, c->sbs.as<uint8_t>(), n, w, h, stride, nullptr);
+}
+
+int orbgpu_pack_soa(orbgpu_ctx* c, int n_images, int n_pairs, void* stream) {
+    if (!c || n_images < 0 || n_images > c->last_images || n_pairs < 0 || n_pairs > c->last_pairs)
+        return fail(ORBGPU_ERR_INVALID, "bad image/pair count");
+    HIP_TRY(hipSetDevice(c->device));
+    const size_t cap = (size_t)c->out_cap;
+    if (c->soa.ensure((size_t)c->max_images * cap * 16 + 256) ||
+        c->m16.ensure((size_t)(c->max_images / 2 + 1) * cap * 6 + 256))
+        return fail(ORBGPU_ERR_HIP, "hipMalloc failed (soa buffers)");
+    const size_t plane = (size_t)c->max_images * cap;
+    const size_t mplane = (size_t)(c->max_images / 2 + 1) * cap;
+    SoaArgs a{};
+    a.kps = c->outkps.p;
+    a.out_n = c->outn.as<int32_t>();
+    a.out_cap = c->out_cap;
+    a.nimages = n_images;
+    a.img0 = 0;
+    a.x = c->soa.as<int32_t>();
+    a.y = a.x + plane;
+    a.angle = a.y + plane;
+    a.level = a.angle + plane;
+    a.nq = c->mnq.as<int32_t>();
+    a.idx1 = c->midx1.as<int32_t>();
+    a.dist1 = c->mdist1.as<int32_t>();
+    a.dist2 = c->mdist2.as<int32_t>();
+    a.idx16 = c->m16.as<int16_t>();
+    a.d1_16 = a.idx16 + mplane;
+    a.d2_16 = a.d1_16 + mplane;
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    int r = join_all(c, s);  // the chunk streams produced the keypoints and matches
+    if (r) return r;
+    r = timed(c, ST_SOA, s, [&] { return launch_pack_soa(a, n_pairs, s); });
+    if (r) return r;
+    c->soa_images = n_images;
+    c->soa_pairs = n_pairs;
+    c->need_fork = true;  // the next batch's chunk streams must not overwrite what this reads
+    return ORBGPU_OK;
+}
+
+int orbgpu_download_soa(orbgpu_ctx* c, int image, int32_t* x, int32_t* y, int32_t* angle, int32_t* level,
+                        uint8_t* orb, int cap, int* count, int* mono) {
+    if (!c || image < 0 || image >= c->soa_images) return fail(ORBGPU_ERR_INVALID, "bad image");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipDeviceSynchronize());
+    int32_t nm[2] = {0, 0};
+    HIP_TRY(hipMemcpy(&nm[0], c->outn.as<int32_t>() + image, 4, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(&nm[1], c->outmono.as<int32_t>() + image, 4, hipMemcpyDeviceToHost));
+    if (count) *count = nm[0];
+    if (mono) *mono = nm[1];
+    if (nm[0] > cap) return fail(ORBGPU_ERR_CAPACITY, "caller capacity too small");
+    const size_t n = (size_t)nm[0];
+    if (!n) return ORBGPU_OK;
+    const size_t plane = (size_t)c->max_images * c->out_cap, o = (size_t)image * c->out_cap;
+    int32_t* dst[4] = {x, y, angle, level};
+    for (int k = 0; k < 4; ++k)
+        if (dst[k]) HIP_TRY(hipMemcpy(dst[k], c->soa.as<int32_t>() + k * plane + o, 4 * n, hipMemcpyDeviceToHost));
+    if (orb) HIP_TRY(hipMemcpy(orb, c->outdesc.as<uint8_t>() + o * 32, 32 * n, hipMemcpyDeviceToHost));
+    return ORBGPU_OK;
+}
+
+int orbgpu_download_matches16(orbgpu_ctx* c, int pair, int16_t* indices, int16_t* dist1, int16_t* dist2,
+                              int cap, int* nq) {
+    if (!c || pair < 0 || pair >= c->soa_pairs) return fail(ORBGPU_ERR_INVALID, "bad pair");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipDeviceSynchronize());
+    int32_t n = 0;
+    HIP_TRY(hipMemcpy(&n, c->mnq.as<int32_t>() + pair, 4, hipMemcpyDeviceToHost));
+    if (nq) *nq = n;
+    if (n > cap) return fail(ORBGPU_ERR_CAPACITY, "caller capacity too small");
+    if (!n) return ORBGPU_OK;
+    const size_t mplane = (size_t)(c->max_images / 2 + 1) * c->out_cap, o = (size_t)pair * c->out_cap;
+    int16_t* dst[3] = {indices, dist1, dist2};
+    for (int k = 0; k < 3; ++k)
+        if (dst[k]) HIP_TRY(hipMemcpy(dst[k], c->m16.as<int16_t>() + k * mplane + o, 2 * (size_t)n, hipMemcpyDeviceToHost));
+    return ORBGPU_OK;
+}
+
+int orbgpu_extract_features(orbgpu_ctx* c, const uint8_t* image, int image_len, int width, int height,
+                            int stride, int threshold, int lap_l0, int lap_l1, int lap_r0, int lap_r1,
+                            int* count_l, int32_t* x_l, int32_t* y_l, int32_t* angle_l, int32_t* level_l,
+                            uint8_t* orb_l, int* count_r, int32_t* x_r, int32_t* y_r, int32_t* angle_r,
+                            int32_t* level_r, uint8_t* orb_r, int kp_cap, int* mono_l, int* mono_r,
+                            int16_t* indices, int16_t* dist1, int16_t* dist2, int match_cap) {
+    (void)threshold;  // the DSP ignores it too (orbslam_dsp.cpp:1003-1087): the ctx's FAST thresholds apply
+    if (!c || !image) return fail(ORBGPU_ERR_INVALID, "null argument");
+    if ((long long)image_len < (long long)stride * (height - 1) + 2LL * width)
+        return fail(ORBGPU_ERR_INVALID, "image_len smaller than the side-by-side frame");
+    int r = orbgpu_upload_sbs(c, image, 1, width, height, stride);
+    if (r) return r;
+    const int32_t laps[4] = {lap_l0, lap_l1, lap_r0, lap_r1};
+    r = orbgpu_run_batch(c, 2, width, height, laps, nullptr);
+    if (!r) r = orbgpu_match_stereo_batch(c, 1, 1, nullptr);
+    if (!r) r = orbgpu_pack_soa(c, 2, 1, nullptr);
+    if (!r) r = orbgpu_download_soa(c, 0, x_l, y_l, angle_l, level_l, orb_l, kp_cap, count_l, mono_l);
+    if (!r) r = orbgpu_download_soa(c, 1, x_r, y_r, angle_r, level_r, orb_r, kp_cap, count_r, mono_r);
+    int nq = 0;
+    if (!r) r = orbgpu_download_matches16(c, 0, indices, dist1, dist2, match_cap, &nq);
+    return r;
 }
 
 int orbgpu_image_bounds(int cols, int rows, const float K[4], const float* dist, int ndist, float bounds[4]) {
