@@ -126,7 +126,7 @@ EUROC_K = (458.654, 457.296, 367.215, 248.375)  # EuRoC cam0 fx fy cx cy
 EUROC_D = (-0.28340811, 0.07395907, 0.00019359, 1.76187114e-05)
 
 
-def cpu_baseline(w, h, nfeatures, seconds):
+def cpu_baseline(w, h, nfeatures, seconds, map_points=3000):
     """The oracle (scalar C++ restatement of the reference CPU ORBextractor + BFMatcher), one
     thread, on a bounded sample of the same workload: pairs until `seconds` elapse."""
     from oracle import oracle_py as O
@@ -135,7 +135,9 @@ def cpu_baseline(w, h, nfeatures, seconds):
     pairs = [synth.stereo_pair(h, w, 1000 + i) for i in range(4)]
     stereo_pyr = [(O.pyramid(L), O.pyramid(R)) for L, R in pairs]
     t_st = [0.0]
-    t_gr = 0.0
+    t_gr = t_sbp = 0.0
+    maps = []
+    n_mp = 0
     nfeat = nq = 0
     t_ex = t_bf = 0.0
     i = 0
@@ -153,9 +155,16 @@ def cpu_baseline(w, h, nfeatures, seconds):
                              47.9, float(np.float32(47.9) / np.float32(435.2)))
             t_st[0] += time.perf_counter() - t2
         t3 = time.perf_counter()
-        O.undistort_grid(kl, EUROC_K, EUROC_D, w, h)
+        xy, b, _, cs, ci = O.undistort_grid(kl, EUROC_K, EUROC_D, w, h)
         O.undistort_grid(kr, EUROC_K, EUROC_D, w, h)
-        t_gr += time.perf_counter() - t3
+        t4 = time.perf_counter()
+        t_gr += t4 - t3
+        if i < len(pairs):  # synthetic maps are generated once per distinct pair
+            maps.append(synth.map_points(xy, kl["octave"], dl, None, n=map_points, seed=7 + i))
+        t4 = time.perf_counter()
+        O.search_by_projection(maps[i % len(pairs)], xy, kl["octave"], dl, None, b, cs, ci)
+        t_sbp += time.perf_counter() - t4
+        n_mp += map_points
         nfeat += len(kl) + len(kr)
         nq += len(dl)
         t_ex += t1 - t0
@@ -164,6 +173,7 @@ def cpu_baseline(w, h, nfeatures, seconds):
     return {"pairs": i, "mfeat_s": nfeat / t_ex / 1e6, "mmatch_s": nq / t_bf / 1e6,
             "stereo_mkp_s": nq / t_st[0] / 1e6 if t_st[0] > 0 else None,
             "grid_mkp_s": nfeat / t_gr / 1e6 if t_gr > 0 else None,
+            "sbp_mmp_s": n_mp / t_sbp / 1e6 if t_sbp > 0 else None,
             "mfeat_s_pipeline": nfeat / (t_ex + t_bf) / 1e6}
 
 
@@ -184,6 +194,8 @@ def main():
     ap.add_argument("--no-stereo", action="store_true", help="skip the ComputeStereoMatches leg")
     ap.add_argument("--no-grid", action="store_true", help="skip the UndistortKeyPoints + grid leg")
     ap.add_argument("--no-wire", action="store_true", help="skip the side-by-side ingest / SoA egress leg")
+    ap.add_argument("--no-sbp", action="store_true", help="skip the SearchByProjection leg")
+    ap.add_argument("--map-points", type=int, default=3000, help="local-map points per frame (SBP leg)")
     ap.add_argument("--no-profile", action="store_true",
                     help="do not bracket launches with HIP events in the timed region")
     args = ap.parse_args()
@@ -381,6 +393,43 @@ def main():
                 "kernel_ms_per_launch": round(gt[0] / gt[1], 4) if gt[1] else None,
                 "images_per_step": 2 * P}
 
+    # ORBmatcher::SearchByProjection on every pair's left frame: a synthetic
+    # local map of --map-points points per frame (projections near the frame's keypoints, several
+    # per keypoint), mvuRight from the stereo leg.  Kernel time from the stage timer; the call
+    # time includes uploading the map points (PCIe, they come from the host each frame).
+    sbp = None
+    if not args.no_sbp and grid is not None:
+        uniq_mps = []
+        for u in range(U):
+            kl_u, dl_u, _ = be.result(2 * u)
+            xy_u, _, _, _ = be.grid_result(2 * u)
+            ur_u = be.stereo_result(u)[0] if stereo is not None else None
+            uniq_mps.append(synth.map_points(xy_u, kl_u["octave"], dl_u, ur_u, n=args.map_points, seed=7 + u))
+        mp_list = [uniq_mps[p % U] for p in range(P)]
+        use_ur = stereo is not None
+        be.undistort_grid(EUROC_K, EUROC_D)
+        be.search_by_projection(mp_list, image_step=2, use_uright=use_ur)
+        be.synchronize()
+        be.set_profiling(True, stages=["k_sbp"])
+        be.reset_stage_times()
+        barrier(dist)
+        q0 = time.perf_counter()
+        for _ in range(args.steps):
+            be.search_by_projection(mp_list, image_step=2, use_uright=use_ur)
+        be.synchronize()
+        q1 = time.perf_counter()
+        q_el = max_over_ranks(dist, q1 - q0)
+        qt = be.stage_times().get("k_sbp", (0.0, 0))
+        be.set_profiling(False)
+        _, nm0 = be.projection_matches(0)
+        n_mp = P * args.map_points
+        k_ms = qt[0] / qt[1] if qt[1] else None
+        sbp = {"metric": "map points searched per second (ORBmatcher::SearchByProjection, pinhole)",
+               "value": round(sum_over_ranks(dist, n_mp) / (k_ms * 1e-3) / 1e6, 3) if k_ms else None,
+               "unit": "Mmappoints/s", "kernel_ms_per_step": round(k_ms, 4) if k_ms else None,
+               "call_ms_per_step": round(q_el / args.steps * 1e3, 4),
+               "map_points_per_frame": args.map_points, "frames_per_step": P, "nmatches_frame0": nm0}
+
     # Wire formats: the P side-by-side frames of a step split from the device
     # staging buffer into the batch layout, and the step's results packed to the IDL SoA layout.
     # Timed on their own (HBM-bound copies; 4 B/px moved by the split, 2 x 28 B read + 16 B
@@ -443,13 +492,14 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cb = cpu_baseline(W, H, args.nfeatures, args.cpu_seconds)
+        cb = cpu_baseline(W, H, args.nfeatures, args.cpu_seconds, args.map_points)
         cpu = {"value": round(cb["mfeat_s"], 5), "unit": "Mfeatures/s", "cores": 1, "kind": "port",
                "sample": "%d synthetic 640x480 stereo pairs, oracle extract (both eyes, 1 thread); "
                          "BF kNN2 %.4f Mmatches/s" % (cb["pairs"], cb["mmatch_s"]),
                "mmatches_s": round(cb["mmatch_s"], 5),
                "stereo_mkeypoints_s": round(cb["stereo_mkp_s"], 5) if cb["stereo_mkp_s"] else None,
-               "undistort_grid_mkeypoints_s": round(cb["grid_mkp_s"], 5) if cb["grid_mkp_s"] else None}
+               "undistort_grid_mkeypoints_s": round(cb["grid_mkp_s"], 5) if cb["grid_mkp_s"] else None,
+               "search_by_projection_mmappoints_s": round(cb["sbp_mmp_s"], 5) if cb["sbp_mmp_s"] else None}
 
     if rank == 0:
         out = {
@@ -478,6 +528,7 @@ def main():
             "cpu_baseline": cpu,
             "stereo_matches": stereo,
             "undistort_grid": grid,
+            "search_by_projection": sbp,
             "wire": wire,
             "cross_camera": cross,
         }

@@ -18,6 +18,7 @@
  *   - cv::BFMatcher(NORM_HAMMING).knnMatch(k=2)  cpp/src/Frame.cc:45,1227
  *   - mvImagePyramid (public member)      cpp/include/ORBextractor_old.h:80
  *   - Frame::ComputeStereoMatches         cpp/include/Frame.h:119, cpp/src/Frame.cc:827-997
+ *   - ORBmatcher::SearchByProjection (Frame&, vector<MapPoint*>)  cpp/src/ORBmatcher.cc:44-214
  *   - Frame::UndistortKeyPoints / ComputeImageBounds / AssignFeaturesToGrid
  *                                         cpp/src/Frame.cc:405-436, 741-825
  */
@@ -143,6 +144,39 @@ int orbgpu_download_matches(orbgpu_ctx* ctx, int pair, int32_t* idx1, int32_t* d
 int orbgpu_stereo_matches_batch(orbgpu_ctx* ctx, int n_pairs, float mbf, float mb, void* stream);
 int orbgpu_download_stereo(orbgpu_ctx* ctx, int pair, float* u_right, float* depth, int32_t* sad,
                            int cap, int* n);
+
+/* ---- ORBmatcher::SearchByProjection (cpp/src/ORBmatcher.cc:44-214, pinhole frames) ---------
+ * Tracking's local-map search: every map point predicted in view is matched against the frame
+ * keypoints in a window around its projection (Frame::GetFeaturesInArea, Frame.cc:673-735, on the
+ * grid of orbgpu_undistort_grid_batch), best/second-best Hamming with TH_HIGH = 100 and the
+ * nnratio test; the keypoint is then taken (later map points skip it when the taker has
+ * observations).  Frames are batch images f * image_step (image_step 2: the left eye of stereo
+ * pair f, whose mvuRight from orbgpu_stereo_matches_batch is used when use_uright != 0;
+ * image_step 1: monocular frames, mvuRight all -1).
+ * A map point carries the MapPoint state the function reads: */
+typedef struct {
+    float proj_x, proj_y;  /* mTrackProjX, mTrackProjY */
+    float proj_xr;         /* mTrackProjXR */
+    float view_cos;        /* mTrackViewCos */
+    float depth;           /* mTrackDepth */
+    int32_t level;         /* mnTrackScaleLevel, in [0, nlevels) (others are skipped) */
+    int32_t flags;         /* ORBGPU_MP_* */
+    uint8_t desc[32];      /* GetDescriptor() */
+} orbgpu_map_point;
+#define ORBGPU_MP_IN_VIEW 1  /* mbTrackInView */
+#define ORBGPU_MP_BAD 2      /* isBad() */
+#define ORBGPU_MP_HAS_OBS 4  /* Observations() > 0 */
+/* mps: all frames' map points, frame f's in [mp_offsets[f], mp_offsets[f + 1]) (host arrays).
+ * kp_block (optional, [n_frames][kp_stride] u8): 1 where F.mvpMapPoints[k] is already set to a
+ * point with observations before the call.  th / nnratio / far_points / th_far as the reference.
+ * orbgpu_download_projection_matches: match[k] = index (within the frame's map points) of the
+ * point assigned to keypoint k by this call, -1 if none; *nmatches = the reference's return. */
+int orbgpu_search_by_projection_batch(orbgpu_ctx* ctx, int n_frames, int image_step, int use_uright,
+                                      const orbgpu_map_point* mps, const int32_t* mp_offsets,
+                                      const uint8_t* kp_block, int kp_stride, float th, float nnratio,
+                                      int far_points, float th_far, void* stream);
+int orbgpu_download_projection_matches(orbgpu_ctx* ctx, int frame, int32_t* match, int cap, int* n_kp,
+                                       int* nmatches);
 
 /* ---- wire formats ---------------------------------------------------------------------------
  * Ingest of side-by-side stereo Y8 frames (the headset's 2W x H AHardwareBuffer,

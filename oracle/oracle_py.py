@@ -273,3 +273,32 @@ def decode_angle(enc):
     c = (enc & 0xFF).astype(np.uint8).view(np.int8).astype(np.float32)
     s = ((enc >> 8) & 0xFF).astype(np.uint8).view(np.int8).astype(np.float32)
     return np.degrees(np.arctan2(s / 64.0, c / 64.0))
+
+
+MP_DTYPE = np.dtype([("proj_x", "<f4"), ("proj_y", "<f4"), ("proj_xr", "<f4"), ("view_cos", "<f4"),
+                     ("depth", "<f4"), ("level", "<i4"), ("flags", "<i4"), ("desc", "u1", (32,))])
+
+
+def search_by_projection(mps, xy_un, octave, desc, uright, bounds, cell_start, cell_idx, kp_block=None,
+                         th=1.0, nnratio=0.8, far_points=False, th_far=50.0, scale_factor=1.2, nlevels=8):
+    """ORBmatcher::SearchByProjection (ORBmatcher.cc:44-214), pinhole -> (match [n], nmatches)."""
+    mps = np.ascontiguousarray(mps, dtype=MP_DTYPE)
+    n = len(octave)
+    xy = np.ascontiguousarray(xy_un, dtype=np.float32).reshape(-1, 2)
+    octv = np.ascontiguousarray(octave, dtype=np.int32)
+    d = np.ascontiguousarray(desc, dtype=np.uint8).reshape(-1, 32)
+    ur = None if uright is None else np.ascontiguousarray(uright, dtype=np.float32)
+    b = np.ascontiguousarray(bounds, dtype=np.float32)
+    cs = np.ascontiguousarray(cell_start, dtype=np.int32)
+    ci = np.ascontiguousarray(cell_idx, dtype=np.int32)
+    if len(ci) == 0:
+        ci = np.zeros(1, np.int32)
+    blk = None if kp_block is None else np.ascontiguousarray(kp_block, dtype=np.uint8)
+    scale = scale_factors(scale_factor, nlevels)[0]
+    match = np.zeros(max(n, 1), np.int32)
+    nm = lib().oracle_search_by_projection(
+        _p(mps) if len(mps) else None, len(mps), _p(xy) if n else None, _p(octv) if n else None,
+        _p(d) if n else None, _p(ur) if ur is not None else None, n, _p(b), _p(cs), _p(ci), _p(scale), nlevels,
+        _p(blk) if blk is not None else None, C.c_float(th), C.c_float(nnratio), int(far_points),
+        C.c_float(th_far), _p(match))
+    return match[:n], nm

@@ -1182,3 +1182,91 @@ void oracle_pack_soa(const oracle_kp* kps, int n, int32_t* x, int32_t* y, int32_
         level[i] = kps[i].octave;
     }
 }
+
+// ---- ORBmatcher::SearchByProjection (ORBmatcher.cc:44-214), pinhole frame ---------------------
+namespace {
+
+// Frame::GetFeaturesInArea (Frame.cc:673-735) on the CSR grid.
+void features_in_area(const float* xy_un, const int32_t* octave, const float bounds[4], const int32_t* cs,
+                      const int32_t* ci, float x, float y, float r, int minLevel, int maxLevel,
+                      std::vector<int>& out) {
+    out.clear();
+    const float wInv = static_cast<float>(64) / (bounds[1] - bounds[0]);
+    const float hInv = static_cast<float>(48) / (bounds[3] - bounds[2]);
+    const int nMinCellX = std::max(0, (int)std::floor((x - bounds[0] - r) * wInv));
+    if (nMinCellX >= 64) return;
+    const int nMaxCellX = std::min(63, (int)std::ceil((x - bounds[0] + r) * wInv));
+    if (nMaxCellX < 0) return;
+    const int nMinCellY = std::max(0, (int)std::floor((y - bounds[2] - r) * hInv));
+    if (nMinCellY >= 48) return;
+    const int nMaxCellY = std::min(47, (int)std::ceil((y - bounds[2] + r) * hInv));
+    if (nMaxCellY < 0) return;
+    const bool bCheckLevels = (minLevel > 0) || (maxLevel >= 0);
+    for (int ix = nMinCellX; ix <= nMaxCellX; ix++)
+        for (int iy = nMinCellY; iy <= nMaxCellY; iy++)
+            for (int j = cs[ix * 48 + iy]; j < cs[ix * 48 + iy + 1]; j++) {
+                const int k = ci[j];
+                if (bCheckLevels) {
+                    if (octave[k] < minLevel) continue;
+                    if (maxLevel >= 0 && octave[k] > maxLevel) continue;
+                }
+                const float distx = xy_un[2 * k] - x, disty = xy_un[2 * k + 1] - y;
+                if (std::fabs(distx) < r && std::fabs(disty) < r) out.push_back(k);
+            }
+}
+
+}  // namespace
+
+int oracle_search_by_projection(const oracle_map_point* mps, int nmp, const float* xy_un, const int32_t* octave,
+                                const uint8_t* desc, const float* uRight, int n, const float bounds[4],
+                                const int32_t* cell_start, const int32_t* cell_idx, const float* scale,
+                                int nlevels, const uint8_t* kp_block, float th, float nnratio,
+                                int far_points, float th_far, int32_t* match) {
+    std::vector<uint8_t> blocked(n, 0);
+    if (kp_block) std::copy(kp_block, kp_block + n, blocked.begin());
+    for (int k = 0; k < n; ++k) match[k] = -1;
+    const bool bFactor = th != 1.0;
+    std::vector<int> cand;
+    int nmatches = 0;
+    for (int i = 0; i < nmp; ++i) {
+        const oracle_map_point& mp = mps[i];
+        if (!(mp.flags & ORACLE_MP_IN_VIEW)) continue;
+        if (far_points && mp.depth > th_far) continue;
+        if (mp.flags & ORACLE_MP_BAD) continue;
+        const int lvl = mp.level;
+        if (lvl < 0 || lvl >= nlevels) continue;  // PredictScale never leaves [0, nlevels)
+        float r = mp.view_cos > 0.998 ? 2.5f : 4.0f;  // RadiusByViewingCos (:216-222)
+        if (bFactor) r *= th;
+        const float rs = r * scale[lvl];
+        features_in_area(xy_un, octave, bounds, cell_start, cell_idx, mp.proj_x, mp.proj_y, rs, lvl - 1, lvl, cand);
+        if (cand.empty()) continue;
+        int bestDist = 256, bestLevel = -1, bestDist2 = 256, bestLevel2 = -1, bestIdx = -1;
+        for (int idx : cand) {
+            if (blocked[idx]) continue;
+            if (uRight && uRight[idx] > 0) {
+                const float er = std::fabs(mp.proj_xr - uRight[idx]);
+                if (er > r * scale[lvl]) continue;
+            }
+            const int dist = oracle_descriptor_distance(mp.desc, desc + (size_t)idx * 32);
+            if (dist < bestDist) {
+                bestDist2 = bestDist;
+                bestDist = dist;
+                bestLevel2 = bestLevel;
+                bestLevel = octave[idx];
+                bestIdx = idx;
+            } else if (dist < bestDist2) {
+                bestLevel2 = octave[idx];
+                bestDist2 = dist;
+            }
+        }
+        if (bestDist <= 100) {  // TH_HIGH
+            if (bestLevel == bestLevel2 && bestDist > nnratio * bestDist2) continue;
+            if (bestLevel != bestLevel2 || bestDist <= nnratio * bestDist2) {
+                match[bestIdx] = i;
+                blocked[bestIdx] = (mp.flags & ORACLE_MP_HAS_OBS) ? 1 : 0;
+                nmatches++;
+            }
+        }
+    }
+    return nmatches;
+}

@@ -111,4 +111,28 @@ void oracle_assign_grid(const float* xy_un, int n, const float bounds[4], int32_
 // (decoded by LynxHardwareAccelerator.cpp:174-178), level = octave.
 void oracle_pack_soa(const oracle_kp* kps, int n, int32_t* x, int32_t* y, int32_t* angle, int32_t* level);
 
+// ORBmatcher::SearchByProjection(Frame&, const vector<MapPoint*>&, th, bFarPoints, thFarPoints)
+// (ORBmatcher.cc:44-214) for a pinhole frame (Nleft == -1), with Frame::GetFeaturesInArea
+// (Frame.cc:673-735) over the 64 x 48 grid of oracle_assign_grid and RadiusByViewingCos
+// (:216-222).  A map point is the MapPoint state the function reads (mbTrackInView,
+// mTrackProjX/Y/XR, mTrackViewCos, mTrackDepth, mnTrackScaleLevel, isBad, Observations() > 0,
+// GetDescriptor()).  kp_block[k] = 1 when F.mvpMapPoints[k] is set with Observations() > 0 before
+// the call (NULL: none); uRight = F.mvuRight (NULL: all -1, a monocular frame).  match[k] = the
+// index of the map point assigned to keypoint k by this call (the last one), -1 otherwise.
+// Returns nmatches.
+typedef struct {
+    float proj_x, proj_y, proj_xr, view_cos, depth;
+    int32_t level;  // mnTrackScaleLevel
+    int32_t flags;  // ORACLE_MP_* bits
+    uint8_t desc[32];
+} oracle_map_point;
+#define ORACLE_MP_IN_VIEW 1
+#define ORACLE_MP_BAD 2
+#define ORACLE_MP_HAS_OBS 4
+int oracle_search_by_projection(const oracle_map_point* mps, int nmp, const float* xy_un, const int32_t* octave,
+                                const uint8_t* desc, const float* uRight, int n, const float bounds[4],
+                                const int32_t* cell_start, const int32_t* cell_idx, const float* scale,
+                                int nlevels, const uint8_t* kp_block, float th, float nnratio,
+                                int far_points, float th_far, int32_t* match);
+
 }  // extern "C"

@@ -18,11 +18,16 @@ import os
 
 import numpy as np
 
-__all__ = ["ORBextractor", "ORBmatcher", "BFMatcher", "BatchExtractor", "KEYPOINT_DTYPE",
+__all__ = ["ORBextractor", "ORBmatcher", "BFMatcher", "BatchExtractor", "KEYPOINT_DTYPE", "MAP_POINT_DTYPE",
            "OrbGpuError", "load_library", "LIB_PATH"]
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "liborbgpu.so")
+
+# orbgpu_map_point (60 B): the MapPoint state ORBmatcher::SearchByProjection reads
+MAP_POINT_DTYPE = np.dtype([("proj_x", "<f4"), ("proj_y", "<f4"), ("proj_xr", "<f4"), ("view_cos", "<f4"),
+                            ("depth", "<f4"), ("level", "<i4"), ("flags", "<i4"), ("desc", "u1", (32,))])
+MP_IN_VIEW, MP_BAD, MP_HAS_OBS = 1, 2, 4
 
 # cv::KeyPoint layout (28 B)
 KEYPOINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
@@ -38,6 +43,7 @@ EXPORTED = [
     "orbgpu_image_bounds", "orbgpu_undistort_grid_batch", "orbgpu_download_grid",
     "orbgpu_device_sbs_input", "orbgpu_upload_sbs", "orbgpu_ingest_sbs", "orbgpu_pack_soa",
     "orbgpu_download_soa", "orbgpu_download_matches16", "orbgpu_extract_features",
+    "orbgpu_search_by_projection_batch", "orbgpu_download_projection_matches",
     "orbgpu_set_profiling", "orbgpu_num_stages", "orbgpu_stage_name", "orbgpu_stage_times",
     "orbgpu_reset_stage_times", "orbgpu_last_error", "orbgpu_abi_version",
 ]
@@ -372,6 +378,36 @@ class BatchExtractor:
         _check(_lib.orbgpu_download_matches16(self.ctx.handle, pair, _p(r[0]), _p(r[1]), _p(r[2]), cap,
                                               C.byref(n)))
         return tuple(a[:n.value] for a in r)
+
+    def search_by_projection(self, map_points, image_step=2, use_uright=True, kp_block=None, th=1.0,
+                             nnratio=0.8, far_points=False, th_far=50.0, stream=None):
+        """ORBmatcher(nnratio).SearchByProjection(F, vpMapPoints, th, bFarPoints, thFarPoints)
+        (ORBmatcher.cc:44-214) for frames f = images f * image_step after undistort_grid();
+        map_points: list (one per frame) of MAP_POINT_DTYPE arrays; kp_block: optional list of u8
+        arrays (1 = keypoint already holds a map point with observations)."""
+        nf = len(map_points)
+        mps = np.ascontiguousarray(np.concatenate([np.asarray(m, MAP_POINT_DTYPE) for m in map_points])
+                                   if nf else np.zeros(0, MAP_POINT_DTYPE))
+        off = np.zeros(nf + 1, np.int32)
+        off[1:] = np.cumsum([len(m) for m in map_points])
+        blk, stride = None, 0
+        if kp_block is not None:
+            stride = max(1, max(len(b) for b in kp_block))
+            blk = np.zeros((nf, stride), np.uint8)
+            for f, b in enumerate(kp_block):
+                blk[f, :len(b)] = b
+        _check(_lib.orbgpu_search_by_projection_batch(
+            self.ctx.handle, nf, int(image_step), int(use_uright), _p(mps) if len(mps) else None, _p(off),
+            _p(blk) if blk is not None else None, stride, C.c_float(th), C.c_float(nnratio),
+            int(far_points), C.c_float(th_far), C.c_void_p(stream) if stream else None))
+
+    def projection_matches(self, frame, cap=65536):
+        """(match [n_kp] int32: map point index or -1, nmatches) of frame `frame`."""
+        m = np.zeros(cap, np.int32)
+        n, nm = C.c_int(0), C.c_int(0)
+        _check(_lib.orbgpu_download_projection_matches(self.ctx.handle, frame, _p(m), cap, C.byref(n),
+                                                       C.byref(nm)))
+        return m[:n.value], nm.value
 
     def undistort_grid(self, K, dist=(), stream=None):
         """Frame::UndistortKeyPoints + AssignFeaturesToGrid (Frame.cc:405-436, 741-825) for every

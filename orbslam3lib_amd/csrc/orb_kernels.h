@@ -188,6 +188,43 @@ struct SoaArgs {
     const int32_t *nq, *idx1, *dist1, *dist2;  // kNN results [pair][out_cap]
     int16_t *idx16, *d1_16, *d2_16;
 };
+// ORBmatcher::SearchByProjection over device-resident frames (orb_sbp.hip).
+struct MapPointIn {  // orbgpu_map_point (60 B)
+    float proj_x, proj_y, proj_xr, view_cos, depth;
+    int32_t level, flags;
+    uint8_t desc[32];
+};
+constexpr int kMpInView = 1, kMpBad = 2, kMpHasObs = 4;
+constexpr int kSbpMaxKp = 65536;  // keypoints per frame (the LDS occupancy bitmap)
+struct SbpCand {  // k_sbp_candidates -> k_sbp_resolve: 4 lowest (distance, window position)
+    int32_t idx[4];
+    int32_t key[4];  // dist | octave << 16
+    int32_t n;       // candidates after the filters; -1: map point skipped
+};
+struct SbpArgs {
+    const MapPointIn* mps;    // all frames' map points, frame f = [mp_off[f], mp_off[f + 1])
+    const int32_t* mp_off;
+    SbpCand* cand;            // [mp]
+    const void* kps;          // out_kps
+    const int32_t* out_n;
+    int out_cap;
+    const float* xy_un;       // grid buffers (orbgpu_undistort_grid_batch)
+    const int32_t* cell_start;
+    const int32_t* cell_idx;
+    const uint8_t* desc;      // out_desc
+    const float* uright;      // [frame][out_cap] mvuRight or nullptr
+    const uint8_t* kp_block;  // [frame][out_cap] pre-call occupant with observations, or nullptr
+    int image_step, img0;     // frame f = batch image (img0 + f) * image_step; img0 = first frame
+    float bounds[4], grid_inv[2];
+    float scale[kMaxLevels];
+    int nlevels;
+    float th, nnratio, th_far;
+    int far_points, factor;
+    int32_t* match;           // [frame][out_cap]
+    int32_t* nmatches;        // [frame]
+};
+hipError_t launch_sbp(const SbpArgs& a, int nframes, int max_mps, hipStream_t st);
+
 hipError_t launch_sbs_split(const SbsArgs& a, hipStream_t st);
 hipError_t launch_pack_soa(const SoaArgs& a, int npairs, hipStream_t st);
 hipError_t launch_knn2_plain(const uint8_t* q, int nq, const uint8_t* t, int nt, int32_t* i1,

@@ -40,12 +40,12 @@ int fail(int code, const std::string& msg) {
     } while (0)
 
 enum Stage { ST_RESIZE, ST_BLUR, ST_FAST48, ST_FAST, ST_FAST_TOP, ST_OCTREE, ST_ORIENT, ST_FINAL, ST_KNN,
-             ST_PYRAMID, ST_STEREO, ST_GRID, ST_SBS, ST_SOA, ST_COUNT };
+             ST_PYRAMID, ST_STEREO, ST_GRID, ST_SBS, ST_SOA, ST_SBP, ST_COUNT };
 // names as rocprofv3 shows the kernels (templates with their argument)
 const char* kStageNames[ST_COUNT] = {"k_resize",         "k_blur",   "k_fast_cells<48>", "k_fast_cells<64>",
                                      "k_fast_cells<80>", "k_octree", "k_orient_desc",    "k_finalize",
                                      "k_knn2",           "k_pyramid", "k_stereo",         "k_undistort_grid",
-                                     "k_sbs_split",      "k_pack_soa"};
+                                     "k_sbs_split",      "k_pack_soa",       "k_sbp"};
 
 struct DevBuf {
     void* p = nullptr;
@@ -103,7 +103,10 @@ struct orbgpu_ctx {
     // device buffers
     DevBuf input, pyr, blur, rtab, cellkeys, cellcnt, octws, lvlkey, lvlangle, lvldesc, lvlcnt,
         status, outkps, outdesc, outn, outmono, laps, midx1, mdist1, midx2, mdist2, mnq, scratch,
-        octdbg, knnpart, strow, stidx, stur, stdepth, stsad, gxy, gcell, gstart, gidx, sbs, soa, m16;
+        octdbg, knnpart, strow, stidx, stur, stdepth, stsad, gxy, gcell, gstart, gidx, sbs, soa, m16,
+        sbpmp, sbpoff, sbpcand, sbpblk, sbpmatch, sbpnm;
+    float grid_bounds[4] = {0, 0, 0, 0}, grid_inv[2] = {0, 0};  // of the last undistort_grid
+    int sbp_frames = 0, sbp_step = 1;
     int soa_images = 0, soa_pairs = 0;  // coverage of the last orbgpu_pack_soa
     int grid_images = 0;   // images of the last orbgpu_undistort_grid_batch
     int stereo_pairs = 0;  // pairs of the last orbgpu_stereo_matches_batch
@@ -584,7 +587,8 @@ int orbgpu_destroy(orbgpu_ctx* c) {
                       &c->mdist1,  &c->midx2,   &c->mdist2, &c->mnq,     &c->scratch, &c->octdbg,
                       &c->knnpart, &c->strow,  &c->stidx, &c->stur,    &c->stdepth,  &c->stsad,
                       &c->gxy,     &c->gcell,  &c->gstart, &c->gidx,    &c->sbs,      &c->soa,
-                      &c->m16};
+                      &c->m16,     &c->sbpmp,  &c->sbpoff, &c->sbpcand, &c->sbpblk,  &c->sbpmatch,
+                      &c->sbpnm};
     for (DevBuf* b : bufs) b->release();
     for (size_t k = 1; k < c->sub.size(); ++k) hipStreamDestroy(c->sub[k]);
     if (c->fork) hipEventDestroy(c->fork);
@@ -1290,6 +1294,96 @@ int orbgpu_extract_features(orbgpu_ctx* c, const uint8_t* image, int image_len, 
     return r;
 }
 
+int orbgpu_search_by_projection_batch(orbgpu_ctx* c, int n_frames, int image_step, int use_uright,
+                                      const orbgpu_map_point* mps, const int32_t* mp_offsets,
+                                      const uint8_t* kp_block, int kp_stride, float th, float nnratio,
+                                      int far_points, float th_far, void* stream) {
+    static_assert(sizeof(orbgpu_map_point) == sizeof(MapPointIn), "map point layout");
+    if (!c || !mp_offsets || n_frames < 1) return fail(ORBGPU_ERR_INVALID, "null argument");
+    if (image_step < 1 || (long long)(n_frames - 1) * image_step >= c->grid_images)
+        return fail(ORBGPU_ERR_INVALID, "frames must lie in the last orbgpu_undistort_grid_batch");
+    if (use_uright && (image_step != 2 || n_frames > c->stereo_pairs))
+        return fail(ORBGPU_ERR_INVALID, "mvuRight needs image_step 2 and a stereo_matches_batch over the pairs");
+    if (c->out_cap > kSbpMaxKp) return fail(ORBGPU_ERR_CAPACITY, "keypoint capacity above the matcher's");
+    if (kp_block && kp_stride < 1) return fail(ORBGPU_ERR_INVALID, "kp_stride");
+    const int total = mp_offsets[n_frames];
+    int max_mps = 0;
+    for (int f = 0; f < n_frames; ++f) {
+        if (mp_offsets[f + 1] < mp_offsets[f] || mp_offsets[0] != 0) return fail(ORBGPU_ERR_INVALID, "mp_offsets");
+        max_mps = std::max(max_mps, mp_offsets[f + 1] - mp_offsets[f]);
+    }
+    if (total > 0 && !mps) return fail(ORBGPU_ERR_INVALID, "null map points");
+    HIP_TRY(hipSetDevice(c->device));
+    const size_t cap = (size_t)c->out_cap;
+    if (c->sbpmp.ensure((size_t)total * sizeof(MapPointIn) + 256) ||
+        c->sbpoff.ensure((size_t)(n_frames + 1) * 4 + 256) ||
+        c->sbpcand.ensure((size_t)total * sizeof(SbpCand) + 256) ||
+        c->sbpmatch.ensure((size_t)n_frames * cap * 4 + 256) || c->sbpnm.ensure((size_t)n_frames * 4 + 256) ||
+        (kp_block && c->sbpblk.ensure((size_t)n_frames * cap + 256)))
+        return fail(ORBGPU_ERR_HIP, "hipMalloc failed (projection search)");
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    int r = join_all(c, s);  // keypoints, grid and mvuRight come from the chunk streams
+    if (r) return r;
+    // host inputs are pageable: copy, then wait so the caller may reuse them on return
+    if (total) HIP_TRY(hipMemcpyAsync(c->sbpmp.p, mps, (size_t)total * sizeof(MapPointIn), hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(c->sbpoff.p, mp_offsets, (size_t)(n_frames + 1) * 4, hipMemcpyHostToDevice, s));
+    if (kp_block) {
+        const size_t wcopy = std::min((size_t)kp_stride, cap);
+        HIP_TRY(hipMemsetAsync(c->sbpblk.p, 0, (size_t)n_frames * cap, s));
+        HIP_TRY(hipMemcpy2DAsync(c->sbpblk.p, cap, kp_block, kp_stride, wcopy, n_frames, hipMemcpyHostToDevice, s));
+    }
+    SbpArgs a{};
+    a.mps = c->sbpmp.as<MapPointIn>();
+    a.mp_off = c->sbpoff.as<int32_t>();
+    a.cand = c->sbpcand.as<SbpCand>();
+    a.kps = c->outkps.p;
+    a.out_n = c->outn.as<int32_t>();
+    a.out_cap = c->out_cap;
+    a.xy_un = c->gxy.as<float>();
+    a.cell_start = c->gstart.as<int32_t>();
+    a.cell_idx = c->gidx.as<int32_t>();
+    a.desc = c->outdesc.as<uint8_t>();
+    a.uright = use_uright ? c->stur.as<float>() : nullptr;
+    a.kp_block = kp_block ? c->sbpblk.as<uint8_t>() : nullptr;
+    a.image_step = image_step;
+    a.img0 = 0;
+    std::memcpy(a.bounds, c->grid_bounds, sizeof a.bounds);
+    std::memcpy(a.grid_inv, c->grid_inv, sizeof a.grid_inv);
+    for (int l = 0; l < kMaxLevels; ++l) a.scale[l] = l < c->prm.nlevels ? c->scale[l] : 1.0f;
+    a.nlevels = c->prm.nlevels;
+    a.th = th;
+    a.nnratio = nnratio;
+    a.th_far = th_far;
+    a.far_points = far_points != 0;
+    a.factor = th != 1.0;  // bFactor (:48)
+    a.match = c->sbpmatch.as<int32_t>();
+    a.nmatches = c->sbpnm.as<int32_t>();
+    r = timed(c, ST_SBP, s, [&] { return launch_sbp(a, n_frames, max_mps, s); });
+    if (r) return r;
+    HIP_TRY(hipStreamSynchronize(s));  // the pageable uploads above
+    c->sbp_frames = n_frames;
+    c->sbp_step = image_step;
+    c->need_fork = true;
+    return ORBGPU_OK;
+}
+
+int orbgpu_download_projection_matches(orbgpu_ctx* c, int frame, int32_t* match, int cap, int* n_kp,
+                                       int* nmatches) {
+    if (!c || frame < 0 || frame >= c->sbp_frames) return fail(ORBGPU_ERR_INVALID, "bad frame");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipDeviceSynchronize());
+    int32_t nk = 0, nm = 0;
+    HIP_TRY(hipMemcpy(&nk, c->outn.as<int32_t>() + (size_t)frame * c->sbp_step, 4, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(&nm, c->sbpnm.as<int32_t>() + frame, 4, hipMemcpyDeviceToHost));
+    if (n_kp) *n_kp = nk;
+    if (nmatches) *nmatches = nm;
+    if (nk > cap) return fail(ORBGPU_ERR_CAPACITY, "caller capacity too small");
+    if (match && nk)
+        HIP_TRY(hipMemcpy(match, c->sbpmatch.as<int32_t>() + (size_t)frame * c->out_cap, 4 * (size_t)nk,
+                          hipMemcpyDeviceToHost));
+    return ORBGPU_OK;
+}
+
 int orbgpu_image_bounds(int cols, int rows, const float K[4], const float* dist, int ndist, float bounds[4]) {
     if (!K || !bounds || (ndist > 0 && !dist) || ndist < 0) return fail(ORBGPU_ERR_INVALID, "null argument");
     image_bounds_host(cols, rows, K, dist, ndist, bounds);
@@ -1337,6 +1431,8 @@ int orbgpu_undistort_grid_batch(orbgpu_ctx* c, int n, const float K[4], const fl
         if (r) return r;
     }
     c->grid_images = n;
+    std::memcpy(c->grid_bounds, g.bounds, sizeof g.bounds);
+    std::memcpy(c->grid_inv, g.grid_inv, sizeof g.grid_inv);
     return ORBGPU_OK;
 }
 

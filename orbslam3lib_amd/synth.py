@@ -86,3 +86,50 @@ def stereo_batch(h: int, w: int, npairs: int, first: int = 0, disparity: int = 1
     for i in range(npairs):
         out[2 * i], out[2 * i + 1] = stereo_pair(h, w, first + i, disparity)
     return out
+
+
+def map_points(xy_un, octave, desc, uright=None, n=2000, seed=0, nlevels=8, scale_factor=1.2):
+    """Synthetic local-map points for ORBmatcher::SearchByProjection (a MAP_POINT_DTYPE array):
+    projections near frame keypoints (several points per keypoint, so they compete), descriptors
+    with 0..60 flipped bits (some unrelated), both RadiusByViewingCos branches, bad / not-in-view /
+    observation-less / far points, and a few projections outside the image."""
+    from . import MAP_POINT_DTYPE, MP_BAD, MP_HAS_OBS, MP_IN_VIEW
+    rng = np.random.default_rng(seed)
+    xy_un = np.asarray(xy_un, np.float32).reshape(-1, 2)
+    octave = np.asarray(octave, np.int32)
+    desc = np.asarray(desc, np.uint8).reshape(-1, 32)
+    nk = len(octave)
+    out = np.zeros(n, MAP_POINT_DTYPE)
+    if nk == 0 or n == 0:
+        return out
+    scale = scale_factor ** np.arange(nlevels, dtype=np.float64)
+    pool = rng.choice(nk, size=max(1, min(nk, n // 2)), replace=False)
+    k = pool[rng.integers(0, len(pool), n)]
+    lvl = np.clip(octave[k] + rng.choice([-1, 0, 0, 0, 1], n), 0, nlevels - 1)
+    noise = rng.normal(0.0, 1.5, (n, 2)) * scale[octave[k]][:, None]
+    p = xy_un[k] + noise
+    outside = rng.random(n) < 0.03
+    p[outside] = rng.uniform(-200, 1200, (int(outside.sum()), 2))
+    out["proj_x"], out["proj_y"] = p[:, 0], p[:, 1]
+    if uright is not None:
+        ur = np.asarray(uright, np.float32)[k]
+        out["proj_xr"] = np.where(ur > 0, ur + rng.normal(0, 2.0, n), p[:, 0] - 20)
+    else:
+        out["proj_xr"] = p[:, 0] - 20
+    out["view_cos"] = rng.choice(np.array([0.9995, 0.999, 0.99, 0.95], np.float32), n)
+    out["depth"] = rng.uniform(0.5, 80.0, n)
+    out["level"] = lvl
+    flags = np.where(rng.random(n) < 0.9, MP_IN_VIEW, 0) | np.where(rng.random(n) < 0.05, MP_BAD, 0) \
+        | np.where(rng.random(n) < 0.9, MP_HAS_OBS, 0)
+    out["flags"] = flags
+    d = desc[k].copy()
+    nflip = rng.choice([0, 2, 5, 10, 20, 35, 60], n)
+    for i in range(n):
+        if nflip[i]:
+            b = np.unpackbits(d[i])
+            b[rng.choice(256, nflip[i], replace=False)] ^= 1
+            d[i] = np.packbits(b)
+    unrelated = rng.random(n) < 0.05
+    d[unrelated] = rng.integers(0, 256, (int(unrelated.sum()), 32), dtype=np.uint8)
+    out["desc"] = d
+    return out
