@@ -195,11 +195,12 @@ struct MapPointIn {  // orbgpu_map_point (60 B)
     uint8_t desc[32];
 };
 constexpr int kMpInView = 1, kMpBad = 2, kMpHasObs = 4;
-constexpr int kSbpMaxKp = 65536;  // keypoints per frame (the LDS occupancy bitmap)
+constexpr int kSbpMaxKp = 18432;  // keypoints per frame: k_sbp_resolve keeps ~8 B per keypoint in LDS
 struct SbpCand {  // k_sbp_candidates -> k_sbp_resolve: 4 lowest (distance, window position)
     int32_t idx[4];
     int32_t key[4];  // dist | octave << 16
     int32_t n;       // candidates after the filters; -1: map point skipped
+    int32_t flags;   // the map point's flags (kMpHasObs decides whether its keypoint is taken)
 };
 struct SbpArgs {
     const MapPointIn* mps;    // all frames' map points, frame f = [mp_off[f], mp_off[f + 1])

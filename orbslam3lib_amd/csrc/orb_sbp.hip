@@ -9,10 +9,12 @@
 //                     The reference's (best, second) pair is exactly the two lowest of that order
 //                     (strict `<` keeps the earlier of equal distances), so removing a candidate
 //                     outside the two lowest changes nothing.
-//   k_sbp_resolve     one wave per frame replays the map points in order from LDS-staged top-4
-//                     lists: the first two candidates not taken during this call are the
-//                     reference's (best, second); only when fewer than two survive out of a window
-//                     holding more than four does it re-walk the window with the live occupancy.
+//   k_sbp_resolve     one wave per frame replays the map points in order, 64 lanes at a time,
+//                     from LDS-staged top-4 lists: the first two candidates not taken so far are
+//                     the reference's (best, second); only when fewer than two survive out of a
+//                     window holding more than four does a lane re-walk its window with the live
+//                     occupancy.  Lanes whose examined candidates an earlier lane of the group
+//                     takes are recomputed after the prefix before them commits.
 #include <hip/hip_runtime.h>
 
 #include "orb_kernels.h"
@@ -139,6 +141,7 @@ __global__ __launch_bounds__(256) void k_sbp_candidates(SbpArgs a) {
     if (i >= m1) return;
     const MapPointIn mp = a.mps[i];
     SbpCand& out = a.cand[i];
+    out.flags = mp.flags;
     float rs;
     if (!mp_window(a, mp, &rs)) {
         out.n = -1;
@@ -164,11 +167,26 @@ __global__ __launch_bounds__(256) void k_sbp_candidates(SbpArgs a) {
     }
 }
 
-constexpr int kResolveChunk = 512;
+constexpr int kResolveChunk = 256;
 
+// Dynamic LDS of k_sbp_resolve for out_cap keypoints: the occupancy bitmap, two per-keypoint
+// lane tables and the staged candidate lists.
+__host__ __device__ inline int sbp_lds_words(int out_cap) { return (out_cap + 31) / 32 + 2 * out_cap; }
+__host__ __device__ inline size_t sbp_lds_bytes(int out_cap) {
+    return 4 * (size_t)sbp_lds_words(out_cap) + sizeof(SbpCand) * kResolveChunk;
+}
+
+// One wave per frame.  The map points are replayed 64 at a time: every pending lane computes
+// its result against the occupancy so far, then the longest prefix of lanes whose examined
+// candidates no earlier lane of the group takes is committed at once (the reference order makes
+// exactly those results final), and the rest retry against the updated occupancy.
 __global__ __launch_bounds__(64) void k_sbp_resolve(SbpArgs a) {
-    __shared__ uint32_t taken[kSbpMaxKp / 32];  // keypoint blocked by an occupant with observations
-    __shared__ SbpCand chunk[kResolveChunk];
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    const int nbits = (a.out_cap + 31) / 32;
+    uint32_t* taken = lds;                       // keypoint held by an occupant with observations
+    uint32_t* owner = lds + nbits;               // lowest lane of the group taking the keypoint
+    int32_t* writer = reinterpret_cast<int32_t*>(owner + a.out_cap);  // last lane assigning it
+    SbpCand* chunk = reinterpret_cast<SbpCand*>(lds + sbp_lds_words(a.out_cap));
     const int f = blockIdx.x, lane = threadIdx.x;
     const int img = (a.img0 + f) * a.image_step;
     const int nkp = a.out_n[img];
@@ -181,60 +199,88 @@ __global__ __launch_bounds__(64) void k_sbp_resolve(SbpArgs a) {
             for (int b = 0; b < 32 && w * 32 + b < nkp; ++b) bits |= (blk[w * 32 + b] ? 1u : 0u) << b;
         taken[w] = bits;
     }
-    for (int k = lane; k < nkp; k += 64) match[k] = -1;
+    for (int k = lane; k < nkp; k += 64) {
+        match[k] = -1;
+        owner[k] = 64;
+        writer[k] = -1;
+    }
     __syncthreads();
     const FrameView F = frame_view(a, f);
+    auto is_taken = [&](int k) { return ((taken[k >> 5] >> (k & 31)) & 1u) != 0; };
     int nmatches = 0;
     for (int c0 = m0; c0 < m1; c0 += kResolveChunk) {
         const int cn = min(kResolveChunk, m1 - c0);
         for (int j = lane; j < cn; j += 64) chunk[j] = a.cand[c0 + j];
         __syncthreads();
-        if (lane == 0) {
-            for (int j = 0; j < cn; ++j) {
-                const SbpCand& c = chunk[j];
-                if (c.n <= 0) continue;
-                int bi = -1, bd = 256, bl = -1, sd = 256, sl = -1, found = 0;
-                for (int t = 0; t < kTop && found < 2; ++t) {
-                    const int k = c.idx[t];
-                    if (k < 0) break;
-                    if ((taken[k >> 5] >> (k & 31)) & 1u) continue;
-                    const int d = c.key[t] & 0xFFFF, l = (int16_t)(c.key[t] >> 16);
-                    if (found == 0) {
-                        bi = k, bd = d, bl = l;
-                    } else {
-                        sd = d, sl = l;
+        for (int g0 = 0; g0 < cn; g0 += 64) {
+            const int j = g0 + lane;
+            bool pending = j < cn;
+            SbpCand c;
+            if (pending) c = chunk[j];
+            while (__ballot(pending)) {
+                int asg = -1, nexam = 0;
+                bool all = false, blocking = false;
+                if (pending && c.n > 0) {
+                    int bi = -1, bd = 256, bl = -1, sd = 256, sl = -1, found = 0;
+                    for (int t = 0; t < kTop && found < 2; ++t) {
+                        const int k = c.idx[t];
+                        if (k < 0) break;
+                        nexam = t + 1;
+                        if (is_taken(k)) continue;
+                        const int d = c.key[t] & 0xFFFF, l = (int16_t)(c.key[t] >> 16);
+                        if (found == 0) {
+                            bi = k, bd = d, bl = l;
+                        } else {
+                            sd = d, sl = l;
+                        }
+                        ++found;
                     }
-                    ++found;
-                }
-                if (found < 2 && c.n > kTop) {  // the top 4 ran dry: walk the window again
-                    const MapPointIn mp = a.mps[c0 + j];
-                    float rs;
-                    mp_window(a, mp, &rs);
-                    uint32_t q[8];
-                    load_desc(mp, q);
-                    bi = -1, bd = 256, bl = -1, sd = 256, sl = -1;
-                    walk_window(a, F, mp, rs, q, [&](int k) { return ((taken[k >> 5] >> (k & 31)) & 1u) != 0; },
-                                [&](int k, int d, int o) {
-                                    if (d < bd) {
-                                        sd = bd, sl = bl;
-                                        bd = d, bl = o, bi = k;
-                                    } else if (d < sd) {
-                                        sd = d, sl = o;
-                                    }
-                                });
-                }
-                if (bd <= 100) {  // TH_HIGH (:124-140)
-                    if (bl == sl && (float)bd > a.nnratio * (float)sd) continue;
-                    if (bl != sl || (float)bd <= a.nnratio * (float)sd) {
-                        match[bi] = c0 + j - m0;
-                        const uint32_t bit = 1u << (bi & 31);
-                        if (a.mps[c0 + j].flags & kMpHasObs)
-                            taken[bi >> 5] |= bit;
-                        else
-                            taken[bi >> 5] &= ~bit;
-                        ++nmatches;
+                    if (found < 2 && c.n > kTop) {  // the top 4 ran dry: walk the window again
+                        all = true;
+                        const MapPointIn mp = a.mps[c0 + j];
+                        float rs;
+                        mp_window(a, mp, &rs);
+                        uint32_t q[8];
+                        load_desc(mp, q);
+                        bi = -1, bd = 256, bl = -1, sd = 256, sl = -1;
+                        walk_window(a, F, mp, rs, q, is_taken, [&](int k, int d, int o) {
+                            if (d < bd) {
+                                sd = bd, sl = bl;
+                                bd = d, bl = o, bi = k;
+                            } else if (d < sd) {
+                                sd = d, sl = o;
+                            }
+                        });
+                    }
+                    // TH_HIGH and the ratio test (:124-140)
+                    if (bd <= 100 && !(bl == sl && (float)bd > a.nnratio * (float)sd) &&
+                        (bl != sl || (float)bd <= a.nnratio * (float)sd)) {
+                        asg = bi;
+                        blocking = (c.flags & kMpHasObs) != 0;
                     }
                 }
+                // a lane is stale if an earlier pending lane takes a candidate it examined (a
+                // lane that walked its whole window: if any earlier lane takes anything)
+                const bool takes = pending && asg >= 0 && blocking;
+                const uint64_t tm = __ballot(takes);
+                if (takes) atomicMin(&owner[asg], (uint32_t)lane);
+                bool stale = false;
+                if (pending) {
+                    if (all) stale = (tm & ((1ull << lane) - 1)) != 0;
+                    for (int t = 0; t < nexam; ++t) stale |= owner[c.idx[t]] < (uint32_t)lane;
+                }
+                if (takes) owner[asg] = 64;
+                const uint64_t st = __ballot(pending && stale);
+                const int first = st ? __builtin_ctzll(st) : 64;
+                const bool commit = pending && lane < first;
+                // the reference keeps the last of several assignments to one keypoint
+                const bool assigns = commit && asg >= 0;
+                if (assigns) atomicMax(&writer[asg], lane);
+                if (assigns && writer[asg] == lane) match[asg] = c0 + j - m0;
+                if (assigns) writer[asg] = -1;
+                if (assigns && blocking) atomicOr(&taken[asg >> 5], 1u << (asg & 31));
+                nmatches += __popcll(__ballot(assigns));
+                pending = pending && !commit;
             }
         }
         __syncthreads();
@@ -248,7 +294,13 @@ hipError_t launch_sbp(const SbpArgs& a, int nframes, int max_mps, hipStream_t st
     if (nframes <= 0) return hipSuccess;
     if (max_mps > 0)
         hipLaunchKernelGGL(k_sbp_candidates, dim3((max_mps + 255) / 256, nframes), dim3(256), 0, st, a);
-    hipLaunchKernelGGL(k_sbp_resolve, dim3(nframes), dim3(64), 0, st, a);
+    const size_t lds = sbp_lds_bytes(a.out_cap);
+    if (lds > 65536) {
+        const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k_sbp_resolve),
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(k_sbp_resolve, dim3(nframes), dim3(64), lds, st, a);
     return hipGetLastError();
 }
 
