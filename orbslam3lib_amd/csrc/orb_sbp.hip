@@ -31,19 +31,21 @@ struct Top4 {
     int n;  // candidates that passed every filter (the window after the skips)
 };
 
+// Insert in (distance, window position) order: candidates arrive in window order, so a new one
+// goes after every kept one of equal distance (strict <).  Fully unrolled so the four slots stay
+// in registers.
 __device__ inline void top_insert(Top4& t, int idx, int dist, int lvl) {
     ++t.n;
-    if (dist >= t.dist[kTop - 1]) return;
-    int j = kTop - 1;
-    while (j > 0 && dist < t.dist[j - 1]) {
-        t.idx[j] = t.idx[j - 1];
-        t.dist[j] = t.dist[j - 1];
-        t.lvl[j] = t.lvl[j - 1];
-        --j;
+    bool shift = false;  // once placed, every later slot moves one down
+#pragma unroll
+    for (int j = 0; j < kTop; ++j) {
+        shift = shift || dist < t.dist[j];
+        if (shift) {
+            const int ti = t.idx[j], td = t.dist[j], tl = t.lvl[j];
+            t.idx[j] = idx, t.dist[j] = dist, t.lvl[j] = lvl;
+            idx = ti, dist = td, lvl = tl;
+        }
     }
-    t.idx[j] = idx;
-    t.dist[j] = dist;
-    t.lvl[j] = lvl;
 }
 
 struct FrameView {
@@ -222,9 +224,10 @@ __global__ __launch_bounds__(64) void k_sbp_resolve(SbpArgs a) {
                 bool all = false, blocking = false;
                 if (pending && c.n > 0) {
                     int bi = -1, bd = 256, bl = -1, sd = 256, sl = -1, found = 0;
-                    for (int t = 0; t < kTop && found < 2; ++t) {
+#pragma unroll
+                    for (int t = 0; t < kTop; ++t) {
                         const int k = c.idx[t];
-                        if (k < 0) break;
+                        if (found >= 2 || k < 0) break;
                         nexam = t + 1;
                         if (is_taken(k)) continue;
                         const int d = c.key[t] & 0xFFFF, l = (int16_t)(c.key[t] >> 16);
@@ -267,7 +270,9 @@ __global__ __launch_bounds__(64) void k_sbp_resolve(SbpArgs a) {
                 bool stale = false;
                 if (pending) {
                     if (all) stale = (tm & ((1ull << lane) - 1)) != 0;
-                    for (int t = 0; t < nexam; ++t) stale |= owner[c.idx[t]] < (uint32_t)lane;
+#pragma unroll
+                    for (int t = 0; t < kTop; ++t)
+                        if (t < nexam) stale |= owner[c.idx[t]] < (uint32_t)lane;
                 }
                 if (takes) owner[asg] = 64;
                 const uint64_t st = __ballot(pending && stale);
