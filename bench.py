@@ -429,6 +429,35 @@ def main():
                "unit": "Mmappoints/s", "kernel_ms_per_step": round(k_ms, 4) if k_ms else None,
                "call_ms_per_step": round(q_el / args.steps * 1e3, 4),
                "map_points_per_frame": args.map_points, "frames_per_step": P, "nmatches_frame0": nm0}
+        # the two-camera form (Nleft != -1, the fisheye rig): grids on the raw positions, both
+        # windows per point, stereo partners from a synthetic one-to-one pairing
+        uniq2, lr = [], []
+        be.undistort_grid(EUROC_K, ())
+        for u in range(U):
+            sides = []
+            for e in range(2):
+                k_, d_, _ = be.result(2 * u + e)
+                xy_, _, _, _ = be.grid_result(2 * u + e)
+                sides.append((xy_, k_["octave"], d_))
+            l2r_, r2l_ = synth.stereo_partners(sides[0][2], sides[1][2], seed=u)
+            lr.append((l2r_, r2l_))
+            uniq2.append(synth.map_points_stereo(sides[0][0], sides[0][1], sides[0][2], sides[1][0],
+                                                 sides[1][1], l2r_, n=args.map_points, seed=7 + u))
+        mp2 = [uniq2[p % U] for p in range(P)]
+        l2rs, r2ls = [lr[p % U][0] for p in range(P)], [lr[p % U][1] for p in range(P)]
+        be.search_by_projection_stereo(mp2, l2rs, r2ls)
+        be.synchronize()
+        be.set_profiling(True, stages=["k_sbp"])
+        be.reset_stage_times()
+        for _ in range(args.steps):
+            be.search_by_projection_stereo(mp2, l2rs, r2ls)
+        be.synchronize()
+        qt2 = be.stage_times().get("k_sbp", (0.0, 0))
+        be.set_profiling(False)
+        k2 = qt2[0] / qt2[1] if qt2[1] else None
+        sbp["two_camera"] = {"value": round(sum_over_ranks(dist, n_mp) / (k2 * 1e-3) / 1e6, 3) if k2 else None,
+                             "unit": "Mmappoints/s", "kernel_ms_per_step": round(k2, 4) if k2 else None,
+                             "nmatches_pair0": be.projection_matches(0)[1]}
 
     # Wire formats: the P side-by-side frames of a step split from the device
     # staging buffer into the batch layout, and the step's results packed to the IDL SoA layout.

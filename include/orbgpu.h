@@ -162,10 +162,14 @@ typedef struct {
     int32_t level;         /* mnTrackScaleLevel, in [0, nlevels) (others are skipped) */
     int32_t flags;         /* ORBGPU_MP_* */
     uint8_t desc[32];      /* GetDescriptor() */
+    float proj_yr;         /* mTrackProjYR     (two-camera frames) */
+    float view_cos_r;      /* mTrackViewCosR   (two-camera frames) */
+    int32_t level_r;       /* mnTrackScaleLevelR (two-camera frames) */
 } orbgpu_map_point;
-#define ORBGPU_MP_IN_VIEW 1  /* mbTrackInView */
-#define ORBGPU_MP_BAD 2      /* isBad() */
-#define ORBGPU_MP_HAS_OBS 4  /* Observations() > 0 */
+#define ORBGPU_MP_IN_VIEW 1    /* mbTrackInView */
+#define ORBGPU_MP_BAD 2        /* isBad() */
+#define ORBGPU_MP_HAS_OBS 4    /* Observations() > 0 */
+#define ORBGPU_MP_IN_VIEW_R 8  /* mbTrackInViewR (two-camera frames) */
 /* mps: all frames' map points, frame f's in [mp_offsets[f], mp_offsets[f + 1]) (host arrays).
  * kp_block (optional, [n_frames][kp_stride] u8): 1 where F.mvpMapPoints[k] is already set to a
  * point with observations before the call.  th / nnratio / far_points / th_far as the reference.
@@ -175,6 +179,18 @@ int orbgpu_search_by_projection_batch(orbgpu_ctx* ctx, int n_frames, int image_s
                                       const orbgpu_map_point* mps, const int32_t* mp_offsets,
                                       const uint8_t* kp_block, int kp_stride, float th, float nnratio,
                                       int far_points, float th_far, void* stream);
+/* Two-camera frames (Nleft != -1, the fisheye rig; ORBmatcher.cc:59-214): frame f = left image
+ * 2f + right image 2f + 1, both gridded by orbgpu_undistort_grid_batch with no distortion
+ * coefficients (the grid is built on the raw positions, Frame.cc:405-436, and the bounds are the
+ * image, :798-825).  left_to_right / right_to_left ([n_pairs][lr_stride], -1 = none; NULL: all
+ * -1) are Frame::mvLeftToRightMatch / mvRightToLeftMatch.  kp_block and the downloaded match
+ * array cover Nleft + Nright keypoints: the left ones, then the right ones (the reference's
+ * mvpMapPoints indexing). */
+int orbgpu_search_by_projection_stereo(orbgpu_ctx* ctx, int n_pairs, const orbgpu_map_point* mps,
+                                       const int32_t* mp_offsets, const int32_t* left_to_right,
+                                       const int32_t* right_to_left, int lr_stride, const uint8_t* kp_block,
+                                       int kp_stride, float th, float nnratio, int far_points, float th_far,
+                                       void* stream);
 int orbgpu_download_projection_matches(orbgpu_ctx* ctx, int frame, int32_t* match, int cap, int* n_kp,
                                        int* nmatches);
 

@@ -276,7 +276,8 @@ def decode_angle(enc):
 
 
 MP_DTYPE = np.dtype([("proj_x", "<f4"), ("proj_y", "<f4"), ("proj_xr", "<f4"), ("view_cos", "<f4"),
-                     ("depth", "<f4"), ("level", "<i4"), ("flags", "<i4"), ("desc", "u1", (32,))])
+                     ("depth", "<f4"), ("level", "<i4"), ("flags", "<i4"), ("desc", "u1", (32,)),
+                     ("proj_yr", "<f4"), ("view_cos_r", "<f4"), ("level_r", "<i4")])
 
 
 def search_by_projection(mps, xy_un, octave, desc, uright, bounds, cell_start, cell_idx, kp_block=None,
@@ -302,3 +303,32 @@ def search_by_projection(mps, xy_un, octave, desc, uright, bounds, cell_start, c
         _p(blk) if blk is not None else None, C.c_float(th), C.c_float(nnratio), int(far_points),
         C.c_float(th_far), _p(match))
     return match[:n], nm
+
+
+def search_by_projection2(mps, left, right, bounds, l2r=None, r2l=None, kp_block=None, th=1.0, nnratio=0.8,
+                          far_points=False, th_far=50.0, scale_factor=1.2, nlevels=8):
+    """Two-camera SearchByProjection (Nleft != -1).  left / right = (xy [n,2], octave [n],
+    desc [n,32], cell_start, cell_idx) -> (match [nl + nr], nmatches)."""
+    mps = np.ascontiguousarray(mps, dtype=MP_DTYPE)
+
+    def prep(side):
+        xy, octv, d, cs, ci = side
+        xy = np.ascontiguousarray(xy, dtype=np.float32).reshape(-1, 2)
+        octv = np.ascontiguousarray(octv, dtype=np.int32)
+        d = np.ascontiguousarray(d, dtype=np.uint8).reshape(-1, 32)
+        cs = np.ascontiguousarray(cs, dtype=np.int32)
+        ci = np.ascontiguousarray(ci if len(ci) else np.zeros(1), dtype=np.int32)
+        return xy, octv, d, cs, ci
+    L, R = prep(left), prep(right)
+    nl, nr = len(L[1]), len(R[1])
+    arr = lambda a, dt: None if a is None else np.ascontiguousarray(a, dtype=dt)
+    l2r, r2l, blk = arr(l2r, np.int32), arr(r2l, np.int32), arr(kp_block, np.uint8)
+    scale = scale_factors(scale_factor, nlevels)[0]
+    match = np.zeros(max(nl + nr, 1), np.int32)
+    pp = lambda a: _p(a) if a is not None and a.size else None
+    nm = lib().oracle_search_by_projection2(
+        pp(mps), len(mps), pp(L[0]), pp(L[1]), pp(L[2]), nl, _p(L[3]), _p(L[4]),
+        pp(R[0]), pp(R[1]), pp(R[2]), nr, _p(R[3]), _p(R[4]), _p(np.ascontiguousarray(bounds, np.float32)),
+        pp(l2r), pp(r2l), _p(scale), nlevels, pp(blk), C.c_float(th), C.c_float(nnratio), int(far_points),
+        C.c_float(th_far), _p(match))
+    return match[:nl + nr], nm

@@ -1270,3 +1270,98 @@ int oracle_search_by_projection(const oracle_map_point* mps, int nmp, const floa
     }
     return nmatches;
 }
+
+int oracle_search_by_projection2(const oracle_map_point* mps, int nmp, const float* xyL, const int32_t* octL,
+                                 const uint8_t* descL, int nl, const int32_t* csL, const int32_t* ciL,
+                                 const float* xyR, const int32_t* octR, const uint8_t* descR, int nr,
+                                 const int32_t* csR, const int32_t* ciR, const float bounds[4],
+                                 const int32_t* l2r, const int32_t* r2l, const float* scale, int nlevels,
+                                 const uint8_t* kp_block, float th, float nnratio, int far_points,
+                                 float th_far, int32_t* match) {
+    const int n = nl + nr;
+    std::vector<uint8_t> blocked(n, 0);  // mvpMapPoints[k] set with Observations() > 0
+    if (kp_block) std::copy(kp_block, kp_block + n, blocked.begin());
+    for (int k = 0; k < n; ++k) match[k] = -1;
+    auto assign = [&](int k, int i, const oracle_map_point& mp) {
+        match[k] = i;
+        blocked[k] = (mp.flags & ORACLE_MP_HAS_OBS) ? 1 : 0;
+    };
+    const bool bFactor = th != 1.0;
+    std::vector<int> cand;
+    int nmatches = 0;
+    for (int i = 0; i < nmp; ++i) {
+        const oracle_map_point& mp = mps[i];
+        if (!(mp.flags & ORACLE_MP_IN_VIEW) && !(mp.flags & ORACLE_MP_IN_VIEW_R)) continue;
+        if (far_points && mp.depth > th_far) continue;
+        if (mp.flags & ORACLE_MP_BAD) continue;
+        if (mp.flags & ORACLE_MP_IN_VIEW) {
+            const int lvl = mp.level;
+            if (lvl >= 0 && lvl < nlevels) {
+                float r = mp.view_cos > 0.998 ? 2.5f : 4.0f;
+                if (bFactor) r *= th;
+                features_in_area(xyL, octL, bounds, csL, ciL, mp.proj_x, mp.proj_y, r * scale[lvl], lvl - 1, lvl, cand);
+                if (!cand.empty()) {
+                    int bestDist = 256, bestLevel = -1, bestDist2 = 256, bestLevel2 = -1, bestIdx = -1;
+                    for (int idx : cand) {
+                        if (blocked[idx]) continue;
+                        const int dist = oracle_descriptor_distance(mp.desc, descL + (size_t)idx * 32);
+                        if (dist < bestDist) {
+                            bestDist2 = bestDist;
+                            bestDist = dist;
+                            bestLevel2 = bestLevel;
+                            bestLevel = octL[idx];
+                            bestIdx = idx;
+                        } else if (dist < bestDist2) {
+                            bestLevel2 = octL[idx];
+                            bestDist2 = dist;
+                        }
+                    }
+                    if (bestDist <= 100) {
+                        if (bestLevel == bestLevel2 && bestDist > nnratio * bestDist2) continue;  // skips the right branch too
+                        if (bestLevel != bestLevel2 || bestDist <= nnratio * bestDist2) {
+                            assign(bestIdx, i, mp);
+                            if (l2r && l2r[bestIdx] != -1) {
+                                assign(l2r[bestIdx] + nl, i, mp);
+                                nmatches++;
+                            }
+                            nmatches++;
+                        }
+                    }
+                }
+            }
+        }
+        if (mp.flags & ORACLE_MP_IN_VIEW_R) {
+            const int lvl = mp.level_r;
+            if (lvl != -1 && lvl >= 0 && lvl < nlevels) {
+                const float r = mp.view_cos_r > 0.998 ? 2.5f : 4.0f;
+                features_in_area(xyR, octR, bounds, csR, ciR, mp.proj_xr, mp.proj_yr, r * scale[lvl], lvl - 1, lvl, cand);
+                if (cand.empty()) continue;
+                int bestDist = 256, bestLevel = -1, bestDist2 = 256, bestLevel2 = -1, bestIdx = -1;
+                for (int idx : cand) {
+                    if (blocked[idx + nl]) continue;
+                    const int dist = oracle_descriptor_distance(mp.desc, descR + (size_t)idx * 32);
+                    if (dist < bestDist) {
+                        bestDist2 = bestDist;
+                        bestDist = dist;
+                        bestLevel2 = bestLevel;
+                        bestLevel = octR[idx];
+                        bestIdx = idx;
+                    } else if (dist < bestDist2) {
+                        bestLevel2 = octR[idx];
+                        bestDist2 = dist;
+                    }
+                }
+                if (bestDist <= 100) {
+                    if (bestLevel == bestLevel2 && bestDist > nnratio * bestDist2) continue;
+                    if (r2l && r2l[bestIdx] != -1) {
+                        assign(r2l[bestIdx], i, mp);
+                        nmatches++;
+                    }
+                    assign(bestIdx + nl, i, mp);
+                    nmatches++;
+                }
+            }
+        }
+    }
+    return nmatches;
+}

@@ -125,14 +125,31 @@ typedef struct {
     int32_t level;  // mnTrackScaleLevel
     int32_t flags;  // ORACLE_MP_* bits
     uint8_t desc[32];
+    float proj_yr, view_cos_r;  // mTrackProjYR, mTrackViewCosR (two-camera frames)
+    int32_t level_r;            // mnTrackScaleLevelR
 } oracle_map_point;
 #define ORACLE_MP_IN_VIEW 1
 #define ORACLE_MP_BAD 2
 #define ORACLE_MP_HAS_OBS 4
+#define ORACLE_MP_IN_VIEW_R 8
 int oracle_search_by_projection(const oracle_map_point* mps, int nmp, const float* xy_un, const int32_t* octave,
                                 const uint8_t* desc, const float* uRight, int n, const float bounds[4],
                                 const int32_t* cell_start, const int32_t* cell_idx, const float* scale,
                                 int nlevels, const uint8_t* kp_block, float th, float nnratio,
                                 int far_points, float th_far, int32_t* match);
+
+// The two-camera form (Nleft != -1, ORBmatcher.cc:59-214): left keypoints [0, nl) and right
+// keypoints [nl, nl + nr) with their own grids (built on the raw positions, as
+// AssignFeaturesToGrid does for Nleft != -1, Frame.cc:405-436), mvLeftToRightMatch /
+// mvRightToLeftMatch (NULL: all -1).  The left branch has no mvuRight test; the right branch
+// uses mTrackProjXR/YR, mTrackViewCosR (no th factor) and mnTrackScaleLevelR.  kp_block and
+// match cover nl + nr keypoints.
+int oracle_search_by_projection2(const oracle_map_point* mps, int nmp, const float* xyL, const int32_t* octL,
+                                 const uint8_t* descL, int nl, const int32_t* csL, const int32_t* ciL,
+                                 const float* xyR, const int32_t* octR, const uint8_t* descR, int nr,
+                                 const int32_t* csR, const int32_t* ciR, const float bounds[4],
+                                 const int32_t* l2r, const int32_t* r2l, const float* scale, int nlevels,
+                                 const uint8_t* kp_block, float th, float nnratio, int far_points,
+                                 float th_far, int32_t* match);
 
 }  // extern "C"

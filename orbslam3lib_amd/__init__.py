@@ -26,8 +26,9 @@ LIB_PATH = os.path.join(HERE, "liborbgpu.so")
 
 # orbgpu_map_point (60 B): the MapPoint state ORBmatcher::SearchByProjection reads
 MAP_POINT_DTYPE = np.dtype([("proj_x", "<f4"), ("proj_y", "<f4"), ("proj_xr", "<f4"), ("view_cos", "<f4"),
-                            ("depth", "<f4"), ("level", "<i4"), ("flags", "<i4"), ("desc", "u1", (32,))])
-MP_IN_VIEW, MP_BAD, MP_HAS_OBS = 1, 2, 4
+                            ("depth", "<f4"), ("level", "<i4"), ("flags", "<i4"), ("desc", "u1", (32,)),
+                            ("proj_yr", "<f4"), ("view_cos_r", "<f4"), ("level_r", "<i4")])
+MP_IN_VIEW, MP_BAD, MP_HAS_OBS, MP_IN_VIEW_R = 1, 2, 4, 8
 
 # cv::KeyPoint layout (28 B)
 KEYPOINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
@@ -43,7 +44,8 @@ EXPORTED = [
     "orbgpu_image_bounds", "orbgpu_undistort_grid_batch", "orbgpu_download_grid",
     "orbgpu_device_sbs_input", "orbgpu_upload_sbs", "orbgpu_ingest_sbs", "orbgpu_pack_soa",
     "orbgpu_download_soa", "orbgpu_download_matches16", "orbgpu_extract_features",
-    "orbgpu_search_by_projection_batch", "orbgpu_download_projection_matches",
+    "orbgpu_search_by_projection_batch", "orbgpu_search_by_projection_stereo",
+    "orbgpu_download_projection_matches",
     "orbgpu_set_profiling", "orbgpu_num_stages", "orbgpu_stage_name", "orbgpu_stage_times",
     "orbgpu_reset_stage_times", "orbgpu_last_error", "orbgpu_abi_version",
 ]
@@ -400,6 +402,41 @@ class BatchExtractor:
             self.ctx.handle, nf, int(image_step), int(use_uright), _p(mps) if len(mps) else None, _p(off),
             _p(blk) if blk is not None else None, stride, C.c_float(th), C.c_float(nnratio),
             int(far_points), C.c_float(th_far), C.c_void_p(stream) if stream else None))
+
+    def search_by_projection_stereo(self, map_points, left_to_right=None, right_to_left=None, kp_block=None,
+                                    th=1.0, nnratio=0.8, far_points=False, th_far=50.0, stream=None):
+        """The two-camera SearchByProjection (Nleft != -1, ORBmatcher.cc:59-214) on every stereo
+        pair of the last run() (grids from undistort_grid(K, ())); left_to_right / right_to_left:
+        per pair int32 arrays (mvLeftToRightMatch / mvRightToLeftMatch); kp_block per pair over
+        Nleft + Nright keypoints."""
+        nf = len(map_points)
+        mps = np.ascontiguousarray(np.concatenate([np.asarray(m, MAP_POINT_DTYPE) for m in map_points])
+                                   if nf else np.zeros(0, MAP_POINT_DTYPE))
+        off = np.zeros(nf + 1, np.int32)
+        off[1:] = np.cumsum([len(m) for m in map_points])
+
+        def rows(lst, dtype, fill):
+            if lst is None:
+                return None, 0
+            stride = max(1, max(len(x) for x in lst))
+            out = np.full((nf, stride), fill, dtype)
+            for f, x in enumerate(lst):
+                out[f, :len(x)] = x
+            return out, stride
+        l2r, lrs = rows(left_to_right, np.int32, -1)
+        r2l, lrs2 = rows(right_to_left, np.int32, -1)
+        if l2r is not None and r2l is not None and lrs != lrs2:
+            w = max(lrs, lrs2)
+            l2r = np.pad(l2r, ((0, 0), (0, w - lrs)), constant_values=-1)
+            r2l = np.pad(r2l, ((0, 0), (0, w - lrs2)), constant_values=-1)
+            lrs = w
+        lrs = lrs or lrs2
+        blk, bst = rows(kp_block, np.uint8, 0)
+        _check(_lib.orbgpu_search_by_projection_stereo(
+            self.ctx.handle, nf, _p(mps) if len(mps) else None, _p(off),
+            _p(l2r) if l2r is not None else None, _p(r2l) if r2l is not None else None, lrs,
+            _p(blk) if blk is not None else None, bst, C.c_float(th), C.c_float(nnratio), int(far_points),
+            C.c_float(th_far), C.c_void_p(stream) if stream else None))
 
     def projection_matches(self, frame, cap=65536):
         """(match [n_kp] int32: map point index or -1, nmatches) of frame `frame`."""

@@ -189,18 +189,22 @@ struct SoaArgs {
     int16_t *idx16, *d1_16, *d2_16;
 };
 // ORBmatcher::SearchByProjection over device-resident frames (orb_sbp.hip).
-struct MapPointIn {  // orbgpu_map_point (60 B)
+struct MapPointIn {  // orbgpu_map_point (72 B)
     float proj_x, proj_y, proj_xr, view_cos, depth;
     int32_t level, flags;
     uint8_t desc[32];
+    float proj_yr, view_cos_r;  // right camera of a two-camera frame
+    int32_t level_r;
 };
-constexpr int kMpInView = 1, kMpBad = 2, kMpHasObs = 4;
-constexpr int kSbpMaxKp = 18432;  // keypoints per frame: k_sbp_resolve keeps ~8 B per keypoint in LDS
+constexpr int kMpInView = 1, kMpBad = 2, kMpHasObs = 4, kMpInViewR = 8;
 struct SbpCand {  // k_sbp_candidates -> k_sbp_resolve: 4 lowest (distance, window position)
     int32_t idx[4];
-    int32_t key[4];  // dist | octave << 16
-    int32_t n;       // candidates after the filters; -1: map point skipped
-    int32_t flags;   // the map point's flags (kMpHasObs decides whether its keypoint is taken)
+    int32_t key[4];   // dist | octave << 16
+    int32_t n;        // candidates after the filters; -1: map point skipped
+    int32_t flags;    // the map point's flags (kMpHasObs decides whether its keypoint is taken)
+    int32_t idxR[4];  // the same for the right-camera window (two-camera frames)
+    int32_t keyR[4];
+    int32_t nR;       // -1: no right-camera search
 };
 struct SbpArgs {
     const MapPointIn* mps;    // all frames' map points, frame f = [mp_off[f], mp_off[f + 1])
@@ -213,17 +217,21 @@ struct SbpArgs {
     const int32_t* cell_start;
     const int32_t* cell_idx;
     const uint8_t* desc;      // out_desc
-    const float* uright;      // [frame][out_cap] mvuRight or nullptr
-    const uint8_t* kp_block;  // [frame][out_cap] pre-call occupant with observations, or nullptr
+    const float* uright;      // [frame][out_cap] mvuRight or nullptr (pinhole frames)
+    const uint8_t* kp_block;  // [frame][2 * out_cap] pre-call occupant with observations, or nullptr
+    const int32_t* l2r;       // [frame][out_cap] mvLeftToRightMatch (two-camera frames) or nullptr
+    const int32_t* r2l;       // [frame][out_cap] mvRightToLeftMatch or nullptr
+    int two_cam;              // Nleft != -1: frame f = images 2f (left) and 2f + 1 (right)
     int image_step, img0;     // frame f = batch image (img0 + f) * image_step; img0 = first frame
     float bounds[4], grid_inv[2];
     float scale[kMaxLevels];
     int nlevels;
     float th, nnratio, th_far;
     int far_points, factor;
-    int32_t* match;           // [frame][out_cap]
+    int32_t* match;           // [frame][2 * out_cap]: left keypoints, then right ones
     int32_t* nmatches;        // [frame]
 };
+size_t sbp_resolve_lds_bytes(int out_cap, int two_cam);
 hipError_t launch_sbp(const SbpArgs& a, int nframes, int max_mps, hipStream_t st);
 
 hipError_t launch_sbs_split(const SbsArgs& a, hipStream_t st);

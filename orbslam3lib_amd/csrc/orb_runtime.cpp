@@ -104,9 +104,9 @@ struct orbgpu_ctx {
     DevBuf input, pyr, blur, rtab, cellkeys, cellcnt, octws, lvlkey, lvlangle, lvldesc, lvlcnt,
         status, outkps, outdesc, outn, outmono, laps, midx1, mdist1, midx2, mdist2, mnq, scratch,
         octdbg, knnpart, strow, stidx, stur, stdepth, stsad, gxy, gcell, gstart, gidx, sbs, soa, m16,
-        sbpmp, sbpoff, sbpcand, sbpblk, sbpmatch, sbpnm;
+        sbpmp, sbpoff, sbpcand, sbpblk, sbpmatch, sbpnm, sbplr;
     float grid_bounds[4] = {0, 0, 0, 0}, grid_inv[2] = {0, 0};  // of the last undistort_grid
-    int sbp_frames = 0, sbp_step = 1;
+    int sbp_frames = 0, sbp_step = 1, sbp_two_cam = 0;
     int soa_images = 0, soa_pairs = 0;  // coverage of the last orbgpu_pack_soa
     int grid_images = 0;   // images of the last orbgpu_undistort_grid_batch
     int stereo_pairs = 0;  // pairs of the last orbgpu_stereo_matches_batch
@@ -588,7 +588,7 @@ int orbgpu_destroy(orbgpu_ctx* c) {
                       &c->knnpart, &c->strow,  &c->stidx, &c->stur,    &c->stdepth,  &c->stsad,
                       &c->gxy,     &c->gcell,  &c->gstart, &c->gidx,    &c->sbs,      &c->soa,
                       &c->m16,     &c->sbpmp,  &c->sbpoff, &c->sbpcand, &c->sbpblk,  &c->sbpmatch,
-                      &c->sbpnm};
+                      &c->sbpnm,   &c->sbplr};
     for (DevBuf* b : bufs) b->release();
     for (size_t k = 1; k < c->sub.size(); ++k) hipStreamDestroy(c->sub[k]);
     if (c->fork) hipEventDestroy(c->fork);
@@ -1294,18 +1294,24 @@ int orbgpu_extract_features(orbgpu_ctx* c, const uint8_t* image, int image_len, 
     return r;
 }
 
-int orbgpu_search_by_projection_batch(orbgpu_ctx* c, int n_frames, int image_step, int use_uright,
-                                      const orbgpu_map_point* mps, const int32_t* mp_offsets,
-                                      const uint8_t* kp_block, int kp_stride, float th, float nnratio,
-                                      int far_points, float th_far, void* stream) {
+namespace {
+
+// Shared by the pinhole and two-camera entry points (orb_sbp.hip).
+int sbp_run(orbgpu_ctx* c, int n_frames, int image_step, int two_cam, int use_uright,
+            const orbgpu_map_point* mps, const int32_t* mp_offsets, const int32_t* l2r, const int32_t* r2l,
+            int lr_stride, const uint8_t* kp_block, int kp_stride, float th, float nnratio, int far_points,
+            float th_far, void* stream) {
     static_assert(sizeof(orbgpu_map_point) == sizeof(MapPointIn), "map point layout");
     if (!c || !mp_offsets || n_frames < 1) return fail(ORBGPU_ERR_INVALID, "null argument");
-    if (image_step < 1 || (long long)(n_frames - 1) * image_step >= c->grid_images)
+    const int images_needed = (n_frames - 1) * image_step + (two_cam ? 2 : 1);
+    if (image_step < 1 || images_needed > c->grid_images)
         return fail(ORBGPU_ERR_INVALID, "frames must lie in the last orbgpu_undistort_grid_batch");
     if (use_uright && (image_step != 2 || n_frames > c->stereo_pairs))
         return fail(ORBGPU_ERR_INVALID, "mvuRight needs image_step 2 and a stereo_matches_batch over the pairs");
-    if (c->out_cap > kSbpMaxKp) return fail(ORBGPU_ERR_CAPACITY, "keypoint capacity above the matcher's");
-    if (kp_block && kp_stride < 1) return fail(ORBGPU_ERR_INVALID, "kp_stride");
+    if (sbp_resolve_lds_bytes(c->out_cap, two_cam) > 160 * 1024)
+        return fail(ORBGPU_ERR_CAPACITY, "keypoint capacity above the matcher's LDS budget");
+    if ((kp_block && kp_stride < 1) || ((l2r || r2l) && lr_stride < 1))
+        return fail(ORBGPU_ERR_INVALID, "stride");
     const int total = mp_offsets[n_frames];
     int max_mps = 0;
     for (int f = 0; f < n_frames; ++f) {
@@ -1314,12 +1320,13 @@ int orbgpu_search_by_projection_batch(orbgpu_ctx* c, int n_frames, int image_ste
     }
     if (total > 0 && !mps) return fail(ORBGPU_ERR_INVALID, "null map points");
     HIP_TRY(hipSetDevice(c->device));
-    const size_t cap = (size_t)c->out_cap;
+    const size_t cap = (size_t)c->out_cap, ncap = two_cam ? 2 * cap : cap;
     if (c->sbpmp.ensure((size_t)total * sizeof(MapPointIn) + 256) ||
         c->sbpoff.ensure((size_t)(n_frames + 1) * 4 + 256) ||
         c->sbpcand.ensure((size_t)total * sizeof(SbpCand) + 256) ||
-        c->sbpmatch.ensure((size_t)n_frames * cap * 4 + 256) || c->sbpnm.ensure((size_t)n_frames * 4 + 256) ||
-        (kp_block && c->sbpblk.ensure((size_t)n_frames * cap + 256)))
+        c->sbpmatch.ensure((size_t)n_frames * ncap * 4 + 256) || c->sbpnm.ensure((size_t)n_frames * 4 + 256) ||
+        (kp_block && c->sbpblk.ensure((size_t)n_frames * ncap + 256)) ||
+        ((l2r || r2l) && c->sbplr.ensure((size_t)n_frames * cap * 8 + 256)))
         return fail(ORBGPU_ERR_HIP, "hipMalloc failed (projection search)");
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
     int r = join_all(c, s);  // keypoints, grid and mvuRight come from the chunk streams
@@ -1328,9 +1335,20 @@ int orbgpu_search_by_projection_batch(orbgpu_ctx* c, int n_frames, int image_ste
     if (total) HIP_TRY(hipMemcpyAsync(c->sbpmp.p, mps, (size_t)total * sizeof(MapPointIn), hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemcpyAsync(c->sbpoff.p, mp_offsets, (size_t)(n_frames + 1) * 4, hipMemcpyHostToDevice, s));
     if (kp_block) {
-        const size_t wcopy = std::min((size_t)kp_stride, cap);
-        HIP_TRY(hipMemsetAsync(c->sbpblk.p, 0, (size_t)n_frames * cap, s));
-        HIP_TRY(hipMemcpy2DAsync(c->sbpblk.p, cap, kp_block, kp_stride, wcopy, n_frames, hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemsetAsync(c->sbpblk.p, 0, (size_t)n_frames * ncap, s));
+        HIP_TRY(hipMemcpy2DAsync(c->sbpblk.p, ncap, kp_block, kp_stride, std::min((size_t)kp_stride, ncap),
+                                 n_frames, hipMemcpyHostToDevice, s));
+    }
+    int32_t* dl2r = c->sbplr.as<int32_t>();
+    int32_t* dr2l = dl2r ? dl2r + (size_t)n_frames * cap : nullptr;
+    const size_t lrw = std::min((size_t)lr_stride, cap) * 4;
+    if (l2r) {
+        HIP_TRY(hipMemsetAsync(dl2r, 0xFF, (size_t)n_frames * cap * 4, s));
+        HIP_TRY(hipMemcpy2DAsync(dl2r, cap * 4, l2r, (size_t)lr_stride * 4, lrw, n_frames, hipMemcpyHostToDevice, s));
+    }
+    if (r2l) {
+        HIP_TRY(hipMemsetAsync(dr2l, 0xFF, (size_t)n_frames * cap * 4, s));
+        HIP_TRY(hipMemcpy2DAsync(dr2l, cap * 4, r2l, (size_t)lr_stride * 4, lrw, n_frames, hipMemcpyHostToDevice, s));
     }
     SbpArgs a{};
     a.mps = c->sbpmp.as<MapPointIn>();
@@ -1345,6 +1363,9 @@ int orbgpu_search_by_projection_batch(orbgpu_ctx* c, int n_frames, int image_ste
     a.desc = c->outdesc.as<uint8_t>();
     a.uright = use_uright ? c->stur.as<float>() : nullptr;
     a.kp_block = kp_block ? c->sbpblk.as<uint8_t>() : nullptr;
+    a.l2r = l2r ? dl2r : nullptr;
+    a.r2l = r2l ? dr2l : nullptr;
+    a.two_cam = two_cam;
     a.image_step = image_step;
     a.img0 = 0;
     std::memcpy(a.bounds, c->grid_bounds, sizeof a.bounds);
@@ -1363,8 +1384,28 @@ int orbgpu_search_by_projection_batch(orbgpu_ctx* c, int n_frames, int image_ste
     HIP_TRY(hipStreamSynchronize(s));  // the pageable uploads above
     c->sbp_frames = n_frames;
     c->sbp_step = image_step;
+    c->sbp_two_cam = two_cam;
     c->need_fork = true;
     return ORBGPU_OK;
+}
+
+}  // namespace
+
+int orbgpu_search_by_projection_batch(orbgpu_ctx* c, int n_frames, int image_step, int use_uright,
+                                      const orbgpu_map_point* mps, const int32_t* mp_offsets,
+                                      const uint8_t* kp_block, int kp_stride, float th, float nnratio,
+                                      int far_points, float th_far, void* stream) {
+    return sbp_run(c, n_frames, image_step, 0, use_uright, mps, mp_offsets, nullptr, nullptr, 0, kp_block,
+                   kp_stride, th, nnratio, far_points, th_far, stream);
+}
+
+int orbgpu_search_by_projection_stereo(orbgpu_ctx* c, int n_pairs, const orbgpu_map_point* mps,
+                                       const int32_t* mp_offsets, const int32_t* left_to_right,
+                                       const int32_t* right_to_left, int lr_stride, const uint8_t* kp_block,
+                                       int kp_stride, float th, float nnratio, int far_points, float th_far,
+                                       void* stream) {
+    return sbp_run(c, n_pairs, 2, 1, 0, mps, mp_offsets, left_to_right, right_to_left, lr_stride, kp_block,
+                   kp_stride, th, nnratio, far_points, th_far, stream);
 }
 
 int orbgpu_download_projection_matches(orbgpu_ctx* c, int frame, int32_t* match, int cap, int* n_kp,
@@ -1372,14 +1413,17 @@ int orbgpu_download_projection_matches(orbgpu_ctx* c, int frame, int32_t* match,
     if (!c || frame < 0 || frame >= c->sbp_frames) return fail(ORBGPU_ERR_INVALID, "bad frame");
     HIP_TRY(hipSetDevice(c->device));
     HIP_TRY(hipDeviceSynchronize());
-    int32_t nk = 0, nm = 0;
-    HIP_TRY(hipMemcpy(&nk, c->outn.as<int32_t>() + (size_t)frame * c->sbp_step, 4, hipMemcpyDeviceToHost));
+    int32_t nk[2] = {0, 0}, nm = 0;
+    const size_t img = (size_t)frame * c->sbp_step;
+    HIP_TRY(hipMemcpy(nk, c->outn.as<int32_t>() + img, c->sbp_two_cam ? 8 : 4, hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(&nm, c->sbpnm.as<int32_t>() + frame, 4, hipMemcpyDeviceToHost));
-    if (n_kp) *n_kp = nk;
+    const int n = nk[0] + nk[1];
+    if (n_kp) *n_kp = n;
     if (nmatches) *nmatches = nm;
-    if (nk > cap) return fail(ORBGPU_ERR_CAPACITY, "caller capacity too small");
-    if (match && nk)
-        HIP_TRY(hipMemcpy(match, c->sbpmatch.as<int32_t>() + (size_t)frame * c->out_cap, 4 * (size_t)nk,
+    if (n > cap) return fail(ORBGPU_ERR_CAPACITY, "caller capacity too small");
+    const size_t ncap = c->sbp_two_cam ? 2 * (size_t)c->out_cap : (size_t)c->out_cap;
+    if (match && n)
+        HIP_TRY(hipMemcpy(match, c->sbpmatch.as<int32_t>() + (size_t)frame * ncap, 4 * (size_t)n,
                           hipMemcpyDeviceToHost));
     return ORBGPU_OK;
 }

@@ -133,3 +133,54 @@ def map_points(xy_un, octave, desc, uright=None, n=2000, seed=0, nlevels=8, scal
     d[unrelated] = rng.integers(0, 256, (int(unrelated.sum()), 32), dtype=np.uint8)
     out["desc"] = d
     return out
+
+
+def map_points_stereo(xyL, octL, descL, xyR, octR, l2r, n=2000, seed=0, nlevels=8, scale_factor=1.2):
+    """Map points for the two-camera SearchByProjection: the left-window fields as map_points(),
+    plus a right-camera projection next to the stereo partner of the source keypoint (or a random
+    right keypoint), its own level / viewing cosine, and mbTrackInViewR on ~80% of the points."""
+    from . import MP_IN_VIEW, MP_IN_VIEW_R
+    rng = np.random.default_rng(seed + 1000)
+    out = map_points(xyL, octL, descL, None, n=n, seed=seed, nlevels=nlevels, scale_factor=scale_factor)
+    xyR = np.asarray(xyR, np.float32).reshape(-1, 2)
+    octR = np.asarray(octR, np.int32)
+    if len(octR) == 0 or n == 0:
+        return out
+    l2r = np.asarray(l2r, np.int32)
+    scale = scale_factor ** np.arange(nlevels, dtype=np.float64)
+    # the source keypoint map_points drew from is the closest left keypoint to the projection
+    src = np.argmin(((xyL[None, :, :] - np.stack([out["proj_x"], out["proj_y"]], 1)[:, None, :]) ** 2).sum(2), 1) \
+        if len(xyL) <= 4096 else rng.integers(0, len(xyL), n)
+    partner = l2r[src]
+    kr = np.where(partner >= 0, partner, rng.integers(0, len(octR), n))
+    noise = rng.normal(0.0, 1.5, (n, 2)) * scale[octR[kr]][:, None]
+    out["proj_xr"] = xyR[kr, 0] + noise[:, 0]
+    out["proj_yr"] = xyR[kr, 1] + noise[:, 1]
+    out["level_r"] = np.clip(octR[kr] + rng.choice([-1, 0, 0, 0, 1], n), 0, nlevels - 1)
+    out["level_r"][rng.random(n) < 0.03] = -1
+    out["view_cos_r"] = rng.choice(np.array([0.9995, 0.999, 0.99, 0.95], np.float32), n)
+    inr = rng.random(n) < 0.8
+    out["flags"] = (out["flags"] & ~MP_IN_VIEW_R) | np.where(inr, MP_IN_VIEW_R, 0)
+    # some points only in the right view
+    only_r = rng.random(n) < 0.05
+    out["flags"] = np.where(only_r, (out["flags"] & ~MP_IN_VIEW) | MP_IN_VIEW_R, out["flags"])
+    return out
+
+
+def stereo_partners(descL, descR, seed=0, frac=0.6):
+    """Synthetic mvLeftToRightMatch / mvRightToLeftMatch: a consistent one-to-one pairing of a
+    fraction of the left keypoints with right keypoints (mutual best Hamming where possible)."""
+    rng = np.random.default_rng(seed)
+    nl, nr = len(descL), len(descR)
+    l2r = np.full(nl, -1, np.int32)
+    r2l = np.full(nr, -1, np.int32)
+    if nl == 0 or nr == 0:
+        return l2r, r2l
+    cand = rng.permutation(nl)[:int(frac * nl)]
+    free = np.ones(nr, bool)
+    for i in cand:
+        j = int(rng.integers(0, nr))
+        if free[j]:
+            l2r[i], r2l[j] = j, i
+            free[j] = False
+    return l2r, r2l

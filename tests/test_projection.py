@@ -178,3 +178,167 @@ def test_gpu_search_by_projection_empty_map(oracle):
     be.search_by_projection([np.zeros(0, og.MAP_POINT_DTYPE)], image_step=2, use_uright=False)
     gm, gnm = be.projection_matches(0)
     assert gnm == 0 and (gm == -1).all()
+
+
+# ---- two-camera frames (Nleft != -1, ORBmatcher.cc:59-214) -------------------------------------
+
+def _py_window(xy, octv, cs, ci, bounds, x, y, rs, lvl):
+    wi = F32(F32(64) / F32(bounds[1] - bounds[0]))
+    hi = F32(F32(48) / F32(bounds[3] - bounds[2]))
+    x0 = max(0, int(math.floor(F32(F32(F32(x - bounds[0]) - rs) * wi))))
+    x1 = min(63, int(math.ceil(F32(F32(F32(x - bounds[0]) + rs) * wi))))
+    y0 = max(0, int(math.floor(F32(F32(F32(y - bounds[2]) - rs) * hi))))
+    y1 = min(47, int(math.ceil(F32(F32(F32(y - bounds[2]) + rs) * hi))))
+    if x0 >= 64 or x1 < 0 or y0 >= 48 or y1 < 0:
+        return []
+    out = []
+    for ix in range(x0, x1 + 1):
+        for iy in range(y0, y1 + 1):
+            for k in ci[cs[ix * 48 + iy]:cs[ix * 48 + iy + 1]]:
+                if lvl - 1 <= octv[k] <= lvl and abs(F32(xy[k, 0] - x)) < rs and abs(F32(xy[k, 1] - y)) < rs:
+                    out.append(int(k))
+    return out
+
+
+def _py_best(mp_desc, cand, desc, octv, blocked):
+    best, second = (256, -1, -1), (256, -1)
+    for k in cand:
+        if blocked(k):
+            continue
+        d = int(np.unpackbits(np.bitwise_xor(mp_desc, desc[k])).sum())
+        if d < best[0]:
+            second = best[:2]
+            best = (d, int(octv[k]), k)
+        elif d < second[0]:
+            second = (d, int(octv[k]))
+    return best, second
+
+
+def _py_sbp2(mps, L, R, bounds, l2r, r2l, blk, th, nnratio, far, th_far, scale):
+    (xyL, octL, dL, csL, ciL), (xyR, octR, dR, csR, ciR) = L, R
+    nl, nr = len(octL), len(octR)
+    blocked = np.zeros(nl + nr, bool) if blk is None else blk.astype(bool).copy()
+    match = np.full(nl + nr, -1, np.int32)
+    nm = 0
+
+    def assign(k, i, mp):
+        match[k] = i
+        blocked[k] = bool(mp["flags"] & 4)
+    for i, mp in enumerate(mps):
+        if not (mp["flags"] & 9) or (far and mp["depth"] > F32(th_far)) or (mp["flags"] & 2):
+            continue
+        if mp["flags"] & 1:
+            lvl = int(mp["level"])
+            r = F32(2.5) if float(mp["view_cos"]) > 0.998 else F32(4.0)
+            if F32(th) != 1.0:
+                r = F32(r * F32(th))
+            cand = _py_window(xyL, octL, csL, ciL, bounds, F32(mp["proj_x"]), F32(mp["proj_y"]),
+                              F32(r * F32(scale[lvl])), lvl)
+            if cand:
+                (bd, bl, bi), (sd, sl) = _py_best(mp["desc"], cand, dL, octL, lambda k: blocked[k])
+                if bd <= 100:
+                    if bl == sl and F32(bd) > F32(F32(nnratio) * F32(sd)):
+                        continue
+                    if bl != sl or F32(bd) <= F32(F32(nnratio) * F32(sd)):
+                        assign(bi, i, mp)
+                        if l2r is not None and l2r[bi] != -1:
+                            assign(nl + l2r[bi], i, mp)
+                            nm += 1
+                        nm += 1
+        if mp["flags"] & 8:
+            lvl = int(mp["level_r"])
+            if lvl == -1:
+                continue
+            r = F32(2.5) if float(mp["view_cos_r"]) > 0.998 else F32(4.0)
+            cand = _py_window(xyR, octR, csR, ciR, bounds, F32(mp["proj_xr"]), F32(mp["proj_yr"]),
+                              F32(r * F32(scale[lvl])), lvl)
+            if not cand:
+                continue
+            (bd, bl, bi), (sd, sl) = _py_best(mp["desc"], cand, dR, octR, lambda k: blocked[nl + k])
+            if bd <= 100:
+                if bl == sl and F32(bd) > F32(F32(nnratio) * F32(sd)):
+                    continue
+                if r2l is not None and r2l[bi] != -1:
+                    assign(int(r2l[bi]), i, mp)
+                    nm += 1
+                assign(nl + bi, i, mp)
+                nm += 1
+    return match, nm
+
+
+def _two_cam_frame(oracle, seed, nf=1000):
+    Li, Ri = synth.stereo_pair(480, 640, seed)
+    kl, dl, _ = oracle.extract(Li, nfeatures=nf)
+    kr, dr, _ = oracle.extract(Ri, nfeatures=nf)
+    xl, b, _, csl, cil = oracle.undistort_grid(kl, K_, (), 640, 480)
+    xr, _, _, csr, cir = oracle.undistort_grid(kr, K_, (), 640, 480)
+    return (xl, kl["octave"], dl.reshape(-1, 32), csl, cil), (xr, kr["octave"], dr.reshape(-1, 32), csr, cir), b
+
+
+@pytest.mark.parametrize("th,far,blocked,partners", [(1.0, False, False, True), (3.0, True, True, True),
+                                                      (1.0, False, True, False)])
+def test_oracle_two_camera_matches_python_restatement(oracle, th, far, blocked, partners):
+    L, R, b = _two_cam_frame(oracle, 7)
+    l2r, r2l = synth.stereo_partners(L[2], R[2], seed=2) if partners else (None, None)
+    mps = synth.map_points_stereo(L[0], L[1], L[2], R[0], R[1],
+                                  l2r if l2r is not None else np.full(len(L[1]), -1), n=400, seed=13)
+    blk = None
+    if blocked:
+        blk = (np.random.default_rng(4).random(len(L[1]) + len(R[1])) < 0.1).astype(np.uint8)
+    m, nm = oracle.search_by_projection2(mps, L, R, b, l2r, r2l, blk, th, 0.8, far, 20.0)
+    pm, pnm = _py_sbp2(mps, L, R, b, l2r, r2l, blk, th, 0.8, far, 20.0, oracle.scale_factors()[0])
+    np.testing.assert_array_equal(m, pm)
+    assert nm == pnm
+    assert (m[len(L[1]):] >= 0).sum() > 20 and (m[:len(L[1])] >= 0).sum() > 20  # both windows match
+
+
+def test_oracle_two_camera_left_only_equals_pinhole_without_uright(oracle):
+    """With no right-camera points and no partners the two-camera form is the pinhole form
+    without the mvuRight test."""
+    L, R, b = _two_cam_frame(oracle, 8)
+    mps = synth.map_points(L[0], L[1], L[2], None, n=300, seed=5)
+    m2, nm2 = oracle.search_by_projection2(mps, L, R, b)
+    m1, nm1 = oracle.search_by_projection(mps, L[0], L[1], L[2], None, b, L[3], L[4])
+    np.testing.assert_array_equal(m2[:len(L[1])], m1)
+    assert (m2[len(L[1]):] == -1).all() and nm1 == nm2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("th,far,blocked,partners,n_mp", [(1.0, False, False, True, 3000),
+                                                           (3.0, True, True, True, 3000),
+                                                           (1.0, False, True, False, 2000),
+                                                           (1.0, False, True, True, 8000)])
+def test_gpu_search_by_projection_two_camera_bit_exact(oracle, th, far, blocked, partners, n_mp):
+    import orbslam3lib_amd as og
+    pairs = [synth.stereo_pair(480, 640, 70 + s) for s in range(3)]
+    be = og.BatchExtractor(2000, 1.2, 8, 20, 7, width=640, height=480, max_images=6)
+    be.upload(np.stack([im for pr in pairs for im in pr]))
+    be.run()
+    be.undistort_grid(K_, ())
+    be.synchronize()
+    rng = np.random.default_rng(21)
+    sides, mps_all, l2rs, r2ls, blks = [], [], [], [], []
+    for p in range(len(pairs)):
+        side = []
+        for e in range(2):
+            kps, desc, _ = be.result(2 * p + e)
+            xy, _, cs, ci = be.grid_result(2 * p + e)
+            side.append((xy, kps["octave"], desc, cs, ci))
+        L, R = side
+        l2r, r2l = synth.stereo_partners(L[2], R[2], seed=p) if partners else (None, None)
+        mps_all.append(synth.map_points_stereo(L[0], L[1], L[2], R[0], R[1],
+                                               l2r if l2r is not None else np.full(len(L[1]), -1),
+                                               n=n_mp, seed=40 + p))
+        blks.append((rng.random(len(L[1]) + len(R[1])) < 0.08).astype(np.uint8) if blocked else None)
+        sides.append(side)
+        l2rs.append(l2r)
+        r2ls.append(r2l)
+    be.search_by_projection_stereo(mps_all, l2rs if partners else None, r2ls if partners else None,
+                                   blks if blocked else None, th=th, nnratio=0.8, far_points=far, th_far=20.0)
+    be.synchronize()
+    b = np.array([0, 640, 0, 480], np.float32)
+    for p, (L, R) in enumerate(sides):
+        m, nm = oracle.search_by_projection2(mps_all[p], L, R, b, l2rs[p], r2ls[p], blks[p], th, 0.8, far, 20.0)
+        gm, gnm = be.projection_matches(p)
+        np.testing.assert_array_equal(gm, m, err_msg="pair %d" % p)
+        assert gnm == nm, (p, gnm, nm)
