@@ -15,4 +15,5 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/pro
 echo prof-done
 bash tools/pmc_traffic.sh $O/pmct
 python3 tools/traffic.py $O/pmct $O/traffic.json > /dev/null
+python3 tools/roofline_check.py $O/bench.json $O/prof/run_kernel_trace.csv > $O/roofline_check.json
 echo all-done
