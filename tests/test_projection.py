@@ -342,3 +342,36 @@ def test_gpu_search_by_projection_two_camera_bit_exact(oracle, th, far, blocked,
         gm, gnm = be.projection_matches(p)
         np.testing.assert_array_equal(gm, m, err_msg="pair %d" % p)
         assert gnm == nm, (p, gnm, nm)
+
+
+@pytest.mark.gpu
+def test_gpu_search_by_projection_1080p_large_lds(oracle):
+    """C5 geometry (1920x1080, 12 levels, 5000 features): the resolve kernel's LDS tables exceed
+    64 KB (two-camera: Nleft + Nright keypoints), the dynamic-LDS attribute path."""
+    import orbslam3lib_amd as og
+    L_, R_ = synth.stereo_pair(1080, 1920, 81)
+    be = og.BatchExtractor(5000, 1.2, 12, 20, 7, width=1920, height=1080, max_images=2)
+    be.upload(np.stack([L_, R_]))
+    be.run()
+    be.undistort_grid((1400.0, 1400.0, 960.0, 540.0), ())
+    be.synchronize()
+    side = []
+    for e in range(2):
+        kps, desc, _ = be.result(e)
+        xy, _, cs, ci = be.grid_result(e)
+        side.append((xy, kps["octave"], desc, cs, ci))
+    Ls, Rs = side
+    l2r, r2l = synth.stereo_partners(Ls[2], Rs[2], seed=3)
+    mps = synth.map_points_stereo(Ls[0], Ls[1], Ls[2], Rs[0], Rs[1], l2r, n=6000, seed=17, nlevels=12)
+    be.search_by_projection_stereo([mps], [l2r], [r2l])
+    b = np.array([0, 1920, 0, 1080], np.float32)
+    m, nm = oracle.search_by_projection2(mps, Ls, Rs, b, l2r, r2l, nlevels=12)
+    gm, gnm = be.projection_matches(0)
+    np.testing.assert_array_equal(gm, m)
+    assert gnm == nm and nm > 100
+    # the pinhole form on the left image of the same frame
+    be.search_by_projection([mps], image_step=2, use_uright=False)
+    m1, nm1 = oracle.search_by_projection(mps, Ls[0], Ls[1], Ls[2], None, b, Ls[3], Ls[4], nlevels=12)
+    gm1, gnm1 = be.projection_matches(0)
+    np.testing.assert_array_equal(gm1, m1)
+    assert gnm1 == nm1
