@@ -136,6 +136,7 @@ def cpu_baseline(w, h, nfeatures, seconds, map_points=3000):
     stereo_pyr = [(O.pyramid(L), O.pyramid(R)) for L, R in pairs]
     t_st = [0.0]
     t_gr = t_sbp = 0.0
+    pair_times = []
     maps = []
     n_mp = 0
     nfeat = nq = 0
@@ -148,6 +149,8 @@ def cpu_baseline(w, h, nfeatures, seconds, map_points=3000):
         kl, dl, _ = O.extract(L, nfeatures=nfeatures, lap=(0, 0))
         kr, dr, _ = O.extract(R, nfeatures=nfeatures, lap=(0, 0))
         t1 = time.perf_counter()
+        if i >= 3:  # after 3 warm-up pairs
+            pair_times.append(t1 - t0)
         O.knn2(dl, dr)
         t2 = time.perf_counter()
         if stereo_pyr is not None:
@@ -170,7 +173,31 @@ def cpu_baseline(w, h, nfeatures, seconds, map_points=3000):
         t_ex += t1 - t0
         t_bf += t2 - t1
         i += 1
+    # SURVEY §8d modes 2 and 3: both eyes of a pair on two threads (Frame.cc:142-145), and a
+    # frames-parallel pool (ctypes releases the GIL inside the oracle); a few seconds each
+    from concurrent.futures import ThreadPoolExecutor
+    pool_threads = max(1, min(16, os.cpu_count() or 1))
+
+    def run_pairs(nthreads, per_pair_split, secs):
+        nf_, npairs, t0 = 0, 0, time.perf_counter()
+        with ThreadPoolExecutor(nthreads) as ex:
+            while time.perf_counter() - t0 < secs or npairs == 0:
+                if per_pair_split:
+                    L, R = pairs[npairs % len(pairs)]
+                    fl, fr = ex.submit(O.extract, L, nfeatures), ex.submit(O.extract, R, nfeatures)
+                    nf_ += len(fl.result()[0]) + len(fr.result()[0])
+                    npairs += 1
+                else:
+                    futs = [ex.submit(O.extract, pairs[(npairs + k) % len(pairs)][k % 2 and 1 or 0], nfeatures)
+                            for k in range(2 * nthreads)]
+                    nf_ += sum(len(f.result()[0]) for f in futs)
+                    npairs += nthreads
+        return nf_ / (time.perf_counter() - t0) / 1e6
+    mode2 = run_pairs(2, True, max(2.0, seconds / 4))
+    mode3 = run_pairs(pool_threads, False, max(2.0, seconds / 4))
     return {"pairs": i, "mfeat_s": nfeat / t_ex / 1e6, "mmatch_s": nq / t_bf / 1e6,
+            "mfeat_s_2threads_per_pair": mode2, "mfeat_s_pool": mode3, "pool_threads": pool_threads,
+            "median_pair_ms": 1e3 * float(np.median(pair_times)) if pair_times else None,
             "stereo_mkp_s": nq / t_st[0] / 1e6 if t_st[0] > 0 else None,
             "grid_mkp_s": nfeat / t_gr / 1e6 if t_gr > 0 else None,
             "sbp_mmp_s": n_mp / t_sbp / 1e6 if t_sbp > 0 else None,
@@ -216,6 +243,11 @@ def main():
     be = og.BatchExtractor(args.nfeatures, 1.2, args.nlevels, 20, 7, device=local, width=W,
                            height=H, max_images=2 * P)
     be.upload(imgs)  # PCIe upload: outside the timed region (inputs resident in HBM)
+    be.synchronize()
+    h0 = time.perf_counter()  # the same upload timed alone, for the H2D-inclusive rate
+    be.upload(imgs)
+    be.synchronize()
+    h2d_s = time.perf_counter() - h0
     laps = np.zeros((2 * P, 2), np.int32)
 
     def step():
@@ -276,6 +308,9 @@ def main():
     total_q = sum_over_ranks(dist, nq_per_step * args.steps)
     total_pairs = sum_over_ranks(dist, pairs_per_step * args.steps)
     mfeat = total_feats / elapsed / 1e6
+    # the PCIe-inclusive rate beside the resident one (never `value`)
+    h2d_max = max_over_ranks(dist, h2d_s)
+    h2d_incl = sum_over_ranks(dist, feats_per_step) / (elapsed / args.steps + h2d_max) / 1e6
     mmatch = total_q / elapsed / 1e6
 
     # roofline of the dominant kernel (per-launch algorithmic bytes / measured avg duration)
@@ -522,7 +557,20 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cb = cpu_baseline(W, H, args.nfeatures, args.cpu_seconds, args.map_points)
+        cpu_model = ""
+        try:
+            for line in open("/proc/cpuinfo"):
+                if line.startswith("model name"):
+                    cpu_model = line.split(":", 1)[1].strip()
+                    break
+        except OSError:
+            pass
         cpu = {"value": round(cb["mfeat_s"], 5), "unit": "Mfeatures/s", "cores": 1, "kind": "port",
+               "label": "oracle restatement, scalar C++ (-O3, no fast-math, no FMA), not OpenCV-SIMD",
+               "host": {"nproc": os.cpu_count(), "model": cpu_model},
+               "median_pair_ms_1thread": round(cb["median_pair_ms"], 2) if cb["median_pair_ms"] else None,
+               "mfeatures_s_2threads_per_pair": round(cb["mfeat_s_2threads_per_pair"], 5),
+               "mfeatures_s_pool": round(cb["mfeat_s_pool"], 5), "pool_threads": cb["pool_threads"],
                "sample": "%d synthetic 640x480 stereo pairs, oracle extract (both eyes, 1 thread); "
                          "BF kNN2 %.4f Mmatches/s" % (cb["pairs"], cb["mmatch_s"]),
                "mmatches_s": round(cb["mmatch_s"], 5),
@@ -551,6 +599,9 @@ def main():
             "matches": {"value": round(mmatch, 3), "unit": "Mmatches/s",
                         "gpairs_s": round(total_pairs / elapsed / 1e9, 3)},
             "features_per_step_per_gpu": feats_per_step,
+            "h2d": {"ms_per_batch_upload": round(h2d_max * 1e3, 3),
+                    "GBps": round(imgs.nbytes / h2d_max / 1e9, 2) if h2d_max > 0 else None,
+                    "mfeatures_s_incl_upload": round(h2d_incl, 3)},
             "roofline": roof,
             "roofline_fast_pyramid": roof_fp,
             "stages": stage_rows,
