@@ -228,6 +228,13 @@ def main():
     args = ap.parse_args()
 
     world, rank, local, dist = dist_setup()
+    # torch before liborbgpu: both then share one HIP runtime (torch bundles its own with the
+    # same soname), so torch.cuda.synchronize() below brackets the same device queues
+    try:
+        import torch
+        has_cuda = torch.cuda.is_available()
+    except Exception:
+        torch, has_cuda = None, False
     import orbslam3lib_amd as og
     from orbslam3lib_amd import synth
 
@@ -262,12 +269,6 @@ def main():
     feats_per_step = int(nk.sum())
     nq_per_step = int(sum(nk[2 * p] for p in range(P)))
     pairs_per_step = int(sum(int(nk[2 * p]) * int(nk[2 * p + 1]) for p in range(P)))
-
-    try:
-        import torch
-        has_cuda = torch.cuda.is_available()
-    except Exception:
-        has_cuda = False
 
     # 1. short untimed pass, every stage one whole-batch launch bracketed by HIP events -> per-stage
     #    table and the dominant kernel; 2. the timed region (production sub-batch streams, one
