@@ -222,6 +222,7 @@ def main():
     ap.add_argument("--no-grid", action="store_true", help="skip the UndistortKeyPoints + grid leg")
     ap.add_argument("--no-wire", action="store_true", help="skip the side-by-side ingest / SoA egress leg")
     ap.add_argument("--no-sbp", action="store_true", help="skip the SearchByProjection leg")
+    ap.add_argument("--no-configs", action="store_true", help="skip the C3 / C5 side lines")
     ap.add_argument("--map-points", type=int, default=3000, help="local-map points per frame (SBP leg)")
     ap.add_argument("--no-profile", action="store_true",
                     help="do not bracket launches with HIP events in the timed region")
@@ -534,6 +535,37 @@ def main():
                     "pack_soa_GBps": round(pack_b / (pk[0] / pk[1] * 1e-3) / 1e9, 1) if pk[1] else None,
                     "frames_per_step": P, "hbm_peak_GBps": HBM_PEAK_GBS}
 
+    # the other BASELINE configs as side lines (the headline stays C2): C3's 752x480 stream
+    # (synthetic, EuRoC geometry) and C5's 1920x1080 / 12 levels / 5000 features, each with its
+    # per-pair kNN2 (left -> right, all rows), resident batches, a few steps
+    configs = None
+    if not args.no_configs:
+        configs = {}
+        for name, (cw, ch, cl, cn, cp) in {"C3": (752, 480, 8, 2000, 64), "C5": (1920, 1080, 12, 5000, 16)}.items():
+            cu = [synth.stereo_pair(ch, cw, 500 + base + i) for i in range(4)]
+            cimg = np.stack([cu[(i // 2) % 4][i % 2] for i in range(2 * cp)])
+            cb_ = og.BatchExtractor(cn, 1.2, cl, 20, 7, device=local, width=cw, height=ch, max_images=2 * cp)
+            cb_.upload(cimg)
+            for _ in range(2):
+                cb_.run()
+                cb_.match_stereo(stereo_rows_only=False)
+            cb_.synchronize()
+            barrier(dist)
+            c0_ = time.perf_counter()
+            for _ in range(5):
+                cb_.run()
+                cb_.match_stereo(stereo_rows_only=False)
+            cb_.synchronize()
+            c_el = max_over_ranks(dist, time.perf_counter() - c0_)
+            cnk, _ = cb_.counts()
+            configs[name] = {"workload": "%dx%d stereo, %d levels, %d feat/frame + per-pair kNN2" % (cw, ch, cl, cn),
+                             "pairs_per_gpu_per_step": cp,
+                             "mfeatures_s": round(sum_over_ranks(dist, float(cnk.sum()) * 5) / c_el / 1e6, 3),
+                             "mmatches_s": round(sum_over_ranks(dist, float(cnk[0::2].sum()) * 5) / c_el / 1e6, 3),
+                             "ms_per_step": round(c_el / 5 * 1e3, 3), "data": "synthetic"}
+            cb_.close() if hasattr(cb_, "close") else None
+            del cb_
+
     # C5's exchange step when several GPUs run: every rank contributes its camera
     # (pair 0's left eye), one RCCL all_gather moves the descriptors, each rank matches its own
     # against all others on its GPU.  Reported beside the headline, never part of it.
@@ -610,6 +642,7 @@ def main():
             "stereo_matches": stereo,
             "undistort_grid": grid,
             "search_by_projection": sbp,
+            "other_configs": configs,
             "wire": wire,
             "cross_camera": cross,
         }
