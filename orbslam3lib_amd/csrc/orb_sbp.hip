@@ -381,10 +381,13 @@ __global__ __launch_bounds__(64) void k_sbp_resolve(SbpArgs a) {
                     }
                 }
                 // staleness against the earlier pending lanes of the group
+                // (pinhole frames: an assignment by a point without observations leaves the
+                // keypoint free, so only the blocking ones can disturb a later lane)
+                const bool reg = pending && na > 0 && (a.two_cam || obs);
                 const uint64_t below = (1ull << lane) - 1;
-                const uint64_t am = __ballot(pending && na > 0);
+                const uint64_t am = __ballot(reg);
                 const uint64_t fm = __ballot(pending && frees);
-                if (pending) {
+                if (reg) {
                     if (na > 0) atomicMin(&owner[ak0], (uint32_t)lane);
                     if (na > 1) atomicMin(&owner[ak1], (uint32_t)lane);
                     if (na > 2) atomicMin(&owner[ak2], (uint32_t)lane);
@@ -399,7 +402,7 @@ __global__ __launch_bounds__(64) void k_sbp_resolve(SbpArgs a) {
                         if (t < nexR) stale |= owner[nl + c.idxR[t]] < (uint32_t)lane;
                     }
                 }
-                if (pending) {
+                if (reg) {
                     if (na > 0) owner[ak0] = 64;
                     if (na > 1) owner[ak1] = 64;
                     if (na > 2) owner[ak2] = 64;
