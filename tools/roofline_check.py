@@ -12,6 +12,8 @@ chunks = int(sys.argv[4]) if len(sys.argv) > 4 else 4
 name = bench["roofline"]["kernel"]
 rows = [r for r in csv.DictReader(open(sys.argv[2])) if name in r["Kernel_Name"].replace("void ", "")]
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+# the headline batch's launches share the first launch's grid (the side-line configs differ)
+rows = [r for r in rows if r["Grid_Size_X"] == rows[0]["Grid_Size_X"] and r["Grid_Size_Y"] == rows[0]["Grid_Size_Y"]]
 d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rows]
 timed = d[-steps * chunks:]
 print(json.dumps({"kernel": name, "bench_avg_us": bench["roofline"]["avg_us"],
