@@ -873,7 +873,7 @@ constexpr int kOdPatchR = 18;                    // |rotated pattern offset| <= 
 constexpr int kOdPatchRows = 2 * kOdPatchR + 1;  // 37
 constexpr int kOdPatchPitch = 48;                // 3 x 16 B: covers x-18..x+18 from the dword below
 
-__global__ __launch_bounds__(256) void k_orient_desc(BatchArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k_orient_desc(BatchArgs a) {
     // per keypoint group: the blurred patch around the keypoint, staged with 16-byte loads
     __shared__ __attribute__((aligned(16))) uint8_t patch[kOdKpBlock][kOdPatchRows * kOdPatchPitch];
     const int wg = xcd_remap(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * gridDim.y);
@@ -891,31 +891,32 @@ __global__ __launch_bounds__(256) void k_orient_desc(BatchArgs a) {
     const __amdgpu_buffer_rsrc_t brs =
         __builtin_amdgcn_make_buffer_rsrc((void*)blr, (short)0, G.bpitch * G.h, 0x00020000);
     const int stride_k = G.od_blocks * kOdKpBlock;
-    // this lane's disc rows and, per row, byte masks of the 32-byte window u = -15..16
-    // restricted to |u| <= umax[|v|] (rows past v = 15 are empty)
+    // per disc row v = s - 15 (s = 0..31): byte masks of the 32-byte window u = -15..16 restricted
+    // to |u| <= umax[|v|] (rows past v = 15 are empty), and the packed test pairs (x0,y0,x1,y1
+    // int8): both in LDS tables shared by the workgroup instead of 16 VGPRs per lane
+    static_assert(kOdRows == 1 && kOdLanes * 8 == 256 && kOdLanes * kOdPairs == 256, "LDS table shapes");
+    __shared__ __attribute__((aligned(16))) uint32_t s_msk[kOdLanes][8];
+    __shared__ __attribute__((aligned(16))) uint32_t s_pat[kOdLanes * kOdPairs];
+    {
+        const int ts = threadIdx.x / 8, ti = threadIdx.x % 8;
+        const int v = ts - 15;
+        const int d = v > 15 ? -1 : c_umax[v < 0 ? -v : v];
+        uint32_t m = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int u = 4 * ti + j - 15;
+            m |= ((u < 0 ? -u : u) <= d ? 0xFFu : 0u) << (8 * j);
+        }
+        s_msk[ts][ti] = m;
+        s_pat[threadIdx.x] = reinterpret_cast<const uint32_t*>(c_pattern.v)[threadIdx.x];
+    }
+    __syncthreads();
     int vrow[kOdRows];
-    uint32_t msk[kOdRows][8];
 #pragma unroll
     for (int h = 0; h < kOdRows; ++h) {
         const int v = sub - 15 + h * kOdLanes;
-        const int d = v > 15 ? -1 : c_umax[v < 0 ? -v : v];
         vrow[h] = v > 15 ? 0 : v;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            uint32_t m = 0;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int u = 4 * i + j - 15;
-                m |= ((u < 0 ? -u : u) <= d ? 0xFFu : 0u) << (8 * j);
-            }
-            msk[h][i] = m;
-        }
     }
-    // this lane's test pairs (x0,y0,x1,y1 int8), packed
-    uint32_t patw[kOdPairs];
-#pragma unroll
-    for (int i = 0; i < kOdPairs; ++i)
-        patw[i] = reinterpret_cast<const uint32_t*>(c_pattern.v)[sub * kOdPairs + i];
     // uniform trip count per wave so the group shuffles see all lanes
     const int wave_first = (bx - G.od_first) * kOdKpBlock + (threadIdx.x >> 6) * (64 / kOdLanes);
     for (int kb = wave_first; kb < count; kb += stride_k) {
@@ -953,7 +954,7 @@ __global__ __launch_bounds__(256) void k_orient_desc(BatchArgs a) {
             uint32_t sacc = 0, uacc = 0;
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
-                const uint32_t b = __builtin_amdgcn_alignbyte(w[i + 1], w[i], shf) & msk[h][i];
+                const uint32_t b = __builtin_amdgcn_alignbyte(w[i + 1], w[i], shf) & s_msk[sub][i];
                 sacc = __builtin_amdgcn_sad_u8(b, 0u, sacc);
                 const uint32_t wu = (uint32_t)(4 * i) * 0x01010101u + 0x03020100u;
                 uacc = __builtin_amdgcn_udot4(b, wu, uacc, false);
@@ -999,7 +1000,7 @@ __global__ __launch_bounds__(256) void k_orient_desc(BatchArgs a) {
         for (int e = 0; e < 2 * kOdPairs; ++e) {
             // the packed pattern word is opaque here, so its float conversions are not hoisted
             // out of the keypoint loop (that would hold 4 VGPRs per pair across it)
-            uint32_t pw = patw[e >> 1];
+            uint32_t pw = s_pat[sub * kOdPairs + (e >> 1)];
             asm volatile("" : "+v"(pw));
             const int sh8 = 16 * (e & 1);
             const float px = (float)(int8_t)(pw >> sh8), py = (float)(int8_t)(pw >> (sh8 + 8));
