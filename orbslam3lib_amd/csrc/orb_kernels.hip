@@ -919,10 +919,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
     }
     // uniform trip count per wave so the group shuffles see all lanes
     const int wave_first = (bx - G.od_first) * kOdKpBlock + (threadIdx.x >> 6) * (64 / kOdLanes);
+    // each iteration's key is loaded one iteration ahead, so its round trip overlaps the
+    // previous keypoint's work
+    auto key_at = [&](int kb) {
+        const int kp = kb + (grp % (64 / kOdLanes));
+        return kp < count ? a.lvlkey[kbase + kp] : a.lvlkey[kbase + kb];
+    };
+    uint32_t key_next = wave_first < count ? key_at(wave_first) : 0u;
     for (int kb = wave_first; kb < count; kb += stride_k) {
         const int kp = kb + (grp % (64 / kOdLanes));
         const bool valid = kp < count;
-        const uint32_t key = valid ? a.lvlkey[kbase + kp] : a.lvlkey[kbase + kb];
+        const uint32_t key = key_next;
+        if (kb + stride_k < count) key_next = key_at(kb + stride_k);
         const int x = key_x(key) + kMinBorder, y = key_y(key) + kMinBorder;
         // IC_Angle moments (ORBextractor_old.cc:78-105): the row window is byte-aligned with
         // v_alignbyte, masked to the disc, then
