@@ -8,7 +8,7 @@ DEVFLAGS := -mllvm -amdgpu-mfma-vgpr-form
 LIB := orbslam3lib_amd/liborbgpu.so
 HDRS := $(wildcard $(CSRC)/*.h) include/orbgpu.h
 
-all: $(LIB) oracle facade_test
+all: $(LIB) oracle facade_test idl_test
 
 # one object per translation unit (each launcher sits beside its kernels: no relocatable device
 # code needed), so `make -j` compiles them in parallel
@@ -34,8 +34,16 @@ $(FACADE_TEST): tests/cpp/facade_test.cpp orbslam3lib_amd/facade/ORBextractor.cc
 	$(CXX) -O2 -std=c++17 -o $@ tests/cpp/facade_test.cpp orbslam3lib_amd/facade/ORBextractor.cc \
 		-L orbslam3lib_amd -lorbgpu -Wl,-rpath,'$$ORIGIN/../../../orbslam3lib_amd' -Wl,-rpath-link,/opt/rocm/lib -ldl
 
+# plain-C consumer of the IDL-shaped entry point (gcc, C99)
+IDL_TEST := tests/c/build/idl_test
+idl_test: $(IDL_TEST)
+$(IDL_TEST): tests/c/idl_test.c include/orbgpu.h $(LIB)
+	@mkdir -p tests/c/build
+	$(CC) -O2 -std=c99 -Wall -Iinclude -o $@ tests/c/idl_test.c -L orbslam3lib_amd -lorbgpu \
+		-Wl,-rpath,'$$ORIGIN/../../../orbslam3lib_amd' -Wl,-rpath-link,/opt/rocm/lib
+
 clean:
 	rm -f $(LIB) $(LIBOBJ)
 	$(MAKE) -s -C oracle clean
 
-.PHONY: all oracle clean facade_test
+.PHONY: all oracle clean facade_test idl_test

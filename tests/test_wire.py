@@ -190,3 +190,40 @@ def test_gpu_extract_features_one_call(oracle):
         None, None, C.byref(nr), None, None, None, None, None, cap, C.byref(ml), C.byref(mr), None,
         None, None, cap) == -3
     ctx.close()
+
+
+def _fnv(arrs):
+    h = 1469598103934665603
+    for a in arrs:
+        for b in np.ascontiguousarray(a).view(np.uint8).ravel().tolist():
+            h = ((h ^ b) * 1099511628211) & 0xFFFFFFFFFFFFFFFF
+    return h
+
+
+@pytest.mark.gpu
+def test_gpu_extract_features_from_plain_c(oracle, tmp_path):
+    """tests/c/idl_test.c (gcc, C99) calls orbgpu_extract_features as the FastRPC host wrapper
+    would; its outputs (hashed) equal the oracle's SoA + stereo-row kNN."""
+    import os
+    import subprocess
+    exe = os.path.join(os.path.dirname(__file__), "c", "build", "idl_test")
+    assert os.path.exists(exe), "built by `make` (idl_test target)"
+    W, H = 640, 480
+    L, R = synth.stereo_pair(H, W, 44)
+    frame = _sbs([(L, R)])[0]
+    path = tmp_path / "sbs.y8"
+    frame.tofile(path)
+    out = subprocess.run([exe, str(path), str(W), str(H)], capture_output=True, text=True, timeout=60)
+    assert out.returncode == 0, out.stderr
+    lines = out.stdout.split("\n")
+    laps = [(300, W), (0, W - 300)]
+    descs = []
+    for e, img in enumerate((L, R)):
+        kps, desc, mono = oracle.extract(img, nfeatures=NF, lap=laps[e])
+        soa = oracle.pack_soa(kps)
+        h = _fnv([soa["x"], soa["y"], soa["angle"], soa["level"], desc.reshape(-1, 32)])
+        assert lines[e] == "eye %d n %d mono %d hash %016x" % (e, len(kps), mono, h), lines[e]
+        descs.append((desc.reshape(-1, 32), mono))
+    (dl, ml), (dr, mr) = descs
+    ri, r1, r2 = _knn_ref(oracle, dl[ml:], dr[mr:])
+    assert lines[2] == "matches %d hash %016x" % (len(ri), _fnv([ri, r1, r2])), lines[2]
