@@ -112,6 +112,7 @@ struct orbgpu_ctx {
     int stereo_pairs = 0;  // pairs of the last orbgpu_stereo_matches_batch
     int input_images = 0;   // images currently sized for in `input`
     hipEvent_t fork = nullptr;
+    hipEvent_t ext_done = nullptr;  // work on a caller's stream (rejoin)
     std::vector<hipEvent_t> join;  // one per sub stream
     // stages launched once over the whole batch on the main stream (join before, fork after), so
     // their per-launch duration is their own; off by default: each join / fork costs ~30 us of
@@ -477,6 +478,25 @@ int join_all(orbgpu_ctx* c, hipStream_t s) {
     return 0;
 }
 
+// After work was enqueued on a caller's stream s (not one of the context's own): the context's
+// streams wait for it before they touch the buffers again (the next batch overwrites what it reads).
+int rejoin(orbgpu_ctx* c, hipStream_t s) {
+    for (hipStream_t t : c->sub)
+        if (t == s) return 0;
+    HIP_TRY(hipEventRecord(c->ext_done, s));
+    HIP_TRY(hipStreamWaitEvent(c->stream, c->ext_done, 0));
+    c->need_fork = true;
+    return 0;
+}
+
+// A per-image count the device wrote: k_finalize stores -5 (octree workspace overflow) or -2
+// (output capacity) instead of a count; map them to the status the caller gets.
+int count_status(int32_t nk) {
+    if (nk == -5) return fail(ORBGPU_ERR_OVERFLOW, "device workspace overflow (octree)");
+    if (nk < 0) return fail(ORBGPU_ERR_CAPACITY, "context output capacity exceeded");
+    return 0;
+}
+
 void resolve_pending(orbgpu_ctx* c) {
     for (auto& p : c->pending) {
         float ms = 0;
@@ -546,7 +566,8 @@ int orbgpu_create(const orbgpu_params* p, int device, int max_width, int max_hei
             if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) break;
             c->sub.push_back(st);
         }
-        bool ok = hipEventCreateWithFlags(&c->fork, hipEventDisableTiming) == hipSuccess;
+        bool ok = hipEventCreateWithFlags(&c->fork, hipEventDisableTiming) == hipSuccess &&
+                  hipEventCreateWithFlags(&c->ext_done, hipEventDisableTiming) == hipSuccess;
         for (size_t k = 0; ok && k < c->sub.size(); ++k) {
             hipEvent_t ev;
             ok = hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess;
@@ -592,6 +613,7 @@ int orbgpu_destroy(orbgpu_ctx* c) {
     for (DevBuf* b : bufs) b->release();
     for (size_t k = 1; k < c->sub.size(); ++k) hipStreamDestroy(c->sub[k]);
     if (c->fork) hipEventDestroy(c->fork);
+    if (c->ext_done) hipEventDestroy(c->ext_done);
     for (hipEvent_t e : c->stagger_ev) hipEventDestroy(e);
     for (auto e : c->join) hipEventDestroy(e);
     if (c->stream) hipStreamDestroy(c->stream);
@@ -859,8 +881,7 @@ int orbgpu_download_result(orbgpu_ctx* c, int img, orbgpu_keypoint* kps, uint8_t
     int32_t nk = 0, nm = 0;
     HIP_TRY(hipMemcpy(&nk, c->outn.as<int32_t>() + img, 4, hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(&nm, c->outmono.as<int32_t>() + img, 4, hipMemcpyDeviceToHost));
-    if (nk == -5) return fail(ORBGPU_ERR_OVERFLOW, "device workspace overflow (octree)");
-    if (nk < 0) return fail(ORBGPU_ERR_CAPACITY, "context output capacity exceeded");
+    if (int e = count_status(nk)) return e;
     if (n) *n = nk;
     if (n_mono) *n_mono = nm;
     if (nk > cap) return fail(ORBGPU_ERR_CAPACITY, "caller capacity too small");
@@ -893,7 +914,11 @@ int orbgpu_extract_stereo(orbgpu_ctx* c, const uint8_t* left, const uint8_t* rig
     if (!left || !right || w <= 0 || h <= 0) return fail(ORBGPU_ERR_EMPTY_IMAGE, "empty image");
     int r = ensure_input(c, 2, w, h);
     if (r) return r;
+    if (stride < w) return fail(ORBGPU_ERR_INVALID, "stride < width");
     HIP_TRY(hipSetDevice(c->device));
+    r = join_all(c, c->stream);  // sub streams of an earlier batch may still read the input
+    if (r) return r;
+    c->need_fork = true;
     HIP_TRY(hipMemcpy2DAsync(c->input.p, w, left, stride, w, h, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemcpy2DAsync(c->input.as<uint8_t>() + (size_t)w * h, w, right, stride, w, h,
                              hipMemcpyHostToDevice, c->stream));
@@ -1049,8 +1074,11 @@ int orbgpu_match_stereo_batch(orbgpu_ctx* c, int n_pairs, int stereo_only, void*
         }
     } else {
         m.pair0 = 0;
-        int r = timed(c, ST_KNN, s, [&] { return launch_knn2_pairs(m, n_pairs, qblocks, c->knnpart.p, s); });
+        int r = join_all(c, s);  // the extraction may have run on the chunk streams
         if (r) return r;
+        r = timed(c, ST_KNN, s, [&] { return launch_knn2_pairs(m, n_pairs, qblocks, c->knnpart.p, s); });
+        if (r) return r;
+        if ((r = rejoin(c, s))) return r;
     }
     c->last_pairs = n_pairs;
     return ORBGPU_OK;
@@ -1123,8 +1151,11 @@ int orbgpu_stereo_matches_batch(orbgpu_ctx* c, int n_pairs, float mbf, float mb,
     } else {
         hipStream_t s = stream ? (hipStream_t)stream : c->stream;
         S.pair0 = 0;
-        int r = timed(c, ST_STEREO, s, [&] { return launch_stereo(S, n_pairs, s); });
+        int r = join_all(c, s);  // the extraction may have run on the chunk streams
         if (r) return r;
+        r = timed(c, ST_STEREO, s, [&] { return launch_stereo(S, n_pairs, s); });
+        if (r) return r;
+        if ((r = rejoin(c, s))) return r;
     }
     c->stereo_pairs = n_pairs;
     return ORBGPU_OK;
@@ -1137,6 +1168,7 @@ int orbgpu_download_stereo(orbgpu_ctx* c, int pair, float* u_right, float* depth
     HIP_TRY(hipDeviceSynchronize());
     int32_t nl = 0;
     HIP_TRY(hipMemcpy(&nl, c->outn.as<int32_t>() + 2 * pair, 4, hipMemcpyDeviceToHost));
+    if (int e = count_status(nl)) return e;
     if (n) *n = nl;
     if (nl > cap) return fail(ORBGPU_ERR_CAPACITY, "caller capacity too small");
     const size_t o = (size_t)pair * c->out_cap;
@@ -1191,7 +1223,9 @@ int orbgpu_upload_sbs(orbgpu_ctx* c, const uint8_t* frames, int n, int w, int h,
     if (c->sbs.ensure(bytes + 256)) return fail(ORBGPU_ERR_HIP, "hipMalloc failed (sbs staging)");
     r = join_all(c, c->stream);
     if (r) return r;
-    HIP_TRY(hipMemcpyAsync(c->sbs.p, frames, bytes, hipMemcpyHostToDevice, c->stream));
+    // 2W bytes of each of the n*h rows: never reads the padding after the last row's pixels
+    HIP_TRY(hipMemcpy2DAsync(c->sbs.p, stride, frames, stride, 2 * (size_t)w, (size_t)n * h,
+                             hipMemcpyHostToDevice, c->stream));
     return orbgpu_ingest_sbs(c, c->sbs.as<uint8_t>(), n, w, h, stride, nullptr);
 }
 
@@ -1241,6 +1275,7 @@ int orbgpu_download_soa(orbgpu_ctx* c, int image, int32_t* x, int32_t* y, int32_
     int32_t nm[2] = {0, 0};
     HIP_TRY(hipMemcpy(&nm[0], c->outn.as<int32_t>() + image, 4, hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(&nm[1], c->outmono.as<int32_t>() + image, 4, hipMemcpyDeviceToHost));
+    if (int e = count_status(nm[0])) return e;
     if (count) *count = nm[0];
     if (mono) *mono = nm[1];
     if (nm[0] > cap) return fail(ORBGPU_ERR_CAPACITY, "caller capacity too small");
@@ -1417,6 +1452,10 @@ int orbgpu_download_projection_matches(orbgpu_ctx* c, int frame, int32_t* match,
     const size_t img = (size_t)frame * c->sbp_step;
     HIP_TRY(hipMemcpy(nk, c->outn.as<int32_t>() + img, c->sbp_two_cam ? 8 : 4, hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(&nm, c->sbpnm.as<int32_t>() + frame, 4, hipMemcpyDeviceToHost));
+    if (int e = count_status(nk[0])) return e;
+    if (c->sbp_two_cam)
+        if (int e = count_status(nk[1])) return e;
+    if (!c->sbp_two_cam) nk[1] = 0;
     const int n = nk[0] + nk[1];
     if (n_kp) *n_kp = n;
     if (nmatches) *nmatches = nm;
@@ -1471,8 +1510,11 @@ int orbgpu_undistort_grid_batch(orbgpu_ctx* c, int n, const float K[4], const fl
     } else {
         hipStream_t s = stream ? (hipStream_t)stream : c->stream;
         g.img0 = 0;
-        int r = timed(c, ST_GRID, s, [&] { return launch_undistort_grid(g, n, s); });
+        int r = join_all(c, s);  // the extraction may have run on the chunk streams
         if (r) return r;
+        r = timed(c, ST_GRID, s, [&] { return launch_undistort_grid(g, n, s); });
+        if (r) return r;
+        if ((r = rejoin(c, s))) return r;
     }
     c->grid_images = n;
     std::memcpy(c->grid_bounds, g.bounds, sizeof g.bounds);

@@ -1,0 +1,244 @@
+"""GPU parity on the configurations the headline numbers run, and on the matcher's segment edges.
+
+* kNN2 past one 4096-row train segment (k_knn2_mfma walks train rows in 4096-row segments with a
+  12-bit local index, orb_kernels.hip knn2_mfma_block): nt in {4095, 4096, 4097, 5000, 8193} with
+  exact-duplicate rows on both sides of every segment boundary, so the cross-segment tie rule
+  (lowest index wins, cv::BFMatcher k=2 / SURVEY §8 a10) is exercised.
+* The batch matcher (orbgpu_match_stereo_batch) with more than 4096 train rows per pair, and the
+  C5 batch the bench's side line runs (1920x1080, 12 levels, 5000 features, 16 pairs).
+* The exact bench batch (bench.py: 128 pairs from 16 distinct seeded pairs, 4 chunk streams,
+  staggered first step, then the steady state), sampled against the oracle.
+* Consumers given an explicit stream right after a multi-stream batch (they must wait
+  for the chunk streams), and the IDL one-call entry with a padded stride and a buffer that ends
+  at the last pixel.
+
+Oracle: oracle/orb_oracle.cpp (the checker), parity pinned as in test_golden.py."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from orbslam3lib_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+
+def _same_kps(a, b):
+    assert len(a) == len(b), (len(a), len(b))
+    for f in ("x", "y", "size", "angle", "response", "octave", "class_id"):
+        np.testing.assert_array_equal(a[f], b[f], err_msg=f)
+
+
+def _same_knn(got, ref, msg=""):
+    for a, b, name in zip(got, ref, ("idx1", "dist1", "idx2", "dist2")):
+        np.testing.assert_array_equal(a, b, err_msg="%s %s" % (msg, name))
+
+
+@pytest.mark.parametrize("nt", [4095, 4096, 4097, 5000, 8193])
+def test_knn2_train_segments(oracle, nt):
+    import orbslam3lib_amd as og
+    ex = og.ORBextractor(500, 1.2, 4, 20, 7, max_width=160, max_height=120, max_images=1)
+    bf = og.BFMatcher(ex)
+    rng = np.random.default_rng(nt)
+    t = rng.integers(0, 256, (nt, 32), dtype=np.uint8)
+    # duplicates straddling each segment boundary (and the ends): the same row at b-2 .. b+1
+    for b in range(4096, nt + 1, 4096):
+        src = t[(b * 7) % 1000].copy()
+        for r in (b - 2, b - 1, b, b + 1):
+            if 0 <= r < nt:
+                t[r] = src
+    t[nt - 1] = t[3]
+    probes = [t[r] for r in range(nt) if r % 4096 in (4094, 4095, 0, 1)] + [t[3], t[nt - 1]]
+    # near-duplicates (one bit flipped) compete with exact ones across segments
+    near = []
+    for p in probes[:8]:
+        x = p.copy()
+        x[5] ^= 0x10
+        near.append(x)
+    q = np.concatenate([np.stack(probes + near), rng.integers(0, 256, (700, 32), dtype=np.uint8)])
+    got = bf.knnMatch(q, t, 2)
+    _same_knn(got, oracle.knn2(q, t), "nt=%d" % nt)
+    # every probe finds itself at distance 0, and its twin (if any) second
+    assert (got[1][:len(probes)] == 0).all()
+
+
+def _batch(og, w, h, L, nf, imgs):
+    be = og.BatchExtractor(nf, 1.2, L, 20, 7, width=w, height=h, max_images=len(imgs))
+    be.upload(imgs)
+    return be
+
+
+def test_batch_knn2_past_4096_train_rows(oracle):
+    """orbgpu_match_stereo_batch with > 4096 keypoints per eye (1920x1080, 12 levels, 8200
+    features): the pair's kNN2 crosses a train segment."""
+    import orbslam3lib_amd as og
+    pairs = [synth.stereo_pair(1080, 1920, 60 + i) for i in range(2)]
+    imgs = np.stack([x for p in pairs for x in p])
+    be = _batch(og, 1920, 1080, 12, 8200, imgs)
+    be.run()
+    be.match_stereo(False)
+    be.synchronize()
+    for p in range(2):
+        _, dl, _ = be.result(2 * p)
+        _, dr, _ = be.result(2 * p + 1)
+        assert len(dr) > 4096 and len(dl) > 4096, (len(dl), len(dr))
+        _same_knn(be.matches(p), oracle.knn2(dl, dr), "pair %d" % p)
+    k, d, m = be.result(3)
+    rk, rd, rm = oracle.extract(imgs[3], nfeatures=8200, nlevels=12)
+    assert m == rm
+    _same_kps(k, rk)
+    np.testing.assert_array_equal(d, rd)
+
+
+def test_c5_batch_16_pairs(oracle):
+    """The C5 side line's batch (bench.py other_configs: 1920x1080, 12 levels, 5000 features,
+    16 pairs tiled from 4 seeded pairs, 4 chunk streams): every pair's 5000 x 5000 kNN2 against
+    the oracle matcher, sampled images against the oracle extractor."""
+    import orbslam3lib_amd as og
+    cu = [synth.stereo_pair(1080, 1920, 500 + i) for i in range(4)]
+    imgs = np.stack([cu[(i // 2) % 4][i % 2] for i in range(32)])
+    be = _batch(og, 1920, 1080, 12, 5000, imgs)
+    for _ in range(2):
+        be.run()
+        be.match_stereo(False)
+    be.synchronize()
+    res = [be.result(i) for i in range(32)]
+    for i in (0, 3):
+        rk, rd, rm = oracle.extract(imgs[i], nfeatures=5000, nlevels=12)
+        assert res[i][2] == rm
+        _same_kps(res[i][0], rk)
+        np.testing.assert_array_equal(res[i][1], rd)
+    for i in range(4, 32):  # tiled copies extract identically on every stream
+        _same_kps(res[i][0], res[i % 8][0])
+        np.testing.assert_array_equal(res[i][1], res[i % 8][1])
+    assert max(len(r[1]) for r in res) > 4096
+    for p in range(16):
+        _same_knn(be.matches(p), oracle.knn2(res[2 * p][1], res[2 * p + 1][1]), "pair %d" % p)
+
+
+def test_bench_batch_128_pairs(oracle):
+    """bench.py's headline batch exactly: 128 pairs (16 distinct seeded pairs tiled), 256
+    images, 4 chunk streams, the staggered first step and the steady state after it."""
+    import orbslam3lib_amd as og
+    from orbslam3lib_amd.dist import pair_seed_base
+    P, U, W, H = 128, 16, 640, 480
+    uniq = [synth.stereo_pair(H, W, pair_seed_base(0) + i) for i in range(U)]
+    imgs = np.empty((2 * P, H, W), np.uint8)
+    for p in range(P):
+        imgs[2 * p], imgs[2 * p + 1] = uniq[p % U]
+    be = og.BatchExtractor(2000, 1.2, 8, 20, 7, width=W, height=H, max_images=2 * P)
+    be.upload(imgs)
+    laps = np.zeros((2 * P, 2), np.int32)
+    ref = {}
+    for u in range(U):
+        for e in range(2):
+            ref[2 * u + e] = oracle.extract(uniq[u][e], nfeatures=2000, lap=(0, 0))
+    sample = sorted(set(list(range(2 * U)) + list(range(2 * U, 2 * P, 13)) + [2 * P - 2, 2 * P - 1]))
+    for step in range(3):  # step 0: staggered layout; then the steady state
+        be.run(laps)
+        be.match_stereo(stereo_rows_only=False)
+        be.synchronize()
+        if step == 1:
+            continue
+        for i in sample:
+            k, d, m = be.result(i)
+            rk, rd, rm = ref[i % (2 * U)]
+            assert m == rm, (step, i)
+            _same_kps(k, rk)
+            np.testing.assert_array_equal(d, rd, err_msg="step %d image %d" % (step, i))
+        for p in sorted(set(list(range(0, P, 9)) + [P - 1])):
+            u = p % U
+            _same_knn(be.matches(p), oracle.knn2(ref[2 * u][1], ref[2 * u + 1][1]), "step %d pair %d" % (step, p))
+
+
+def _hip():
+    lib = C.CDLL("libamdhip64.so.7")  # the runtime liborbgpu.so is linked against
+    lib.hipStreamCreate.argtypes = [C.POINTER(C.c_void_p)]
+    lib.hipStreamDestroy.argtypes = [C.c_void_p]
+    return lib
+
+
+def test_explicit_stream_after_chunked_batch(oracle):
+    """A 256-image batch runs on the 4 chunk streams; kNN2, stereo matching and the grid are
+    then launched on a caller stream without synchronising first: they must wait for the chunks
+    (orbgpu_match_stereo_batch / stereo_matches_batch / undistort_grid_batch join the context's
+    streams), and the next batch must wait for them."""
+    import orbslam3lib_amd as og
+    P, U, W, H = 128, 8, 640, 480
+    uniq = [synth.stereo_pair(H, W, 900 + i) for i in range(U)]
+    imgs = np.stack([uniq[(i // 2) % U][i % 2] for i in range(2 * P)])
+    be = og.BatchExtractor(2000, 1.2, 8, 20, 7, width=W, height=H, max_images=2 * P)
+    be.upload(imgs)
+    hip = _hip()
+    s = C.c_void_p()
+    assert hip.hipStreamCreate(C.byref(s)) == 0
+    mbf = 47.9
+    mb = float(np.float32(mbf) / np.float32(435.2))
+    K = (458.654, 457.296, 367.215, 248.375)
+    try:
+        for _ in range(2):
+            be.run()
+            be.match_stereo(False, stream=s.value)
+            be.stereo_matches(mbf, mb, stream=s.value)
+            be.undistort_grid(K, (), stream=s.value)
+        be.synchronize()
+        for p in (0, 5, P - 1):
+            u = p % U
+            kl, dl, _ = be.result(2 * p)
+            kr, dr, _ = be.result(2 * p + 1)
+            rk, rd, _ = oracle.extract(uniq[u][0], nfeatures=2000)
+            _same_kps(kl, rk)
+            _same_knn(be.matches(p), oracle.knn2(dl, dr), "pair %d" % p)
+            ur, dep, _ = be.stereo_result(p)
+            rur, rdep, _ = oracle.stereo_matches(kl, dl, kr, dr, oracle.pyramid(uniq[u][0]),
+                                                 oracle.pyramid(uniq[u][1]), mbf, mb)
+            np.testing.assert_array_equal(ur, rur)
+            np.testing.assert_array_equal(dep, rdep)
+            xy, cell, cs, ci = be.grid_result(2 * p)
+            rxy, _, rcell, rcs, rci = oracle.undistort_grid(kl, K, (), W, H)
+            np.testing.assert_array_equal(cell, rcell)
+            np.testing.assert_array_equal(ci, rci)
+    finally:
+        be.synchronize()
+        hip.hipStreamDestroy(s)
+
+
+def test_extract_features_padded_stride_exact_buffer(oracle):
+    """orbgpu_extract_features with stride > 2W and a buffer that ends at the last row's last
+    pixel (image_len = stride * (H - 1) + 2W): accepted, nothing past it is read (the upload
+    copies 2W bytes per row), results equal the unpadded call's."""
+    import orbslam3lib_amd as og
+    lib = og.load_library()
+    W, H, pad = 640, 480, 96
+    L, R = synth.stereo_pair(H, W, 41)
+    stride = 2 * W + pad
+    n = stride * (H - 1) + 2 * W
+    buf = np.full(n, 255, np.uint8)  # an exactly-sized buffer, padding bytes 255
+    for y in range(H):
+        buf[y * stride:y * stride + W] = L[y]
+        buf[y * stride + W:y * stride + 2 * W] = R[y]
+    ctx = og._Context(2000, 1.2, 8, 20, 7, 0, W, H, 2)
+    cap = 20000
+    outs = {k: np.zeros(cap, np.int32) for k in ("xl", "yl", "al", "ll", "xr", "yr", "ar", "lr")}
+    orb_l, orb_r = np.zeros((cap, 32), np.uint8), np.zeros((cap, 32), np.uint8)
+    idx, d1, d2 = (np.zeros(cap, np.int16) for _ in range(3))
+    nl, nr, ml, mr = (C.c_int(0) for _ in range(4))
+    P = og._p
+    rc = lib.orbgpu_extract_features(
+        ctx.handle, P(buf), n, W, H, stride, 20, 0, 0, 0, 0,
+        C.byref(nl), P(outs["xl"]), P(outs["yl"]), P(outs["al"]), P(outs["ll"]), P(orb_l),
+        C.byref(nr), P(outs["xr"]), P(outs["yr"]), P(outs["ar"]), P(outs["lr"]), P(orb_r), cap,
+        C.byref(ml), C.byref(mr), P(idx), P(d1), P(d2), cap)
+    assert rc == 0, lib.orbgpu_last_error()
+    kl, dl, _ = oracle.extract(L, nfeatures=2000)
+    kr, dr, _ = oracle.extract(R, nfeatures=2000)
+    assert (nl.value, nr.value) == (len(kl), len(kr))
+    np.testing.assert_array_equal(orb_l[:nl.value], dl)
+    np.testing.assert_array_equal(orb_r[:nr.value], dr)
+    np.testing.assert_array_equal(outs["xl"][:nl.value], oracle.pack_soa(kl)["x"])
+    # one byte short of the last pixel: refused
+    assert lib.orbgpu_extract_features(
+        ctx.handle, P(buf), n - 1, W, H, stride, 20, 0, 0, 0, 0, C.byref(nl), None, None, None,
+        None, None, C.byref(nr), None, None, None, None, None, cap, C.byref(ml), C.byref(mr), None,
+        None, None, cap) == -3
+    ctx.close()
