@@ -29,9 +29,12 @@ oracle:
 # C++ facade (what an ORB-SLAM3 build compiles) + its GPU test program
 FACADE_TEST := tests/cpp/build/facade_test
 facade_test: $(FACADE_TEST)
-$(FACADE_TEST): tests/cpp/facade_test.cpp orbslam3lib_amd/facade/ORBextractor.cc include/orbslam3/ORBextractor.h include/orbslam3/cv_shim.h $(LIB)
+FACADE_SRC := orbslam3lib_amd/facade/ORBextractor.cc orbslam3lib_amd/facade/LynxHardwareAccelerator.cc
+FACADE_HDR := include/orbslam3/ORBextractor.h include/orbslam3/cv_shim.h \
+	include/orbslam3/LynxHardwareAcceleration/LynxHardwareAccelerator.h
+$(FACADE_TEST): tests/cpp/facade_test.cpp $(FACADE_SRC) $(FACADE_HDR) $(LIB)
 	@mkdir -p tests/cpp/build
-	$(CXX) -O2 -std=c++17 -o $@ tests/cpp/facade_test.cpp orbslam3lib_amd/facade/ORBextractor.cc \
+	$(CXX) -O2 -std=c++17 -Wall -o $@ tests/cpp/facade_test.cpp $(FACADE_SRC) -pthread \
 		-L orbslam3lib_amd -lorbgpu -Wl,-rpath,'$$ORIGIN/../../../orbslam3lib_amd' -Wl,-rpath-link,/opt/rocm/lib -ldl
 
 # plain-C consumer of the IDL-shaped entry point (gcc, C99)

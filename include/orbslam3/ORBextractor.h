@@ -2,15 +2,18 @@
 //
 // Same public surface as the reference's CPU extractor (cpp/include/ORBextractor_old.h:45-116):
 // the 5-parameter ctor, operator()(image, mask, keypoints, descriptors, vLappingArea) returning
-// monoIndex, the scale getters and the public mvImagePyramid, plus the stereo entry point of the
-// DSP-backed extractor (cpp/include/ORBextractor.h:52-57) taking two images instead of an
-// AHardwareBuffer.  ORBmatcher::DescriptorDistance (cpp/include/ORBmatcher.h:44) is provided as
-// a static helper.  Everything computes on the GPU through include/orbgpu.h; Tracking / Frame
-// code compiles unchanged against it.
+// monoIndex, the scale getters and the public mvImagePyramid; plus the stereo entry point of the
+// DSP-backed extractor (cpp/include/ORBextractor.h:52-57), which returns the frame id whose
+// matches LynxHardwareAccelerator::BFMatchORB fetches (Frame.cc:1164).  The stereo form takes
+// the side-by-side Y8 frame the AHardwareBuffer holds as a cv::Mat (2W x H), or two images.
+// ORBmatcher stays the reference's own class (cpp/include/ORBmatcher.h:37-44); its
+// DescriptorDistance body can call orbgpu::DescriptorDistance below.
+// Everything computes on the GPU through include/orbgpu.h.
 #pragma once
 #include <vector>
 
 #include "../orbgpu.h"
+#include "LynxHardwareAcceleration/LynxHardwareAccelerator.h"
 #include "cv_shim.h"
 
 namespace ORB_SLAM3 {
@@ -26,11 +29,21 @@ public:
 
     // Compute the ORB features and descriptors on an image (mask is ignored, as in the
     // reference).  Returns the number of keypoints outside vLappingArea (written first); the
-    // lapping-area keypoints follow in reverse order.  -1 on an empty image.
+    // lapping-area keypoints follow in reverse order.  -1 on an empty image (:1092-1093) or a
+    // device error (lastStatus()).
     int operator()(cv::InputArray _image, cv::InputArray _mask, std::vector<cv::KeyPoint>& _keypoints,
                    cv::OutputArray _descriptors, std::vector<int>& vLappingArea);
 
-    // Stereo form: both eyes in one device pass (ORBextractor.h:52-57 semantics).
+    // Stereo form (ORBextractor.h:52-57, ORBextractor.cc:118-165): _image is one side-by-side Y8
+    // frame, left eye in columns [0, W), right eye in [W, 2W).  Both eyes and the stereo-row kNN2
+    // in one device pass; returns the frame id (for LynxHardwareAccelerator::BFMatchORB), -1 on
+    // an error.
+    int operator()(cv::InputArray _image, std::vector<cv::KeyPoint>& _keypointsLeft,
+                   cv::OutputArray _descriptorsLeft, std::vector<int>& vLappingAreaLeft,
+                   std::vector<cv::KeyPoint>& _keypointsRight, cv::OutputArray _descriptorsRight,
+                   std::vector<int>& vLappingAreaRight, int& monoLeft, int& monoRight);
+
+    // Same on two separate images of one rectified pair.
     int operator()(cv::InputArray left, cv::InputArray right, std::vector<cv::KeyPoint>& keypointsLeft,
                    cv::OutputArray descriptorsLeft, std::vector<int>& vLappingAreaLeft,
                    std::vector<cv::KeyPoint>& keypointsRight, cv::OutputArray descriptorsRight,
@@ -48,12 +61,13 @@ public:
     std::vector<cv::Mat> mvImagePyramid;
     bool mbExportPyramid = true;
 
-    // Device, image-size limits and status of the underlying context.
+    // Status of the last call (orbgpu status code, 0 = OK).
     int lastStatus() const { return mStatus; }
 
 protected:
     int ensureContext(int width, int height);
     void exportPyramid(int image);
+    LynxHardwareAccelerator* accelerator(int width, int height);
 
     int nfeatures;
     double scaleFactor;
@@ -69,15 +83,15 @@ protected:
     orbgpu_ctx* mCtx = nullptr;
     int mCtxW = 0, mCtxH = 0;
     int mStatus = 0;
-    std::vector<orbgpu_keypoint> mKps[2];
+    std::vector<orbgpu_keypoint> mKps;
+    std::vector<uint8_t> mDesc;
 };
 
-class ORBmatcher {
-public:
-    // Bit-count Hamming distance of two 32-byte descriptors (ORBmatcher.cc:2107-2123).
-    static int DescriptorDistance(const cv::Mat& a, const cv::Mat& b) {
-        return orbgpu_descriptor_distance(a.ptr(0), b.ptr(0));
-    }
-};
+namespace orbgpu {
+// ORBmatcher::DescriptorDistance (ORBmatcher.cc:2107-2123) on two 32-byte descriptor rows.
+inline int DescriptorDistance(const cv::Mat& a, const cv::Mat& b) {
+    return orbgpu_descriptor_distance(a.ptr<unsigned char>(0), b.ptr<unsigned char>(0));
+}
+}  // namespace orbgpu
 
 }  // namespace ORB_SLAM3

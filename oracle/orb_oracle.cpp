@@ -392,12 +392,26 @@ float ic_angle(const uint8_t* image, int step, float px, float py, const std::ve
     return fast_atan2((float)m_01, (float)m_10);
 }
 
+// 0: cos / sin of computeOrbDescriptor as the reference source calls them (float overloads);
+// 1: (float)cos((double)angle) -- only to measure how often the two differ (oracle_set_trig_double).
+static int g_trig_double = 0;
+
 // computeOrbDescriptor (ORBextractor_old.cc:108-148).
 const float factorPI = (float)(M_PI / 180.f);
 void orb_descriptor(const KeyPoint& kpt, const uint8_t* img, int step, const int* pattern,
                     uint8_t* desc) {
     float angle = (float)kpt.angle * factorPI;
-    float a = (float)std::cos((double)angle), b = (float)std::sin((double)angle);
+    // `(float)cos(angle)` with a float angle under `using namespace std` (:68, :114-115) is the
+    // float overload std::cos(float) = libm cosf; g_trig_double selects the double-evaluated
+    // alternative for the deviation measurement of tests/test_oracle.py only
+    float a, b;
+    if (g_trig_double) {
+        a = (float)std::cos((double)angle);
+        b = (float)std::sin((double)angle);
+    } else {
+        a = (float)std::cos(angle);
+        b = (float)std::sin(angle);
+    }
     const uint8_t* center = img + (size_t)cvRound(kpt.y) * step + cvRound(kpt.x);
     auto get = [&](const int* p, int idx) {
         float px = (float)p[2 * idx], py = (float)p[2 * idx + 1];
@@ -911,6 +925,8 @@ int oracle_descriptor_distance(const uint8_t* a, const uint8_t* b) {
     return dist;
 }
 
+void oracle_set_trig_double(int on) { g_trig_double = on ? 1 : 0; }
+
 void oracle_knn2(const uint8_t* q, int nq, const uint8_t* t, int nt, int32_t* idx1, int32_t* d1,
                  int32_t* idx2, int32_t* d2) {
     // cv::batchDistance(K=2, NORM_HAMMING) insertion rule; knnMatch drops idx<0 entries.
@@ -1174,7 +1190,7 @@ void oracle_assign_grid(const float* xy_un, int n, const float bounds[4], int32_
 void oracle_pack_soa(const oracle_kp* kps, int n, int32_t* x, int32_t* y, int32_t* angle, int32_t* level) {
     for (int i = 0; i < n; ++i) {
         const float rad = (float)kps[i].angle * factorPI;
-        const float a = (float)std::cos((double)rad), b = (float)std::sin((double)rad);
+        const float a = (float)std::cos(rad), b = (float)std::sin(rad);  // as the descriptor
         const int c8 = (int)std::nearbyint(64.0f * a), s8 = (int)std::nearbyint(64.0f * b);
         x[i] = (int32_t)kps[i].x;
         y[i] = (int32_t)kps[i].y;

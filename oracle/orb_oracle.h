@@ -81,6 +81,9 @@ void oracle_scale_factors(float scale_factor, int nlevels, float* scale, float* 
 // ORBmatcher::DescriptorDistance (ORBmatcher.cc:2107-2123).
 int oracle_descriptor_distance(const uint8_t* a, const uint8_t* b);
 // cv::BFMatcher(NORM_HAMMING).knnMatch(q, t, m, 2) -> per query (idx1,d1,idx2,d2); idx=-1 absent.
+/* Measurement switch (tests only): 1 evaluates the descriptor's cos / sin as (float)cos((double)a)
+ * instead of the reference's float overloads; 0 (default) follows the reference. */
+void oracle_set_trig_double(int on);
 void oracle_knn2(const uint8_t* q, int nq, const uint8_t* t, int nt, int32_t* idx1, int32_t* d1,
                  int32_t* idx2, int32_t* d2);
 // Reference-ordered sort (std::sort + compareNodes, ORBextractor_old.cc:540-555,702) on

@@ -11,7 +11,7 @@
 //          orbslam_dsp.cpp:447-453; coordinates are >= 0 so this is floor)
 //   angle  (cos8 & 0xFF) | ((sin8 & 0xFF) << 8), cos8/sin8 = rint(64 * cos/sin of the keypoint
 //          angle) with the same single-precision cos/sin the descriptor rotation uses
-//          (ORBextractor_old.cc:115-116): the encoding the host decodes with
+//          (ORBextractor_old.cc:114-115, libm cosf / sinf): the encoding the host decodes with
 //          atan2(sin8 / 64, cos8 / 64) (LynxHardwareAccelerator.cpp:174-178)
 //   level  octave
 //   indices/distances: idx1 (-1 if absent), dist1, dist2 clamped to 32767 (absent = 32767)
@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 
 #include "orb_kernels.h"
+#include "orb_math.h"
 
 namespace orbgpu {
 
@@ -72,12 +73,12 @@ __global__ __launch_bounds__(256) void k_pack_soa(SoaArgs a) {
         const float* kp = reinterpret_cast<const float*>(static_cast<const uint8_t*>(a.kps) + o * 28);
         const float x = kp[0], y = kp[1], ang = kp[3];
         const int oct = reinterpret_cast<const int32_t*>(kp)[5];
-        // the descriptor rotation's cos/sin (ORBextractor_old.cc:115-116): angle * factorPI in
-        // float, cos/sin in double, rounded to float
+        // the descriptor rotation's cos/sin (ORBextractor_old.cc:114-115): angle * factorPI in
+        // float, then the float overloads std::cos / std::sin (libm cosf / sinf)
         const float rad = ang * (float)(3.14159265358979323846 / 180.0);
-        double sd, cd;
-        sincos((double)rad, &sd, &cd);
-        const int c8 = (int)rintf(64.0f * (float)cd), s8 = (int)rintf(64.0f * (float)sd);
+        float sd, cd;
+        libm_sincosf(rad, &sd, &cd);
+        const int c8 = (int)rintf(64.0f * cd), s8 = (int)rintf(64.0f * sd);
         a.x[o] = (int32_t)x;
         a.y[o] = (int32_t)y;
         a.angle[o] = (c8 & 0xFF) | ((s8 & 0xFF) << 8);

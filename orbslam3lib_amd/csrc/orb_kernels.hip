@@ -979,9 +979,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
         // computeOrbDescriptor (:108-148): lane `sub` makes bits [sub * kOdPairs, + kOdPairs)
         const float factorPI = (float)(3.14159265358979323846 / 180.0);
         const float ang = angle * factorPI;
-        double sd, cd;
-        sincos((double)ang, &sd, &cd);
-        const float ca = (float)cd, sn = (float)sd;
+        float sn, ca;  // std::sin(float) / std::cos(float) (:114-115): libm sinf / cosf
+        libm_sincosf(ang, &sn, &ca);
         // the 37 x 37 blurred patch (rows y-18..y+18 from the dword at or below x-18) goes to
         // LDS with 16-byte buffer loads (out-of-range bytes read as 0 and are never sampled),
         // then every sample is an LDS byte read: 4 vector-memory instructions per lane

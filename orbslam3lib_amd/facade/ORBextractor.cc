@@ -1,8 +1,10 @@
 // ORBextractor.cc -- the ORB_SLAM3::ORBextractor facade over the C ABI (include/orbgpu.h).
 //
 // Compiled by the integrating project (with -DORBGPU_WITH_OPENCV and its OpenCV), or against
-// include/orbslam3/cv_shim.h as in tests/cpp.  Mirrors cpp/src/ORBextractor_old.cc:411-471
-// (ctor tables) and :1088-1191 (operator() output contract); the compute is liborbgpu.so.
+// include/orbslam3/cv_shim.h as in tests/cpp; both modes see OpenCV's API shape (CV_8U macros,
+// InputArray = const _InputArray&).  Mirrors cpp/src/ORBextractor_old.cc:411-471 (ctor tables)
+// and :1088-1191 (operator() output contract), and cpp/src/ORBextractor.cc:118-165 (the stereo
+// operator() over the accelerator session); the compute is liborbgpu.so.
 #include "../../include/orbslam3/ORBextractor.h"
 
 #include <cstring>
@@ -23,8 +25,8 @@ ORBextractor::ORBextractor(int _nfeatures, float _scaleFactor, int _nlevels, int
     mvInvLevelSigma2.resize(nlevels);
     mnFeaturesPerLevel.resize(nlevels);
     mvImagePyramid.resize(nlevels);
-    // Tables come from the library (same float/double arithmetic as :416-447); the context
-    // itself is created lazily at the first image size, like LynxHardwareAccelerator.
+    // Tables come from the library (same float/double arithmetic as :416-447); the context grows
+    // to the largest image seen.
     if (ensureContext(640, 480) != ORBGPU_OK)
         throw std::runtime_error(std::string("orbgpu: ") + orbgpu_last_error());
     orbgpu_get_scale_tables(mCtx, mvScaleFactor.data(), mvInvScaleFactor.data(), mvLevelSigma2.data(),
@@ -49,8 +51,9 @@ void ORBextractor::exportPyramid(int image) {
     for (int l = 0; l < nlevels; ++l) {
         int w = 0, h = 0;
         orbgpu_get_pyramid_level(mCtx, image, l, 0, nullptr, 0, &w, &h);
-        mvImagePyramid[l].create(h, w, cv::CV_8U);
-        orbgpu_get_pyramid_level(mCtx, image, l, 0, mvImagePyramid[l].ptr(0), (int)mvImagePyramid[l].step, &w, &h);
+        mvImagePyramid[l].create(h, w, CV_8U);
+        orbgpu_get_pyramid_level(mCtx, image, l, 0, mvImagePyramid[l].ptr<unsigned char>(0),
+                                 (int)mvImagePyramid[l].step[0], &w, &h);
     }
 }
 
@@ -71,62 +74,85 @@ static void to_cv(const std::vector<orbgpu_keypoint>& src, int n, std::vector<cv
 int ORBextractor::operator()(cv::InputArray _image, cv::InputArray /*_mask*/,
                              std::vector<cv::KeyPoint>& _keypoints, cv::OutputArray _descriptors,
                              std::vector<int>& vLappingArea) {
+    if (_image.empty()) return -1;  // :1092-1093
     cv::Mat image = _image.getMat();
-    if (image.empty()) return -1;  // :1092-1093
-    if (image.type() != cv::CV_8UC1) return -1;
+    if (image.type() != CV_8UC1) return -1;  // assert :1096
     if ((mStatus = ensureContext(image.cols, image.rows)) != ORBGPU_OK) return -1;
     const int cap = 8 * nfeatures + 64 * nlevels + 4096;
-    mKps[0].resize(cap);
-    std::vector<uint8_t> desc((size_t)cap * 32);
+    mKps.resize(cap);
+    mDesc.resize((size_t)cap * 32);
     int n = 0, mono = 0;
     const int lap0 = vLappingArea.size() > 0 ? vLappingArea[0] : 0;
     const int lap1 = vLappingArea.size() > 1 ? vLappingArea[1] : 0;
-    mStatus = orbgpu_extract(mCtx, image.ptr(0), image.cols, image.rows, (int)image.step1(), lap0, lap1,
-                             mKps[0].data(), desc.data(), cap, &n, &mono);
+    mStatus = orbgpu_extract(mCtx, image.ptr<unsigned char>(0), image.cols, image.rows, (int)image.step[0], lap0,
+                             lap1, mKps.data(), mDesc.data(), cap, &n, &mono);
     if (mStatus != ORBGPU_OK) return -1;
-    to_cv(mKps[0], n, _keypoints);
+    to_cv(mKps, n, _keypoints);
     if (n == 0) {
         _descriptors.release();  // :1120-1121
     } else {
-        _descriptors.create(n, 32, cv::CV_8U);
+        _descriptors.create(n, 32, CV_8U);
         cv::Mat d = _descriptors.getMat();
-        for (int i = 0; i < n; ++i) std::memcpy(d.ptr(i), desc.data() + 32 * (size_t)i, 32);
+        for (int i = 0; i < n; ++i) std::memcpy(d.ptr<unsigned char>(i), mDesc.data() + 32 * (size_t)i, 32);
     }
     exportPyramid(0);
     return mono;
 }
 
-int ORBextractor::operator()(cv::InputArray left, cv::InputArray right,
-                             std::vector<cv::KeyPoint>& kl, cv::OutputArray dl, std::vector<int>& lapL,
-                             std::vector<cv::KeyPoint>& kr, cv::OutputArray dr, std::vector<int>& lapR,
-                             int& monoLeft, int& monoRight) {
-    cv::Mat L = left.getMat(), R = right.getMat();
-    if (L.empty() || R.empty() || L.rows != R.rows || L.cols != R.cols || L.step1() != R.step1()) return -1;
-    if ((mStatus = ensureContext(L.cols, L.rows)) != ORBGPU_OK) return -1;
-    const int cap = 8 * nfeatures + 64 * nlevels + 4096;
-    mKps[0].resize(cap);
-    mKps[1].resize(cap);
-    std::vector<uint8_t> d0((size_t)cap * 32), d1((size_t)cap * 32);
-    int la[2] = {lapL.size() > 0 ? lapL[0] : 0, lapL.size() > 1 ? lapL[1] : 0};
-    int ra[2] = {lapR.size() > 0 ? lapR[0] : 0, lapR.size() > 1 ? lapR[1] : 0};
-    int nl = 0, nr = 0;
-    mStatus = orbgpu_extract_stereo(mCtx, L.ptr(0), R.ptr(0), L.cols, L.rows, (int)L.step1(), la, ra,
-                                    mKps[0].data(), d0.data(), &nl, &monoLeft, mKps[1].data(), d1.data(),
-                                    &nr, &monoRight, cap);
-    if (mStatus != ORBGPU_OK) return -1;
-    to_cv(mKps[0], nl, kl);
-    to_cv(mKps[1], nr, kr);
-    struct { cv::Mat* m; std::vector<uint8_t>* d; int n; } outs[2] = {{&dl, &d0, nl}, {&dr, &d1, nr}};
-    for (auto& o : outs) {
-        if (o.n == 0) {
-            o.m->release();
-            continue;
-        }
-        o.m->create(o.n, 32, cv::CV_8U);
-        for (int i = 0; i < o.n; ++i) std::memcpy(o.m->ptr(i), o.d->data() + 32 * (size_t)i, 32);
+LynxHardwareAccelerator* ORBextractor::accelerator(int width, int height) {
+    // ORBextractor.cc:125-128: the session is created on first use (with this extractor's
+    // parameters and geometry here, the DSP's were fixed)
+    if (!LynxHardwareAccelerator::lynxHardwareAccelerator)
+        LynxHardwareAccelerator::lynxHardwareAccelerator.reset(
+            new LynxHardwareAccelerator(nfeatures, (float)scaleFactor, nlevels, iniThFAST, minThFAST, width, height));
+    return LynxHardwareAccelerator::lynxHardwareAccelerator.get();
+}
+
+int ORBextractor::operator()(cv::InputArray _image, std::vector<cv::KeyPoint>& kl, cv::OutputArray dl,
+                             std::vector<int>& lapL, std::vector<cv::KeyPoint>& kr, cv::OutputArray dr,
+                             std::vector<int>& lapR, int& monoLeft, int& monoRight) {
+    if (_image.empty()) return -1;
+    cv::Mat sbs = _image.getMat();
+    if (sbs.type() != CV_8UC1 || sbs.cols < 2 || (sbs.cols & 1)) return -1;
+    const int W = sbs.cols / 2, H = sbs.rows;
+    try {
+        LynxHardwareAccelerator* acc = accelerator(W, H);
+        acc->StoreInputBuffer(sbs.ptr<unsigned char>(0), W, H, (int)sbs.step[0]);
+        int nl = 0, nr = 0;
+        const int id = acc->ExtractORB(nl, nr, kl, kr, dl, dr, lapL.size() > 0 ? lapL[0] : 0,
+                                       lapL.size() > 1 ? lapL[1] : 0, lapR.size() > 0 ? lapR[0] : 0,
+                                       lapR.size() > 1 ? lapR[1] : 0, monoLeft, monoRight);
+        if (id < 0) return -1;
+        if (mbExportPyramid) acc->ExportPyramid(0, mvImagePyramid);
+        return id;
+    } catch (const std::exception&) {
+        mStatus = ORBGPU_ERR_HIP;
+        return -1;
     }
-    exportPyramid(0);
-    return 0;
+}
+
+int ORBextractor::operator()(cv::InputArray left, cv::InputArray right, std::vector<cv::KeyPoint>& kl,
+                             cv::OutputArray dl, std::vector<int>& lapL, std::vector<cv::KeyPoint>& kr,
+                             cv::OutputArray dr, std::vector<int>& lapR, int& monoLeft, int& monoRight) {
+    if (left.empty() || right.empty()) return -1;
+    cv::Mat L = left.getMat(), R = right.getMat();
+    if (L.rows != R.rows || L.cols != R.cols || L.step[0] != R.step[0] || L.type() != CV_8UC1 ||
+        R.type() != CV_8UC1)
+        return -1;
+    try {
+        LynxHardwareAccelerator* acc = accelerator(L.cols, L.rows);
+        int nl = 0, nr = 0;
+        const int id = acc->ExtractORBPair(L.ptr<unsigned char>(0), R.ptr<unsigned char>(0), L.cols, L.rows,
+                                           (int)L.step[0], nl, nr, kl, kr, dl, dr, lapL.size() > 0 ? lapL[0] : 0,
+                                           lapL.size() > 1 ? lapL[1] : 0, lapR.size() > 0 ? lapR[0] : 0,
+                                           lapR.size() > 1 ? lapR[1] : 0, monoLeft, monoRight);
+        if (id < 0) return -1;
+        if (mbExportPyramid) acc->ExportPyramid(0, mvImagePyramid);
+        return id;
+    } catch (const std::exception&) {
+        mStatus = ORBGPU_ERR_HIP;
+        return -1;
+    }
 }
 
 }  // namespace ORB_SLAM3

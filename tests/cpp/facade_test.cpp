@@ -13,6 +13,7 @@
 typedef struct { float x, y, size, angle, response; int32_t octave, class_id; } okp;
 typedef int (*oracle_extract_t)(int, float, int, int, int, const uint8_t*, int, int, int, int, int,
                                 okp*, uint8_t*, int, int*);
+typedef void (*oracle_knn2_t)(const uint8_t*, int, const uint8_t*, int, int32_t*, int32_t*, int32_t*, int32_t*);
 
 static std::vector<uint8_t> texture(int w, int h, uint32_t seed) {
     std::vector<uint8_t> img((size_t)w * h);
@@ -41,8 +42,26 @@ static int compare(const char* tag, const std::vector<cv::KeyPoint>& k, const cv
             printf("%s: keypoint %d differs\n", tag, i);
             return 1;
         }
-        if (std::memcmp(d.ptr(i), rd + 32 * (size_t)i, 32)) {
+        if (std::memcmp(d.ptr<unsigned char>(i), rd + 32 * (size_t)i, 32)) {
             printf("%s: descriptor %d differs\n", tag, i);
+            return 1;
+        }
+    }
+    return 0;
+}
+
+static int compare_knn(const char* tag, const std::vector<uint16_t>& idx, const std::vector<uint16_t>& d1,
+                       const std::vector<uint16_t>& d2, const int32_t* ri1, const int32_t* rd1, const int32_t* rd2,
+                       int nq) {
+    if ((int)idx.size() != nq || (int)d1.size() != nq || (int)d2.size() != nq) {
+        printf("%s: %zu matches vs %d queries\n", tag, idx.size(), nq);
+        return 1;
+    }
+    for (int i = 0; i < nq; ++i) {
+        const uint16_t ei1 = (uint16_t)(int16_t)ri1[i];
+        const uint16_t ed1 = (uint16_t)(rd1[i] > 32767 ? 32767 : rd1[i]), ed2 = (uint16_t)(rd2[i] > 32767 ? 32767 : rd2[i]);
+        if (idx[i] != ei1 || d1[i] != ed1 || d2[i] != ed2) {
+            printf("%s: match %d differs (%d %d %d vs %d %d %d)\n", tag, i, idx[i], d1[i], d2[i], ri1[i], rd1[i], rd2[i]);
             return 1;
         }
     }
@@ -54,11 +73,13 @@ int main(int argc, char** argv) {
     void* h = dlopen(oracle_path, RTLD_NOW);
     if (!h) { printf("cannot load oracle %s\n", oracle_path); return 2; }
     auto ox = (oracle_extract_t)dlsym(h, "oracle_extract");
+    auto oknn = (oracle_knn2_t)dlsym(h, "oracle_knn2");
+    if (!ox || !oknn) { printf("oracle symbols\n"); return 2; }
     const int W = 640, H = 480;
     std::vector<uint8_t> L = texture(W, H, 7), R = texture(W, H, 8);
     ORB_SLAM3::ORBextractor ex(2000, 1.2f, 8, 20, 7);
     if (ex.GetLevels() != 8 || ex.GetScaleFactors().size() != 8) { printf("getters\n"); return 1; }
-    cv::Mat im(H, W, cv::CV_8U, L.data(), W), desc;
+    cv::Mat im(H, W, CV_8U, L.data(), W), desc;
     std::vector<cv::KeyPoint> kps;
     std::vector<int> lap = {0, 1000};
     const int mono = ex(im, cv::Mat(), kps, desc, lap);
@@ -71,17 +92,58 @@ int main(int argc, char** argv) {
         printf("pyramid export\n");
         bad = 1;
     }
-    cv::Mat ir(H, W, cv::CV_8U, R.data(), W), dl, dr;
-    std::vector<cv::KeyPoint> kl, kr;
-    std::vector<int> lapL = {0, 0}, lapR = {100, 600};
-    int ml = 0, mr = 0;
-    ex(im, ir, kl, dl, lapL, kr, dr, lapR, ml, mr);
-    rmono = ox(2000, 1.2f, 8, 20, 7, L.data(), W, H, W, 0, 0, rk.data(), rd.data(), 20000, &rn);
-    bad |= compare("stereo-left", kl, dl, ml, rk.data(), rd.data(), rn, rmono);
-    rmono = ox(2000, 1.2f, 8, 20, 7, R.data(), W, H, W, 100, 600, rk.data(), rd.data(), 20000, &rn);
-    bad |= compare("stereo-right", kr, dr, mr, rk.data(), rd.data(), rn, rmono);
-    int dd = ORB_SLAM3::ORBmatcher::DescriptorDistance(dl.rowRange(0, 1), dr.rowRange(0, 1));
-    if (dd < 0 || dd > 256) bad = 1;
+    // stereo forms: the side-by-side frame (ORBextractor.h:52-57) and two images; each returns
+    // the frame id whose matches LynxHardwareAccelerator::BFMatchORB returns (Frame.cc:1164)
+    std::vector<uint8_t> sbs((size_t)2 * W * H);
+    for (int y = 0; y < H; ++y) {
+        std::memcpy(sbs.data() + (size_t)y * 2 * W, L.data() + (size_t)y * W, W);
+        std::memcpy(sbs.data() + (size_t)y * 2 * W + W, R.data() + (size_t)y * W, W);
+    }
+    cv::Mat frame(H, 2 * W, CV_8U, sbs.data(), 2 * W), ir(H, W, CV_8U, R.data(), W);
+    std::vector<int> lapL = {300, 640}, lapR = {0, 340};
+    std::vector<okp> rkl(20000), rkr(20000);
+    std::vector<uint8_t> rdl(20000 * 32), rdr(20000 * 32);
+    int rnl = 0, rnr = 0;
+    const int rml = ox(2000, 1.2f, 8, 20, 7, L.data(), W, H, W, lapL[0], lapL[1], rkl.data(), rdl.data(), 20000, &rnl);
+    const int rmr = ox(2000, 1.2f, 8, 20, 7, R.data(), W, H, W, lapR[0], lapR[1], rkr.data(), rdr.data(), 20000, &rnr);
+    const int nq = rnl - rml;
+    std::vector<int32_t> ri1(nq + 1), rd1(nq + 1), ri2(nq + 1), rd2(nq + 1);
+    oknn(rdl.data() + 32 * (size_t)rml, nq, rdr.data() + 32 * (size_t)rmr, rnr - rmr, ri1.data(), rd1.data(),
+         ri2.data(), rd2.data());
+    int ids[2] = {0, 0};
+    for (int form = 0; form < 2; ++form) {
+        cv::Mat dl, dr;
+        std::vector<cv::KeyPoint> kl, kr;
+        int ml = -1, mr = -1;
+        ids[form] = form == 0 ? ex(frame, kl, dl, lapL, kr, dr, lapR, ml, mr)
+                              : ex(im, ir, kl, dl, lapL, kr, dr, lapR, ml, mr);
+        const char* tag = form == 0 ? "sbs" : "pair";
+        if (ids[form] <= 0) { printf("%s: frame id %d\n", tag, ids[form]); bad = 1; continue; }
+        bad |= compare(tag, kl, dl, ml, rkl.data(), rdl.data(), rnl, rml);
+        bad |= compare(tag, kr, dr, mr, rkr.data(), rdr.data(), rnr, rmr);
+        std::vector<uint16_t> idx, d1, d2;
+        ORB_SLAM3::LynxHardwareAccelerator::lynxHardwareAccelerator->BFMatchORB(
+            ids[form], dr.rowRange(mr, dr.rows), dl.rowRange(ml, dl.rows), idx, d1, d2);
+        bad |= compare_knn(tag, idx, d1, d2, ri1.data(), rd1.data(), rd2.data(), nq);
+        if (ex.mvImagePyramid[0].cols != W) { printf("%s: pyramid\n", tag); bad = 1; }
+    }
+    if (ids[1] != ids[0] + 1) { printf("frame ids %d %d\n", ids[0], ids[1]); bad = 1; }
+    // a frame id that left the 3-frame cache: matched again on the device from the rows given
+    {
+        cv::Mat dl, dr;
+        std::vector<cv::KeyPoint> kl, kr;
+        int ml = 0, mr = 0;
+        for (int k = 0; k < 3; ++k) ex(im, ir, kl, dl, lapL, kr, dr, lapR, ml, mr);
+        std::vector<uint16_t> idx, d1, d2;
+        ORB_SLAM3::LynxHardwareAccelerator::lynxHardwareAccelerator->BFMatchORB(
+            ids[0], dr.rowRange(mr, dr.rows), dl.rowRange(ml, dl.rows), idx, d1, d2);
+        bad |= compare_knn("stale id", idx, d1, d2, ri1.data(), rd1.data(), rd2.data(), nq);
+    }
+    cv::Mat d0 = desc.rowRange(0, 1), d1 = desc.rowRange(1, 2);
+    const int dd = ORB_SLAM3::orbgpu::DescriptorDistance(d0, d1);
+    int ref = 0;
+    for (int b = 0; b < 32; ++b) ref += __builtin_popcount(d0.ptr<unsigned char>(0)[b] ^ d1.ptr<unsigned char>(0)[b]);
+    if (dd != ref) { printf("DescriptorDistance %d vs %d\n", dd, ref); bad = 1; }
     cv::Mat empty;
     if (ex(empty, cv::Mat(), kps, desc, lap) != -1) bad = 1;
     printf(bad ? "FACADE FAIL\n" : "FACADE OK %zu keypoints\n", kps.size());

@@ -15,6 +15,25 @@ using namespace orbgpu;
 
 extern "C" {
 
+// libm_sincosf (orb_math.h) against the host's own sinf / cosf on every `stride`-th float of
+// [lo, hi): returns the number of mismatching values (sin or cos), *checked = floats visited.
+long long harness_libm_sincosf_mismatches(float lo, float hi, int stride, long long* checked) {
+    uint32_t u = __builtin_bit_cast(uint32_t, lo);
+    const uint32_t end = __builtin_bit_cast(uint32_t, hi);
+    long long bad = 0, n = 0;
+    for (; u < end; u += (uint32_t)stride) {
+        volatile float y = __builtin_bit_cast(float, u);
+        const float c = cosf(y), s = sinf(y);
+        float ms, mc;
+        libm_sincosf(y, &ms, &mc);
+        bad += (__builtin_bit_cast(uint32_t, c) != __builtin_bit_cast(uint32_t, mc)) ||
+               (__builtin_bit_cast(uint32_t, s) != __builtin_bit_cast(uint32_t, ms));
+        ++n;
+    }
+    if (checked) *checked = n;
+    return bad;
+}
+
 int harness_octree(const uint32_t* keys, int n, int W, int H, int N, uint32_t* out, int out_cap) {
     const int nIni = std::max(1, (int)std::round((float)W / (float)H));
     const int cap = std::max(N + 3, 4 * nIni) + 8;

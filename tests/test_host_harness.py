@@ -169,3 +169,28 @@ def test_cells_thresholds_and_fallback(harness, oracle, ini, mn):
         np.testing.assert_array_equal(x, oc["x"])
         np.testing.assert_array_equal(y, oc["y"])
         np.testing.assert_array_equal(r, oc["response"])
+
+
+def test_libm_sincosf_restatement_equals_host_libm(harness):
+    """orb_math.h libm_sincosf (what k_orient_desc / k_pack_soa evaluate for the descriptor's
+    std::cos(float) / std::sin(float), ORBextractor_old.cc:114-115) equals the host's libm cosf /
+    sinf: every 61st float of [0, 2 pi) plus every float within 2^14 ulps of each multiple of
+    pi/4 (the reduction's quadrant edges) and of the 2^-12 / pi/4 branch points.  The exhaustive
+    pass over all 1,086,918,649 floats of [0, 6.2832) is tools/sincosf_exhaustive.py (0
+    mismatches)."""
+    import math
+    f = harness.harness_libm_sincosf_mismatches
+    f.restype = C.c_longlong
+    f.argtypes = [C.c_float, C.c_float, C.c_int, C.POINTER(C.c_longlong)]
+    n = C.c_longlong(0)
+    assert f(0.0, 6.2832, 61, C.byref(n)) == 0
+    assert n.value > 17_000_000
+    total = 0
+    edges = [k * math.pi / 4 for k in range(9)] + [2.0 ** -12, 0.7853982]
+    for e in edges:
+        u = int(np.float32(e).view(np.uint32))
+        lo = np.uint32(max(u - (1 << 14), 0)).view(np.float32)
+        hi = np.uint32(u + (1 << 14)).view(np.float32)
+        assert f(float(lo), float(hi), 1, C.byref(n)) == 0, e
+        total += n.value
+    assert total > 300_000

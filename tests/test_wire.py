@@ -28,9 +28,13 @@ def _sbs(pairs, pad=0):
 
 
 def _np_soa(kps):
+    # the descriptor's std::cos(float) / std::sin(float) (ORBextractor_old.cc:114-115): libm cosf
+    libm = C.CDLL("libm.so.6")
+    libm.cosf.restype = libm.sinf.restype = C.c_float
+    libm.cosf.argtypes = libm.sinf.argtypes = [C.c_float]
     rad = (kps["angle"].astype(np.float32) * np.float32(np.pi / 180.0)).astype(np.float32)
-    a = np.cos(rad.astype(np.float64)).astype(np.float32)
-    b = np.sin(rad.astype(np.float64)).astype(np.float32)
+    a = np.array([libm.cosf(float(r)) for r in rad], np.float32)
+    b = np.array([libm.sinf(float(r)) for r in rad], np.float32)
     c8 = np.rint(np.float32(64) * a).astype(np.int32)
     s8 = np.rint(np.float32(64) * b).astype(np.int32)
     return {"x": kps["x"].astype(np.int32), "y": kps["y"].astype(np.int32),
