@@ -26,6 +26,9 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12  # 256 CU x 4 SIMD32 x 32 lanes x 2.4 GHz, int32 ops
+# dense int8 MFMA: 2x the BF16 rate per clock (MI355X_MICROARCH.md, matrix-core table: I8 32x32x32
+# takes the cycles of BF16 32x32x16), BF16 dense ~2.5 PF -> ~5.0 POPS
+MFMA_I8_PEAK_TOPS = 5000.0
 
 
 def level_sizes(w, h, sf=1.2, L=8):
@@ -131,6 +134,7 @@ def cpu_baseline(w, h, nfeatures, seconds, map_points=3000):
     thread, on a bounded sample of the same workload: pairs until `seconds` elapse."""
     from oracle import oracle_py as O
     from orbslam3lib_amd import synth
+    native = O.use_native()  # -O3 -march=native -ffp-contract=off, built on this host (SURVEY §8d)
     O.lib()
     pairs = [synth.stereo_pair(h, w, 1000 + i) for i in range(4)]
     stereo_pyr = [(O.pyramid(L), O.pyramid(R)) for L, R in pairs]
@@ -173,30 +177,37 @@ def cpu_baseline(w, h, nfeatures, seconds, map_points=3000):
         t_ex += t1 - t0
         t_bf += t2 - t1
         i += 1
-    # SURVEY §8d modes 2 and 3: both eyes of a pair on two threads (Frame.cc:142-145), and a
-    # frames-parallel pool (ctypes releases the GIL inside the oracle); a few seconds each
-    from concurrent.futures import ThreadPoolExecutor
-    pool_threads = max(1, min(16, os.cpu_count() or 1))
-
-    def run_pairs(nthreads, per_pair_split, secs):
-        nf_, npairs, t0 = 0, 0, time.perf_counter()
-        with ThreadPoolExecutor(nthreads) as ex:
-            while time.perf_counter() - t0 < secs or npairs == 0:
-                if per_pair_split:
-                    L, R = pairs[npairs % len(pairs)]
-                    fl, fr = ex.submit(O.extract, L, nfeatures), ex.submit(O.extract, R, nfeatures)
-                    nf_ += len(fl.result()[0]) + len(fr.result()[0])
-                    npairs += 1
-                else:
-                    futs = [ex.submit(O.extract, pairs[(npairs + k) % len(pairs)][k % 2 and 1 or 0], nfeatures)
-                            for k in range(2 * nthreads)]
-                    nf_ += sum(len(f.result()[0]) for f in futs)
-                    npairs += nthreads
+    # SURVEY §8d modes 2 and 3, inside the oracle (std::thread, no Python in the loop): both eyes of
+    # a pair on two threads (Frame.cc:142-145), and a frames-parallel pool over every core this
+    # process may run on (and over 16, the box's CPU share per GPU, as a second figure)
+    def pool_rate(nthreads, nimg, secs):
+        batch = np.stack([pairs[(k // 2) % len(pairs)][k % 2] for k in range(nimg)])
+        nf_, t0, reps = 0, time.perf_counter(), 0
+        while time.perf_counter() - t0 < secs or reps == 0:
+            nf_ += O.extract_many(batch, nthreads, nfeatures)
+            reps += 1
         return nf_ / (time.perf_counter() - t0) / 1e6
-    mode2 = run_pairs(2, True, max(2.0, seconds / 4))
-    mode3 = run_pairs(pool_threads, False, max(2.0, seconds / 4))
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        quota = None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    # the cores this process can actually use: its affinity mask, capped by its cgroup CPU quota
+    # (the GPU box gives each GPU's job 16 CPUs of a 256-thread host: 256 threads there run at
+    # the speed of 16, and slower than 16 threads)
+    cores = avail if quota is None else max(1, min(avail, int(quota)))
+    mode2 = pool_rate(2, 2, max(2.0, seconds / 6))
+    mode3 = pool_rate(cores, max(4 * cores, 32), max(3.0, seconds / 3))
+    mode3_all = pool_rate(avail, 4 * avail, 2.0) if avail != cores else mode3
     return {"pairs": i, "mfeat_s": nfeat / t_ex / 1e6, "mmatch_s": nq / t_bf / 1e6,
-            "mfeat_s_2threads_per_pair": mode2, "mfeat_s_pool": mode3, "pool_threads": pool_threads,
+            "mfeat_s_2threads_per_pair": mode2, "mfeat_s_pool": mode3, "pool_threads": cores,
+            "affinity": avail, "mfeat_s_pool_affinity": mode3_all, "cgroup_cpu_quota": quota,
+            "native": native is not None,
             "median_pair_ms": 1e3 * float(np.median(pair_times)) if pair_times else None,
             "stereo_mkp_s": nq / t_st[0] / 1e6 if t_st[0] > 0 else None,
             "grid_mkp_s": nfeat / t_gr / 1e6 if t_gr > 0 else None,
@@ -306,13 +317,34 @@ def main():
     if dom_name and stages_timed.get(dom_name, (0, 0))[1] > 0:
         stages[dom_name] = stages_timed[dom_name]  # live measurement from the timed region
 
+    # streaming ingest (C3's shape: every batch arrives from the host): each step's 2P frames are
+    # copied from pinned host memory on the copy stream while the previous step computes
+    # (orbgpu_upload_images_async); K uploads + K steps in the timed loop, the first upload exposed
+    pin = be.pinned(imgs.shape)
+    pin[:] = imgs
+    for _ in range(2):  # warm-up: creates the copy stream, touches both input buffers
+        be.upload_async(pin)
+        step()
+    be.synchronize()
+    barrier(dist)
+    p0 = time.perf_counter()
+    be.upload_async(pin)
+    for k in range(args.steps):
+        step()
+        if k + 1 < args.steps:
+            be.upload_async(pin)
+    be.synchronize()
+    p_el = max_over_ranks(dist, time.perf_counter() - p0)
+    be.free_pinned()
+
     total_feats = sum_over_ranks(dist, feats_per_step * args.steps)
     total_q = sum_over_ranks(dist, nq_per_step * args.steps)
     total_pairs = sum_over_ranks(dist, pairs_per_step * args.steps)
     mfeat = total_feats / elapsed / 1e6
     # the PCIe-inclusive rate beside the resident one (never `value`)
     h2d_max = max_over_ranks(dist, h2d_s)
-    h2d_incl = sum_over_ranks(dist, feats_per_step) / (elapsed / args.steps + h2d_max) / 1e6
+    h2d_serial = sum_over_ranks(dist, feats_per_step) / (elapsed / args.steps + h2d_max) / 1e6
+    h2d_incl = total_feats / p_el / 1e6
     mmatch = total_q / elapsed / 1e6
 
     # roofline of the dominant kernel (per-launch algorithmic bytes / measured avg duration)
@@ -336,8 +368,13 @@ def main():
             row["GBps"] = round(bytes_launch / (avg_ms * 1e-3) / 1e9, 1)
             row["frac_hbm"] = round(row["GBps"] / HBM_PEAK_GBS, 4)
         if name == "k_knn2":
-            ops = 16.0 * pairs_per_step
-            row["Tops"] = round(ops / (avg_ms * 1e-3) / 1e12, 2)
+            # the kernel runs on the i8 matrix cores: 2 x 256 int8 ops per (query, train)
+            # pair are what it issues; the 16-op VALU popcount figure is kept beside it
+            nsteps = args.steps if row["source"] == "timed region" else 3
+            pairs_launch = pairs_per_step / (cnt / nsteps)
+            row["Tops_i8"] = round(512.0 * pairs_launch / (avg_ms * 1e-3) / 1e12, 1)
+            row["frac_mfma_i8"] = round(row["Tops_i8"] / MFMA_I8_PEAK_TOPS, 4)
+            row["Tops"] = round(16.0 * pairs_launch / (avg_ms * 1e-3) / 1e12, 2)
             row["frac_valu"] = round(row["Tops"] / VALU_PEAK_TOPS, 4)
         stage_rows[name] = row
     # the dominant kernel is picked on the all-stage pass; its row holds the timed-region events
@@ -356,9 +393,9 @@ def main():
             roof = {"kernel": dom, "bound": "hbm", "achieved": r["GBps"], "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": r["frac_hbm"], "traffic": traffic,
                     "bytes_per_launch": r["bytes_per_launch"], "avg_us": r["avg_us"]}
-        elif "Tops" in r:
-            roof = {"kernel": dom, "bound": "valu", "achieved": r["Tops"], "peak": round(VALU_PEAK_TOPS, 1),
-                    "unit": "Tops/s", "frac": r["frac_valu"], "traffic": traffic, "avg_us": r["avg_us"]}
+        elif "Tops_i8" in r:
+            roof = {"kernel": dom, "bound": "mfma_i8", "achieved": r["Tops_i8"], "peak": MFMA_I8_PEAK_TOPS,
+                    "unit": "Tops/s", "frac": r["frac_mfma_i8"], "traffic": traffic, "avg_us": r["avg_us"]}
         else:
             roof = {"kernel": dom, "bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": None, "traffic": traffic, "avg_us": r["avg_us"]}
@@ -377,6 +414,14 @@ def main():
         roof_fp = {"kernels": fp_names, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
                    "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "bytes_per_step": int(fp_bytes),
                    "us_per_step": round(fp_ms * 1e3, 1)}
+
+    # the matcher's own roofline (north_star: "Hamming BFMatch"): it runs on the int8 matrix cores
+    kr = stage_rows.get("k_knn2")
+    roof_knn = None
+    if kr and "Tops_i8" in kr:
+        roof_knn = {"kernel": "k_knn2", "bound": "mfma_i8", "achieved": kr["Tops_i8"], "peak": MFMA_I8_PEAK_TOPS,
+                    "unit": "Tops/s", "frac": kr["frac_mfma_i8"], "avg_us": kr["avg_us"],
+                    "ops_per_pair": 512, "valu_equivalent_Tops": kr["Tops"], "frac_valu_int32": kr["frac_valu"]}
 
     # Frame::ComputeStereoMatches on the same resident batch, timed on its own
     # (not part of the headline step): EuRoC-like rig, baseline 0.11 m, fx 435.2
@@ -598,15 +643,23 @@ def main():
                     break
         except OSError:
             pass
-        cpu = {"value": round(cb["mfeat_s"], 5), "unit": "Mfeatures/s", "cores": 1, "kind": "port",
-               "label": "oracle restatement, scalar C++ (-O3, no fast-math, no FMA), not OpenCV-SIMD",
-               "host": {"nproc": os.cpu_count(), "model": cpu_model},
+        cpu = {"value": round(cb["mfeat_s_pool"], 4), "unit": "Mfeatures/s", "cores": cb["pool_threads"],
+               "kind": "port",
+               "label": "oracle restatement, scalar C++ (-O3%s -ffp-contract=off, no fast-math), not OpenCV-SIMD; "
+                        "frames-parallel pool of %d std::threads = every CPU this process may use (affinity %d "
+                        "threads, cgroup quota %s CPUs)" % (" -march=native" if cb["native"] else "",
+                                                            cb["pool_threads"], cb["affinity"], cb["cgroup_cpu_quota"]),
+               "host": {"nproc": os.cpu_count(), "affinity": cb["affinity"], "cgroup_cpu_quota": cb["cgroup_cpu_quota"],
+                        "model": cpu_model},
+               "mfeatures_s_1thread": round(cb["mfeat_s"], 5),
                "median_pair_ms_1thread": round(cb["median_pair_ms"], 2) if cb["median_pair_ms"] else None,
                "mfeatures_s_2threads_per_pair": round(cb["mfeat_s_2threads_per_pair"], 5),
-               "mfeatures_s_pool": round(cb["mfeat_s_pool"], 5), "pool_threads": cb["pool_threads"],
-               "sample": "%d synthetic 640x480 stereo pairs, oracle extract (both eyes, 1 thread); "
-                         "BF kNN2 %.4f Mmatches/s" % (cb["pairs"], cb["mmatch_s"]),
-               "mmatches_s": round(cb["mmatch_s"], 5),
+               "mfeatures_s_pool_all_affinity_threads": round(cb["mfeat_s_pool_affinity"], 4),
+               "mfeatures_s_whole_host_linear_estimate": round(cb["mfeat_s_pool"] / cb["pool_threads"] *
+                                                               (os.cpu_count() or 1), 3),
+               "sample": "4 synthetic 640x480 stereo pairs: %d pairs extracted on 1 thread (both eyes) + BF kNN2, "
+                         "then the pool over >= 32 frames for >= %.0f s" % (cb["pairs"], max(3.0, args.cpu_seconds / 3)),
+               "mmatches_s_1thread": round(cb["mmatch_s"], 5),
                "stereo_mkeypoints_s": round(cb["stereo_mkp_s"], 5) if cb["stereo_mkp_s"] else None,
                "undistort_grid_mkeypoints_s": round(cb["grid_mkp_s"], 5) if cb["grid_mkp_s"] else None,
                "search_by_projection_mmappoints_s": round(cb["sbp_mmp_s"], 5) if cb["sbp_mmp_s"] else None}
@@ -634,9 +687,13 @@ def main():
             "features_per_step_per_gpu": feats_per_step,
             "h2d": {"ms_per_batch_upload": round(h2d_max * 1e3, 3),
                     "GBps": round(imgs.nbytes / h2d_max / 1e9, 2) if h2d_max > 0 else None,
-                    "mfeatures_s_incl_upload": round(h2d_incl, 3)},
+                    "mfeatures_s_incl_upload": round(h2d_incl, 3),
+                    "ms_per_step_incl_upload": round(p_el / args.steps * 1e3, 4),
+                    "mode": "pinned host batch, async copy stream, upload of step k+1 beside step k",
+                    "mfeatures_s_upload_then_compute": round(h2d_serial, 3)},
             "roofline": roof,
             "roofline_fast_pyramid": roof_fp,
+            "roofline_knn2": roof_knn,
             "stages": stage_rows,
             "cpu_baseline": cpu,
             "stereo_matches": stereo,

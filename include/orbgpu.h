@@ -98,6 +98,17 @@ int orbgpu_extract_stereo(orbgpu_ctx* ctx, const uint8_t* left, const uint8_t* r
 int orbgpu_upload_images(orbgpu_ctx* ctx, const uint8_t* images, int n_images, int width,
                          int height, int stride);
 uint8_t* orbgpu_device_input(orbgpu_ctx* ctx); /* device pointer of the input buffer */
+/* Streaming ingest (C3: one frame pair after another, LynxHardwareAccelerator.cpp:121-123 copies
+ * each frame in): stage the NEXT batch's pixels while the current batch computes.  The copy runs
+ * on the context's copy stream into the second input buffer, after every kernel that read that
+ * buffer; the next orbgpu_run_batch reads it once the copy has landed.  `images` should be pinned
+ * (orbgpu_host_alloc) for the copy to run asynchronously at full PCIe rate.  One staged upload at
+ * a time (ORBGPU_ERR_INVALID otherwise). */
+int orbgpu_upload_images_async(orbgpu_ctx* ctx, const uint8_t* images, int n_images, int width,
+                               int height, int stride);
+/* Page-locked host memory for the async upload (hipHostMalloc / hipHostFree). */
+int orbgpu_host_alloc(size_t bytes, void** ptr);
+int orbgpu_host_free(void* ptr);
 int orbgpu_run_batch(orbgpu_ctx* ctx, int n_images, int width, int height, const int32_t* laps,
                      void* stream);
 /* Copy image i's results to the host (after orbgpu_synchronize or on the same stream). */

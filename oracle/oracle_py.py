@@ -35,11 +35,43 @@ def lib():
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             build()
-        _lib = C.CDLL(LIB_PATH)
-        _lib.oracle_fast_atan2.restype = C.c_float
-        _lib.oracle_fast_atan2.argtypes = [C.c_float, C.c_float]
-        _lib.oracle_ic_angle.restype = C.c_float
+        _load(LIB_PATH)
     return _lib
+
+
+def use_native():
+    """Switch to the -march=native build (bench.py's CPU baseline); builds it if needed.  Returns
+    the library path, or None when it cannot be built (the default build stays in use)."""
+    global _lib
+    path = os.path.join(HERE, "build", "liborb_oracle_native.so")
+    try:
+        subprocess.check_call(["make", "-s", "-C", HERE, "native"])
+    except (OSError, subprocess.CalledProcessError):
+        return None
+    _lib = None
+    _load(path)
+    return path
+
+
+def _load(path):
+    global _lib
+    _lib = C.CDLL(path)
+    _lib.oracle_fast_atan2.restype = C.c_float
+    _lib.oracle_fast_atan2.argtypes = [C.c_float, C.c_float]
+    _lib.oracle_ic_angle.restype = C.c_float
+    _lib.oracle_extract_many.restype = C.c_longlong
+    return _lib
+
+
+def extract_many(imgs, nthreads, nfeatures=1000, scale_factor=1.2, nlevels=8, ini_th=20, min_th=7):
+    """Frames-parallel pool inside the oracle (std::thread): imgs [n, h, w] -> total keypoints."""
+    imgs = np.ascontiguousarray(imgs, dtype=np.uint8)
+    n, h, w = imgs.shape
+    r = lib().oracle_extract_many(nfeatures, C.c_float(scale_factor), nlevels, ini_th, min_th, _p(imgs), n, w, h,
+                                  int(nthreads), None)
+    if r < 0:
+        raise RuntimeError("oracle_extract_many failed: %d" % r)
+    return int(r)
 
 
 def _p(a):

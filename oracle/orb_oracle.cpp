@@ -10,6 +10,8 @@
 #include "orb_oracle.h"
 
 #include <algorithm>
+#include <atomic>
+#include <thread>
 #include <cfloat>
 #include <climits>
 #include <cmath>
@@ -19,6 +21,8 @@
 #include <list>
 #include <utility>
 #include <vector>
+#include <atomic>
+#include <thread>
 
 #include "orb_pattern_data.h"
 
@@ -923,6 +927,35 @@ int oracle_descriptor_distance(const uint8_t* a, const uint8_t* b) {
         dist += (((v + (v >> 4)) & 0xF0F0F0F) * 0x1010101) >> 24;
     }
     return dist;
+}
+
+// The CPU baseline's frames-parallel pool (SURVEY §8d mode 3): n_images frames of w x h (pitch w)
+// extracted by `nthreads` std::threads, each taking the next frame from a shared counter; per-frame
+// keypoint counts out.  Returns the total keypoint count (< 0 on an error).
+long long oracle_extract_many(int nfeatures, float scale_factor, int nlevels, int ini_th, int min_th,
+                              const uint8_t* imgs, int n_images, int w, int h, int nthreads, int32_t* counts) {
+    if (!imgs || n_images < 0 || nthreads < 1) return -1;
+    std::atomic<int> next{0};
+    std::atomic<long long> total{0};
+    std::atomic<int> err{0};
+    auto work = [&] {
+        const int cap = 4 * nfeatures + 64 * nlevels + 4096;
+        std::vector<oracle_kp> kps(cap);
+        std::vector<uint8_t> desc((size_t)cap * 32);
+        for (int i = next++; i < n_images; i = next++) {
+            int n = 0;
+            const int r = oracle_extract(nfeatures, scale_factor, nlevels, ini_th, min_th, imgs + (size_t)i * w * h, w,
+                                         h, w, 0, 0, kps.data(), desc.data(), cap, &n);
+            if (r < 0) err = r;
+            if (counts) counts[i] = n;
+            total += n;
+        }
+    };
+    std::vector<std::thread> pool;
+    for (int t = 1; t < nthreads; ++t) pool.emplace_back(work);
+    work();
+    for (auto& t : pool) t.join();
+    return err ? (long long)err : total.load();
 }
 
 void oracle_set_trig_double(int on) { g_trig_double = on ? 1 : 0; }

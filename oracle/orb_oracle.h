@@ -84,6 +84,9 @@ int oracle_descriptor_distance(const uint8_t* a, const uint8_t* b);
 /* Measurement switch (tests only): 1 evaluates the descriptor's cos / sin as (float)cos((double)a)
  * instead of the reference's float overloads; 0 (default) follows the reference. */
 void oracle_set_trig_double(int on);
+/* Frames-parallel pool: n_images frames (pitch w) over nthreads threads; total keypoints. */
+long long oracle_extract_many(int nfeatures, float scale_factor, int nlevels, int ini_th, int min_th,
+                              const uint8_t* imgs, int n_images, int w, int h, int nthreads, int32_t* counts);
 void oracle_knn2(const uint8_t* q, int nq, const uint8_t* t, int nt, int32_t* idx1, int32_t* d1,
                  int32_t* idx2, int32_t* d2);
 // Reference-ordered sort (std::sort + compareNodes, ORBextractor_old.cc:540-555,702) on

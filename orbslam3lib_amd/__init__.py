@@ -45,7 +45,8 @@ EXPORTED = [
     "orbgpu_device_sbs_input", "orbgpu_upload_sbs", "orbgpu_ingest_sbs", "orbgpu_pack_soa",
     "orbgpu_download_soa", "orbgpu_download_matches16", "orbgpu_extract_features",
     "orbgpu_search_by_projection_batch", "orbgpu_search_by_projection_stereo",
-    "orbgpu_download_projection_matches",
+    "orbgpu_download_projection_matches", "orbgpu_upload_images_async", "orbgpu_host_alloc",
+    "orbgpu_host_free",
     "orbgpu_set_profiling", "orbgpu_num_stages", "orbgpu_stage_name", "orbgpu_stage_times",
     "orbgpu_reset_stage_times", "orbgpu_last_error", "orbgpu_abi_version",
 ]
@@ -79,6 +80,8 @@ def load_library(path: str = LIB_PATH):
     lib.orbgpu_device_input.argtypes = [C.c_void_p]
     lib.orbgpu_device_sbs_input.restype = C.c_void_p
     lib.orbgpu_device_sbs_input.argtypes = [C.c_void_p]
+    lib.orbgpu_host_alloc.argtypes = [C.c_size_t, C.POINTER(C.c_void_p)]
+    lib.orbgpu_host_free.argtypes = [C.c_void_p]
     for name in ("orbgpu_destroy", "orbgpu_synchronize", "orbgpu_set_profiling",
                  "orbgpu_reset_stage_times"):
         getattr(lib, name).argtypes = [C.c_void_p] + ([C.c_int] if name == "orbgpu_set_profiling" else [])
@@ -281,6 +284,28 @@ class BatchExtractor:
         _check(_lib.orbgpu_upload_images(self.ctx.handle, _p(imgs), n, w, h, w))
         self.n, self.height, self.width = n, h, w
         _check(_lib.orbgpu_synchronize(self.ctx.handle))
+
+    def upload_async(self, images):
+        """Stage the NEXT batch (orbgpu_upload_images_async): the copy runs beside the current
+        batch's kernels; the next run() reads it.  `images` should come from pinned()."""
+        imgs = np.ascontiguousarray(images, dtype=np.uint8)
+        n, h, w = imgs.shape
+        _check(_lib.orbgpu_upload_images_async(self.ctx.handle, _p(imgs), n, w, h, w))
+        self.n, self.height, self.width = n, h, w
+
+    def pinned(self, shape):
+        """A uint8 numpy array over page-locked host memory (freed with the extractor)."""
+        nbytes = int(np.prod(shape))
+        ptr = C.c_void_p()
+        _check(_lib.orbgpu_host_alloc(nbytes, C.byref(ptr)))
+        self._pinned = getattr(self, "_pinned", []) + [ptr]
+        buf = (C.c_uint8 * nbytes).from_address(ptr.value)
+        return np.frombuffer(buf, np.uint8).reshape(shape)
+
+    def free_pinned(self):
+        for ptr in getattr(self, "_pinned", []):
+            _lib.orbgpu_host_free(ptr)
+        self._pinned = []
 
     def run(self, laps=None, stream=None):
         n = self.n

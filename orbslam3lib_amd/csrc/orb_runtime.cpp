@@ -113,6 +113,14 @@ struct orbgpu_ctx {
     int input_images = 0;   // images currently sized for in `input`
     hipEvent_t fork = nullptr;
     hipEvent_t ext_done = nullptr;  // work on a caller's stream (rejoin)
+    // double-buffered input (orbgpu_upload_images_async): batch k reads slot in_slot while the copy
+    // stream fills the other slot for batch k + 1; slot_free[j] = sub stream j's work enqueued before
+    // the current batch began (everything that read the other slot), slot_ready = the async copy
+    DevBuf input2;
+    int in_slot = 0, pending_slot = -1;
+    hipStream_t copy = nullptr;
+    hipEvent_t slot_ready = nullptr;
+    std::vector<hipEvent_t> slot_free;
     std::vector<hipEvent_t> join;  // one per sub stream
     // stages launched once over the whole batch on the main stream (join before, fork after), so
     // their per-launch duration is their own; off by default: each join / fork costs ~30 us of
@@ -510,12 +518,23 @@ void resolve_pending(orbgpu_ctx* c) {
     c->pending.clear();
 }
 
-int ensure_input(orbgpu_ctx* c, int n_images, int w, int h) {
+DevBuf& in_buf(orbgpu_ctx* c, int slot) { return slot ? c->input2 : c->input; }
+uint8_t* cur_input(orbgpu_ctx* c) { return in_buf(c, c->in_slot).as<uint8_t>(); }
+
+int ensure_input(orbgpu_ctx* c, int n_images, int w, int h, int slot = -1) {
     if (n_images < 1 || n_images > c->max_images)
         return fail(ORBGPU_ERR_CAPACITY, "n_images exceeds the context's max_images");
     if (w > c->max_w || h > c->max_h) return fail(ORBGPU_ERR_CAPACITY, "image larger than context max");
-    if (c->input.ensure((size_t)c->max_images * c->max_w * c->max_h + 256))
+    if (in_buf(c, slot < 0 ? c->in_slot : slot).ensure((size_t)c->max_images * c->max_w * c->max_h + 256))
         return fail(ORBGPU_ERR_HIP, "hipMalloc failed (input)");
+    return 0;
+}
+
+// A synchronous upload / ingest replaces whatever an async upload staged for the next batch.
+int drop_pending_upload(orbgpu_ctx* c) {
+    if (c->pending_slot < 0) return 0;
+    HIP_TRY(hipStreamSynchronize(c->copy));
+    c->pending_slot = -1;
     return 0;
 }
 
@@ -559,8 +578,12 @@ int orbgpu_create(const orbgpu_params* p, int device, int max_width, int max_hei
     }
     c->sub.push_back(c->stream);
     {
+        // 3 chunk streams: with the copy stream of orbgpu_upload_images_async that is 4, the
+        // hardware queues a process gets (GPU_MAX_HW_QUEUES = 4); a 5th stream shares a queue
+        // and the ingest copy then serialises with the kernels (measured: 3.16 vs 1.75 ms per
+        // 128-pair step with the upload beside it; 3 and 4 chunk streams compute equally fast)
         const char* e = getenv("ORBGPU_STREAMS");
-        const int ns = std::max(1, std::min(8, e ? atoi(e) : 4));
+        const int ns = std::max(1, std::min(8, e ? atoi(e) : 3));
         for (int k = 1; k < ns; ++k) {
             hipStream_t st;
             if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) break;
@@ -602,7 +625,8 @@ int orbgpu_destroy(orbgpu_ctx* c) {
     if (c->stream) hipStreamSynchronize(c->stream);
     resolve_pending(c);
     for (auto e : c->event_pool) hipEventDestroy(e);
-    DevBuf* bufs[] = {&c->input,   &c->pyr,     &c->blur,   &c->rtab,    &c->cellkeys, &c->cellcnt,
+    if (c->copy) hipStreamSynchronize(c->copy);
+    DevBuf* bufs[] = {&c->input, &c->input2, &c->pyr,     &c->blur,   &c->rtab,    &c->cellkeys, &c->cellcnt,
                       &c->octws,   &c->lvlkey,  &c->lvlangle, &c->lvldesc, &c->lvlcnt, &c->status,
                       &c->outkps,  &c->outdesc, &c->outn,   &c->outmono, &c->laps,     &c->midx1,
                       &c->mdist1,  &c->midx2,   &c->mdist2, &c->mnq,     &c->scratch, &c->octdbg,
@@ -614,6 +638,9 @@ int orbgpu_destroy(orbgpu_ctx* c) {
     for (size_t k = 1; k < c->sub.size(); ++k) hipStreamDestroy(c->sub[k]);
     if (c->fork) hipEventDestroy(c->fork);
     if (c->ext_done) hipEventDestroy(c->ext_done);
+    if (c->slot_ready) hipEventDestroy(c->slot_ready);
+    for (auto e : c->slot_free) hipEventDestroy(e);
+    if (c->copy) hipStreamDestroy(c->copy);
     for (hipEvent_t e : c->stagger_ev) hipEventDestroy(e);
     for (auto e : c->join) hipEventDestroy(e);
     if (c->stream) hipStreamDestroy(c->stream);
@@ -634,7 +661,7 @@ int orbgpu_get_scale_tables(const orbgpu_ctx* c, float* scale, float* inv_scale,
     return ORBGPU_OK;
 }
 
-uint8_t* orbgpu_device_input(orbgpu_ctx* c) { return c ? c->input.as<uint8_t>() : nullptr; }
+uint8_t* orbgpu_device_input(orbgpu_ctx* c) { return c ? cur_input(c) : nullptr; }
 
 int orbgpu_upload_images(orbgpu_ctx* c, const uint8_t* images, int n, int w, int h, int stride) {
     if (!c || !images) return fail(ORBGPU_ERR_INVALID, "null argument");
@@ -643,11 +670,51 @@ int orbgpu_upload_images(orbgpu_ctx* c, const uint8_t* images, int n, int w, int
     int r = ensure_input(c, n, w, h);
     if (r) return r;
     HIP_TRY(hipSetDevice(c->device));
+    if ((r = drop_pending_upload(c))) return r;
     r = join_all(c, c->stream);  // sub streams may still read the previous images
     if (r) return r;
-    HIP_TRY(hipMemcpy2DAsync(c->input.p, w, images, stride, w, (size_t)h * n, hipMemcpyHostToDevice,
+    HIP_TRY(hipMemcpy2DAsync(cur_input(c), w, images, stride, w, (size_t)h * n, hipMemcpyHostToDevice,
                              c->stream));
     c->need_fork = true;
+    return ORBGPU_OK;
+}
+
+int orbgpu_upload_images_async(orbgpu_ctx* c, const uint8_t* images, int n, int w, int h, int stride) {
+    if (!c || !images) return fail(ORBGPU_ERR_INVALID, "null argument");
+    if (w <= 0 || h <= 0) return fail(ORBGPU_ERR_EMPTY_IMAGE, "empty image");
+    if (stride < w) return fail(ORBGPU_ERR_INVALID, "stride < width");
+    if (c->pending_slot >= 0) return fail(ORBGPU_ERR_INVALID, "an async upload is already staged (run a batch first)");
+    const int slot = 1 - c->in_slot;
+    int r = ensure_input(c, n, w, h, slot);
+    if (r) return r;
+    HIP_TRY(hipSetDevice(c->device));
+    if (!c->copy) {
+        HIP_TRY(hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking));
+        HIP_TRY(hipEventCreateWithFlags(&c->slot_ready, hipEventDisableTiming));
+        for (size_t k = 0; k < c->sub.size(); ++k) {
+            hipEvent_t e;
+            HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            c->slot_free.push_back(e);
+        }
+    }
+    // the slot was last read by work enqueued before the current batch began (slot_free)
+    for (size_t k = 0; k < c->slot_free.size(); ++k) HIP_TRY(hipStreamWaitEvent(c->copy, c->slot_free[k], 0));
+    HIP_TRY(hipMemcpy2DAsync(in_buf(c, slot).p, w, images, stride, w, (size_t)h * n, hipMemcpyHostToDevice,
+                             c->copy));
+    HIP_TRY(hipEventRecord(c->slot_ready, c->copy));
+    c->pending_slot = slot;
+    return ORBGPU_OK;
+}
+
+int orbgpu_host_alloc(size_t bytes, void** ptr) {
+    if (!ptr) return fail(ORBGPU_ERR_INVALID, "null argument");
+    *ptr = nullptr;
+    HIP_TRY(hipHostMalloc(ptr, bytes ? bytes : 1, hipHostMallocDefault));
+    return ORBGPU_OK;
+}
+
+int orbgpu_host_free(void* ptr) {
+    if (ptr) HIP_TRY(hipHostFree(ptr));
     return ORBGPU_OK;
 }
 
@@ -685,7 +752,18 @@ int orbgpu_run_batch(orbgpu_ctx* c, int n, int w, int h, const int32_t* laps, vo
             A.octdbg = c->octdbg.as<unsigned long long>();
         }
     }
-    A.lvl_base[0] = c->input.as<uint8_t>();
+    // an async upload staged the next batch in the other input slot: read it once the copy lands
+    // (each chunk stream waits on the copy alone, so the chunks keep their steady-state offsets);
+    // first note what every stream has enqueued so far -- the readers of the slot we leave
+    bool slot_switch = false;
+    if (c->pending_slot >= 0) {
+        c->in_slot = c->pending_slot;
+        c->pending_slot = -1;
+        slot_switch = true;
+    }
+    for (size_t k = 0; k < c->sub.size() && k < c->slot_free.size(); ++k)
+        HIP_TRY(hipEventRecord(c->slot_free[k], c->sub[k]));
+    A.lvl_base[0] = cur_input(c);
     A.lv[0].img_stride = (long long)w * h;
     // Sub-batches (whole stereo pairs) on parallel streams: the stages have complementary
     // bottlenecks (octree latency, FAST VALU, blur/resize HBM), so their phases overlap.
@@ -714,6 +792,8 @@ int orbgpu_run_batch(orbgpu_ctx* c, int n, int w, int h, const int32_t* laps, vo
     } else {
         chunks.push_back({0, n, s});
     }
+    if (slot_switch)
+        for (const Chunk& ch : chunks) HIP_TRY(hipStreamWaitEvent(ch.st, c->slot_ready, 0));
     // first step of a layout: chunk k starts after chunk k-1 finished its pyramid + blur, so the
     // chunks run different stages (memory-, VALU- and latency-bound ones) at the same time
     const bool stagger = relayout && c->stagger && chunks.size() > 1 && !c->serialize;
@@ -916,11 +996,12 @@ int orbgpu_extract_stereo(orbgpu_ctx* c, const uint8_t* left, const uint8_t* rig
     if (r) return r;
     if (stride < w) return fail(ORBGPU_ERR_INVALID, "stride < width");
     HIP_TRY(hipSetDevice(c->device));
+    if ((r = drop_pending_upload(c))) return r;
     r = join_all(c, c->stream);  // sub streams of an earlier batch may still read the input
     if (r) return r;
     c->need_fork = true;
-    HIP_TRY(hipMemcpy2DAsync(c->input.p, w, left, stride, w, h, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemcpy2DAsync(c->input.as<uint8_t>() + (size_t)w * h, w, right, stride, w, h,
+    HIP_TRY(hipMemcpy2DAsync(cur_input(c), w, left, stride, w, h, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpy2DAsync(cur_input(c) + (size_t)w * h, w, right, stride, w, h,
                              hipMemcpyHostToDevice, c->stream));
     int32_t laps[4] = {lap_left ? lap_left[0] : 0, lap_left ? lap_left[1] : 0,
                        lap_right ? lap_right[0] : 0, lap_right ? lap_right[1] : 0};
@@ -947,7 +1028,7 @@ int orbgpu_get_pyramid_level(orbgpu_ctx* c, int img, int level, int blurred, uin
         src = c->A.blur_base[level] + (size_t)img * c->blur_img;
         pitch = G.bpitch;
     } else if (level == 0) {
-        src = c->input.as<uint8_t>() + (size_t)img * c->last_w * c->last_h;
+        src = cur_input(c) + (size_t)img * c->last_w * c->last_h;
         pitch = c->last_w;
     } else {
         src = c->A.lvl_base[level] + (size_t)img * c->pyr_img;
@@ -1121,7 +1202,7 @@ int orbgpu_stereo_matches_batch(orbgpu_ctx* c, int n_pairs, float mbf, float mb,
     S.nlevels = A.nlevels;
     S.H0 = H0;
     for (int l = 0; l < A.nlevels; ++l) {
-        S.lvl_base[l] = l == 0 ? c->input.as<uint8_t>() : A.lvl_base[l];
+        S.lvl_base[l] = l == 0 ? cur_input(c) : A.lvl_base[l];
         S.limg_stride[l] = l == 0 ? (long long)A.lv[0].w * A.lv[0].h : A.lv[l].img_stride;
         S.lw[l] = A.lv[l].w;
         S.lh[l] = A.lv[l].h;
@@ -1205,9 +1286,10 @@ int orbgpu_ingest_sbs(orbgpu_ctx* c, const uint8_t* frames, int n, int w, int h,
     if (r) return r;
     HIP_TRY(hipSetDevice(c->device));
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    if ((r = drop_pending_upload(c))) return r;
     r = join_all(c, s);  // sub streams may still read the previous images
     if (r) return r;
-    SbsArgs a{frames, (long long)h * stride, stride, w, h, n, c->input.as<uint8_t>()};
+    SbsArgs a{frames, (long long)h * stride, stride, w, h, n, cur_input(c)};
     r = timed(c, ST_SBS, s, [&] { return launch_sbs_split(a, s); });
     if (r) return r;
     c->need_fork = true;

@@ -242,3 +242,44 @@ def test_extract_features_padded_stride_exact_buffer(oracle):
         None, None, C.byref(nr), None, None, None, None, None, cap, C.byref(ml), C.byref(mr), None,
         None, None, cap) == -3
     ctx.close()
+
+
+def test_async_upload_pipeline(oracle):
+    """orbgpu_upload_images_async: batch k + 1's pixels are copied into the second input buffer
+    while batch k computes; three batches of different frames through both slots, every batch's
+    results (and its level-0 pyramid / stereo consumers) equal the oracle's for its own frames."""
+    import orbslam3lib_amd as og
+    P, W, H = 8, 640, 480
+    sets = [np.stack([x for i in range(P) for x in synth.stereo_pair(H, W, 700 + 20 * b + i)]) for b in range(3)]
+    be = og.BatchExtractor(2000, 1.2, 8, 20, 7, width=W, height=H, max_images=2 * P)
+    pin = [be.pinned(s.shape) for s in sets]
+    for p_, s_ in zip(pin, sets):
+        p_[:] = s_
+    be.upload(sets[0])
+    try:
+        for b in range(3):
+            be.run()
+            be.match_stereo(False)
+            if b + 1 < 3:
+                be.upload_async(pin[b + 1])   # overlaps this batch's kernels
+            be.synchronize()
+            for i in (0, 5, 2 * P - 1):
+                k, d, m = be.result(i)
+                rk, rd, rm = oracle.extract(sets[b][i], nfeatures=2000)
+                _same_kps(k, rk)
+                np.testing.assert_array_equal(d, rd, err_msg="batch %d image %d" % (b, i))
+            _, dl, _ = be.result(2)
+            _, dr, _ = be.result(3)
+            _same_knn(be.matches(1), oracle.knn2(dl, dr), "batch %d" % b)
+        # a staged upload must be consumed before another is staged
+        be.upload_async(pin[0])
+        with pytest.raises(og.OrbGpuError):
+            be.upload_async(pin[1])
+        be.run()
+        be.synchronize()
+        k, d, _ = be.result(1)
+        rk, rd, _ = oracle.extract(sets[0][1], nfeatures=2000)
+        np.testing.assert_array_equal(d, rd)
+    finally:
+        be.synchronize()
+        be.free_pinned()
