@@ -65,11 +65,12 @@ def algorithmic_bytes(w, h, L, nkp, sf=1.2, ncand=0.0):
     k64 = max(k48, fast_split(w, h, sf, L, 64))
     return {
         "k_pyramid": sum(A[l - 1] + A[l] for l in range(1, L)) + 2 * sum(A),
-        "k_resize": sum(A[l - 1] + A[l] for l in range(1, L)),
+        # one pass over level l-1 per launch: read it, write its blur and level l
+        "k_blur_resize": sum(2 * A[l - 1] + A[l] for l in range(1, L)),
         "k_fast_cells<48>": sum(A[:k48]),
         "k_fast_cells<64>": sum(A[k48:k64]),
         "k_fast_cells<80>": sum(A[k64:]),
-        "k_blur": 2 * sum(A),
+        "k_blur": 2 * A[L - 1],  # the last level's blur (the others ride in k_blur_resize)
         "k_orient_desc": 48 * nkp,
         "k_octree": 4 * ncand + 4 * nkp,
     }
@@ -403,16 +404,20 @@ def main():
             roof["note"] = ("DistributeOctTree is barrier/LDS-latency bound (serial list rounds per "
                             "(image, level)); its HBM bytes are the 4-B keys in and out")
 
-    # the north_star's named pair, FAST + pyramid, as one figure: B_fp per image over
-    # the summed per-step time of the k_resize and k_fast_cells launches of the serialized pass
-    fp_names = [k for k in stages_all if k == "k_resize" or k.startswith("k_fast_cells")]
+    # the north_star's named pair, FAST + pyramid, as one figure over the summed per-step time of
+    # the serialized pass.  The pyramid kernel also writes each level's blur (k_blur_resize reads
+    # level l-1 once for both), so its time carries the blur: the bytes are SURVEY §8d's B_fp plus
+    # the blur's 2 sum(A_l) (B_extract without the 48 B per keypoint)
+    fp_names = [k for k in stages_all if k in ("k_blur_resize", "k_blur") or k.startswith("k_fast_cells")]
     fp_ms = sum(stages_all[k][0] for k in fp_names) / 3.0  # 3 serialized steps
     roof_fp = None
     if fp_ms > 0:
-        fp_bytes = fast_pyramid_bytes(W, H, args.nlevels) * n_img
+        A_ = [a_ * b_ for a_, b_ in level_sizes(W, H, 1.2, args.nlevels)]
+        fp_bytes = (fast_pyramid_bytes(W, H, args.nlevels) + 2 * sum(A_)) * n_img
         ach = fp_bytes / (fp_ms * 1e-3) / 1e9
         roof_fp = {"kernels": fp_names, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
                    "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "bytes_per_step": int(fp_bytes),
+                   "includes": "pyramid + blur (fused) + FAST; bytes = B_fp + 2 sum(A_l)",
                    "us_per_step": round(fp_ms * 1e3, 1)}
 
     # the matcher's own roofline (north_star: "Hamming BFMatch"): it runs on the int8 matrix cores

@@ -33,6 +33,11 @@ struct LevelGeom {
     int tiles_x, tiles_y, tile_first;  // blur tiling (128 x 32)
     int xtab_off, ytab_off, simd_end;  // resize tables (levels >= 1)
     int area2;                 // exact 2x downscale: OpenCV switches to INTER_AREA (2x2 mean)
+    // k_blur_resize (levels >= 1): ownership of this level's output rows / column quads by the
+    // 128 x 32 blur tiles of level l - 1 (int views of rtab): band_row[b] = first output row whose
+    // first source row is >= 32 b (tiles_y(l-1) + 1 entries), tile_quad[j] = first quad whose first
+    // source column is >= 128 j (tiles_x(l-1) + 1 entries)
+    int band_row_off, tile_quad_off;
     int od_blocks, od_first;   // orientation/descriptor blocks for this level
 };
 
@@ -156,6 +161,12 @@ __host__ __device__ inline OctLayout oct_layout(int n_cap, int C) {
 // Kernel launchers (orb_kernels.hip).  Each returns hipGetLastError() of its launch.
 hipError_t launch_resize(const BatchArgs& a, int level, hipStream_t s);
 hipError_t launch_blur(const BatchArgs& a, hipStream_t s);
+constexpr int kBrMaxQuads = 40;  // k_blur_resize: level-l column quads / rows one blur tile owns
+constexpr int kBrMaxRows = 34;
+// The blur of level l - 1 and the resize to level l in one launch (every level except the last
+// blur, which launch_blur_level does).
+hipError_t launch_blur_resize(const BatchArgs& a, int level, hipStream_t s);
+hipError_t launch_blur_level(const BatchArgs& a, int level, hipStream_t s);
 // the whole pyramid (levels 1..L-1) and every blurred level in one launch: one workgroup per
 // (image, row stripe), 2^stripe_log2 stripes per image
 hipError_t launch_pyramid(const BatchArgs& a, int stripe_log2, hipStream_t s);

@@ -375,18 +375,20 @@ __device__ inline void blur_tile_compute(const LevelGeom& G, int tx0, int ty0, u
 // Persistent over the tiles of the launch (images x levels x tiles): the next tile's window
 // is loaded into registers while the current one is filtered, so the global-memory round
 // trip is hidden behind the arithmetic of the previous tile.
-__global__ __launch_bounds__(256) void k_blur(BatchArgs a) {
+__global__ __launch_bounds__(256) void k_blur(BatchArgs a, int tile0, int ntile) {
     constexpr int IW = kBlurTW + 32, IH = kBlurTH + 8, IWQ = IW / 16, NRP = IH / 2;
     constexpr int NCH = (IH * IWQ + 255) / 256;  // window chunks per thread
     __shared__ uint4 tin4[IH][IWQ];
     __shared__ uint4 hp[NRP][kBlurTW / 4];  // [row pair][column quad]: 4 columns x (row0,row1)
-    const int total = a.total_tiles * a.nimages;
+    // tiles [tile0, tile0 + ntile) of every image (all levels: 0, total_tiles)
+    auto tile_of = [&](int t) { return (t / ntile) * a.total_tiles + tile0 + t % ntile; };
+    const int total = ntile * a.nimages;
     // a contiguous run of tiles per workgroup, runs placed XCD-contiguously (xcd_remap)
     const int lb = xcd_remap(blockIdx.x, gridDim.x);
     const int t_end = (int)((long long)(lb + 1) * total / gridDim.x);
     int t = (int)((long long)lb * total / gridDim.x);
     if (t >= t_end) return;
-    BlurTile bt = blur_tile(a, t);
+    BlurTile bt = blur_tile(a, tile_of(t));
     uint4 pre[NCH];
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
@@ -406,7 +408,7 @@ __global__ __launch_bounds__(256) void k_blur(BatchArgs a) {
         }
         const int tn = t + 1;
         if (tn < t_end) {  // prefetch the next window
-            bt = blur_tile(a, tn);
+            bt = blur_tile(a, tile_of(tn));
 #pragma unroll
             for (int c = 0; c < NCH; ++c) {
                 const int i = threadIdx.x + 256 * c;
@@ -416,6 +418,94 @@ __global__ __launch_bounds__(256) void k_blur(BatchArgs a) {
         __syncthreads();
         blur_tile_compute(G, tx0, ty0, dst, tin4, hp, 0, G.h);
     }
+}
+
+// ---------------------------------------------------------------------------------------------
+// k_blur_resize: one read of level l - 1 serves two stages.  A workgroup stages the 128 x 32
+// blur tile's window of level l - 1 (rows ty0-4 .. ty0+35, columns tx0-16 .. tx0+143, 16-byte
+// buffer loads, REFLECT_101 rows) once, filters it (GaussianBlur of level l - 1, :1146-1147) and
+// makes the level-l outputs whose first source row / column fall inside the tile (cv::resize of
+// ComputePyramid, :1342-1344; exact-2x levels by INTER_AREA): their taps (source rows <= ty0+32,
+// columns <= tx0+134 for scales <= 2) all lie in the window's real pixels, so level l needs no
+// second read of level l - 1 and the blur of level l - 1 none of its own.  Ownership tables
+// (band_row / tile_quad) come from the host with the resize coefficients.
+static_assert(kBrMaxQuads >= kBlurTW / 4 + 1 && kBrMaxRows >= kBlurTH + 1, "ownership caps");
+
+__global__ __launch_bounds__(256) void k_blur_resize(BatchArgs a, int l) {
+    constexpr int IW = kBlurTW + 32, IH = kBlurTH + 8, IWQ = IW / 16, NRP = IH / 2;
+    constexpr int NCH = (IH * IWQ + 255) / 256;
+    __shared__ uint4 tin4[IH][IWQ];
+    __shared__ uint4 hp[NRP][kBlurTW / 4];
+    __shared__ int4 xts[4 * kBrMaxQuads];
+    __shared__ int4 yts[kBrMaxRows];
+    const LevelGeom& S = a.lv[l - 1];
+    const LevelGeom& G = a.lv[l];
+    const int per = S.tiles_x * S.tiles_y;
+    const int wg = xcd_remap(blockIdx.x, gridDim.x);  // an image's tiles on one XCD
+    const int img = a.img0 + wg / per, k = wg % per;
+    BlurTile bt;
+    bt.l = l - 1;
+    bt.ty0 = (k / S.tiles_x) * kBlurTH;
+    bt.tx0 = (k % S.tiles_x) * kBlurTW;
+    bt.src = a.lvl_base[l - 1] + (long long)img * S.img_stride;
+    bt.dst = a.blur_base[l - 1] + (long long)img * S.bimg_stride;
+    uint4 pre[NCH];
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+        const int i = threadIdx.x + 256 * c;
+        if (i < IH * IWQ) pre[c] = blur_chunk(a, bt, i, IWQ);
+    }
+    // the level-l outputs this tile owns, and their coefficients
+    const int* band_row = reinterpret_cast<const int*>(a.rtab) + G.band_row_off;
+    const int* tile_quad = reinterpret_cast<const int*>(a.rtab) + G.tile_quad_off;
+    const int by = k / S.tiles_x, bx = k % S.tiles_x;
+    const int r0 = band_row[by], r1 = band_row[by + 1];
+    const int q0 = tile_quad[bx], q1 = tile_quad[bx + 1];
+    const int nr = min(r1 - r0, kBrMaxRows), nq = min(q1 - q0, kBrMaxQuads);
+    if (!G.area2) {
+        for (int i = threadIdx.x; i < 4 * nq; i += 256) xts[i] = a.rtab[G.xtab_off + min(4 * q0 + i, G.w - 1)];
+        if (threadIdx.x < nr) yts[threadIdx.x] = a.rtab[G.ytab_off + r0 + threadIdx.x];
+    }
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+        const int i = threadIdx.x + 256 * c;
+        if (i < IH * IWQ) (&tin4[0][0])[i] = pre[c];
+    }
+    __syncthreads();
+    blur_tile_compute(S, bt.tx0, bt.ty0, bt.dst, tin4, hp, 0, S.h);  // fixes only off-plane columns
+    // resize from the window: window row r = source row ty0 - 4 + r, column c = tx0 - 16 + c
+    const uint8_t* wb = reinterpret_cast<const uint8_t*>(&tin4[0][0]);
+    const int wy0 = bt.ty0 - 4, wx0 = bt.tx0 - 16;
+    uint8_t* dst = a.lvl_base[l] + (long long)img * G.img_stride;
+    const float inv_nq = nq > 0 ? 1.f / (float)nq : 0.f;
+    for (int it = threadIdx.x; it < nr * nq; it += 256) {
+        const int rr = (int)(((float)it + 0.5f) * inv_nq);  // exact: it < 34 * 40
+        const int q = it - rr * nq;
+        const int dy = r0 + rr, dx0 = 4 * (q0 + q);
+        uint32_t packed = 0;
+        if (G.area2) {
+            const uint8_t* s0 = wb + (2 * dy - wy0) * IW - wx0;
+            const uint8_t* s1 = s0 + IW;
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) {
+                const int dx = min(dx0 + kk, G.w - 1);
+                const int o = (s0[2 * dx] + s0[2 * dx + 1] + s1[2 * dx] + s1[2 * dx + 1] + 2) >> 2;
+                packed |= (uint32_t)o << (8 * kk);
+            }
+        } else {
+            const int4 yt = yts[rr];
+            const uint8_t* row0 = wb + (yt.x - wy0) * IW - wx0;
+            const uint8_t* row1 = wb + (yt.y - wy0) * IW - wx0;
+            packed = rs_quad(row0, row1, xts + 4 * q, yt.z, yt.w, dx0, G.simd_end);
+        }
+        *reinterpret_cast<uint32_t*>(dst + (long long)dy * G.pitch + dx0) = packed;
+    }
+}
+
+hipError_t launch_blur_resize(const BatchArgs& a, int l, hipStream_t s) {
+    const LevelGeom& S = a.lv[l - 1];
+    hipLaunchKernelGGL(k_blur_resize, dim3(S.tiles_x * S.tiles_y * a.nimages), dim3(256), 0, s, a, l);
+    return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1424,7 +1514,13 @@ hipError_t launch_resize(const BatchArgs& a, int level, hipStream_t s) {
 hipError_t launch_blur(const BatchArgs& a, hipStream_t s) {
     // persistent: 8192 workgroups (32 per CU, about 4 resident at a time) loop over the tiles
     const int total = a.total_tiles * a.nimages;
-    hipLaunchKernelGGL(k_blur, dim3(std::min(total, 8192)), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_blur, dim3(std::min(total, 8192)), dim3(256), 0, s, a, 0, a.total_tiles);
+    return hipGetLastError();
+}
+hipError_t launch_blur_level(const BatchArgs& a, int l, hipStream_t s) {
+    const LevelGeom& G = a.lv[l];
+    const int n = G.tiles_x * G.tiles_y;
+    hipLaunchKernelGGL(k_blur, dim3(std::min(n * a.nimages, 8192)), dim3(256), 0, s, a, G.tile_first, n);
     return hipGetLastError();
 }
 hipError_t launch_pyramid(const BatchArgs& a, int stripe_log2, hipStream_t s) {

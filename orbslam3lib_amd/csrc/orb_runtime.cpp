@@ -42,7 +42,7 @@ int fail(int code, const std::string& msg) {
 enum Stage { ST_RESIZE, ST_BLUR, ST_FAST48, ST_FAST, ST_FAST_TOP, ST_OCTREE, ST_ORIENT, ST_FINAL, ST_KNN,
              ST_PYRAMID, ST_STEREO, ST_GRID, ST_SBS, ST_SOA, ST_SBP, ST_COUNT };
 // names as rocprofv3 shows the kernels (templates with their argument)
-const char* kStageNames[ST_COUNT] = {"k_resize",         "k_blur",   "k_fast_cells<48>", "k_fast_cells<64>",
+const char* kStageNames[ST_COUNT] = {"k_blur_resize",    "k_blur",   "k_fast_cells<48>", "k_fast_cells<64>",
                                      "k_fast_cells<80>", "k_octree", "k_orient_desc",    "k_finalize",
                                      "k_knn2",           "k_pyramid", "k_stereo",         "k_undistort_grid",
                                      "k_sbs_split",      "k_pack_soa",       "k_sbp"};
@@ -326,6 +326,31 @@ int set_geometry(orbgpu_ctx* c, int w, int h) {
             G.ytab_off = (int)c->rtab_host.size();
             c->rtab_host.insert(c->rtab_host.end(), yt.begin(), yt.end());
             G.simd_end = simd_end(G.w);
+            // k_blur_resize ownership: output row dy / column quad q belongs to the blur tile of
+            // level l - 1 holding its first source row / column (monotone in dy / q)
+            auto push_ints = [&](const std::vector<int>& v) {
+                const int off = 4 * (int)c->rtab_host.size();
+                for (size_t i = 0; i < v.size(); i += 4)
+                    c->rtab_host.push_back(make_int4(v[i], i + 1 < v.size() ? v[i + 1] : 0,
+                                                     i + 2 < v.size() ? v[i + 2] : 0, i + 3 < v.size() ? v[i + 3] : 0));
+                return off;
+            };
+            std::vector<int> band(S.tiles_y + 1), tq(S.tiles_x + 1);
+            const int nquads = (G.w + 3) / 4;
+            for (int b = 0, dy = 0; b <= S.tiles_y; ++b) {
+                while (dy < G.h && (b == S.tiles_y || (G.area2 ? 2 * dy : yt[dy].x) < 32 * b)) ++dy;
+                band[b] = b == S.tiles_y ? G.h : dy;
+            }
+            for (int j = 0, q = 0; j <= S.tiles_x; ++j) {
+                while (q < nquads && (j == S.tiles_x || (G.area2 ? 8 * q : xt[4 * q].x) < 128 * j)) ++q;
+                tq[j] = j == S.tiles_x ? nquads : q;
+            }
+            for (int b = 0; b < S.tiles_y; ++b)
+                if (band[b + 1] - band[b] > kBrMaxRows) return fail(ORBGPU_ERR_INVALID, "resize band table");
+            for (int j = 0; j < S.tiles_x; ++j)
+                if (tq[j + 1] - tq[j] > kBrMaxQuads) return fail(ORBGPU_ERR_INVALID, "resize quad table");
+            G.band_row_off = push_ints(band);
+            G.tile_quad_off = push_ints(tq);
         }
     }
     // k_pyramid stripe tables (1, 2, 4, 8, 16 stripes per image): own rows k*h/S .. (k+1)*h/S of
@@ -844,8 +869,9 @@ int orbgpu_run_batch(orbgpu_ctx* c, int n, int w, int h, const int32_t* laps, vo
                 if ((r = timed(c, ST_PYRAMID, ch.st, [&] { return launch_pyramid(B, sl, ch.st); }))) return r;
             } else {
                 for (int l = 1; l < A.nlevels; ++l)
-                    if ((r = timed(c, ST_RESIZE, ch.st, [&] { return launch_resize(B, l, ch.st); }))) return r;
-                if ((r = timed(c, ST_BLUR, ch.st, [&] { return launch_blur(B, ch.st); }))) return r;
+                    if ((r = timed(c, ST_RESIZE, ch.st, [&] { return launch_blur_resize(B, l, ch.st); }))) return r;
+                const int lt = A.nlevels - 1;
+                if ((r = timed(c, ST_BLUR, ch.st, [&] { return launch_blur_level(B, lt, ch.st); }))) return r;
             }
             HIP_TRY(hipEventRecord(c->stagger_ev[k], ch.st));
         }
@@ -853,11 +879,13 @@ int orbgpu_run_batch(orbgpu_ctx* c, int n, int w, int h, const int32_t* laps, vo
         r = each(ST_PYRAMID, [&](const BatchArgs& B, hipStream_t st) { return launch_pyramid(B, sl, st); });
         if (r) return r;
     } else {
+        // level l - 1's blur and level l in one pass over level l - 1, then the last level's blur
         for (int l = 1; l < A.nlevels; ++l) {
-            r = each(ST_RESIZE, [&](const BatchArgs& B, hipStream_t st) { return launch_resize(B, l, st); });
+            r = each(ST_RESIZE, [&](const BatchArgs& B, hipStream_t st) { return launch_blur_resize(B, l, st); });
             if (r) return r;
         }
-        if ((r = each(ST_BLUR, [](const BatchArgs& B, hipStream_t st) { return launch_blur(B, st); }))) return r;
+        const int lt = A.nlevels - 1;
+        if ((r = each(ST_BLUR, [&](const BatchArgs& B, hipStream_t st) { return launch_blur_level(B, lt, st); }))) return r;
     }
     {   // the FAST tiles as one group: one join / fork around all of them when isolated
         const int tiles[3] = {kCellPitchTiny, kCellPitchSmall, kCellMax};

@@ -252,7 +252,7 @@ def _check_pyramid(ex, oracle, imgs, sf=1.2, L=8):
 def test_pyramid_stripes_and_per_level_path(oracle, monkeypatch, mode):
     """k_pyramid (one launch, 2^k row stripes per image, each stripe recomputing the rows its
     blur halo and its later levels' source cones need) at every stripe count, and the per-level
-    k_resize + k_blur path (ORBGPU_PYR=0): pyramid and blurred levels of a stereo pair."""
+    k_blur_resize + last-level k_blur path (ORBGPU_PYR=0): pyramid and blurred levels of a stereo pair."""
     if mode == "per-level":
         monkeypatch.setenv("ORBGPU_PYR", "0")
     else:
@@ -267,7 +267,7 @@ def test_pyramid_stripes_and_per_level_path(oracle, monkeypatch, mode):
 @pytest.mark.parametrize("pyr", ["0", "1"])
 def test_pyramid_exact_2x_area_path(oracle, monkeypatch, pyr):
     """Scale factor 2 on a 640x480 frame: every level is an exact 2x downscale, which OpenCV
-    serves with INTER_AREA (2x2 mean) instead of INTER_LINEAR -- k_resize and k_pyramid."""
+    serves with INTER_AREA (2x2 mean) instead of INTER_LINEAR -- k_blur_resize and k_pyramid."""
     monkeypatch.setenv("ORBGPU_PYR", pyr)
     img = synth.frame(480, 640, 6)
     ex = _extractor(nf=500, L=3, sf=2.0)
