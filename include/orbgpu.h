@@ -137,6 +137,19 @@ int orbgpu_get_level_keypoints(orbgpu_ctx* ctx, int image, orbgpu_keypoint* kps,
  * idx = -1 / dist = INT32_MAX when absent (nt < 2).  Host pointers, n x 32 B each. */
 int orbgpu_match_knn2(orbgpu_ctx* ctx, const uint8_t* query, int nq, const uint8_t* train, int nt,
                       int32_t* idx1, int32_t* dist1, int32_t* idx2, int32_t* dist2);
+/* Device-pointer forms for multi-GPU exchange (C5 cross-camera BFMatch, SURVEY §8e: the
+ * descriptors go from this context's HBM straight into a collective's buffer and back into the
+ * matcher; nothing touches the host):
+ *   orbgpu_export_descriptors: rows [row0, n) of batch image `image` -> device_dst (cap_rows x 32 B),
+ *     *n_rows = rows copied (host); device-to-device on `stream` (NULL = the context's stream),
+ *     ordered after the batch that produced them;
+ *   orbgpu_match_knn2_device: orbgpu_match_knn2 with query / train / outputs in device memory
+ *     (idx1, dist1, idx2, dist2: int32 [nq] each), on `stream`. */
+int orbgpu_export_descriptors(orbgpu_ctx* ctx, int image, int row0, uint8_t* device_dst, int cap_rows,
+                              int* n_rows, void* stream);
+int orbgpu_match_knn2_device(orbgpu_ctx* ctx, const uint8_t* d_query, int nq, const uint8_t* d_train, int nt,
+                             int32_t* d_idx1, int32_t* d_dist1, int32_t* d_idx2, int32_t* d_dist2, void* stream);
+
 /* Batch stereo matching on device-resident results of the last orbgpu_run_batch: pair p
  * matches image 2p (query) against image 2p+1 (train), rows [mono..n) of each when
  * stereo_rows_only != 0 (Frame::ComputeStereoFishEyeMatches, Frame.cc:1142-1148) or all rows.

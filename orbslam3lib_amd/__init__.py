@@ -46,7 +46,7 @@ EXPORTED = [
     "orbgpu_download_soa", "orbgpu_download_matches16", "orbgpu_extract_features",
     "orbgpu_search_by_projection_batch", "orbgpu_search_by_projection_stereo",
     "orbgpu_download_projection_matches", "orbgpu_upload_images_async", "orbgpu_host_alloc",
-    "orbgpu_host_free",
+    "orbgpu_host_free", "orbgpu_export_descriptors", "orbgpu_match_knn2_device",
     "orbgpu_set_profiling", "orbgpu_num_stages", "orbgpu_stage_name", "orbgpu_stage_times",
     "orbgpu_reset_stage_times", "orbgpu_last_error", "orbgpu_abi_version",
 ]
@@ -82,6 +82,10 @@ def load_library(path: str = LIB_PATH):
     lib.orbgpu_device_sbs_input.argtypes = [C.c_void_p]
     lib.orbgpu_host_alloc.argtypes = [C.c_size_t, C.POINTER(C.c_void_p)]
     lib.orbgpu_host_free.argtypes = [C.c_void_p]
+    lib.orbgpu_export_descriptors.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_int,
+                                              C.POINTER(C.c_int), C.c_void_p]
+    lib.orbgpu_match_knn2_device.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int] + \
+        [C.c_void_p] * 5
     for name in ("orbgpu_destroy", "orbgpu_synchronize", "orbgpu_set_profiling",
                  "orbgpu_reset_stage_times"):
         getattr(lib, name).argtypes = [C.c_void_p] + ([C.c_int] if name == "orbgpu_set_profiling" else [])
@@ -284,6 +288,21 @@ class BatchExtractor:
         _check(_lib.orbgpu_upload_images(self.ctx.handle, _p(imgs), n, w, h, w))
         self.n, self.height, self.width = n, h, w
         _check(_lib.orbgpu_synchronize(self.ctx.handle))
+
+    def export_descriptors(self, image, device_ptr, cap_rows, row0=0, stream=None):
+        """Rows [row0, n) of image's descriptors into device memory (device-to-device);
+        returns the row count."""
+        n = C.c_int(0)
+        _check(_lib.orbgpu_export_descriptors(self.ctx.handle, int(image), int(row0), C.c_void_p(device_ptr),
+                                              int(cap_rows), C.byref(n), C.c_void_p(stream) if stream else None))
+        return n.value
+
+    def match_knn2_device(self, d_query, nq, d_train, nt, d_out, stream=None):
+        """kNN2 on device buffers; d_out: device int32 [4, nq] (idx1, dist1, idx2, dist2)."""
+        _check(_lib.orbgpu_match_knn2_device(self.ctx.handle, C.c_void_p(d_query), int(nq), C.c_void_p(d_train),
+                                             int(nt), C.c_void_p(d_out), C.c_void_p(d_out + 4 * nq),
+                                             C.c_void_p(d_out + 8 * nq), C.c_void_p(d_out + 12 * nq),
+                                             C.c_void_p(stream) if stream else None))
 
     def upload_async(self, images):
         """Stage the NEXT batch (orbgpu_upload_images_async): the copy runs beside the current

@@ -429,20 +429,24 @@ __global__ __launch_bounds__(256) void k_blur(BatchArgs a, int tile0, int ntile)
 // columns <= tx0+134 for scales <= 2) all lie in the window's real pixels, so level l needs no
 // second read of level l - 1 and the blur of level l - 1 none of its own.  Ownership tables
 // (band_row / tile_quad) come from the host with the resize coefficients.
+constexpr int kSc1 = 16;  // buffer-load aux bit: sc1
 static_assert(kBrMaxQuads >= kBlurTW / 4 + 1 && kBrMaxRows >= kBlurTH + 1, "ownership caps");
 
-__global__ __launch_bounds__(256) void k_blur_resize(BatchArgs a, int l) {
-    constexpr int IW = kBlurTW + 32, IH = kBlurTH + 8, IWQ = IW / 16, NRP = IH / 2;
+struct BrSmem {
+    uint4 tin4[kBlurTH + 8][(kBlurTW + 32) / 16];
+    uint4 hp[(kBlurTH + 8) / 2][kBlurTW / 4];
+    int4 xts[4 * kBrMaxQuads];
+    int4 yts[kBrMaxRows];
+};
+
+// Blur tile k of level s = l - 1 of image img, and (resize) the level-l outputs it owns.  kAux:
+// cache policy of the window loads (sc1 where level s was written by this launch).
+template <int kAux>
+__device__ inline void br_tile(const BatchArgs& a, int l, bool resize, int img, int k, BrSmem& sm) {
+    constexpr int IW = kBlurTW + 32, IH = kBlurTH + 8, IWQ = IW / 16;
     constexpr int NCH = (IH * IWQ + 255) / 256;
-    __shared__ uint4 tin4[IH][IWQ];
-    __shared__ uint4 hp[NRP][kBlurTW / 4];
-    __shared__ int4 xts[4 * kBrMaxQuads];
-    __shared__ int4 yts[kBrMaxRows];
     const LevelGeom& S = a.lv[l - 1];
-    const LevelGeom& G = a.lv[l];
-    const int per = S.tiles_x * S.tiles_y;
-    const int wg = xcd_remap(blockIdx.x, gridDim.x);  // an image's tiles on one XCD
-    const int img = a.img0 + wg / per, k = wg % per;
+    const LevelGeom& G = a.lv[resize ? l : l - 1];
     BlurTile bt;
     bt.l = l - 1;
     bt.ty0 = (k / S.tiles_x) * kBlurTH;
@@ -453,28 +457,33 @@ __global__ __launch_bounds__(256) void k_blur_resize(BatchArgs a, int l) {
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
         const int i = threadIdx.x + 256 * c;
-        if (i < IH * IWQ) pre[c] = blur_chunk(a, bt, i, IWQ);
+        if (i < IH * IWQ) pre[c] = blur_chunk<kAux>(a, bt, i, IWQ);
     }
     // the level-l outputs this tile owns, and their coefficients
-    const int* band_row = reinterpret_cast<const int*>(a.rtab) + G.band_row_off;
-    const int* tile_quad = reinterpret_cast<const int*>(a.rtab) + G.tile_quad_off;
-    const int by = k / S.tiles_x, bx = k % S.tiles_x;
-    const int r0 = band_row[by], r1 = band_row[by + 1];
-    const int q0 = tile_quad[bx], q1 = tile_quad[bx + 1];
-    const int nr = min(r1 - r0, kBrMaxRows), nq = min(q1 - q0, kBrMaxQuads);
-    if (!G.area2) {
-        for (int i = threadIdx.x; i < 4 * nq; i += 256) xts[i] = a.rtab[G.xtab_off + min(4 * q0 + i, G.w - 1)];
-        if (threadIdx.x < nr) yts[threadIdx.x] = a.rtab[G.ytab_off + r0 + threadIdx.x];
+    int r0 = 0, nr = 0, q0 = 0, nq = 0;
+    if (resize) {
+        const int* band_row = reinterpret_cast<const int*>(a.rtab) + G.band_row_off;
+        const int* tile_quad = reinterpret_cast<const int*>(a.rtab) + G.tile_quad_off;
+        const int by = k / S.tiles_x, bx = k % S.tiles_x;
+        r0 = band_row[by];
+        q0 = tile_quad[bx];
+        nr = min(band_row[by + 1] - r0, kBrMaxRows);
+        nq = min(tile_quad[bx + 1] - q0, kBrMaxQuads);
+        if (!G.area2) {
+            for (int i = threadIdx.x; i < 4 * nq; i += 256) sm.xts[i] = a.rtab[G.xtab_off + min(4 * q0 + i, G.w - 1)];
+            if (threadIdx.x < nr) sm.yts[threadIdx.x] = a.rtab[G.ytab_off + r0 + threadIdx.x];
+        }
     }
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
         const int i = threadIdx.x + 256 * c;
-        if (i < IH * IWQ) (&tin4[0][0])[i] = pre[c];
+        if (i < IH * IWQ) (&sm.tin4[0][0])[i] = pre[c];
     }
     __syncthreads();
-    blur_tile_compute(S, bt.tx0, bt.ty0, bt.dst, tin4, hp, 0, S.h);  // fixes only off-plane columns
+    blur_tile_compute(S, bt.tx0, bt.ty0, bt.dst, sm.tin4, sm.hp, 0, S.h);  // fixes only off-plane columns
+    if (!resize) return;
     // resize from the window: window row r = source row ty0 - 4 + r, column c = tx0 - 16 + c
-    const uint8_t* wb = reinterpret_cast<const uint8_t*>(&tin4[0][0]);
+    const uint8_t* wb = reinterpret_cast<const uint8_t*>(&sm.tin4[0][0]);
     const int wy0 = bt.ty0 - 4, wx0 = bt.tx0 - 16;
     uint8_t* dst = a.lvl_base[l] + (long long)img * G.img_stride;
     const float inv_nq = nq > 0 ? 1.f / (float)nq : 0.f;
@@ -493,14 +502,23 @@ __global__ __launch_bounds__(256) void k_blur_resize(BatchArgs a, int l) {
                 packed |= (uint32_t)o << (8 * kk);
             }
         } else {
-            const int4 yt = yts[rr];
+            const int4 yt = sm.yts[rr];
             const uint8_t* row0 = wb + (yt.x - wy0) * IW - wx0;
             const uint8_t* row1 = wb + (yt.y - wy0) * IW - wx0;
-            packed = rs_quad(row0, row1, xts + 4 * q, yt.z, yt.w, dx0, G.simd_end);
+            packed = rs_quad(row0, row1, sm.xts + 4 * q, yt.z, yt.w, dx0, G.simd_end);
         }
         *reinterpret_cast<uint32_t*>(dst + (long long)dy * G.pitch + dx0) = packed;
     }
 }
+
+__global__ __launch_bounds__(256) void k_blur_resize(BatchArgs a, int l) {
+    __shared__ BrSmem sm;
+    const LevelGeom& S = a.lv[l - 1];
+    const int per = S.tiles_x * S.tiles_y;
+    const int wg = xcd_remap(blockIdx.x, gridDim.x);  // an image's tiles on one XCD
+    br_tile<0>(a, l, true, a.img0 + wg / per, wg % per, sm);
+}
+
 
 hipError_t launch_blur_resize(const BatchArgs& a, int l, hipStream_t s) {
     const LevelGeom& S = a.lv[l - 1];
@@ -517,7 +535,6 @@ hipError_t launch_blur_resize(const BatchArgs& a, int l, hipStream_t s) {
 // rows it wrote itself: the phases are separated by a vmcnt drain + workgroup barrier, and
 // every load of a level written in this launch is an sc1 load (from L2, never a stale L1
 // line).  Rows in the overlap of two stripes are computed by both, with identical values.
-constexpr int kSc1 = 16;  // buffer-load aux bit: sc1
 
 union PyrSmem {
     struct {

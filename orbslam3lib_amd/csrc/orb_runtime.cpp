@@ -1137,6 +1137,39 @@ int orbgpu_match_knn2(orbgpu_ctx* c, const uint8_t* q, int nq, const uint8_t* t,
     return ORBGPU_OK;
 }
 
+int orbgpu_export_descriptors(orbgpu_ctx* c, int img, int row0, uint8_t* dst, int cap, int* n_rows, void* stream) {
+    if (!c || img < 0 || img >= c->last_images || row0 < 0 || (cap > 0 && !dst))
+        return fail(ORBGPU_ERR_INVALID, "bad arguments");
+    HIP_TRY(hipSetDevice(c->device));
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    int r = join_all(c, s);  // the descriptors come from the chunk streams
+    if (r) return r;
+    int32_t nk = 0;  // the count decides the copy size: read it once the batch is done
+    HIP_TRY(hipMemcpyAsync(&nk, c->outn.as<int32_t>() + img, 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (int e = count_status(nk)) return e;
+    const int n = nk > row0 ? nk - row0 : 0;
+    if (n_rows) *n_rows = n;
+    if (n > cap) return fail(ORBGPU_ERR_CAPACITY, "caller capacity too small");
+    if (n)
+        HIP_TRY(hipMemcpyAsync(dst, c->outdesc.as<uint8_t>() + ((size_t)img * c->out_cap + row0) * 32, 32 * (size_t)n,
+                               hipMemcpyDeviceToDevice, s));
+    return rejoin(c, s);
+}
+
+int orbgpu_match_knn2_device(orbgpu_ctx* c, const uint8_t* q, int nq, const uint8_t* t, int nt, int32_t* i1,
+                             int32_t* d1, int32_t* i2, int32_t* d2, void* stream) {
+    if (!c || nq < 0 || nt < 0 || (nq && (!q || !i1 || !d1 || !i2 || !d2)) || (nt && !t))
+        return fail(ORBGPU_ERR_INVALID, "bad args");
+    if (nt > 65535) return fail(ORBGPU_ERR_INVALID, "train set larger than 65535 rows");
+    if (nq == 0) return ORBGPU_OK;
+    HIP_TRY(hipSetDevice(c->device));
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    int r = timed(c, ST_KNN, s, [&] { return launch_knn2_plain(q, nq, t, nt, i1, d1, i2, d2, s); });
+    if (r) return r;
+    return rejoin(c, s);
+}
+
 int orbgpu_match_stereo_batch(orbgpu_ctx* c, int n_pairs, int stereo_only, void* stream) {
     if (!c || n_pairs < 1 || 2 * n_pairs > c->last_images) return fail(ORBGPU_ERR_INVALID, "bad pair count");
     HIP_TRY(hipSetDevice(c->device));

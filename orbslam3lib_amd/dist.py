@@ -40,6 +40,42 @@ def cross_camera_match(dist, desc, matcher, device=None):
     return {r: matcher(desc, rows[r][:counts[r]].cpu().numpy()) for r in range(world) if r != rank}
 
 
+def cross_camera_match_device(dist, be, image=0, row0=0):
+    """C5 cross-camera BFMatch with the descriptors kept on the GPUs: this rank's
+    camera = batch image `image` of BatchExtractor `be` (rows [row0, n)).  The rows go from the
+    extractor's HBM straight into a torch buffer (orbgpu_export_descriptors, device to device),
+    one RCCL all_gather moves every camera's rows over xGMI, and every other camera is matched on
+    this GPU from device memory (orbgpu_match_knn2_device) on torch's current stream.  Only the
+    per-camera row counts (one int each) pass through the host.  Returns {rank: int32 device
+    tensor [4, n] (idx1, dist1, idx2, dist2)} for the other ranks."""
+    import torch
+    world, rank = dist.get_world_size(), dist.get_rank()
+    if dist.get_backend() == "nccl":
+        dev = torch.device("cuda", torch.cuda.current_device())
+        stream = torch.cuda.current_stream().cuda_stream
+    else:  # gloo rehearsal: host tensors, `be` then works on host addresses (tests)
+        dev, stream = torch.device("cpu"), None
+    nk, _ = be.counts()
+    n_local = max(int(nk[image]) - int(row0), 0)
+    n = torch.tensor([n_local], dtype=torch.int64, device=dev)
+    counts = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(counts, n)
+    counts = [int(c.item()) for c in counts]
+    maxn = max(max(counts), 1)
+    buf = torch.zeros((maxn, 32), dtype=torch.uint8, device=dev)
+    be.export_descriptors(image, buf.data_ptr(), maxn, row0, stream)
+    rows = [torch.empty_like(buf) for _ in range(world)]
+    dist.all_gather(rows, buf)
+    out = {}
+    for r in range(world):
+        if r == rank:
+            continue
+        res = torch.empty((4, max(n_local, 1)), dtype=torch.int32, device=dev)
+        be.match_knn2_device(buf.data_ptr(), n_local, rows[r].data_ptr(), counts[r], res.data_ptr(), stream)
+        out[r] = res[:, :n_local]
+    return out
+
+
 def reduce_scalar(dist, x: float, op: str = "max") -> float:
     if dist is None:
         return x

@@ -283,3 +283,51 @@ def test_async_upload_pipeline(oracle):
     finally:
         be.synchronize()
         be.free_pinned()
+
+
+def test_device_descriptor_export_and_knn2(oracle):
+    """The C5 exchange's device path (dist.cross_camera_match_device): orbgpu_export_descriptors
+    copies an image's rows [row0, n) device to device, orbgpu_match_knn2_device matches device
+    buffers; checked against the oracle matcher on the downloaded descriptors (raw HIP buffers
+    here: the multi-rank RCCL exchange around them runs in bench.py on 8-GPU nodes, its gloo
+    rehearsal in test_distributed.py)."""
+    import orbslam3lib_amd as og
+    hip = _hip()
+    hip.hipMalloc.argtypes = [C.POINTER(C.c_void_p), C.c_size_t]
+    hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+    hip.hipFree.argtypes = [C.c_void_p]
+    hip.hipDeviceSynchronize.argtypes = []
+    P, W, H = 2, 640, 480
+    imgs = np.stack([x for i in range(P) for x in synth.stereo_pair(H, W, 70 + i)])
+    be = og.BatchExtractor(2000, 1.2, 8, 20, 7, width=W, height=H, max_images=2 * P)
+    be.upload(imgs)
+    be.run()
+    bufs = []
+    try:
+        cap = 4096
+        for _ in range(3):
+            p = C.c_void_p()
+            assert hip.hipMalloc(C.byref(p), cap * 32) == 0
+            bufs.append(p)
+        na = be.export_descriptors(0, bufs[0].value, cap)
+        nb = be.export_descriptors(3, bufs[1].value, cap, row0=100)
+        _, da, _ = be.result(0)
+        _, db, _ = be.result(3)
+        assert na == len(da) and nb == len(db) - 100
+        ref = oracle.knn2(da, db[100:])
+        be.match_knn2_device(bufs[0].value, na, bufs[1].value, nb, bufs[2].value)
+        assert hip.hipDeviceSynchronize() == 0
+        out = np.zeros((4, na), np.int32)
+        assert hip.hipMemcpy(out.ctypes.data, bufs[2].value, out.nbytes, 2) == 0
+        for a, b in zip(out, ref):
+            np.testing.assert_array_equal(a, b)
+        # the exported rows are the image's descriptors byte for byte
+        back = np.zeros((na, 32), np.uint8)
+        assert hip.hipMemcpy(back.ctypes.data, bufs[0].value, back.nbytes, 2) == 0
+        np.testing.assert_array_equal(back, da)
+        with pytest.raises(og.OrbGpuError):
+            be.export_descriptors(0, bufs[0].value, 10)  # capacity too small
+    finally:
+        be.synchronize()
+        for p in bufs:
+            hip.hipFree(p)

@@ -92,3 +92,74 @@ def test_shard_range_partitions(total, world):
     assert spans[0][0] == 0 and spans[-1][1] == total
     for (a, b), (c, d) in zip(spans, spans[1:]):
         assert b == c and b >= a
+
+
+class _HostExtractor:
+    """Stands in for BatchExtractor on the CPU: the same pointer-based calls
+    (export_descriptors / match_knn2_device) over host addresses, the oracle as the matcher."""
+
+    def __init__(self, desc):
+        import numpy as np
+        self.desc = np.ascontiguousarray(desc, dtype=np.uint8)
+
+    def counts(self):
+        import numpy as np
+        return np.array([len(self.desc)], np.int32), np.zeros(1, np.int32)
+
+    def export_descriptors(self, image, ptr, cap, row0=0, stream=None):
+        import ctypes
+        n = max(len(self.desc) - row0, 0)
+        assert n <= cap and stream is None
+        ctypes.memmove(ptr, self.desc[row0:].ctypes.data, 32 * n)
+        return n
+
+    def match_knn2_device(self, dq, nq, dt, nt, dout, stream=None):
+        import ctypes
+
+        import numpy as np
+
+        from oracle import oracle_py as O
+        q = np.ctypeslib.as_array((ctypes.c_uint8 * (32 * nq)).from_address(dq)).reshape(nq, 32)
+        t = np.ctypeslib.as_array((ctypes.c_uint8 * (32 * max(nt, 1))).from_address(dt))[:32 * nt].reshape(nt, 32)
+        res = np.stack(O.knn2(q, t)).astype(np.int32)
+        ctypes.memmove(dout, res.ctypes.data, res.nbytes)
+
+
+def _cross_dev_worker(rank, world, port, q):
+    import numpy as np
+    import torch.distributed as dist
+
+    from oracle import oracle_py as O
+    from orbslam3lib_amd import dist as od
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    cams = [np.random.default_rng(80 + r).integers(0, 256, (40 + 9 * r, 32), dtype=np.uint8)
+            for r in range(world)]
+    row0 = 3
+    got = od.cross_camera_match_device(dist, _HostExtractor(cams[rank]), 0, row0)
+    ok = sorted(got) == [r for r in range(world) if r != rank]
+    for r, res in got.items():
+        ref = O.knn2(cams[rank][row0:], cams[r][row0:])
+        ok &= all(np.array_equal(a.numpy(), b) for a, b in zip(res, ref))
+    dist.barrier()
+    q.put((rank, bool(ok)))
+    dist.destroy_process_group()
+
+
+def test_gloo_cross_camera_match_device_path_world2():
+    """dist.cross_camera_match_device (the RCCL path of bench.py on 8-GPU nodes) under gloo: the
+    counts exchange, the padded all_gather of exported rows and the per-camera matcher calls,
+    with host tensors and a host stand-in for the extractor's device entry points."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_cross_dev_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(ok for _, ok in res)
