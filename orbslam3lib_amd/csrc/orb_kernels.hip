@@ -897,9 +897,27 @@ __device__ __attribute__((always_inline)) inline void octree_level(const BatchAr
     uint32_t* out_keys = a.lvlkey + (long long)img * a.lvlkp_img_stride + G.kp_off;
     unsigned long long* dbg = a.octdbg ? a.octdbg + ((long long)img * kMaxLevels + l) * 8 : nullptr;
     int r = n > G.cand_cap ? -3 : 0;
-    const bool fits = off_in_lds && G.oct_cap <= a.oct_lds_nodes && n <= kOctLdsKeys && !a.oct_force_retry;
-    if (kLdsPath && r == 0 && !fits) r = kOctRetry;
-    if (kLdsPath && r == 0) {
+    // node state and cell offsets in LDS; the per-key labels too up to kOctLdsKeys keys, in the
+    // global workspace above that (dense levels of large frames: the label passes are parallel
+    // and streaming, the serial node phases stay in LDS)
+    const bool nodes_fit = off_in_lds && G.oct_cap <= a.oct_lds_nodes && !a.oct_force_retry;
+    if (kLdsPath && r == 0 && !nodes_fit) r = kOctRetry;
+    if (kLdsPath && r == 0 && n > kOctLdsKeys) {
+        OctWST<kLdsAS, kGlobalAS, kGlobalAS> w;
+        w.keys = (asp<kGlobalAS, uint32_t>)keys;
+        w.n = n;
+        w.nq = (asp<kGlobalAS, uint16_t>)(ws + L.nq);
+        w.m = oct_nodemem_carve<kLdsAS>(nodemem_lds, G.oct_cap);
+        w.cap = G.oct_cap;
+        w.out_keys = (asp<kGlobalAS, uint32_t>)out_keys;
+        w.out_cap = G.kp_cap;
+        w.dbg = dbg;
+        w.cell_off = (asp<kLdsAS, const int32_t>)cell_off;
+        w.cellkeys = (asp<kGlobalAS, const uint32_t>)ck;
+        w.ncells = G.ncells;
+        w.cell_cap = G.cell_cap;
+        r = octree_distribute(p, w, (asp<kLdsAS, OctShared>)&sh, G.W, G.H, G.N);
+    } else if (kLdsPath && r == 0) {
         // everything node- and label-sized in LDS: ds_* accesses throughout
         OctWST<kLdsAS, kGlobalAS> w;
         w.keys = (asp<kGlobalAS, uint32_t>)keys;

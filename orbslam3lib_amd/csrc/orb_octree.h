@@ -85,13 +85,14 @@ __host__ __device__ inline OctNodeMemT<AS> oct_nodemem_carve(void* base, int C) 
     return m;
 }
 
-// LAS: address space of the node state, the per-key labels and the cell offsets (LDS on the
-// fast GPU path); GAS: address space of the key arrays (global on the GPU).
-template <int LAS, int GAS>
+// LAS: address space of the node state and the cell offsets (LDS on the GPU); GAS: address
+// space of the key arrays (global on the GPU); NAS: address space of the per-key labels (LDS
+// while they fit, global for levels with more than kOctLdsKeys candidate keys).
+template <int LAS, int GAS, int NAS = LAS>
 struct OctWST {
     asp<GAS, uint32_t> keys;    // [n] in vToDistributeKeys order (written by the gather if any)
     int n;
-    asp<LAS, uint16_t> nq;      // [n] node index << 2 | quadrant of each key
+    asp<NAS, uint16_t> nq;      // [n] node index << 2 | quadrant of each key
     OctNodeMemT<LAS> m;
     int cap;                    // node capacity C (>= max(N+3, 4*nIni) + 4)
     asp<GAS, uint32_t> out_keys;  // [out_cap]
@@ -160,8 +161,8 @@ __host__ __device__ inline void on_st(NP a, int i, OctNode n) {
     a[i].cnt = n.cnt;
 }
 
-template <int LAS, int GAS, class P>
-__host__ __device__ __attribute__((always_inline)) inline int octree_distribute(P& p, const OctWST<LAS, GAS> ws,
+template <int LAS, int GAS, int NAS, class P>
+__host__ __device__ __attribute__((always_inline)) inline int octree_distribute(P& p, const OctWST<LAS, GAS, NAS> ws,
                                           asp<LAS, OctShared> sh, int W, int H, int N) {
     const int tid = p.tid(), NT = p.nthreads();
     const int n = ws.n;

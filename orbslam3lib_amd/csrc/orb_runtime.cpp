@@ -406,13 +406,12 @@ int set_geometry(orbgpu_ctx* c, int w, int h) {
     A.oct_nq_off = ((int)oct_nodemem_bytes(std::max(lds_nodes, 1)) + 15) & ~15;
     A.oct_lds_bytes = std::max(A.oct_nq_off + 2 * kOctLdsKeys, std::min(4 * max_cells, 65536));
     A.oct_lds_bytes = (A.oct_lds_bytes + 15) & ~15;
-    // a level can miss the LDS instantiation only if its node capacity, its cell offsets or its
-    // worst-case candidate count (cand_cap) does not fit
+    // a level misses k_octree (labels in LDS or in the workspace) only if its node capacity or
+    // its cell offsets do not fit LDS; then k_octree_retry redoes it with generic pointers
     A.oct_may_retry = 0;
     for (int l = 0; l < L; ++l) {
         const LevelGeom& G = A.lv[l];
-        if (G.oct_cap > lds_nodes || G.ncells > A.oct_nq_off / 4 || G.cand_cap > kOctLdsKeys)
-            A.oct_may_retry = 1;
+        if (G.oct_cap > lds_nodes || G.ncells > A.oct_nq_off / 4) A.oct_may_retry = 1;
     }
     A.oct_force_retry = getenv("ORBGPU_OCT_GENERIC") ? 1 : 0;  // diagnostics / tests
     if (A.oct_force_retry) A.oct_may_retry = 1;
