@@ -1021,7 +1021,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
     // int8): both in LDS tables shared by the workgroup instead of 16 VGPRs per lane
     static_assert(kOdRows == 1 && kOdLanes * 8 == 256 && kOdLanes * kOdPairs == 256, "LDS table shapes");
     __shared__ __attribute__((aligned(16))) uint32_t s_msk[kOdLanes][8];
-    __shared__ __attribute__((aligned(16))) uint32_t s_pat[kOdLanes * kOdPairs];
+    // test pair j as floats {x0, x1, y0, y1}: the two samples of a pair rotate as one packed pair
+    __shared__ __attribute__((aligned(16))) uint4 s_pat[kOdLanes * kOdPairs];
     {
         const int ts = threadIdx.x / 8, ti = threadIdx.x % 8;
         const int v = ts - 15;
@@ -1033,7 +1034,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
             m |= ((u < 0 ? -u : u) <= d ? 0xFFu : 0u) << (8 * j);
         }
         s_msk[ts][ti] = m;
-        s_pat[threadIdx.x] = reinterpret_cast<const uint32_t*>(c_pattern.v)[threadIdx.x];
+        const int8_t* pv = c_pattern.v + 4 * threadIdx.x;  // x0, y0, x1, y1
+        s_pat[threadIdx.x] = make_uint4(__float_as_uint((float)pv[0]), __float_as_uint((float)pv[2]),
+                                        __float_as_uint((float)pv[1]), __float_as_uint((float)pv[3]));
     }
     __syncthreads();
     int vrow[kOdRows];
@@ -1127,22 +1130,29 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         const int pc = kOdPatchR * kOdPatchPitch + (x - xb);  // patch offset of the keypoint
-        uint32_t t[2 * kOdPairs];
-#pragma unroll
-        for (int e = 0; e < 2 * kOdPairs; ++e) {
-            // the packed pattern word is opaque here, so its float conversions are not hoisted
-            // out of the keypoint loop (that would hold 4 VGPRs per pair across it)
-            uint32_t pw = s_pat[sub * kOdPairs + (e >> 1)];
-            asm volatile("" : "+v"(pw));
-            const int sh8 = 16 * (e & 1);
-            const float px = (float)(int8_t)(pw >> sh8), py = (float)(int8_t)(pw >> (sh8 + 8));
-            const int ry = cv_round(px * sn + py * ca);
-            const int rx = cv_round(px * ca - py * sn);
-            t[e] = pt[pc + ry * kOdPatchPitch + rx];
-        }
+        // both samples of a test pair as a float pair (each element an IEEE single operation, no
+        // contraction): row = x*b + y*a, col = x*a - y*b as the reference's float expressions
+        // (:116-121), then cvRound by adding 1.5 * 2^23 (round to nearest even, |value| < 19),
+        // whose low 24 bits are 2^22 + the rounded value: the LDS offset is one v_mad_u32_u24 of
+        // the two bit patterns and a per-keypoint constant (no v_rndne / v_cvt per sample)
+        const float magic = 12582912.0f;
+        const uint32_t kofs = (uint32_t)pc - 0x4B400000u - 0x400000u * (uint32_t)kOdPatchPitch;
         uint32_t bits = 0;
 #pragma unroll
-        for (int b = 0; b < kOdPairs; ++b) bits |= (uint32_t)(t[2 * b] < t[2 * b + 1]) << b;
+        for (int b = 0; b < kOdPairs; ++b) {
+            uint4 pw = s_pat[sub * kOdPairs + b];  // float bit patterns {x0, x1, y0, y1}
+            asm volatile("" : "+v"(pw.x), "+v"(pw.y), "+v"(pw.z), "+v"(pw.w));  // not hoisted
+            const float x0 = __uint_as_float(pw.x), x1 = __uint_as_float(pw.y);
+            const float y0 = __uint_as_float(pw.z), y1 = __uint_as_float(pw.w);
+            const uint32_t r0 = __float_as_uint((x0 * sn + y0 * ca) + magic);
+            const uint32_t c0 = __float_as_uint((x0 * ca - y0 * sn) + magic);
+            const uint32_t r1 = __float_as_uint((x1 * sn + y1 * ca) + magic);
+            const uint32_t c1 = __float_as_uint((x1 * ca - y1 * sn) + magic);
+            // the unsigned sums wrap to the small patch offsets; index with them as int
+            const int o0 = (int)(__umul24(r0, (uint32_t)kOdPatchPitch) + c0 + kofs);
+            const int o1 = (int)(__umul24(r1, (uint32_t)kOdPatchPitch) + c1 + kofs);
+            bits |= (uint32_t)(pt[o0] < pt[o1]) << b;
+        }
         if (valid) {
             if (sub == 0) a.lvlangle[kbase + kp] = angle;
             uint8_t* dd = a.lvldesc + (kbase + kp) * 32;
