@@ -22,7 +22,8 @@ __all__ = ["ORBextractor", "ORBmatcher", "BFMatcher", "BatchExtractor", "KEYPOIN
            "OrbGpuError", "load_library", "LIB_PATH"]
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "liborbgpu.so")
+# ORBGPU_LIB names another build of the same library (measurement variants under tools/)
+LIB_PATH = os.environ.get("ORBGPU_LIB") or os.path.join(HERE, "liborbgpu.so")
 
 # orbgpu_map_point (60 B): the MapPoint state ORBmatcher::SearchByProjection reads
 MAP_POINT_DTYPE = np.dtype([("proj_x", "<f4"), ("proj_y", "<f4"), ("proj_xr", "<f4"), ("view_cos", "<f4"),

@@ -155,6 +155,34 @@ def test_flat_and_empty_images(oracle):
     assert m == -1 and len(k) == 0
 
 
+def _two_sided_frames():
+    """Frames where most pixels pass the compass pre-test on BOTH sides (a steep diagonal ramp:
+    ring points 0/4 brighter, 8/12 darker: 77% of pixels), a mix of ramp and noise inside one
+    cell (23%), and a 3-px checkerboard where every pixel is a one-sided candidate -- the densest
+    candidate lists k_fast_cells builds."""
+    h, w = 480, 640
+    y, x = np.mgrid[0:h, 0:w]
+    ramp = (((x + y) * 10) & 255).astype(np.uint8)
+    noise = synth.frame(h, w, 4)
+    mixed = noise.copy()
+    mixed[:, ::70] = ramp[:, ::70]
+    band = (x // 17 + y // 13) % 2 == 0
+    mixed[band] = ramp[band]
+    checker = (((x // 3 + y // 3) % 2) * 200 + 20).astype(np.uint8)
+    return ramp, mixed, checker
+
+
+def test_fast_two_sided_candidates(oracle):
+    ex = _extractor()
+    for img in _two_sided_frames():
+        for lap in ((0, 0), (0, 1000)):
+            k, d, m = ex(img, None, lap)
+            rk, rd, rm = oracle.extract(img, nfeatures=2000, lap=lap)
+            assert m == rm
+            _same_kps(k, rk)
+            np.testing.assert_array_equal(d, rd)
+
+
 def test_descriptor_distance_matches_reference(oracle):
     import orbslam3lib_amd as og
     rng = np.random.default_rng(3)

@@ -1,0 +1,14 @@
+#!/bin/bash
+# Single-stream kernel stats of tools/profile_batch.py for each library under orbslam3lib_amd/variants
+# (plus the default build).  Usage: tools/time_variants.sh [KERNEL_SUBSTRING]
+cd "$(dirname "$0")/.."
+export TMPDIR=/tmp ORBGPU_STREAMS=1
+K=${1:-k_fast_cells}
+for lib in orbslam3lib_amd/liborbgpu.so orbslam3lib_amd/variants/*.so; do
+  n=$(basename $lib .so)
+  O=gpurun_out/variants/$n
+  mkdir -p $O
+  ORBGPU_LIB=$PWD/$lib timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $O -o run -- python3 tools/profile_batch.py > $O/log.txt 2>&1 || { tail $O/log.txt; exit 1; }
+  f=$(find $O -name "run_kernel_stats.csv" | head -1)
+  echo "== $n"; grep "$K" $f | cut -d, -f1-5
+done
