@@ -74,6 +74,11 @@ struct BatchArgs {
     int oct_lds_nodes;               // node capacity of k_octree's dynamic LDS (0: all global)
     int oct_lds_bytes;
     int oct_nq_off;                  // byte offset of the per-key labels in that LDS
+    // levels [oct_split, nlevels) run in a second k_octree launch of kOctSmallThreads-thread
+    // workgroups with their own, smaller LDS layout (more workgroups per CU for the short levels)
+    int oct_split;
+    int oct2_threads;                // 128 or 256
+    int oct2_lds_nodes, oct2_lds_bytes, oct2_nq_off, oct2_lds_keys;
     int oct_may_retry;               // some level can exceed the LDS instantiation of k_octree
     int oct_force_retry;             // diagnostics: every level through the generic instantiation
     // k_pyramid stripe tables in rtab, one per stripe count 2^i (i < kPyrStripeKinds):
@@ -140,6 +145,15 @@ constexpr int kOctLdsNodes = 1024;
 constexpr int kOdKpBlock = 8;  // keypoints per k_orient_desc block (256 threads / 32 lanes)
 
 constexpr int kOctLdsKeys = 16384;  // per-key node labels (u16) kept in LDS up to this many keys
+constexpr int kOctSmallThreads = 256;  // default workgroup size of the short-level k_octree launch
+constexpr int kOctSmallLds = 36 * 1024;  // default dynamic LDS of that launch: 4 workgroups per CU with the static part
+
+// LDS layout of one k_octree launch
+struct OctCfg {
+    int nq_off;     // byte offset of the per-key labels
+    int lds_nodes;  // node capacity in LDS
+    int lds_keys;   // labels kept in LDS up to this many keys (global workspace above)
+};
 
 struct OctLayout {
     long long keys, nq, nodemem, total;

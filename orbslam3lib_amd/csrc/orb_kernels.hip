@@ -869,7 +869,7 @@ constexpr int kOctRetry = -7;
 template <bool kLdsPath>
 __device__ __attribute__((always_inline)) inline void octree_level(const BatchArgs& a, int img, int l,
                                                                    uint8_t* nodemem_lds, int* scratch,
-                                                                   OctShared& sh) {
+                                                                   OctShared& sh, const OctCfg q) {
     const LevelGeom& G = a.lv[l];
     DevPolicy p{scratch};
     const int32_t* cnt = a.cellcnt + (long long)img * a.cellcnt_img_stride + G.cellcnt_off;
@@ -877,11 +877,11 @@ __device__ __attribute__((always_inline)) inline void octree_level(const BatchAr
     uint8_t* ws = a.octws + (long long)img * a.octws_img_stride + G.oct_off;
     const OctLayout L = oct_layout(G.cand_cap, G.oct_cap);
     uint32_t* keys = reinterpret_cast<uint32_t*>(ws + L.keys);
-    void* nm = G.oct_cap <= a.oct_lds_nodes ? (void*)nodemem_lds : (void*)(ws + L.nodemem);
+    void* nm = G.oct_cap <= q.lds_nodes ? (void*)nodemem_lds : (void*)(ws + L.nodemem);
     // exclusive scan of the cell counts into LDS (the node area is free until the octree's
     // gather has read it)
     int32_t* cell_off = reinterpret_cast<int32_t*>(nodemem_lds);
-    const bool off_in_lds = G.ncells <= a.oct_nq_off / 4;
+    const bool off_in_lds = G.ncells <= q.nq_off / 4;
     if (!off_in_lds) cell_off = reinterpret_cast<int32_t*>(ws + L.nq);  // huge levels only
     int carry = 0;
     for (int base = 0; base < G.ncells; base += blockDim.x) {
@@ -897,12 +897,12 @@ __device__ __attribute__((always_inline)) inline void octree_level(const BatchAr
     uint32_t* out_keys = a.lvlkey + (long long)img * a.lvlkp_img_stride + G.kp_off;
     unsigned long long* dbg = a.octdbg ? a.octdbg + ((long long)img * kMaxLevels + l) * 8 : nullptr;
     int r = n > G.cand_cap ? -3 : 0;
-    // node state and cell offsets in LDS; the per-key labels too up to kOctLdsKeys keys, in the
+    // node state and cell offsets in LDS; the per-key labels too up to q.lds_keys keys, in the
     // global workspace above that (dense levels of large frames: the label passes are parallel
     // and streaming, the serial node phases stay in LDS)
-    const bool nodes_fit = off_in_lds && G.oct_cap <= a.oct_lds_nodes && !a.oct_force_retry;
+    const bool nodes_fit = off_in_lds && G.oct_cap <= q.lds_nodes && !a.oct_force_retry;
     if (kLdsPath && r == 0 && !nodes_fit) r = kOctRetry;
-    if (kLdsPath && r == 0 && n > kOctLdsKeys) {
+    if (kLdsPath && r == 0 && n > q.lds_keys) {
         OctWST<kLdsAS, kGlobalAS, kGlobalAS> w;
         w.keys = (asp<kGlobalAS, uint32_t>)keys;
         w.n = n;
@@ -922,7 +922,7 @@ __device__ __attribute__((always_inline)) inline void octree_level(const BatchAr
         OctWST<kLdsAS, kGlobalAS> w;
         w.keys = (asp<kGlobalAS, uint32_t>)keys;
         w.n = n;
-        w.nq = (asp<kLdsAS, uint16_t>)(nodemem_lds + a.oct_nq_off);
+        w.nq = (asp<kLdsAS, uint16_t>)(nodemem_lds + q.nq_off);
         w.m = oct_nodemem_carve<kLdsAS>(nodemem_lds, G.oct_cap);
         w.cap = G.oct_cap;
         w.out_keys = (asp<kGlobalAS, uint32_t>)out_keys;
@@ -938,7 +938,7 @@ __device__ __attribute__((always_inline)) inline void octree_level(const BatchAr
         OctWST<kGeneric, kGeneric> w;
         w.keys = keys;
         w.n = n;
-        w.nq = n <= kOctLdsKeys && off_in_lds ? reinterpret_cast<uint16_t*>(nodemem_lds + a.oct_nq_off)
+        w.nq = n <= q.lds_keys && off_in_lds ? reinterpret_cast<uint16_t*>(nodemem_lds + q.nq_off)
                                              : reinterpret_cast<uint16_t*>(ws + L.nq);
         w.m = oct_nodemem_carve<kGeneric>(nm, G.oct_cap);
         w.cap = G.oct_cap;
@@ -949,7 +949,7 @@ __device__ __attribute__((always_inline)) inline void octree_level(const BatchAr
         w.cellkeys = ck;
         w.ncells = G.ncells;
         w.cell_cap = G.cell_cap;
-        if (!off_in_lds && n > kOctLdsKeys) r = -3;  // cell offsets occupy L.nq
+        if (!off_in_lds && n > q.lds_keys) r = -3;  // cell offsets occupy L.nq
         else r = octree_distribute(p, w, &sh, G.W, G.H, G.N);
     }
     if (threadIdx.x == 0) {
@@ -958,12 +958,14 @@ __device__ __attribute__((always_inline)) inline void octree_level(const BatchAr
     }
 }
 
-// One workgroup per (image, level), level-major dispatch: the long level-0 groups go first.
-__global__ __launch_bounds__(512, 4) void k_octree(BatchArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t nodemem_lds[];  // a.oct_lds_bytes
+// One workgroup per (image, level l0 + blockIdx.y), level-major dispatch: the long level-0
+// groups go first.  NT = 512 for the leading levels, kOctSmallThreads for the short ones.
+template <int NT>
+__global__ __launch_bounds__(NT) void k_octree(BatchArgs a, int l0, OctCfg q) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t nodemem_lds[];  // per-launch size
     __shared__ int scratch[16];
     __shared__ OctShared sh;
-    octree_level<true>(a, a.img0 + blockIdx.x, blockIdx.y, nodemem_lds, scratch, sh);
+    octree_level<true>(a, a.img0 + blockIdx.x, l0 + blockIdx.y, nodemem_lds, scratch, sh, q);
 }
 
 // The levels k_octree left with kOctRetry, redone with generic pointers: a small persistent
@@ -975,7 +977,7 @@ __global__ __launch_bounds__(512, 1) void k_octree_retry(BatchArgs a) {
     for (int s = blockIdx.x; s < a.nimages * a.nlevels; s += gridDim.x) {
         const int img = a.img0 + s / a.nlevels, l = s % a.nlevels;
         if (a.status[img * kMaxLevels + l] != kOctRetry) continue;  // uniform per workgroup
-        octree_level<false>(a, img, l, nodemem_lds, scratch, sh);
+        octree_level<false>(a, img, l, nodemem_lds, scratch, sh, OctCfg{a.oct_nq_off, a.oct_lds_nodes, kOctLdsKeys});
         __syncthreads();
     }
 }
@@ -1607,14 +1609,26 @@ hipError_t launch_fast_cells(const BatchArgs& a, int tile, hipStream_t s) {
 }
 hipError_t launch_octree(const BatchArgs& a, hipStream_t s) {
     if (a.oct_lds_bytes > 65536) {
-        for (const void* f : {reinterpret_cast<const void*>(k_octree),
+        for (const void* f : {reinterpret_cast<const void*>(k_octree<512>),
                               reinterpret_cast<const void*>(k_octree_retry)}) {
             hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, a.oct_lds_bytes);
             if (e != hipSuccess) return e;
         }
     }
-    hipLaunchKernelGGL(k_octree, dim3(a.nimages, a.nlevels), dim3(512), a.oct_lds_bytes, s, a);
-    // levels that did not fit the LDS instantiation (rare: > kOctLdsKeys candidates)
+    const int split = std::min(a.oct_split, a.nlevels);
+    if (split > 0)
+        hipLaunchKernelGGL(k_octree<512>, dim3(a.nimages, split), dim3(512), a.oct_lds_bytes, s, a, 0,
+                           OctCfg{a.oct_nq_off, a.oct_lds_nodes, kOctLdsKeys});
+    if (split < a.nlevels) {
+        const OctCfg q{a.oct2_nq_off, a.oct2_lds_nodes, a.oct2_lds_keys};
+        if (a.oct2_threads == 128)
+            hipLaunchKernelGGL(k_octree<128>, dim3(a.nimages, a.nlevels - split), dim3(128), a.oct2_lds_bytes, s, a,
+                               split, q);
+        else
+            hipLaunchKernelGGL(k_octree<256>, dim3(a.nimages, a.nlevels - split), dim3(256), a.oct2_lds_bytes, s, a,
+                               split, q);
+    }
+    // levels that did not fit the LDS instantiation (rare: node state or cell offsets too large)
     if (a.oct_may_retry)
         hipLaunchKernelGGL(k_octree_retry, dim3(std::min(a.nimages * a.nlevels, 64)), dim3(512),
                            a.oct_lds_bytes, s, a);

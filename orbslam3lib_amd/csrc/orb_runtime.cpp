@@ -406,12 +406,43 @@ int set_geometry(orbgpu_ctx* c, int w, int h) {
     A.oct_nq_off = ((int)oct_nodemem_bytes(std::max(lds_nodes, 1)) + 15) & ~15;
     A.oct_lds_bytes = std::max(A.oct_nq_off + 2 * kOctLdsKeys, std::min(4 * max_cells, 65536));
     A.oct_lds_bytes = (A.oct_lds_bytes + 15) & ~15;
+    // Levels [oct_split, L) run as a second k_octree launch of smaller workgroups (kOctSmallThreads)
+    // with an LDS layout of kOctSmallLds: node state + cell offsets of those levels, then labels
+    // for as many keys as fit (the global workspace above that).  More workgroups fit a CU, which
+    // is what the node phases' serial latency needs.  oct_split = the first level from which on
+    // the node state leaves room for >= 1024 labels (0 for 640x480-class pyramids: every level).
+    {
+        const char* eb = getenv("ORBGPU_OCT_SMALL_LDS");
+        const int budget = eb ? atoi(eb) : kOctSmallLds;
+        const char* et = getenv("ORBGPU_OCT_SMALL_THREADS");
+        A.oct2_threads = et && atoi(et) == 128 ? 128 : kOctSmallThreads;
+        auto layout = [&](int s0) {
+            int n2 = 0, c2 = 0;
+            for (int l = s0; l < L; ++l) {
+                if (A.lv[l].oct_cap <= kOctLdsNodes) n2 = std::max(n2, A.lv[l].oct_cap);
+                c2 = std::max(c2, A.lv[l].ncells);
+            }
+            A.oct2_lds_nodes = n2;
+            A.oct2_nq_off = std::max(((int)oct_nodemem_bytes(std::max(n2, 1)) + 15) & ~15, (4 * c2 + 15) & ~15);
+            A.oct2_lds_keys = std::max(0, (budget - A.oct2_nq_off) / 2);
+            A.oct2_lds_bytes = (A.oct2_nq_off + 2 * A.oct2_lds_keys + 15) & ~15;
+            return A.oct2_lds_keys >= 1024;
+        };
+        if (const char* e = getenv("ORBGPU_OCT_SPLIT")) {
+            A.oct_split = std::max(0, std::min(L, atoi(e)));
+            if (A.oct_split < L && !layout(A.oct_split)) A.oct_split = L;
+        } else {
+            A.oct_split = 0;
+            while (A.oct_split < L && !layout(A.oct_split)) ++A.oct_split;
+        }
+    }
     // a level misses k_octree (labels in LDS or in the workspace) only if its node capacity or
     // its cell offsets do not fit LDS; then k_octree_retry redoes it with generic pointers
     A.oct_may_retry = 0;
     for (int l = 0; l < L; ++l) {
         const LevelGeom& G = A.lv[l];
         if (G.oct_cap > lds_nodes || G.ncells > A.oct_nq_off / 4) A.oct_may_retry = 1;
+        if (l >= A.oct_split && (G.oct_cap > A.oct2_lds_nodes || G.ncells > A.oct2_nq_off / 4)) A.oct_may_retry = 1;
     }
     A.oct_force_retry = getenv("ORBGPU_OCT_GENERIC") ? 1 : 0;  // diagnostics / tests
     if (A.oct_force_retry) A.oct_may_retry = 1;

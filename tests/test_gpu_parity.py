@@ -230,6 +230,30 @@ def test_gpu_matches_golden_fixtures():
         np.testing.assert_array_equal(a, g[key])
 
 
+@pytest.mark.parametrize("env", [{"ORBGPU_OCT_SPLIT": "8"}, {"ORBGPU_OCT_SPLIT": "3"},
+                                 {"ORBGPU_OCT_SMALL_THREADS": "128"},
+                                 {"ORBGPU_OCT_SMALL_LDS": "65536", "ORBGPU_OCT_SPLIT": "1"}])
+def test_octree_launch_shapes(oracle, monkeypatch, env):
+    """k_octree's two launch shapes: 512-thread workgroups with the full LDS layout for levels
+    [0, split) and 256/128-thread workgroups with the short layout for the rest (default at
+    640x480: split 0, most labels in the global workspace).  Every split, both small workgroup
+    sizes and a layout with all labels in LDS give the oracle's keypoints (batch of 4 frames)."""
+    import orbslam3lib_amd as og
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    imgs = synth.stereo_batch(480, 640, 2, first=11)
+    be = og.BatchExtractor(2000, 1.2, 8, 20, 7, width=640, height=480, max_images=4)
+    be.upload(imgs)
+    be.run()
+    be.synchronize()
+    for i in range(4):
+        k, d, m = be.result(i)
+        rk, rd, rm = oracle.extract(imgs[i], nfeatures=2000)
+        assert m == rm
+        _same_kps(k, rk)
+        np.testing.assert_array_equal(d, rd)
+
+
 @pytest.mark.parametrize("pitch", ["64", "80"])
 def test_forced_fast_tile(oracle, frame0, monkeypatch, pitch):
     """The 64- and 80-byte-pitch FAST tiles (the runtime uses 48 bytes for the leading levels of
