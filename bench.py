@@ -455,6 +455,38 @@ def main():
                   "kernel_ms_per_launch": round(st[0] / st[1], 4) if st[1] else None,
                   "pairs_per_step": P, "matched_frac_pair0": round(float((ur >= 0).mean()), 3) if len(ur) else 0.0}
 
+    # Frame::ComputeStereoFishEyeMatches (Frame.cc:1142-1201) on the same resident batch, timed on
+    # its own: stereo-row kNN2 + KannalaBrandt8 triangulation, TUM-VI-like fisheye rig (0.1 m)
+    fisheye = None
+    if not args.no_stereo:
+        import orbslam3lib_amd as og
+        kb = [250.0, 249.9, 320.5, 240.2, 0.0034823894, 0.00071503485, -0.0020532361, 0.00020293674]
+        rig = og.KB8Rig.make(kb, kb, None, (0.101, 0.0, 0.0))
+        be.fisheye_stereo(rig)
+        be.synchronize()
+        be.set_profiling(True, stages=["k_fisheye_stereo", "k_knn2"])
+        be.reset_stage_times()
+        barrier(dist)
+        be.synchronize()
+        f0 = time.perf_counter()
+        for _ in range(args.steps):
+            be.fisheye_stereo(rig)
+        be.synchronize()
+        f1 = time.perf_counter()
+        fe_el = max_over_ranks(dist, f1 - f0)
+        times = be.stage_times()
+        fk = times.get("k_fisheye_stereo", (0.0, 0))
+        kk = times.get("k_knn2", (0.0, 0))
+        be.set_profiling(False)
+        r0 = be.fisheye_result(0)
+        fisheye = {"metric": "left keypoints through ComputeStereoFishEyeMatches per second (stereo-row kNN2 + "
+                             "KannalaBrandt8 triangulation)",
+                   "value": round(sum_over_ranks(dist, nq_per_step * args.steps) / fe_el / 1e6, 3),
+                   "unit": "Mkeypoints/s", "ms_per_step": round(fe_el / args.steps * 1e3, 4),
+                   "triangulation_ms_per_launch": round(fk[0] / fk[1], 4) if fk[1] else None,
+                   "knn2_ms_per_launch": round(kk[0] / kk[1], 4) if kk[1] else None,
+                   "pairs_per_step": P, "n_matches_pair0": r0["n_matches"]}
+
     # Frame::UndistortKeyPoints + AssignFeaturesToGrid over every image of the
     # resident batch, timed on its own: EuRoC cam0 calibration (k1 k2 p1 p2)
     grid = None
@@ -731,6 +763,7 @@ def main():
             "stages": stage_rows,
             "cpu_baseline": cpu,
             "stereo_matches": stereo,
+            "fisheye_stereo_matches": fisheye,
             "undistort_grid": grid,
             "search_by_projection": sbp,
             "other_configs": configs,

@@ -169,6 +169,28 @@ int orbgpu_stereo_matches_batch(orbgpu_ctx* ctx, int n_pairs, float mbf, float m
 int orbgpu_download_stereo(orbgpu_ctx* ctx, int pair, float* u_right, float* depth, int32_t* sad,
                            int cap, int* n);
 
+/* ---- fisheye stereo ------------------------------------------------------------------------
+ * Frame::ComputeStereoFishEyeMatches (cpp/src/Frame.cc:1142-1201, called from the two-camera
+ * Frame ctor :1121 and FrameAHB.cc:320) on the device-resident results of the last
+ * orbgpu_run_batch: pair p = left image 2p (mvKeys), right image 2p+1 (mvKeysRight).  Runs the
+ * stereo-row kNN2 (BFMatchORB, :1164 = orbgpu_match_stereo_batch with stereo_rows_only = 1; its
+ * result stays readable through orbgpu_download_matches), then per left stereo row: dist1 == 0
+ * skipped, dist1 < 70 triangulated with KannalaBrandt8::TriangulateMatches
+ * (CameraModels/KannalaBrandt8.cpp:300-366; sigmas = mvLevelSigma2 of the two octaves) and
+ * accepted when the depth > 1e-4.  Parity with the reference is unpinned (Eigen's JacobiSVD
+ * order and FMA use, the Android libm's atan2f / tanf): see DESIGN.md and tests/test_fisheye.py. */
+typedef struct {
+    float cam_left[8], cam_right[8];   /* KannalaBrandt8 mvParameters: fx fy cx cy k0 k1 k2 k3 */
+    float precision_left, precision_right;  /* KannalaBrandt8::precision (1e-6 by default) */
+    float R12[9];                      /* Frame::mRlr, row-major */
+    float t12[3];                      /* Frame::mtlr */
+} orbgpu_kb8_rig;
+int orbgpu_fisheye_stereo_batch(orbgpu_ctx* ctx, int n_pairs, const orbgpu_kb8_rig* rig, void* stream);
+/* Per pair: mvLeftToRightMatch [n_left], mvRightToLeftMatch [n_right] (-1 = none), mvDepth
+ * [n_left] (-1 = none), mvStereo3Dpoints [n_left][3] (0 where none), nMatches. */
+int orbgpu_download_fisheye(orbgpu_ctx* ctx, int pair, int32_t* l2r, int32_t* r2l, float* depth, float* p3d,
+                            int cap, int* n_left, int* n_right, int* n_matches);
+
 /* ---- ORBmatcher::SearchByProjection (cpp/src/ORBmatcher.cc:44-214, pinhole frames) ---------
  * Tracking's local-map search: every map point predicted in view is matched against the frame
  * keypoints in a window around its projection (Frame::GetFeaturesInArea, Frame.cc:673-735, on the

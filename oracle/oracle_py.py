@@ -271,6 +271,32 @@ def stereo_matches(kps_l, desc_l, kps_r, desc_r, pyr_l, pyr_r, mbf, mb, scale_fa
     return ur, dep, sad
 
 
+def fisheye_stereo(kps_l, mono_l, kps_r, mono_r, idx1, dist1, rig, sigma2):
+    """Frame::ComputeStereoFishEyeMatches (Frame.cc:1142-1201) on one frame's stereo-row kNN2
+    (idx1 / dist1 from knn2(desc_l[mono_l:], desc_r[mono_r:])).  rig: dict with cam_left /
+    cam_right (8 KannalaBrandt8 parameters), precision_left / precision_right, R12 (3x3), t12.
+    Returns dict: l2r, r2l, depth, p3d, code, margins, n_matches (parity unpinned: see
+    orb_fisheye.cpp)."""
+    kl = np.ascontiguousarray(kps_l, dtype=KP_DTYPE)
+    kr = np.ascontiguousarray(kps_r, dtype=KP_DTYPE)
+    nl, nr = len(kl), len(kr)
+    nq = max(nl - mono_l, 0)
+    i1 = np.ascontiguousarray(idx1[:nq], dtype=np.int32)
+    d1 = np.ascontiguousarray(dist1[:nq], dtype=np.int32)
+    f32 = lambda a: np.ascontiguousarray(a, dtype=np.float32).ravel()
+    cl, cr = f32(rig["cam_left"]), f32(rig["cam_right"])
+    R, t, s2 = f32(rig["R12"]), f32(rig["t12"]), f32(sigma2)
+    out = dict(l2r=np.zeros(nl, np.int32), r2l=np.zeros(nr, np.int32), depth=np.zeros(nl, np.float32),
+               p3d=np.zeros((nl, 3), np.float32), code=np.zeros(nq, np.int32),
+               margins=np.zeros((nq, 5), np.float64))
+    out["n_matches"] = lib().oracle_fisheye_stereo(
+        _p(kl), nl, mono_l, _p(kr), nr, mono_r, _p(i1), _p(d1), _p(cl), _p(cr),
+        C.c_float(rig.get("precision_left", 1e-6)), C.c_float(rig.get("precision_right", 1e-6)),
+        _p(R), _p(t), _p(s2), _p(out["l2r"]), _p(out["r2l"]), _p(out["depth"]), _p(out["p3d"]),
+        _p(out["code"]), _p(out["margins"]))
+    return out
+
+
 def undistort_grid(kps, K, dist, cols, rows):
     """Frame::UndistortKeyPoints + ComputeImageBounds + AssignFeaturesToGrid (Frame.cc:405-436,
     741-825) -> (xy_un [n,2] f32, bounds [4] f32, cell [n] i32, cell_start [3073], cell_idx)."""

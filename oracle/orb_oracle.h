@@ -158,4 +158,16 @@ int oracle_search_by_projection2(const oracle_map_point* mps, int nmp, const flo
                                  const uint8_t* kp_block, float th, float nnratio, int far_points,
                                  float th_far, int32_t* match);
 
+// Frame::ComputeStereoFishEyeMatches (Frame.cc:1142-1201) on one frame's stereo-row kNN2
+// (orb_fisheye.cpp; parity unpinned, see there).  idx1 / dist1: [nL - monoL]; cam*: KannalaBrandt8
+// mvParameters; R12 row-major (mRlr), t12 (mtlr); sigma2: mvLevelSigma2.  Outputs: l2r [nL],
+// r2l [nR], depth [nL], p3d [nL][3]; per stereo row: code (1 dist 0, 2 dist >= 70, 3 index,
+// 4 parallax, 5 z1, 6 z2, 7 reprojection 1, 8 reprojection 2, 9 depth <= 1e-4, 10 accepted) and
+// margins [5] (cos parallax, z1, z2, err1 - bound1, err2 - bound2; NaN where not reached).
+// Returns nMatches.
+int oracle_fisheye_stereo(const oracle_kp* kpsL, int nL, int monoL, const oracle_kp* kpsR, int nR, int monoR,
+                          const int32_t* idx1, const int32_t* dist1, const float* camL, const float* camR,
+                          float precL, float precR, const float* R12, const float* t12, const float* sigma2,
+                          int32_t* l2r, int32_t* r2l, float* depth, float* p3d, int32_t* code, double* margins);
+
 }  // extern "C"

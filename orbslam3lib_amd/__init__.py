@@ -50,7 +50,31 @@ EXPORTED = [
     "orbgpu_host_free", "orbgpu_export_descriptors", "orbgpu_match_knn2_device",
     "orbgpu_set_profiling", "orbgpu_num_stages", "orbgpu_stage_name", "orbgpu_stage_times",
     "orbgpu_reset_stage_times", "orbgpu_last_error", "orbgpu_abi_version",
+    "orbgpu_fisheye_stereo_batch", "orbgpu_download_fisheye",
 ]
+
+
+class KB8Rig(C.Structure):
+    """orbgpu_kb8_rig: the two KannalaBrandt8 cameras and Frame::mRlr / mtlr."""
+    _fields_ = [("cam_left", C.c_float * 8), ("cam_right", C.c_float * 8), ("precision_left", C.c_float),
+                ("precision_right", C.c_float), ("R12", C.c_float * 9), ("t12", C.c_float * 3)]
+
+    @classmethod
+    def make(cls, cam_left, cam_right, R12=None, t12=(0.0, 0.0, 0.0), precision_left=1e-6,
+             precision_right=1e-6):
+        r = cls()
+        r.cam_left[:] = [float(v) for v in cam_left]
+        r.cam_right[:] = [float(v) for v in cam_right]
+        r.precision_left, r.precision_right = precision_left, precision_right
+        R = np.eye(3, dtype=np.float32) if R12 is None else np.asarray(R12, np.float32).reshape(9)
+        r.R12[:] = [float(v) for v in np.ravel(R)]
+        r.t12[:] = [float(v) for v in t12]
+        return r
+
+    def as_dict(self):
+        return dict(cam_left=list(self.cam_left), cam_right=list(self.cam_right),
+                    precision_left=self.precision_left, precision_right=self.precision_right,
+                    R12=np.array(list(self.R12), np.float32).reshape(3, 3), t12=list(self.t12))
 
 
 class OrbGpuError(RuntimeError):
@@ -385,6 +409,26 @@ class BatchExtractor:
         _check(_lib.orbgpu_download_stereo(self.ctx.handle, pair, _p(ur), _p(dp), _p(sad), cap,
                                            C.byref(n)))
         return ur[:n.value], dp[:n.value], sad[:n.value]
+
+    def fisheye_stereo(self, rig, stream=None):
+        """Frame::ComputeStereoFishEyeMatches (Frame.cc:1142-1201) for every pair 2p / 2p+1 of the
+        last run(): the stereo-row kNN2 (matches() returns it afterwards) and the KannalaBrandt8
+        triangulation (rig: KB8Rig); results stay in HBM (fisheye_result)."""
+        _check(_lib.orbgpu_fisheye_stereo_batch(self.ctx.handle, self.n // 2, C.byref(rig),
+                                                C.c_void_p(stream) if stream else None))
+
+    def fisheye_result(self, pair, cap=65536):
+        """dict(l2r, r2l, depth, p3d, n_matches) of pair `pair` (mvLeftToRightMatch,
+        mvRightToLeftMatch, mvDepth, mvStereo3Dpoints)."""
+        l2r = np.zeros(cap, np.int32)
+        r2l = np.zeros(cap, np.int32)
+        dp = np.zeros(cap, np.float32)
+        p3 = np.zeros((cap, 3), np.float32)
+        nl, nr, nm = C.c_int(0), C.c_int(0), C.c_int(0)
+        _check(_lib.orbgpu_download_fisheye(self.ctx.handle, pair, _p(l2r), _p(r2l), _p(dp), _p(p3), cap,
+                                            C.byref(nl), C.byref(nr), C.byref(nm)))
+        return dict(l2r=l2r[:nl.value], r2l=r2l[:nr.value], depth=dp[:nl.value], p3d=p3[:nl.value],
+                    n_matches=nm.value)
 
     def upload_sbs(self, frames, width=None):
         """Side-by-side stereo Y8 frames [n, H, S] (row stride S >= 2W; W = S // 2 by default) ->

@@ -121,6 +121,28 @@ struct StereoArgs {
     int pair0;                       // first pair of this launch
 };
 
+// Frame::ComputeStereoFishEyeMatches over a batch (orb_fisheye.hip): pair p = left image 2p,
+// right image 2p+1, on the stereo-row kNN2 of orbgpu_match_stereo_batch(stereo_only = 1).
+struct FisheyeArgs {
+    const void* kps;                 // out_kps: orbgpu_keypoint [img][out_cap]
+    const int32_t* out_n;            // [img]
+    const int32_t* out_mono;         // [img]
+    int out_cap;
+    const int32_t* idx1;             // [pair][out_cap] kNN2 best train row (stereo rows)
+    const int32_t* dist1;            // [pair][out_cap]
+    float cam_l[8], cam_r[8];        // KannalaBrandt8 mvParameters: fx fy cx cy k0 k1 k2 k3
+    float prec_l, prec_r;            // KannalaBrandt8::precision
+    float R12[9], t12[3];            // Frame::mRlr (row-major), Frame::mtlr
+    float sigma2[kMaxLevels];        // mvLevelSigma2
+    int32_t* l2r;                    // [pair][out_cap] mvLeftToRightMatch
+    int32_t* r2l;                    // [pair][out_cap] mvRightToLeftMatch (pre-set to -1)
+    float* depth;                    // [pair][out_cap] mvDepth
+    float* p3d;                      // [pair][out_cap][3] mvStereo3Dpoints
+    int32_t* counts;                 // [pair][2] nMatches, descMatches (pre-set to 0)
+    int pair0;                       // first pair of this launch
+};
+hipError_t launch_fisheye(const FisheyeArgs& f, int npairs, hipStream_t s);
+
 // Frame::UndistortKeyPoints + AssignFeaturesToGrid over a batch's keypoints (orb_frame.hip).
 constexpr int kGridCols = 64, kGridRows = 48;  // FRAME_GRID_COLS / ROWS (Frame.h:46-47)
 struct GridArgs {

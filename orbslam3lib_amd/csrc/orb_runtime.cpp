@@ -40,12 +40,13 @@ int fail(int code, const std::string& msg) {
     } while (0)
 
 enum Stage { ST_RESIZE, ST_BLUR, ST_FAST48, ST_FAST, ST_FAST_TOP, ST_OCTREE, ST_ORIENT, ST_FINAL, ST_KNN,
-             ST_PYRAMID, ST_STEREO, ST_GRID, ST_SBS, ST_SOA, ST_SBP, ST_COUNT };
+             ST_PYRAMID, ST_STEREO, ST_GRID, ST_SBS, ST_SOA, ST_SBP, ST_FISHEYE, ST_COUNT };
 // names as rocprofv3 shows the kernels (templates with their argument)
 const char* kStageNames[ST_COUNT] = {"k_blur_resize",    "k_blur",   "k_fast_cells<48>", "k_fast_cells<64>",
                                      "k_fast_cells<80>", "k_octree", "k_orient_desc",    "k_finalize",
                                      "k_knn2",           "k_pyramid", "k_stereo",         "k_undistort_grid",
-                                     "k_sbs_split",      "k_pack_soa",       "k_sbp"};
+                                     "k_sbs_split",      "k_pack_soa",       "k_sbp",
+                                     "k_fisheye_stereo"};
 
 struct DevBuf {
     void* p = nullptr;
@@ -104,12 +105,13 @@ struct orbgpu_ctx {
     DevBuf input, pyr, blur, rtab, cellkeys, cellcnt, octws, lvlkey, lvlangle, lvldesc, lvlcnt,
         status, outkps, outdesc, outn, outmono, laps, midx1, mdist1, midx2, mdist2, mnq, scratch,
         octdbg, knnpart, strow, stidx, stur, stdepth, stsad, gxy, gcell, gstart, gidx, sbs, soa, m16,
-        sbpmp, sbpoff, sbpcand, sbpblk, sbpmatch, sbpnm, sbplr;
+        sbpmp, sbpoff, sbpcand, sbpblk, sbpmatch, sbpnm, sbplr, fel2r, fer2l, fedepth, fep3d, fecnt;
     float grid_bounds[4] = {0, 0, 0, 0}, grid_inv[2] = {0, 0};  // of the last undistort_grid
     int sbp_frames = 0, sbp_step = 1, sbp_two_cam = 0;
     int soa_images = 0, soa_pairs = 0;  // coverage of the last orbgpu_pack_soa
     int grid_images = 0;   // images of the last orbgpu_undistort_grid_batch
     int stereo_pairs = 0;  // pairs of the last orbgpu_stereo_matches_batch
+    int fisheye_pairs = 0;  // pairs of the last orbgpu_fisheye_stereo_batch
     int input_images = 0;   // images currently sized for in `input`
     hipEvent_t fork = nullptr;
     hipEvent_t ext_done = nullptr;  // work on a caller's stream (rejoin)
@@ -688,7 +690,8 @@ int orbgpu_destroy(orbgpu_ctx* c) {
                       &c->knnpart, &c->strow,  &c->stidx, &c->stur,    &c->stdepth,  &c->stsad,
                       &c->gxy,     &c->gcell,  &c->gstart, &c->gidx,    &c->sbs,      &c->soa,
                       &c->m16,     &c->sbpmp,  &c->sbpoff, &c->sbpcand, &c->sbpblk,  &c->sbpmatch,
-                      &c->sbpnm,   &c->sbplr};
+                      &c->sbpnm,   &c->sbplr,  &c->fel2r,  &c->fer2l,   &c->fedepth, &c->fep3d,
+                      &c->fecnt};
     for (DevBuf* b : bufs) b->release();
     for (size_t k = 1; k < c->sub.size(); ++k) hipStreamDestroy(c->sub[k]);
     if (c->fork) hipEventDestroy(c->fork);
@@ -1349,6 +1352,90 @@ int orbgpu_download_stereo(orbgpu_ctx* c, int pair, float* u_right, float* depth
         if (depth) HIP_TRY(hipMemcpy(depth, c->stdepth.as<float>() + o, 4 * (size_t)nl, hipMemcpyDeviceToHost));
         if (sad) HIP_TRY(hipMemcpy(sad, c->stsad.as<int32_t>() + o, 4 * (size_t)nl, hipMemcpyDeviceToHost));
     }
+    return ORBGPU_OK;
+}
+
+// ---- Frame::ComputeStereoFishEyeMatches (orb_fisheye.hip) -------------------------------------
+int orbgpu_fisheye_stereo_batch(orbgpu_ctx* c, int n_pairs, const orbgpu_kb8_rig* rig, void* stream) {
+    if (!c || !rig || n_pairs < 1 || 2 * n_pairs > c->last_images) return fail(ORBGPU_ERR_INVALID, "bad pair count");
+    for (int k = 0; k < 2; ++k)
+        if (!(rig->cam_left[k] != 0.f) || !(rig->cam_right[k] != 0.f))
+            return fail(ORBGPU_ERR_INVALID, "zero focal length");
+    // BFMatchORB of the stereo rows (Frame.cc:1164), then the triangulation on the same streams
+    if (int r = orbgpu_match_stereo_batch(c, n_pairs, 1, stream)) return r;
+    HIP_TRY(hipSetDevice(c->device));
+    const size_t np = (size_t)n_pairs, oc = (size_t)c->out_cap;
+    if (c->fel2r.ensure(np * oc * 4 + 256) || c->fer2l.ensure(np * oc * 4 + 256) ||
+        c->fedepth.ensure(np * oc * 4 + 256) || c->fep3d.ensure(np * oc * 12 + 256) || c->fecnt.ensure(np * 8 + 256))
+        return fail(ORBGPU_ERR_HIP, "hipMalloc failed (fisheye buffers)");
+    FisheyeArgs F{};
+    F.kps = c->outkps.p;
+    F.out_n = c->outn.as<int32_t>();
+    F.out_mono = c->outmono.as<int32_t>();
+    F.out_cap = c->out_cap;
+    F.idx1 = c->midx1.as<int32_t>();
+    F.dist1 = c->mdist1.as<int32_t>();
+    for (int k = 0; k < 8; ++k) {
+        F.cam_l[k] = rig->cam_left[k];
+        F.cam_r[k] = rig->cam_right[k];
+    }
+    F.prec_l = rig->precision_left;
+    F.prec_r = rig->precision_right;
+    for (int k = 0; k < 9; ++k) F.R12[k] = rig->R12[k];
+    for (int k = 0; k < 3; ++k) F.t12[k] = rig->t12[k];
+    for (int l = 0; l < kMaxLevels; ++l) F.sigma2[l] = l < c->A.nlevels ? c->sigma2[l] : 0.f;
+    F.l2r = c->fel2r.as<int32_t>();
+    F.r2l = c->fer2l.as<int32_t>();
+    F.depth = c->fedepth.as<float>();
+    F.p3d = c->fep3d.as<float>();
+    F.counts = c->fecnt.as<int32_t>();
+    auto run = [&](int p0, int npp, hipStream_t st) {
+        HIP_TRY(hipMemsetAsync(F.r2l + (size_t)p0 * oc, 0xFF, (size_t)npp * oc * 4, st));  // -1
+        HIP_TRY(hipMemsetAsync(F.counts + 2 * (size_t)p0, 0, (size_t)npp * 8, st));
+        FisheyeArgs FF = F;
+        FF.pair0 = p0;
+        return timed(c, ST_FISHEYE, st, [&] { return launch_fisheye(FF, npp, st); });
+    };
+    bool chunked = !stream && !c->last_chunks.empty();
+    for (const auto& ch : c->last_chunks) chunked &= (ch.img0 % 2) == 0 && (ch.n % 2) == 0;
+    if (chunked) {
+        for (const auto& ch : c->last_chunks) {
+            const int p0 = ch.img0 / 2, npp = std::min(ch.n / 2, n_pairs - p0);
+            if (npp <= 0) continue;
+            if (int r = run(p0, npp, ch.st)) return r;
+        }
+    } else {
+        hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+        int r = join_all(c, s);
+        if (r) return r;
+        if ((r = run(0, n_pairs, s))) return r;
+        if ((r = rejoin(c, s))) return r;
+    }
+    c->fisheye_pairs = n_pairs;
+    return ORBGPU_OK;
+}
+
+int orbgpu_download_fisheye(orbgpu_ctx* c, int pair, int32_t* l2r, int32_t* r2l, float* depth, float* p3d, int cap,
+                            int* n_left, int* n_right, int* n_matches) {
+    if (!c || pair < 0 || pair >= c->fisheye_pairs) return fail(ORBGPU_ERR_INVALID, "bad pair");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipDeviceSynchronize());
+    int32_t n[2] = {0, 0}, cnt[2] = {0, 0};
+    HIP_TRY(hipMemcpy(n, c->outn.as<int32_t>() + 2 * pair, 8, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(cnt, c->fecnt.as<int32_t>() + 2 * pair, 8, hipMemcpyDeviceToHost));
+    if (int e = count_status(n[0])) return e;
+    if (int e = count_status(n[1])) return e;
+    if (n_left) *n_left = n[0];
+    if (n_right) *n_right = n[1];
+    if (n_matches) *n_matches = cnt[0];
+    if (n[0] > cap || n[1] > cap) return fail(ORBGPU_ERR_CAPACITY, "caller capacity too small");
+    const size_t o = (size_t)pair * c->out_cap;
+    if (n[0]) {
+        if (l2r) HIP_TRY(hipMemcpy(l2r, c->fel2r.as<int32_t>() + o, 4 * (size_t)n[0], hipMemcpyDeviceToHost));
+        if (depth) HIP_TRY(hipMemcpy(depth, c->fedepth.as<float>() + o, 4 * (size_t)n[0], hipMemcpyDeviceToHost));
+        if (p3d) HIP_TRY(hipMemcpy(p3d, c->fep3d.as<float>() + 3 * o, 12 * (size_t)n[0], hipMemcpyDeviceToHost));
+    }
+    if (n[1] && r2l) HIP_TRY(hipMemcpy(r2l, c->fer2l.as<int32_t>() + o, 4 * (size_t)n[1], hipMemcpyDeviceToHost));
     return ORBGPU_OK;
 }
 

@@ -37,7 +37,7 @@ def test_host_entry_points():
     assert lib.orbgpu_abi_version() == 1
     names = [lib.orbgpu_stage_name(i) for i in range(lib.orbgpu_num_stages())]
     assert names == [b"k_blur_resize", b"k_blur", b"k_fast_cells<48>", b"k_fast_cells<64>", b"k_fast_cells<80>", b"k_octree",
-                     b"k_orient_desc", b"k_finalize", b"k_knn2", b"k_pyramid", b"k_stereo", b"k_undistort_grid", b"k_sbs_split", b"k_pack_soa", b"k_sbp"]
+                     b"k_orient_desc", b"k_finalize", b"k_knn2", b"k_pyramid", b"k_stereo", b"k_undistort_grid", b"k_sbs_split", b"k_pack_soa", b"k_sbp", b"k_fisheye_stereo"]
     a = np.arange(32, dtype=np.uint8)
     b = np.full(32, 255, np.uint8)
     assert og.ORBmatcher.DescriptorDistance(a, b) == int(np.unpackbits(a ^ b).sum())
