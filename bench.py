@@ -14,6 +14,7 @@ from __future__ import annotations
 
 import argparse
 import ctypes
+import glob
 import json
 import os
 import sys
@@ -58,7 +59,8 @@ def fast_split(w, h, sf=1.2, L=8, tile=64):
 def algorithmic_bytes(w, h, L, nkp, sf=1.2, ncand=0.0):
     """Per-image bytes by stage: pyramid sum(A_{l-1}+A_l), FAST sum(A_l) (split
     between the 48-, 64- and 80-byte tile launches), blur 2*sum(A_l), 48 B per output keypoint
-    (16 B keypoint + 32 B descriptor); k_pyramid = pyramid + blur in one launch; the octree reads
+    (16 B keypoint + 32 B descriptor) plus, for k_orient_desc, one read of the raw and the
+    blurred pyramid (its windows' pixel support); k_pyramid = pyramid + blur in one launch; the octree reads
     its 4-byte candidate keys and writes 4 bytes per kept keypoint."""
     A = [a * b for a, b in level_sizes(w, h, sf, L)]
     k48 = fast_split(w, h, sf, L, 48)
@@ -71,7 +73,9 @@ def algorithmic_bytes(w, h, L, nkp, sf=1.2, ncand=0.0):
         "k_fast_cells<64>": sum(A[k48:k64]),
         "k_fast_cells<80>": sum(A[k64:]),
         "k_blur": 2 * A[L - 1],  # the last level's blur (the others ride in k_blur_resize)
-        "k_orient_desc": 48 * nkp,
+        # both planes read once (the 31-px moment discs and 37-px patches of ~2000 keypoints per
+        # image cover nearly all of every level) + 48 B out per keypoint
+        "k_orient_desc": 2 * sum(A) + 48 * nkp,
         "k_octree": 4 * ncand + 4 * nkp,
     }
 
@@ -384,8 +388,10 @@ def main():
     if dom is not None:
         r = stage_rows[dom]
         traffic = None
-        tp = os.path.join(ROOT, "profiles", "traffic_r01.json")
-        if os.path.exists(tp):
+        # the newest round's FETCH_SIZE / WRITE_SIZE passes (tools/pmc_traffic.sh + tools/traffic.py)
+        tps = sorted(glob.glob(os.path.join(ROOT, "profiles", "traffic_r*.json")))
+        tp = tps[-1] if tps else ""
+        if tp and os.path.exists(tp):
             try:
                 traffic = json.load(open(tp)).get(dom, {}).get("hbm_bytes_per_launch")
             except Exception:
@@ -454,38 +460,6 @@ def main():
                   "unit": "Mkeypoints/s", "ms_per_step": round(st_el / args.steps * 1e3, 4),
                   "kernel_ms_per_launch": round(st[0] / st[1], 4) if st[1] else None,
                   "pairs_per_step": P, "matched_frac_pair0": round(float((ur >= 0).mean()), 3) if len(ur) else 0.0}
-
-    # Frame::ComputeStereoFishEyeMatches (Frame.cc:1142-1201) on the same resident batch, timed on
-    # its own: stereo-row kNN2 + KannalaBrandt8 triangulation, TUM-VI-like fisheye rig (0.1 m)
-    fisheye = None
-    if not args.no_stereo:
-        import orbslam3lib_amd as og
-        kb = [250.0, 249.9, 320.5, 240.2, 0.0034823894, 0.00071503485, -0.0020532361, 0.00020293674]
-        rig = og.KB8Rig.make(kb, kb, None, (0.101, 0.0, 0.0))
-        be.fisheye_stereo(rig)
-        be.synchronize()
-        be.set_profiling(True, stages=["k_fisheye_stereo", "k_knn2"])
-        be.reset_stage_times()
-        barrier(dist)
-        be.synchronize()
-        f0 = time.perf_counter()
-        for _ in range(args.steps):
-            be.fisheye_stereo(rig)
-        be.synchronize()
-        f1 = time.perf_counter()
-        fe_el = max_over_ranks(dist, f1 - f0)
-        times = be.stage_times()
-        fk = times.get("k_fisheye_stereo", (0.0, 0))
-        kk = times.get("k_knn2", (0.0, 0))
-        be.set_profiling(False)
-        r0 = be.fisheye_result(0)
-        fisheye = {"metric": "left keypoints through ComputeStereoFishEyeMatches per second (stereo-row kNN2 + "
-                             "KannalaBrandt8 triangulation)",
-                   "value": round(sum_over_ranks(dist, nq_per_step * args.steps) / fe_el / 1e6, 3),
-                   "unit": "Mkeypoints/s", "ms_per_step": round(fe_el / args.steps * 1e3, 4),
-                   "triangulation_ms_per_launch": round(fk[0] / fk[1], 4) if fk[1] else None,
-                   "knn2_ms_per_launch": round(kk[0] / kk[1], 4) if kk[1] else None,
-                   "pairs_per_step": P, "n_matches_pair0": r0["n_matches"]}
 
     # Frame::UndistortKeyPoints + AssignFeaturesToGrid over every image of the
     # resident batch, timed on its own: EuRoC cam0 calibration (k1 k2 p1 p2)
@@ -616,6 +590,40 @@ def main():
                     "pack_soa_us": round(pk[0] / pk[1] * 1e3, 2) if pk[1] else None,
                     "pack_soa_GBps": round(pack_b / (pk[0] / pk[1] * 1e-3) / 1e9, 1) if pk[1] else None,
                     "frames_per_step": P, "hbm_peak_GBps": HBM_PEAK_GBS}
+
+    # Frame::ComputeStereoFishEyeMatches (Frame.cc:1142-1201) on the same resident images, timed on
+    # its own: stereo-row kNN2 + KannalaBrandt8 triangulation, TUM-VI-like fisheye rig (0.1 m).
+    # The batch is re-extracted first (untimed) with lapping areas over the whole frame, so every
+    # keypoint is a stereo row (the headline's zero lapping areas leave none).
+    fisheye = None
+    if not args.no_stereo:
+        kb = [250.0, 249.9, 320.5, 240.2, 0.0034823894, 0.00071503485, -0.0020532361, 0.00020293674]
+        rig = og.KB8Rig.make(kb, kb, None, (0.101, 0.0, 0.0))
+        be.run(np.tile(np.array([0, W], np.int32), (2 * P, 1)))
+        be.fisheye_stereo(rig)
+        be.synchronize()
+        be.set_profiling(True, stages=["k_fisheye_stereo", "k_knn2"])
+        be.reset_stage_times()
+        barrier(dist)
+        be.synchronize()
+        f0 = time.perf_counter()
+        for _ in range(args.steps):
+            be.fisheye_stereo(rig)
+        be.synchronize()
+        f1 = time.perf_counter()
+        fe_el = max_over_ranks(dist, f1 - f0)
+        times = be.stage_times()
+        fk = times.get("k_fisheye_stereo", (0.0, 0))
+        kk = times.get("k_knn2", (0.0, 0))
+        be.set_profiling(False)
+        r0 = be.fisheye_result(0)
+        fisheye = {"metric": "left keypoints through ComputeStereoFishEyeMatches per second (stereo-row kNN2 + "
+                             "KannalaBrandt8 triangulation)",
+                   "value": round(sum_over_ranks(dist, nq_per_step * args.steps) / fe_el / 1e6, 3),
+                   "unit": "Mkeypoints/s", "ms_per_step": round(fe_el / args.steps * 1e3, 4),
+                   "triangulation_ms_per_launch": round(fk[0] / fk[1], 4) if fk[1] else None,
+                   "knn2_ms_per_launch": round(kk[0] / kk[1], 4) if kk[1] else None,
+                   "pairs_per_step": P, "n_matches_pair0": r0["n_matches"]}
 
     # the other BASELINE configs as side lines (the headline stays C2): C3's 752x480 stream
     # (synthetic, EuRoC geometry) and C5's 1920x1080 / 12 levels / 5000 features, each with its

@@ -8,7 +8,7 @@ import sys
 
 bench = json.load(open(sys.argv[1]))
 steps = int(sys.argv[3]) if len(sys.argv) > 3 else bench["steps"]
-chunks = int(sys.argv[4]) if len(sys.argv) > 4 else 4
+chunks = int(sys.argv[4]) if len(sys.argv) > 4 else 3  # ORBGPU_STREAMS default
 name = bench["roofline"]["kernel"]
 rows = [r for r in csv.DictReader(open(sys.argv[2])) if name in r["Kernel_Name"].replace("void ", "")]
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
