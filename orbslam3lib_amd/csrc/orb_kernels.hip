@@ -1000,6 +1000,18 @@ constexpr int kOdPatchR = 18;                    // |rotated pattern offset| <= 
 constexpr int kOdPatchRows = 2 * kOdPatchR + 1;  // 37
 constexpr int kOdPatchPitch = 48;                // 3 x 16 B: covers x-18..x+18 from the dword below
 
+// Sum of v over each 32-lane half of the wave, in every lane: DPP quad_perm xor 1 / xor 2, row
+// half-mirror (pairs the two quads of 8 lanes) and row mirror (the two halves of a 16-lane row),
+// then the other row of the 32 through ds_swizzle (xor mask 16).
+__device__ inline int od_sum32(int v) {
+    v += __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+    v += __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+    v += __builtin_amdgcn_update_dpp(0, v, 0x141, 0xF, 0xF, false);  // row_half_mirror
+    v += __builtin_amdgcn_update_dpp(0, v, 0x140, 0xF, 0xF, false);  // row_mirror
+    v += __builtin_amdgcn_ds_swizzle(v, 0x401F);                     // lane ^ 16 within 32
+    return v;
+}
+
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k_orient_desc(BatchArgs a) {
     // per keypoint group: the blurred patch around the keypoint, staged with 16-byte loads
     __shared__ __attribute__((aligned(16))) uint8_t patch[kOdKpBlock][kOdPatchRows * kOdPatchPitch];
@@ -1069,26 +1081,42 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
         const int x0 = x - 15;
         const int xa = raw_dw ? (x0 & ~3) : x0;
         const int shf = x0 - xa;
-#pragma unroll
-        for (int h = 0; h < kOdRows; ++h) {
-            const uint8_t* row = lvl + (long long)(y + vrow[h]) * G.pitch;
-            uint32_t w[9];
-            if (raw_dw) {  // 2 x dwordx4 + 1 dword (global loads need only dword alignment)
-                const uint4 A = *reinterpret_cast<const uint4*>(row + xa);
-                const uint4 B = *reinterpret_cast<const uint4*>(row + xa + 16);
-                w[0] = A.x; w[1] = A.y; w[2] = A.z; w[3] = A.w;
-                w[4] = B.x; w[5] = B.y; w[6] = B.z; w[7] = B.w;
-                w[8] = *reinterpret_cast<const uint32_t*>(row + xa + 32);
-            } else {
+        // the moment row (round trip 1) and the 37 x 37 blurred patch (rows y-18..y+18 from the
+        // dword at or below x-18, 16-byte buffer loads, out-of-range bytes read as 0 and never
+        // sampled) are both requested before either is used, so the two round trips overlap
+        const uint8_t* row = lvl + (long long)(y + vrow[0]) * G.pitch;
+        uint32_t w[9];
+        if (raw_dw) {  // 2 x dwordx4 + 1 dword (global loads need only dword alignment)
+            const uint4 A = *reinterpret_cast<const uint4*>(row + xa);
+            const uint4 B = *reinterpret_cast<const uint4*>(row + xa + 16);
+            w[0] = A.x; w[1] = A.y; w[2] = A.z; w[3] = A.w;
+            w[4] = B.x; w[5] = B.y; w[6] = B.z; w[7] = B.w;
+            w[8] = *reinterpret_cast<const uint32_t*>(row + xa + 32);
+        } else {
 #pragma unroll
             for (int i = 0; i < 9; ++i) {
-                {
-                    const uint8_t* q = row + xa + 4 * i;
-                    w[i] = (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16) |
-                           ((uint32_t)q[3] << 24);
-                }
+                const uint8_t* q = row + xa + 4 * i;
+                w[i] = (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16) | ((uint32_t)q[3] << 24);
             }
+        }
+        const int pitch = G.bpitch;
+        const int xb = (x - kOdPatchR) & ~3;
+        const int pofs = (y - kOdPatchR) * pitch + xb;
+        constexpr int kPatchChunks = kOdPatchRows * 3, kPatchIt = (kPatchChunks + kOdLanes - 1) / kOdLanes;
+        uint4 pv[kPatchIt];
+#pragma unroll
+        for (int it = 0; it < kPatchIt; ++it) {
+            const int c = sub + it * kOdLanes;
+            const int r = c / 3, part = c - 3 * r;
+            if (c < kPatchChunks) {
+                const auto v = __builtin_amdgcn_raw_buffer_load_b128(brs, pofs + r * pitch + 16 * part, 0, 0);
+                pv[it] = make_uint4(v[0], v[1], v[2], v[3]);
             }
+        }
+        // IC_Angle moments (ORBextractor_old.cc:78-105): the row window is byte-aligned with
+        // v_alignbyte, masked to the disc, then
+        //   s = sum of bytes (v_sad_u8), sum u*p = dot4(bytes, {4i..4i+3}) - 15 s
+        {
             uint32_t sacc = 0, uacc = 0;
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
@@ -1097,36 +1125,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
                 const uint32_t wu = (uint32_t)(4 * i) * 0x01010101u + 0x03020100u;
                 uacc = __builtin_amdgcn_udot4(b, wu, uacc, false);
             }
-            m10 += (int)uacc - 15 * (int)sacc;
-            m01 += vrow[h] * (int)sacc;
+            m10 = (int)uacc - 15 * (int)sacc;
+            m01 = vrow[0] * (int)sacc;
         }
-#pragma unroll
-        for (int o = kOdLanes / 2; o >= 1; o >>= 1) {
-            m10 += __shfl_xor(m10, o, kOdLanes);
-            m01 += __shfl_xor(m01, o, kOdLanes);
-        }
+        // sums over the keypoint's 32 lanes: xor 1, xor 2 (quad_perm), the 8- and 16-lane mirrors
+        // (DPP, no LDS round trip), then lane ^ 16 (ds_swizzle)
+        m10 = od_sum32(m10);
+        m01 = od_sum32(m01);
         const float angle = fast_atan2_deg((float)m01, (float)m10);
         // computeOrbDescriptor (:108-148): lane `sub` makes bits [sub * kOdPairs, + kOdPairs)
         const float factorPI = (float)(3.14159265358979323846 / 180.0);
         const float ang = angle * factorPI;
         float sn, ca;  // std::sin(float) / std::cos(float) (:114-115): libm sinf / cosf
         libm_sincosf(ang, &sn, &ca);
-        // the 37 x 37 blurred patch (rows y-18..y+18 from the dword at or below x-18) goes to
-        // LDS with 16-byte buffer loads (out-of-range bytes read as 0 and are never sampled),
-        // then every sample is an LDS byte read: 4 vector-memory instructions per lane
-        // instead of one scattered byte load per sample
-        const int pitch = G.bpitch;
-        const int xb = (x - kOdPatchR) & ~3;
-        const int pofs = (y - kOdPatchR) * pitch + xb;
+        // the patch to LDS: every sample is then an LDS byte read (4 vector-memory instructions
+        // per lane instead of one scattered byte load per sample)
         uint8_t* pt = patch[grp];
 #pragma unroll
-        for (int it = 0; it < (kOdPatchRows * 3 + kOdLanes - 1) / kOdLanes; ++it) {
+        for (int it = 0; it < kPatchIt; ++it) {
             const int c = sub + it * kOdLanes;
-            if (c < kOdPatchRows * 3) {
-                const int r = c / 3, part = c - 3 * r;
-                const auto v = __builtin_amdgcn_raw_buffer_load_b128(brs, pofs + r * pitch + 16 * part, 0, 0);
-                *reinterpret_cast<uint4*>(pt + r * kOdPatchPitch + 16 * part) = make_uint4(v[0], v[1], v[2], v[3]);
-            }
+            const int r = c / 3, part = c - 3 * r;
+            if (c < kPatchChunks) *reinterpret_cast<uint4*>(pt + r * kOdPatchPitch + 16 * part) = pv[it];
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the group's own lanes read it
         __builtin_amdgcn_wave_barrier();

@@ -260,6 +260,10 @@ int set_geometry(orbgpu_ctx* c, int w, int h) {
     long long pyr_off[kMaxLevels] = {}, blur_off[kMaxLevels] = {};
     long long pyr = 0, blr = 0, ck = 0, ows = 0;
     int cc = 0, kpo = 0, cell_first = 0, tile_first = 0, od_first = 0;
+    // keypoints per k_orient_desc workgroup: kOdKpBlock per pass, od_iters passes (the key of the
+    // next pass is prefetched during the current one; the table setup is paid once)
+    const char* odi = getenv("ORBGPU_OD_ITERS");
+    const int od_per_block = kOdKpBlock * std::max(1, odi ? atoi(odi) : 4);
     for (int l = 0; l < L; ++l) {
         LevelGeom& G = A.lv[l];
         G.w = cv_round_f((float)w * c->inv_scale[l]);   // ComputePyramid :1336
@@ -315,7 +319,7 @@ int set_geometry(orbgpu_ctx* c, int w, int h) {
         G.tiles_y = (G.h + 31) / 32;
         G.tile_first = tile_first;
         tile_first += G.tiles_x * G.tiles_y;
-        G.od_blocks = std::max(1, (G.N + 16 + kOdKpBlock - 1) / kOdKpBlock);  // k_orient_desc blocks
+        G.od_blocks = std::max(1, (G.N + 16 + od_per_block - 1) / od_per_block);  // k_orient_desc blocks
         G.od_first = od_first;
         od_first += G.od_blocks;
         G.area2 = 0;
