@@ -77,6 +77,7 @@ struct BatchArgs {
     // levels [oct_split, nlevels) run in a second k_octree launch of kOctSmallThreads-thread
     // workgroups with their own, smaller LDS layout (more workgroups per CU for the short levels)
     int oct_split;
+    int oct_split_min_images;        // below this many images per launch: every level at 512 threads
     int oct2_threads;                // 128 or 256
     int oct2_lds_nodes, oct2_lds_bytes, oct2_nq_off, oct2_lds_keys;
     int oct_may_retry;               // some level can exceed the LDS instantiation of k_octree
@@ -168,6 +169,7 @@ constexpr int kOdKpBlock = 8;  // keypoints per k_orient_desc block (256 threads
 
 constexpr int kOctLdsKeys = 16384;  // per-key node labels (u16) kept in LDS up to this many keys
 constexpr int kOctSmallThreads = 256;  // default workgroup size of the short-level k_octree launch
+constexpr int kOctSmallMinImages = 32;  // launches with fewer images keep the 512-thread shape
 constexpr int kOctSmallLds = 36 * 1024;  // default dynamic LDS of that launch: 4 workgroups per CU with the static part
 
 // LDS layout of one k_octree launch

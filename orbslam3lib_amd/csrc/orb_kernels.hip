@@ -1634,7 +1634,7 @@ hipError_t launch_octree(const BatchArgs& a, hipStream_t s) {
             if (e != hipSuccess) return e;
         }
     }
-    const int split = std::min(a.oct_split, a.nlevels);
+    const int split = a.nimages < a.oct_split_min_images ? a.nlevels : std::min(a.oct_split, a.nlevels);
     if (split > 0)
         hipLaunchKernelGGL(k_octree<512>, dim3(a.nimages, split), dim3(512), a.oct_lds_bytes, s, a, 0,
                            OctCfg{a.oct_nq_off, a.oct_lds_nodes, kOctLdsKeys});

@@ -434,12 +434,18 @@ int set_geometry(orbgpu_ctx* c, int w, int h) {
             A.oct2_lds_bytes = (A.oct2_nq_off + 2 * A.oct2_lds_keys + 15) & ~15;
             return A.oct2_lds_keys >= 1024;
         };
+        // Default: every level in the small shape when all of them fit it (640x480-class
+        // pyramids), else every level in the 512-thread shape: a partial split runs the two
+        // launches back to back and measured slower (C5: 90 vs 98 Mfeatures/s).  Launches of
+        // fewer than kOctSmallMinImages images stay in the 512-thread shape too (latency, not
+        // occupancy, bounds them: C4 0.31 vs 0.26 ms per pair).  ORBGPU_OCT_SPLIT forces a split.
         if (const char* e = getenv("ORBGPU_OCT_SPLIT")) {
             A.oct_split = std::max(0, std::min(L, atoi(e)));
             if (A.oct_split < L && !layout(A.oct_split)) A.oct_split = L;
+            A.oct_split_min_images = 0;
         } else {
-            A.oct_split = 0;
-            while (A.oct_split < L && !layout(A.oct_split)) ++A.oct_split;
+            A.oct_split = layout(0) ? 0 : L;
+            A.oct_split_min_images = kOctSmallMinImages;
         }
     }
     // a level misses k_octree (labels in LDS or in the workspace) only if its node capacity or

@@ -230,14 +230,15 @@ def test_gpu_matches_golden_fixtures():
         np.testing.assert_array_equal(a, g[key])
 
 
-@pytest.mark.parametrize("env", [{"ORBGPU_OCT_SPLIT": "8"}, {"ORBGPU_OCT_SPLIT": "3"},
-                                 {"ORBGPU_OCT_SMALL_THREADS": "128"},
+@pytest.mark.parametrize("env", [{"ORBGPU_OCT_SPLIT": "0"}, {"ORBGPU_OCT_SPLIT": "3"},
+                                 {"ORBGPU_OCT_SPLIT": "0", "ORBGPU_OCT_SMALL_THREADS": "128"},
                                  {"ORBGPU_OCT_SMALL_LDS": "65536", "ORBGPU_OCT_SPLIT": "1"}])
 def test_octree_launch_shapes(oracle, monkeypatch, env):
     """k_octree's two launch shapes: 512-thread workgroups with the full LDS layout for levels
-    [0, split) and 256/128-thread workgroups with the short layout for the rest (default at
-    640x480: split 0, most labels in the global workspace).  Every split, both small workgroup
-    sizes and a layout with all labels in LDS give the oracle's keypoints (batch of 4 frames)."""
+    [0, split) and 256/128-thread workgroups with the small layout for the rest (default: every
+    level small for 640x480-class launches of >= 32 images, most labels in the global workspace;
+    the 128-pair bench batch of test_batch_edges runs that).  Forced splits on a 4-frame batch,
+    both small workgroup sizes and a layout with all labels in LDS give the oracle's keypoints."""
     import orbslam3lib_amd as og
     for k, v in env.items():
         monkeypatch.setenv(k, v)
