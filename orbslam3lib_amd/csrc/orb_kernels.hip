@@ -738,7 +738,7 @@ __global__ __launch_bounds__(256) void k_pyramid(BatchArgs a, int S, int tab) {
 constexpr int kFastThreads = 128;  // one workgroup (2 waves) per cell
 
 template <int CP>
-__global__ __launch_bounds__(kFastThreads) void k_fast_cells(BatchArgs a, int cell0) {
+__global__ __launch_bounds__(kFastThreads) void k_fast_cells(BatchArgs a, int cell0, uint32_t ncell_magic) {
     constexpr int kList = cell_list_cap<CP>();
     __shared__ __attribute__((aligned(16))) uint8_t T[CP * CP];
     __shared__ __attribute__((aligned(16))) uint8_t M[CP * CP];  // 16-byte rows when CP % 16 == 0
@@ -746,26 +746,27 @@ __global__ __launch_bounds__(kFastThreads) void k_fast_cells(BatchArgs a, int ce
     __shared__ int32_t wcnt[kFastThreads / 64];
     __shared__ int scratch[16];
     const int wg = xcd_remap(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * gridDim.y);
-    const int img = a.img0 + wg / gridDim.x;
-    const int gcell = cell0 + wg % gridDim.x;  // flattened over the levels
-    int l = 0;
-    while (l + 1 < a.nlevels && gcell >= a.lv[l + 1].cell_first) ++l;
+    // wg / gridDim.x by the host's magic multiplier (exact for wg < 2^32 / gridDim.x)
+    const int irel = gridDim.x == 1 ? wg : (int)__umulhi((uint32_t)wg, ncell_magic);
+    const int img = a.img0 + irel;
+    const int gcell = cell0 + (wg - irel * (int)gridDim.x);  // flattened over the levels
+    // the cell's record (host: the cell loop's geometry, :807-821)
+    const int4 e0 = a.rtab[a.fast_tab_off + 2 * gcell];
+    const int4 e1 = a.rtab[a.fast_tab_off + 2 * gcell + 1];
+    const int l = e0.x;
     const LevelGeom& G = a.lv[l];
-    const int cell = gcell - G.cell_first;
-    const int ci = cell / G.nCols, cj = cell % G.nCols;
-    int32_t* cnt_out = a.cellcnt + (long long)img * a.cellcnt_img_stride + G.cellcnt_off + cell;
-    uint32_t* key_out = a.cellkeys + (long long)img * a.cellkeys_img_stride + G.cellkey_off +
-                        (long long)cell * G.cell_cap;
+    int32_t* cnt_out = a.cellcnt + (long long)img * a.cellcnt_img_stride + e1.x;
+    uint32_t* key_out = a.cellkeys + (long long)img * a.cellkeys_img_stride + e1.y;
     CellGeom g;
-    g.iniY = kMinBorder + ci * G.hCell;
-    g.iniX = kMinBorder + cj * G.wCell;
+    g.iniX = e0.y;
+    g.iniY = e0.z;
     g.minBorder = kMinBorder;
-    if (g.iniY >= G.maxBY - 3 || g.iniX >= G.maxBX - 6) {  // :812, :821
+    if (e1.z) {  // :812, :821
         if (threadIdx.x == 0) *cnt_out = 0;
         return;
     }
-    g.rows = min(g.iniY + G.hCell + 6, G.maxBY) - g.iniY;
-    g.cols = min(g.iniX + G.wCell + 6, G.maxBX) - g.iniX;
+    g.rows = e0.w & 0xFFFF;
+    g.cols = e0.w >> 16;
     const bool dword_ok = ((G.pitch | G.img_stride) & 3) == 0;
     const int sh = dword_ok ? (g.iniX & 3) : 0;
     const uint8_t* base = a.lvl_base[l] + (long long)img * G.img_stride;
@@ -1621,9 +1622,11 @@ hipError_t launch_fast_cells(const BatchArgs& a, int tile, hipStream_t s) {
         return hipGetLastError();
     }
     const dim3 grid(c1 - c0, a.nimages), block(kFastThreads);
-    if (tile == kCellPitchTiny) hipLaunchKernelGGL(k_fast_cells<kCellPitchTiny>, grid, block, 0, s, a, c0);
-    else if (tile == kCellPitchSmall) hipLaunchKernelGGL(k_fast_cells<kCellPitchSmall>, grid, block, 0, s, a, c0);
-    else hipLaunchKernelGGL(k_fast_cells<kCellMax>, grid, block, 0, s, a, c0);
+    const uint32_t d = (uint32_t)(c1 - c0);
+    const uint32_t magic = d > 1 ? 0xFFFFFFFFu / d + 1u : 0u;  // ceil(2^32 / d) for d >= 2
+    if (tile == kCellPitchTiny) hipLaunchKernelGGL(k_fast_cells<kCellPitchTiny>, grid, block, 0, s, a, c0, magic);
+    else if (tile == kCellPitchSmall) hipLaunchKernelGGL(k_fast_cells<kCellPitchSmall>, grid, block, 0, s, a, c0, magic);
+    else hipLaunchKernelGGL(k_fast_cells<kCellMax>, grid, block, 0, s, a, c0, magic);
     return hipGetLastError();
 }
 hipError_t launch_octree(const BatchArgs& a, hipStream_t s) {

@@ -459,6 +459,23 @@ int set_geometry(orbgpu_ctx* c, int w, int h) {
     A.oct_force_retry = getenv("ORBGPU_OCT_GENERIC") ? 1 : 0;  // diagnostics / tests
     if (A.oct_force_retry) A.oct_may_retry = 1;
     A.total_cells = cell_first;
+    // k_fast_cells per-cell records, two int4 per flattened cell: {level, iniX, iniY, rows | cols
+    // << 16} and {cell-count index, cell-key index, skip, 0} (the cell loop's :807-821 geometry).
+    // One scalar load replaces each workgroup's level search and cell-grid divisions.
+    A.fast_tab_off = (int)c->rtab_host.size();
+    for (int l = 0; l < L; ++l) {
+        const LevelGeom& G = A.lv[l];
+        for (int cell = 0; cell < G.ncells; ++cell) {
+            const int ci = cell / G.nCols, cj = cell % G.nCols;
+            const int iniY = kMinBorder + ci * G.hCell, iniX = kMinBorder + cj * G.wCell;
+            const int skip = (iniY >= G.maxBY - 3 || iniX >= G.maxBX - 6) ? 1 : 0;  // :812, :821
+            const int rows = skip ? 0 : std::min(iniY + G.hCell + 6, G.maxBY) - iniY;
+            const int cols = skip ? 0 : std::min(iniX + G.wCell + 6, G.maxBX) - iniX;
+            c->rtab_host.push_back(make_int4(l, iniX, iniY, rows | (cols << 16)));
+            c->rtab_host.push_back(make_int4(G.cellcnt_off + cell, (int)(G.cellkey_off + (long long)cell * G.cell_cap),
+                                             skip, 0));
+        }
+    }
     // FAST LDS tiles: the 48-byte one for the leading levels whose cell ROIs (+3 alignment
     // bytes) fit it, then the 64-byte one; cells grow with the level (fewer, wider cells), so the
     // rest use the 80-byte one
