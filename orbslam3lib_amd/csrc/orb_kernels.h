@@ -69,6 +69,7 @@ struct BatchArgs {
     const int32_t* laps;             // [img][2]
     int total_cells, total_tiles, total_od_blocks;
     int fast_tab_off;  // rtab index of k_fast_cells' per-cell records (2 int4 per flattened cell)
+    int od_tab_off;    // rtab index of k_orient_desc's per-block records {level, 0, 0, 0}
     int fast_split48;  // levels [0, fast_split48) run the 48-byte FAST tile,
     int fast_split;    // [fast_split48, fast_split) the 64-byte one, the rest the 80-byte one
     unsigned long long* octdbg;      // diagnostic: [img][kMaxLevels][8] phase clocks, or null

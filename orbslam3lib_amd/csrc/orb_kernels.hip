@@ -1013,13 +1013,16 @@ __device__ inline int od_sum32(int v) {
     return v;
 }
 
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k_orient_desc(BatchArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k_orient_desc(BatchArgs a,
+                                                                                          uint32_t nblk_magic) {
     // per keypoint group: the blurred patch around the keypoint, staged with 16-byte loads
     __shared__ __attribute__((aligned(16))) uint8_t patch[kOdKpBlock][kOdPatchRows * kOdPatchPitch];
     const int wg = xcd_remap(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * gridDim.y);
-    const int img = a.img0 + wg / gridDim.x, bx = wg % gridDim.x;
-    int l = 0;
-    while (l + 1 < a.nlevels && bx >= a.lv[l + 1].od_first) ++l;
+    // wg / gridDim.x by the host's magic multiplier; the block's level from a host record (no
+    // level search with dependent kernarg loads)
+    const int irel = gridDim.x == 1 ? wg : (int)__umulhi((uint32_t)wg, nblk_magic);
+    const int img = a.img0 + irel, bx = wg - irel * (int)gridDim.x;
+    const int l = a.rtab[a.od_tab_off + bx].x;
     const LevelGeom& G = a.lv[l];
     const int sub = threadIdx.x % kOdLanes, grp = threadIdx.x / kOdLanes;
     const int count = a.lvlcnt[img * kMaxLevels + l];
@@ -1657,7 +1660,9 @@ hipError_t launch_octree(const BatchArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 hipError_t launch_orient_desc(const BatchArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(k_orient_desc, dim3(a.total_od_blocks, a.nimages), dim3(256), 0, s, a);
+    const uint32_t d = (uint32_t)a.total_od_blocks;
+    const uint32_t magic = d > 1 ? 0xFFFFFFFFu / d + 1u : 0u;  // ceil(2^32 / d) for d >= 2
+    hipLaunchKernelGGL(k_orient_desc, dim3(a.total_od_blocks, a.nimages), dim3(256), 0, s, a, magic);
     return hipGetLastError();
 }
 hipError_t launch_finalize(const BatchArgs& a, hipStream_t s) {

@@ -494,6 +494,9 @@ int set_geometry(orbgpu_ctx* c, int w, int h) {
     }
     A.total_tiles = tile_first;
     A.total_od_blocks = od_first;
+    A.od_tab_off = (int)c->rtab_host.size();
+    for (int l = 0; l < L; ++l)
+        for (int b = 0; b < A.lv[l].od_blocks; ++b) c->rtab_host.push_back(make_int4(l, b, 0, 0));
     for (int l = 0; l < L; ++l) {
         if (l > 0) A.lv[l].img_stride = c->pyr_img;
         A.lv[l].bimg_stride = c->blur_img;
