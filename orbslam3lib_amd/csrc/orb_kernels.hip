@@ -1458,11 +1458,16 @@ __device__ __attribute__((always_inline)) inline void knn2_mfma_block(
         const int row = min(tile * 32 + er, nt - 1);
         return *reinterpret_cast<const uint32_t*>(t + (long long)row * 32 + 4 * ed);
     };
+    // the 8 threads of a row write 256 contiguous bytes as two 16-byte stores each; threads
+    // ed >= 4 store their upper half first, so each store instruction's 8 chunks start on 8
+    // distinct 4-bank boundaries (ds_write_b128 banks: (a / 4) mod 32) instead of 4 twice
+    const bool kswap = ed >= 4;
     auto store_expanded = [&](int buf, uint32_t w) __attribute__((always_inline)) {
         uint8_t* dst = lds + buf * (32 * kKnnPitch) + er * kKnnPitch + 32 * ed;
-        const knn_v4i lo = knn_expand16(w & 0xFFFFu), hi = knn_expand16(w >> 16);
-        *reinterpret_cast<knn_v4i*>(dst) = lo;
-        *reinterpret_cast<knn_v4i*>(dst + 16) = hi;
+        const uint32_t ws = kswap ? __builtin_amdgcn_alignbit(w, w, 16) : w;  // halves swapped
+        const knn_v4i first = knn_expand16(ws & 0xFFFFu), second = knn_expand16(ws >> 16);
+        *reinterpret_cast<knn_v4i*>(dst + (kswap ? 16 : 0)) = first;
+        *reinterpret_cast<knn_v4i*>(dst + (kswap ? 0 : 16)) = second;
     };
     // packed train words run two tiles ahead of the MFMAs (one in LDS, one in flight): the word
     // of tile u lives in pk[u & 1]; loads are unconditional (clamped rows) so waits stay counted
