@@ -399,7 +399,12 @@ def main():
         if "GBps" in r:
             roof = {"kernel": dom, "bound": "hbm", "achieved": r["GBps"], "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": r["frac_hbm"], "traffic": traffic,
-                    "bytes_per_launch": r["bytes_per_launch"], "avg_us": r["avg_us"]}
+                    "bytes_per_launch": r["bytes_per_launch"], "avg_us": r["avg_us"],
+                    "timed_launches": r.get("launches"),
+                    # the same kernel alone on the GPU (serialized whole-batch pass), for the
+                    # rocprofv3 cross-check: no other stream's kernels beside it
+                    "serialized_avg_us": round(stages_all[dom][0] / stages_all[dom][1] * 1e3, 2)
+                    if stages_all.get(dom, (0, 0))[1] else None}
         elif "Tops_i8" in r:
             roof = {"kernel": dom, "bound": "mfma_i8", "achieved": r["Tops_i8"], "peak": MFMA_I8_PEAK_TOPS,
                     "unit": "Tops/s", "frac": r["frac_mfma_i8"], "traffic": traffic, "avg_us": r["avg_us"]}

@@ -12,10 +12,40 @@ chunks = int(sys.argv[4]) if len(sys.argv) > 4 else 3  # ORBGPU_STREAMS default
 name = bench["roofline"]["kernel"]
 rows = [r for r in csv.DictReader(open(sys.argv[2])) if name in r["Kernel_Name"].replace("void ", "")]
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-# the headline batch's launches share the first launch's grid (the side-line configs differ)
-rows = [r for r in rows if r["Grid_Size_X"] == rows[0]["Grid_Size_X"] and r["Grid_Size_Y"] == rows[0]["Grid_Size_Y"]]
-d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rows]
-timed = d[-steps * chunks:]
+# the headline steps launch the kernel on the chunk streams with the chunk grids (one grid per
+# level and chunk size for a per-level kernel); the bench's serialized profiling pass (whole-batch
+# grids) and the side-line configs (other grids) interrupt them: the timed region is the end of
+# the longest run of launches whose grids occur among the first step's
+grid = lambda r: (r["Grid_Size_X"], r["Grid_Size_Y"], r["Grid_Size_Z"])
+first = {grid(r) for r in rows[:24]}
+runs, cur = [], []
+for r in rows:
+    if grid(r) in first:
+        cur.append(r)
+    else:
+        if cur:
+            runs.append(cur)
+        cur = []
+if cur:
+    runs.append(cur)
+head = max(runs, key=len)
+# the serialized pass (whole-batch grids, the kernel alone on the GPU) is the first run of other
+# grids after the warm-up steps
+ser, cur, seen_head = [], [], False
+for r in rows:
+    if grid(r) in first:
+        if cur:
+            break
+        continue
+    cur.append(r)
+ser = cur
+d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in head]
+n = bench["roofline"].get("timed_launches") or steps * chunks
+timed = d[-n:]
+ds = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in ser]
 print(json.dumps({"kernel": name, "bench_avg_us": bench["roofline"]["avg_us"],
                   "rocprof_timed_region_avg_us": round(sum(timed) / len(timed), 2),
-                  "rocprof_all_launches_avg_us": round(sum(d) / len(d), 2), "launches": len(d)}))
+                  "rocprof_headline_launches_avg_us": round(sum(d) / len(d), 2), "launches": len(d),
+                  "bench_serialized_avg_us": bench["roofline"].get("serialized_avg_us"),
+                  "rocprof_serialized_avg_us": round(sum(ds) / len(ds), 2) if ds else None,
+                  "serialized_launches": len(ds)}))
