@@ -225,7 +225,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--pairs", type=int, default=128, help="stereo pairs per GPU per step")
+    ap.add_argument("--pairs", type=int, default=256, help="stereo pairs per GPU per step")
     ap.add_argument("--unique-pairs", type=int, default=16,
                     help="distinct synthetic pairs generated per rank (tiled to --pairs)")
     ap.add_argument("--width", type=int, default=640)

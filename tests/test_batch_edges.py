@@ -116,12 +116,13 @@ def test_c5_batch_16_pairs(oracle):
         _same_knn(be.matches(p), oracle.knn2(res[2 * p][1], res[2 * p + 1][1]), "pair %d" % p)
 
 
-def test_bench_batch_128_pairs(oracle):
-    """bench.py's headline batch exactly: 128 pairs (16 distinct seeded pairs tiled), 256
-    images, 4 chunk streams, the staggered first step and the steady state after it."""
+@pytest.mark.parametrize("P", [128, 256])
+def test_bench_batch_pairs(oracle, P):
+    """bench.py's headline batch exactly (256 pairs since round 2; 128 in round 1): 16 distinct
+    seeded pairs tiled, 3 chunk streams, the staggered first step and the steady state after it."""
     import orbslam3lib_amd as og
     from orbslam3lib_amd.dist import pair_seed_base
-    P, U, W, H = 128, 16, 640, 480
+    U, W, H = 16, 640, 480
     uniq = [synth.stereo_pair(H, W, pair_seed_base(0) + i) for i in range(U)]
     imgs = np.empty((2 * P, H, W), np.uint8)
     for p in range(P):

@@ -1,10 +1,10 @@
-"""Runs a few bench-shaped steps (128 stereo pairs, extract + kNN2) for rocprofv3 passes."""
+"""Runs a few bench-shaped steps (256 stereo pairs, extract + kNN2) for rocprofv3 passes."""
 import os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np
 import orbslam3lib_amd as og
 from orbslam3lib_amd import synth
-P = int(os.environ.get("PAIRS", "128"))
+P = int(os.environ.get("PAIRS", "256"))  # bench.py --pairs default
 steps = int(os.environ.get("STEPS", "3"))
 U = 8
 uniq = [synth.stereo_pair(480, 640, i) for i in range(U)]
