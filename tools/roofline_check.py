@@ -17,7 +17,9 @@ rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 # grids) and the side-line configs (other grids) interrupt them: the timed region is the end of
 # the longest run of launches whose grids occur among the first step's
 grid = lambda r: (r["Grid_Size_X"], r["Grid_Size_Y"], r["Grid_Size_Z"])
-first = {grid(r) for r in rows[:24]}
+n_timed = bench["roofline"].get("timed_launches") or steps * chunks
+per_chunk_step = max(1, n_timed // (steps * chunks))  # launches per chunk per step (levels)
+first = {grid(r) for r in rows[:bench.get("warmup", 3) * chunks * per_chunk_step]}  # warm-up steps
 runs, cur = [], []
 for r in rows:
     if grid(r) in first:
@@ -40,8 +42,7 @@ for r in rows:
     cur.append(r)
 ser = cur
 d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in head]
-n = bench["roofline"].get("timed_launches") or steps * chunks
-timed = d[-n:]
+timed = d[-n_timed:]
 ds = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in ser]
 print(json.dumps({"kernel": name, "bench_avg_us": bench["roofline"]["avg_us"],
                   "rocprof_timed_region_avg_us": round(sum(timed) / len(timed), 2),
