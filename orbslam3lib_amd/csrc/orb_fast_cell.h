@@ -78,7 +78,12 @@ __device__ inline uint32_t fw_compass4(uint32_t C, uint32_t Cm, uint32_t Cp, uin
                                                       __builtin_elementwise_max(p4, p12));
         // dk < v - t  <=>  sat(lo - dk) > 0;   bk > v + t  <=>  sat(bk - hi) > 0
         const fw_u16x2 r = __builtin_elementwise_sub_sat(lo, dk) | __builtin_elementwise_sub_sat(bk, hi);
-        return fw_as32(__builtin_elementwise_min(r, (fw_u16x2)(1)));
+        // min(r, 1) per half as one v_pk_min_u16 (left to itself the compiler rewrites it as two
+        // compares, two selects and a v_perm); the constant in a register: an inline constant of
+        // a packed op reaches the high half only through op_sel_hi
+        uint32_t one;
+        asm("v_pk_min_u16 %0, %1, %2" : "=v"(one) : "v"(fw_as32(r)), "s"(0x00010001u));
+        return one;
     };
     const uint32_t e = test(0x0c020c00u), o = test(0x0c030c01u);  // pixels (0, 2) and (1, 3)
     const uint32_t comb = e | (o << 1);                           // halves: p0 | p1 << 1, p2 | p3 << 1
@@ -193,24 +198,28 @@ __host__ __device__ int fast_cell_detect(Pol& p, int sh, const CellGeom& g, int 
             constexpr int RW = CP / 4;
             const uint32_t* T32 = reinterpret_cast<const uint32_t*>(T);
             const uint32_t tt = (uint32_t)t * 0x00010001u;
+            // detection pixels of the first / last dword group of a row (wave-uniform masks)
+            const uint32_t first4 = 0xFu & ~((1u << (xs - 4 * g0)) - 1u);
+            const uint32_t last4 = (1u << (xe - 4 * (g0 + ng - 1))) - 1u;
+            auto rank = [](uint64_t b) {  // set lanes of b below this lane
+                return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32),
+                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
+            };
             for (int base = j0; base < j1; base += L) {
                 const int i = base + lane;
                 uint32_t m4 = 0;
                 int o = 0;
                 if (i < j1) {
                     const int r = (int)(((float)i + 0.5f) * inv_ng);  // exact: i < 69 * 19
-                    const int gg = g0 + (i - r * ng);
-                    const int dw = (r + 3) * RW + gg;
+                    const int q = i - r * ng;
+                    const int dw = (r + 3) * RW + g0 + q;
                     m4 = fw_compass4(T32[dw], T32[dw - 1], T32[dw + 1], T32[dw - 3 * RW], T32[dw + 3 * RW], tt);
-                    const int x0 = 4 * gg;
-                    const int lo_cut = xs - x0 > 0 ? xs - x0 : 0;
-                    const int hi_cut = xe - x0 < 4 ? xe - x0 : 4;
-                    m4 &= ((1u << hi_cut) - 1u) & ~((1u << lo_cut) - 1u);
-                    o = (r + 3) * CP + x0;
+                    m4 &= (q == 0 ? first4 : 0xFu) & (q == ng - 1 ? last4 : 0xFu);
+                    o = 4 * dw;
                 }
                 const int c = __builtin_popcount(m4);
                 const uint64_t b0 = p.ballot(c & 1), b1 = p.ballot(c & 2), b2 = p.ballot(c & 4);
-                int pos = na + p.popc64(b0 & lt) + 2 * p.popc64(b1 & lt) + 4 * p.popc64(b2 & lt);
+                int pos = na + rank(b0) + 2 * rank(b1) + 4 * rank(b2);
 #pragma unroll
                 for (int k = 0; k < 4; ++k)
                     if ((m4 >> k) & 1u) list[pos++] = (uint16_t)(o + k);
