@@ -442,15 +442,15 @@ struct BrSmem {
 // Blur tile k of level s = l - 1 of image img, and (resize) the level-l outputs it owns.  kAux:
 // cache policy of the window loads (sc1 where level s was written by this launch).
 template <int kAux>
-__device__ inline void br_tile(const BatchArgs& a, int l, bool resize, int img, int k, BrSmem& sm) {
+__device__ inline void br_tile(const BatchArgs& a, int l, bool resize, int img, int by, int bx, BrSmem& sm) {
     constexpr int IW = kBlurTW + 32, IH = kBlurTH + 8, IWQ = IW / 16;
     constexpr int NCH = (IH * IWQ + 255) / 256;
     const LevelGeom& S = a.lv[l - 1];
     const LevelGeom& G = a.lv[resize ? l : l - 1];
     BlurTile bt;
     bt.l = l - 1;
-    bt.ty0 = (k / S.tiles_x) * kBlurTH;
-    bt.tx0 = (k % S.tiles_x) * kBlurTW;
+    bt.ty0 = by * kBlurTH;
+    bt.tx0 = bx * kBlurTW;
     bt.src = a.lvl_base[l - 1] + (long long)img * S.img_stride;
     bt.dst = a.blur_base[l - 1] + (long long)img * S.bimg_stride;
     uint4 pre[NCH];
@@ -464,7 +464,6 @@ __device__ inline void br_tile(const BatchArgs& a, int l, bool resize, int img, 
     if (resize) {
         const int* band_row = reinterpret_cast<const int*>(a.rtab) + G.band_row_off;
         const int* tile_quad = reinterpret_cast<const int*>(a.rtab) + G.tile_quad_off;
-        const int by = k / S.tiles_x, bx = k % S.tiles_x;
         r0 = band_row[by];
         q0 = tile_quad[bx];
         nr = min(band_row[by + 1] - r0, kBrMaxRows);
@@ -511,18 +510,29 @@ __device__ inline void br_tile(const BatchArgs& a, int l, bool resize, int img, 
     }
 }
 
-__global__ __launch_bounds__(256) void k_blur_resize(BatchArgs a, int l) {
+// n / d for a launch constant d by a mul-high with the host's magic ceil(2^32 / d) (d >= 2;
+// magic 0 stands for d == 1); exact for 0 <= n < 2^32 / d
+__device__ inline int div_magic(int n, uint32_t magic) {
+    return magic ? (int)__umulhi((uint32_t)n, magic) : n;
+}
+
+__global__ __launch_bounds__(256) void k_blur_resize(BatchArgs a, int l, uint32_t per_magic, uint32_t tx_magic) {
     __shared__ BrSmem sm;
     const LevelGeom& S = a.lv[l - 1];
     const int per = S.tiles_x * S.tiles_y;
     const int wg = xcd_remap(blockIdx.x, gridDim.x);  // an image's tiles on one XCD
-    br_tile<0>(a, l, true, a.img0 + wg / per, wg % per, sm);
+    const int irel = div_magic(wg, per_magic);
+    const int k = wg - irel * per;
+    const int by = div_magic(k, tx_magic), bx = k - by * S.tiles_x;
+    br_tile<0>(a, l, true, a.img0 + irel, by, bx, sm);
 }
 
 
 hipError_t launch_blur_resize(const BatchArgs& a, int l, hipStream_t s) {
     const LevelGeom& S = a.lv[l - 1];
-    hipLaunchKernelGGL(k_blur_resize, dim3(S.tiles_x * S.tiles_y * a.nimages), dim3(256), 0, s, a, l);
+    auto magic = [](uint32_t d) { return d > 1 ? 0xFFFFFFFFu / d + 1u : 0u; };  // exact for n < 2^32 / d
+    hipLaunchKernelGGL(k_blur_resize, dim3(S.tiles_x * S.tiles_y * a.nimages), dim3(256), 0, s, a, l,
+                       magic((uint32_t)(S.tiles_x * S.tiles_y)), magic((uint32_t)S.tiles_x));
     return hipGetLastError();
 }
 

@@ -10,6 +10,6 @@ for setting in "$@"; do
   mkdir -p $O
   env $setting timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $O -o run -- python3 tools/profile_batch.py > $O/log.txt 2>&1 || { tail $O/log.txt; exit 1; }
   f=$(find $O -name "run_kernel_stats.csv" | head -1)
-  echo "== $setting"; grep "$K" $f | cut -d, -f1-5
+  echo "== $setting"; python3 -c "import csv,sys;[print('%s  calls %s  avg_us %.1f' % (r['Name'][:70], r['Calls'], float(r['AverageNs']) / 1e3)) for r in csv.DictReader(open(sys.argv[1])) if sys.argv[2] in r['Name']]" $f "$K"
   i=$((i+1))
 done
