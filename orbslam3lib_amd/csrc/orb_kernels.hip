@@ -1444,6 +1444,19 @@ __device__ inline knn_v4i knn_expand16(uint32_t b) {  // 16 bits -> 16 int8
     return v;
 }
 
+// v_med3_i32 / v_max3_i32 as single instructions (the compiler's CSE of max(k1, x) otherwise
+// splits the pair into two v_max_i32 plus a v_med3_i32)
+__device__ inline int knn_med3_i32(int a, int b, int c) {
+    int r;
+    asm("v_med3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+__device__ inline int knn_max3_i32(int a, int b, int c) {
+    int r;
+    asm("v_max3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
 // One workgroup: queries [qb * 128, +128) of q against all nt train rows of t.
 __device__ __attribute__((always_inline)) inline void knn2_mfma_block(
     const uint8_t* q, int nq, const uint8_t* t, int nt, int qb, int32_t* i1, int32_t* d1, int32_t* i2,
@@ -1494,14 +1507,16 @@ __device__ __attribute__((always_inline)) inline void knn2_mfma_block(
         // two independent top-2 chains (even / odd accumulator rows), segment-local keys,
         // lexicographic max; the selection of tile ti - 1 runs while tile ti's MFMAs are in flight
         int ka1 = INT_MIN, ka2 = INT_MIN, kb1 = INT_MIN, kb2 = INT_MIN;
+        // two candidates per step and chain (keys are distinct): the new best is max3(k1, x, y),
+        // the new second max(k2, med3(k1, x, y)) -- 3 VALU per 2 candidates instead of 4
         auto select = [&](const knn_v16i& v) __attribute__((always_inline)) {
 #pragma unroll
-            for (int g = 0; g < 16; g += 2) {
-                const int x = v[g], y = v[g + 1];
-                ka2 = max(min(ka1, ka2), min(max(ka1, ka2), x));  // v_med3_i32
-                ka1 = max(ka1, x);
-                kb2 = max(min(kb1, kb2), min(max(kb1, kb2), y));
-                kb1 = max(kb1, y);
+            for (int g = 0; g < 16; g += 4) {
+                const int x0 = v[g], y0 = v[g + 1], x1 = v[g + 2], y1 = v[g + 3];
+                ka2 = max(ka2, knn_med3_i32(ka1, x0, y0));
+                ka1 = knn_max3_i32(ka1, x0, y0);
+                kb2 = max(kb2, knn_med3_i32(kb1, x1, y1));
+                kb1 = knn_max3_i32(kb1, x1, y1);
             }
         };
         // one tile: PAR = ti & 1 picks the LDS buffer, the accumulator and the packed word
