@@ -20,7 +20,9 @@ timeout -k 10 300 python bench.py > $O/bench.json 2> $O/bench.err
 echo bench-done
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 bench.py > $O/prof.log 2>&1
 echo prof-done
-python3 tools/roofline_check.py $O/bench.json $O/prof/run_kernel_trace.csv > $O/roofline_check.json
+grep '"metric"' $O/prof.log > $O/bench_profiled.json
+python3 tools/roofline_check.py $O/bench_profiled.json $O/prof/run_kernel_trace.csv > $O/roofline_check.json
+python3 tools/roofline_check.py $O/bench.json $O/prof/run_kernel_trace.csv > $O/roofline_check_unprofiled_run.json
 bash tools/pmc.sh $O/pmc > $O/pmc.log 2>&1
 python3 tools/pmc_summary.py $O/pmc > $O/pmc_summary.txt
 echo all-done
