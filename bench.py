@@ -44,16 +44,16 @@ def level_sizes(w, h, sf=1.2, L=8):
     return out
 
 
-def fast_split(w, h, sf=1.2, L=8, tile=64):
-    """First level at or after which the FAST cells stop fitting the `tile`-byte LDS tile
-    (orb_runtime.cpp rule: wCell + 9 <= tile and hCell + 6 <= tile, levels taken in order)."""
-    for l, (lw, lh) in enumerate(level_sizes(w, h, sf, L)):
+def fast_tiers(w, h, sf=1.2, L=8):
+    """FAST LDS tile per level (orb_runtime.cpp rule: the smallest of 48 / 64 / 80 bytes with
+    wCell + 9 <= tile and hCell + 6 <= tile, chosen per level)."""
+    out = []
+    for lw, lh in level_sizes(w, h, sf, L):
         W, H = np.float32(lw - 32), np.float32(lh - 32)
         nc, nr = int(W / np.float32(35)), int(H / np.float32(35))
         wc, hc = int(np.ceil(W / np.float32(nc))), int(np.ceil(H / np.float32(nr)))
-        if wc + 9 > tile or hc + 6 > tile:
-            return l
-    return L
+        out.append(next((t for t in (48, 64) if wc + 9 <= t and hc + 6 <= t), 80))
+    return out
 
 
 def algorithmic_bytes(w, h, L, nkp, sf=1.2, ncand=0.0):
@@ -63,15 +63,14 @@ def algorithmic_bytes(w, h, L, nkp, sf=1.2, ncand=0.0):
     blurred pyramid (its windows' pixel support); k_pyramid = pyramid + blur in one launch; the octree reads
     its 4-byte candidate keys and writes 4 bytes per kept keypoint."""
     A = [a * b for a, b in level_sizes(w, h, sf, L)]
-    k48 = fast_split(w, h, sf, L, 48)
-    k64 = max(k48, fast_split(w, h, sf, L, 64))
+    tier = fast_tiers(w, h, sf, L)
     return {
         "k_pyramid": sum(A[l - 1] + A[l] for l in range(1, L)) + 2 * sum(A),
         # one pass over level l-1 per launch: read it, write its blur and level l
         "k_blur_resize": sum(2 * A[l - 1] + A[l] for l in range(1, L)),
-        "k_fast_cells<48>": sum(A[:k48]),
-        "k_fast_cells<64>": sum(A[k48:k64]),
-        "k_fast_cells<80>": sum(A[k64:]),
+        "k_fast_cells<48>": sum(a for a, t in zip(A, tier) if t == 48),
+        "k_fast_cells<64>": sum(a for a, t in zip(A, tier) if t == 64),
+        "k_fast_cells<80>": sum(a for a, t in zip(A, tier) if t == 80),
         "k_blur": 2 * A[L - 1],  # the last level's blur (the others ride in k_blur_resize)
         # both planes read once (the 31-px moment discs and 37-px patches of ~2000 keypoints per
         # image cover nearly all of every level) + 48 B out per keypoint

@@ -70,8 +70,9 @@ struct BatchArgs {
     int total_cells, total_tiles, total_od_blocks;
     int fast_tab_off;  // rtab index of k_fast_cells' per-cell records (2 int4 per flattened cell)
     int od_tab_off;    // rtab index of k_orient_desc's per-block records {level, 0, 0, 0}
-    int fast_split48;  // levels [0, fast_split48) run the 48-byte FAST tile,
-    int fast_split;    // [fast_split48, fast_split) the 64-byte one, the rest the 80-byte one
+    int fast_n48;  // k_fast_cells records [0, fast_n48) run the 48-byte FAST tile,
+    int fast_n64;  // [fast_n48, fast_n64) the 64-byte one, the rest the 80-byte one (records are
+                   // grouped by tile, levels in order inside each group)
     unsigned long long* octdbg;      // diagnostic: [img][kMaxLevels][8] phase clocks, or null
     int oct_lds_nodes;               // node capacity of k_octree's dynamic LDS (0: all global)
     int oct_lds_bytes;

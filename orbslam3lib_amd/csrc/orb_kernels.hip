@@ -1629,8 +1629,7 @@ hipError_t launch_pyramid(const BatchArgs& a, int stripe_log2, hipStream_t s) {
     return hipGetLastError();
 }
 void fast_cell_range(const BatchArgs& a, int tile, int* c0, int* c1) {
-    auto first = [&](int l) { return l < a.nlevels ? a.lv[l].cell_first : a.total_cells; };
-    const int s48 = first(a.fast_split48), s64 = first(a.fast_split);
+    const int s48 = a.fast_n48, s64 = a.fast_n64;
     *c0 = tile == kCellPitchTiny ? 0 : tile == kCellPitchSmall ? s48 : s64;
     *c1 = tile == kCellPitchTiny ? s48 : tile == kCellPitchSmall ? s64 : a.total_cells;
 }

@@ -459,39 +459,50 @@ int set_geometry(orbgpu_ctx* c, int w, int h) {
     A.oct_force_retry = getenv("ORBGPU_OCT_GENERIC") ? 1 : 0;  // diagnostics / tests
     if (A.oct_force_retry) A.oct_may_retry = 1;
     A.total_cells = cell_first;
-    // k_fast_cells per-cell records, two int4 per flattened cell: {level, iniX, iniY, rows | cols
-    // << 16} and {cell-count index, cell-key index, skip, 0} (the cell loop's :807-821 geometry).
-    // One scalar load replaces each workgroup's level search and cell-grid divisions.
-    A.fast_tab_off = (int)c->rtab_host.size();
-    for (int l = 0; l < L; ++l) {
-        const LevelGeom& G = A.lv[l];
-        for (int cell = 0; cell < G.ncells; ++cell) {
-            const int ci = cell / G.nCols, cj = cell % G.nCols;
-            const int iniY = kMinBorder + ci * G.hCell, iniX = kMinBorder + cj * G.wCell;
-            const int skip = (iniY >= G.maxBY - 3 || iniX >= G.maxBX - 6) ? 1 : 0;  // :812, :821
-            const int rows = skip ? 0 : std::min(iniY + G.hCell + 6, G.maxBY) - iniY;
-            const int cols = skip ? 0 : std::min(iniX + G.wCell + 6, G.maxBX) - iniX;
-            c->rtab_host.push_back(make_int4(l, iniX, iniY, rows | (cols << 16)));
-            c->rtab_host.push_back(make_int4(G.cellcnt_off + cell, (int)(G.cellkey_off + (long long)cell * G.cell_cap),
-                                             skip, 0));
-        }
-    }
-    // FAST LDS tiles: the 48-byte one for the leading levels whose cell ROIs (+3 alignment
-    // bytes) fit it, then the 64-byte one; cells grow with the level (fewer, wider cells), so the
-    // rest use the 80-byte one
+    // FAST LDS tiles: each level takes the smallest tile its cell ROIs (+3 alignment bytes) fit:
+    // 48 bytes, else 64, else 80.  Cells grow as the levels shrink (fewer, wider cells) but not
+    // monotonically in both directions (640x480: level 6's cells are 51 rows tall, level 7's 42),
+    // so the tiers are chosen per level.  The one-wave FAST kernel finds a cell's level from the
+    // flattened index, so under ORBGPU_FAST_WAVE the tiers stay level prefixes.
     auto fits = [&](int l, int P) { return A.lv[l].wCell + 9 <= P && A.lv[l].hCell + 6 <= P; };
-    A.fast_split48 = 0;
-    while (A.fast_split48 < L && fits(A.fast_split48, kCellPitchTiny)) ++A.fast_split48;
-    A.fast_split = A.fast_split48;
-    while (A.fast_split < L && fits(A.fast_split, kCellPitchSmall)) ++A.fast_split;
-    if (const char* fp = getenv("ORBGPU_FAST_PITCH")) {  // diagnostics: force one tile size
+    int tier[kMaxLevels];
+    const bool prefix_tiers = getenv("ORBGPU_FAST_WAVE") != nullptr;
+    int min_tier = 0;
+    if (const char* fp = getenv("ORBGPU_FAST_PITCH")) {  // diagnostics: force the larger tiles
         const int P = atoi(fp);
-        if (P == kCellMax) A.fast_split48 = A.fast_split = 0;
-        if (P == kCellPitchSmall) {
-            A.fast_split48 = A.fast_split = 0;
-            while (A.fast_split < L && fits(A.fast_split, kCellPitchSmall)) ++A.fast_split;
-        }
+        min_tier = P == kCellMax ? 2 : P == kCellPitchSmall ? 1 : 0;
     }
+    for (int l = 0, floor_t = min_tier; l < L; ++l) {
+        int t = fits(l, kCellPitchTiny) ? 0 : fits(l, kCellPitchSmall) ? 1 : 2;
+        t = std::max(t, prefix_tiers ? floor_t : min_tier);
+        floor_t = t;
+        tier[l] = t;
+    }
+    // k_fast_cells per-cell records, two int4 per cell: {level, iniX, iniY, rows | cols << 16} and
+    // {cell-count index, cell-key index, skip, 0} (the cell loop's :807-821 geometry), grouped by
+    // tier.  One scalar load replaces each workgroup's level search and cell-grid divisions.
+    A.fast_tab_off = (int)c->rtab_host.size();
+    int tier_end[3] = {0, 0, 0}, nrec = 0;
+    for (int t = 0; t < 3; ++t) {
+        for (int l = 0; l < L; ++l) {
+            if (tier[l] != t) continue;
+            const LevelGeom& G = A.lv[l];
+            for (int cell = 0; cell < G.ncells; ++cell) {
+                const int ci = cell / G.nCols, cj = cell % G.nCols;
+                const int iniY = kMinBorder + ci * G.hCell, iniX = kMinBorder + cj * G.wCell;
+                const int skip = (iniY >= G.maxBY - 3 || iniX >= G.maxBX - 6) ? 1 : 0;  // :812, :821
+                const int rows = skip ? 0 : std::min(iniY + G.hCell + 6, G.maxBY) - iniY;
+                const int cols = skip ? 0 : std::min(iniX + G.wCell + 6, G.maxBX) - iniX;
+                c->rtab_host.push_back(make_int4(l, iniX, iniY, rows | (cols << 16)));
+                c->rtab_host.push_back(make_int4(G.cellcnt_off + cell,
+                                                 (int)(G.cellkey_off + (long long)cell * G.cell_cap), skip, 0));
+                ++nrec;
+            }
+        }
+        tier_end[t] = nrec;
+    }
+    A.fast_n48 = tier_end[0];
+    A.fast_n64 = tier_end[1];
     A.total_tiles = tile_first;
     A.total_od_blocks = od_first;
     A.od_tab_off = (int)c->rtab_host.size();
