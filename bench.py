@@ -6,9 +6,11 @@ Workload (BASELINE.json configs[1], C2): 640x480 stereo pairs, 8-level pyramid (
 right descriptors (2000 x 2000 kNN2, the C3 matcher step).  A "step" = one pass of the hot path
 over a device-resident batch of `--pairs` stereo pairs per GPU (inputs already in HBM).
 
-Multi-GPU: one process per GPU (torch.distributed.run); every rank extracts its own shard of
-pairs (frames are independent -> weak scaling, no data-path collective); barrier + max over
-ranks bracket the timed region.  Prints ONE JSON line on rank 0.
+Multi-GPU: one process per GPU; every rank extracts its own shard of pairs (frames are
+independent -> weak scaling, no data-path collective); barrier + max over ranks bracket the timed
+region.  Launched either by torch.distributed.run (RANK / WORLD_SIZE in the environment) or as
+`python bench.py --gpus N`, which starts the N ranks itself (spawn_ranks) before this process
+touches torch or the GPU.  Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
 
@@ -59,23 +61,21 @@ def fast_tiers(w, h, sf=1.2, L=8):
 def algorithmic_bytes(w, h, L, nkp, sf=1.2, ncand=0.0):
     """Per-image bytes by stage: pyramid sum(A_{l-1}+A_l), FAST sum(A_l) (split
     between the 48-, 64- and 80-byte tile launches), blur 2*sum(A_l), 48 B per output keypoint
-    (16 B keypoint + 32 B descriptor) plus, for k_orient_desc, one read of the raw and the
-    blurred pyramid (its windows' pixel support); k_pyramid = pyramid + blur in one launch; the octree reads
-    its 4-byte candidate keys and writes 4 bytes per kept keypoint."""
+    (16 B keypoint + 32 B descriptor) for orientation + descriptor; the octree reads its 4-byte
+    candidate keys and writes 4 bytes per kept keypoint; the assembly reads the level keypoint
+    (key, angle, descriptor: 40 B) and writes the cv::KeyPoint and the descriptor (60 B)."""
     A = [a * b for a, b in level_sizes(w, h, sf, L)]
     tier = fast_tiers(w, h, sf, L)
     return {
-        "k_pyramid": sum(A[l - 1] + A[l] for l in range(1, L)) + 2 * sum(A),
         # one pass over level l-1 per launch: read it, write its blur and level l
         "k_blur_resize": sum(2 * A[l - 1] + A[l] for l in range(1, L)),
         "k_fast_cells<48>": sum(a for a, t in zip(A, tier) if t == 48),
         "k_fast_cells<64>": sum(a for a, t in zip(A, tier) if t == 64),
         "k_fast_cells<80>": sum(a for a, t in zip(A, tier) if t == 80),
         "k_blur": 2 * A[L - 1],  # the last level's blur (the others ride in k_blur_resize)
-        # both planes read once (the 31-px moment discs and 37-px patches of ~2000 keypoints per
-        # image cover nearly all of every level) + 48 B out per keypoint
-        "k_orient_desc": 2 * sum(A) + 48 * nkp,
+        "k_orient_desc": 48 * nkp,
         "k_octree": 4 * ncand + 4 * nkp,
+        "k_finalize": 100 * nkp,
     }
 
 
@@ -83,6 +83,47 @@ def fast_pyramid_bytes(w, h, L, sf=1.2):
     """B_fp per image: pyramid sum_{l>=1}(A_{l-1}+A_l) + FAST sum_l A_l."""
     A = [a * b for a, b in level_sizes(w, h, sf, L)]
     return sum(A[l - 1] + A[l] for l in range(1, L)) + sum(A)
+
+
+def spawn_ranks(n):
+    """`bench.py --gpus N` with no launcher: start N ranks of this script (rank r on GPU r,
+    RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT in each child's environment, the
+    rendezvous on 127.0.0.1).  This process never imports torch or liborbgpu: the children are
+    started before anything touches the GPU.  Rank 0 prints the JSON line (its stdout is this
+    process's); a rank that fails ends the others (their rendezvous would wait for it).  Returns
+    the worst exit code."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=None if r == 0 else subprocess.DEVNULL))
+    codes = [None] * n
+    while any(c is None for c in codes):
+        for r, p in enumerate(procs):
+            if codes[r] is None:
+                codes[r] = p.poll()
+        if any(c not in (None, 0) for c in codes):
+            for r, p in enumerate(procs):
+                if codes[r] is None:
+                    p.terminate()
+            for r, p in enumerate(procs):
+                if codes[r] is None:
+                    try:
+                        codes[r] = p.wait(timeout=30)
+                    except subprocess.TimeoutExpired:
+                        p.kill()
+                        codes[r] = p.wait()
+            break
+        time.sleep(0.2)
+    bad = [c for c in codes if c]
+    return max(bad, key=abs) if bad else 0
 
 
 def dist_setup():
@@ -93,12 +134,15 @@ def dist_setup():
     if world > 1:
         import torch
         import torch.distributed as td
-        # ORBGPU_BENCH_BACKEND=gloo + ORBGPU_BENCH_DEVICE=0 rehearse several ranks on one GPU
-        backend = os.environ.get("ORBGPU_BENCH_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
+        # device_count() does not initialise the GPU (torch reads it from the driver); RCCL needs
+        # one device per rank, so fewer devices than ranks (the one-GPU rehearsal) run gloo with
+        # the ranks sharing the devices; ORBGPU_BENCH_BACKEND / ORBGPU_BENCH_DEVICE override
+        ndev = torch.cuda.device_count()
+        backend = os.environ.get("ORBGPU_BENCH_BACKEND") or ("nccl" if ndev >= world else "gloo")
         if backend == "nccl":
             torch.cuda.set_device(local)
         else:
-            local = int(os.environ.get("ORBGPU_BENCH_DEVICE", local))
+            local = int(os.environ.get("ORBGPU_BENCH_DEVICE", local % max(ndev, 1)))
         td.init_process_group(backend=backend)
         dist = td
     return world, rank, local, dist
@@ -241,18 +285,35 @@ def main():
     ap.add_argument("--map-points", type=int, default=3000, help="local-map points per frame (SBP leg)")
     ap.add_argument("--no-profile", action="store_true",
                     help="do not bracket launches with HIP events in the timed region")
+    ap.add_argument("--stub-gpu", action="store_true",
+                    help="CPU test of the launch / rendezvous / reduction path only: a host stand-in "
+                         "(tests/bench_stub.py) replaces liborbgpu; the line says data: stub")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return spawn_ranks(args.gpus)
     world, rank, local, dist = dist_setup()
+    if args.gpus != world and rank == 0:
+        print("bench: --gpus %d but %d rank(s) launched; reporting the launched ranks" % (args.gpus, world),
+              file=sys.stderr)
     # torch before liborbgpu: both then share one HIP runtime (torch bundles its own with the
     # same soname), so torch.cuda.synchronize() below brackets the same device queues
     try:
         import torch
-        has_cuda = torch.cuda.is_available()
+        has_cuda = torch.cuda.is_available() and not args.stub_gpu
     except Exception:
         torch, has_cuda = None, False
-    import orbslam3lib_amd as og
+    if args.stub_gpu:
+        from tests import bench_stub as og
+    else:
+        import orbslam3lib_amd as og
     from orbslam3lib_amd import synth
+    # where every rank runs (rank, device, host pid): the line shows that all ranks joined
+    placement = [(rank, local, os.getpid())]
+    if dist is not None:
+        allp = [None] * world
+        dist.all_gather_object(allp, placement[0])
+        placement = allp
 
     P, W, H = args.pairs, args.width, args.height
     U = max(1, min(args.unique_pairs, P))
@@ -317,9 +378,6 @@ def main():
     elapsed = max_over_ranks(dist, t1 - t0)
     stages_timed = be.stage_times()
     be.set_profiling(False)
-    stages = dict(stages_all)
-    if dom_name and stages_timed.get(dom_name, (0, 0))[1] > 0:
-        stages[dom_name] = stages_timed[dom_name]  # live measurement from the timed region
 
     # streaming ingest (C3's shape: every batch arrives from the host): each step's 2P frames are
     # copied from pinned host memory on the copy stream while the previous step computes
@@ -351,65 +409,78 @@ def main():
     h2d_incl = total_feats / p_el / 1e6
     mmatch = total_q / elapsed / 1e6
 
-    # roofline of the dominant kernel (per-launch algorithmic bytes / measured avg duration)
+    # per-stage table from the serialized pass: each stage one whole-batch launch per step (one per
+    # level for k_blur_resize), alone on the GPU, so its duration is the kernel's own and the
+    # rocprofv3 trace of the same command reproduces it (tools/roofline_check.py).  Bytes are
+    # SURVEY §8d's algorithmic bytes per launch; `traffic` is the counter-measured HBM bytes per
+    # launch of the same whole-batch launch (profiles/traffic_r*.json, per image and step there)
     n_img = 2 * P
+    nser = 3
     per_img = algorithmic_bytes(W, H, args.nlevels, feats_per_step / n_img, ncand=cand_per_img)
+    traffic_tab, traffic_src = {}, None
+    tps = sorted(glob.glob(os.path.join(ROOT, "profiles", "traffic_r*.json")))
+    if tps:
+        try:
+            tt = json.load(open(tps[-1]))
+            if tt.get("_config", {}).get("width") == W and tt.get("_config", {}).get("height") == H:
+                traffic_tab = {k: v for k, v in tt.items() if isinstance(v, dict) and "hbm_bytes_per_image_step" in v}
+                traffic_src = os.path.relpath(tps[-1], ROOT)
+        except Exception:
+            traffic_tab = {}
     stage_rows = {}
-    for name, (ms, cnt) in stages.items():
+    for name, (ms, cnt) in stages_all.items():
         if cnt == 0:
             continue
         avg_ms = ms / cnt
+        launches_per_step = cnt / nser
         row = {"avg_us": round(avg_ms * 1e3, 2), "launches": cnt, "total_ms": round(ms, 3),
-               "source": "timed region" if name == dom_name and stages_timed.get(name, (0, 0))[1]
-               else "3-step profiled pass"}
+               "us_per_step": round(ms / nser * 1e3, 1), "source": "serialized pass (kernel alone)"}
         if name in per_img:
-            # launches per step as measured: one whole-batch launch per stage (per level for
-            # k_resize) in the serialized pass, one per sub-batch stream in the timed region
-            nsteps = args.steps if row["source"] == "timed region" else 3
-            launches_per_step = cnt / nsteps
             bytes_launch = per_img[name] * n_img / launches_per_step
             row["bytes_per_launch"] = int(bytes_launch)
             row["GBps"] = round(bytes_launch / (avg_ms * 1e-3) / 1e9, 1)
             row["frac_hbm"] = round(row["GBps"] / HBM_PEAK_GBS, 4)
+            if name in traffic_tab:
+                tb = traffic_tab[name]["hbm_bytes_per_image_step"] * n_img / launches_per_step
+                row["traffic_per_launch"] = int(tb)
+                row["traffic_over_algorithmic"] = round(tb / bytes_launch, 2) if bytes_launch else None
         if name == "k_knn2":
             # the kernel runs on the i8 matrix cores: 2 x 256 int8 ops per (query, train)
             # pair are what it issues; the 16-op VALU popcount figure is kept beside it
-            nsteps = args.steps if row["source"] == "timed region" else 3
-            pairs_launch = pairs_per_step / (cnt / nsteps)
+            pairs_launch = pairs_per_step / launches_per_step
             row["Tops_i8"] = round(512.0 * pairs_launch / (avg_ms * 1e-3) / 1e12, 1)
             row["frac_mfma_i8"] = round(row["Tops_i8"] / MFMA_I8_PEAK_TOPS, 4)
             row["Tops"] = round(16.0 * pairs_launch / (avg_ms * 1e-3) / 1e12, 2)
             row["frac_valu"] = round(row["Tops"] / VALU_PEAK_TOPS, 4)
         stage_rows[name] = row
-    # the dominant kernel is picked on the all-stage pass; its row holds the timed-region events
+    # the dominant kernel: the largest serialized total; its timed-region (concurrent) launches
+    # were bracketed with HIP events on their own streams and sit beside the kernel-alone figure
     dom = dom_name if dom_name in stage_rows else None
+    if dom is not None and stages_timed.get(dom, (0, 0))[1] > 0 and "bytes_per_launch" in stage_rows[dom]:
+        tms, tcnt = stages_timed[dom]
+        tb = per_img[dom] * n_img / (tcnt / args.steps)
+        stage_rows[dom]["concurrent"] = {
+            "source": "timed region, HIP events on the chunk streams (other chunks' stages run beside it)",
+            "avg_us": round(tms / tcnt * 1e3, 2), "launches": tcnt, "bytes_per_launch": int(tb),
+            "GBps": round(tb / (tms / tcnt * 1e-3) / 1e9, 1),
+            "frac_hbm": round(tb / (tms / tcnt * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
     roof = None
     if dom is not None:
         r = stage_rows[dom]
-        traffic = None
-        # the newest round's FETCH_SIZE / WRITE_SIZE passes (tools/pmc_traffic.sh + tools/traffic.py)
-        tps = sorted(glob.glob(os.path.join(ROOT, "profiles", "traffic_r*.json")))
-        tp = tps[-1] if tps else ""
-        if tp and os.path.exists(tp):
-            try:
-                traffic = json.load(open(tp)).get(dom, {}).get("hbm_bytes_per_launch")
-            except Exception:
-                traffic = None
         if "GBps" in r:
             roof = {"kernel": dom, "bound": "hbm", "achieved": r["GBps"], "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": r["frac_hbm"], "traffic": traffic,
+                    "unit": "GB/s", "frac": r["frac_hbm"], "traffic": r.get("traffic_per_launch"),
+                    "traffic_over_algorithmic": r.get("traffic_over_algorithmic"), "traffic_source": traffic_src,
                     "bytes_per_launch": r["bytes_per_launch"], "avg_us": r["avg_us"],
-                    "timed_launches": r.get("launches"),
-                    # the same kernel alone on the GPU (serialized whole-batch pass), for the
-                    # rocprofv3 cross-check: no other stream's kernels beside it
-                    "serialized_avg_us": round(stages_all[dom][0] / stages_all[dom][1] * 1e3, 2)
-                    if stages_all.get(dom, (0, 0))[1] else None}
+                    "launch": "whole batch (%d images), serialized pass, kernel alone" % n_img,
+                    "launches": r["launches"], "concurrent": r.get("concurrent")}
         elif "Tops_i8" in r:
             roof = {"kernel": dom, "bound": "mfma_i8", "achieved": r["Tops_i8"], "peak": MFMA_I8_PEAK_TOPS,
-                    "unit": "Tops/s", "frac": r["frac_mfma_i8"], "traffic": traffic, "avg_us": r["avg_us"]}
+                    "unit": "Tops/s", "frac": r["frac_mfma_i8"], "traffic": r.get("traffic_per_launch"),
+                    "avg_us": r["avg_us"]}
         else:
             roof = {"kernel": dom, "bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": None, "traffic": traffic, "avg_us": r["avg_us"]}
+                    "unit": "GB/s", "frac": None, "traffic": r.get("traffic_per_launch"), "avg_us": r["avg_us"]}
         if dom == "k_octree":
             roof["note"] = ("DistributeOctTree is barrier/LDS-latency bound (serial list rounds per "
                             "(image, level)); its HBM bytes are the 4-B keys in and out")
@@ -565,14 +636,15 @@ def main():
         lib = og.load_library()
         dptr = lib.orbgpu_device_sbs_input(be.ctx.handle)
         if dptr and be.ctx.max_images >= 2:
-            # fill the staging buffer from the resident batch (device to device, untimed)
-            hip = ctypes.CDLL("libamdhip64.so.7")  # the runtime liborbgpu.so loaded
+            # fill the staging buffer from the resident batch (device to device, untimed) through
+            # the HIP runtime liborbgpu.so itself is bound to
+            memcpy2d = og.hip_function("hipMemcpy2D")
             vp, sz = ctypes.c_void_p, ctypes.c_size_t
-            hip.hipMemcpy2D.argtypes = [vp, sz, vp, sz, sz, sz, ctypes.c_int]
+            memcpy2d.argtypes = [vp, sz, vp, sz, sz, sz, ctypes.c_int]
             src = lib.orbgpu_device_input(be.ctx.handle)
             for p in range(P):
                 for e in range(2):
-                    hip.hipMemcpy2D(dptr + p * H * 2 * W + e * W, 2 * W, src + (2 * p + e) * H * W, W, W, H, 3)
+                    memcpy2d(dptr + p * H * 2 * W + e * W, 2 * W, src + (2 * p + e) * H * W, W, W, H, 3)
             be.ingest_sbs(dptr, P, 2 * W)
             be.run()
             be.match_stereo(stereo_rows_only=False)
@@ -691,22 +763,35 @@ def main():
         try:
             from orbslam3lib_amd.dist import cross_camera_match, cross_camera_match_device
             kl0, dl0, _ = be.result(0)
-            device_path = dist.get_backend() == "nccl"
-            barrier(dist)
-            c0 = time.perf_counter()
-            if device_path:  # descriptors stay in HBM: export -> RCCL all_gather -> device kNN2
-                res = cross_camera_match_device(dist, be, 0)
-                torch.cuda.synchronize()
-            else:  # gloo rehearsal on one GPU: the host-staged exchange
-                bfm = og.BFMatcher.__new__(og.BFMatcher)
-                bfm._ctx = be.ctx
-                res = cross_camera_match(dist, dl0, lambda q, t: bfm.knnMatch(q, t, 2))
-            c1 = time.perf_counter()
+            device_path = has_cuda
+            res = None
+            for _ in range(2):  # the first exchange sets up the communicator and buffers
+                barrier(dist)
+                c0 = time.perf_counter()
+                if device_path:
+                    # descriptors stay in HBM: export -> all_gather (RCCL over xGMI; under gloo
+                    # staged through the host) -> device kNN2 on every other camera
+                    res = cross_camera_match_device(dist, be, 0)
+                    torch.cuda.synchronize()
+                else:  # no GPU (the stub test): the host exchange
+                    res = cross_camera_match(dist, dl0, be.knn_match)
+                c1 = time.perf_counter()
             cel = max_over_ranks(dist, c1 - c0)
             nqm = sum_over_ranks(dist, len(dl0) * len(res))
+            # every rank checks its device results against the host matcher on the same rows
+            ok = 1.0
+            if device_path:
+                from orbslam3lib_amd.dist import cross_camera_match as host_x
+                ref = host_x(dist, dl0, be.knn_match)
+                for r_, got in res.items():
+                    g = got.cpu().numpy()
+                    ok = min(ok, float(all(np.array_equal(g[k], ref[r_][k]) for k in range(4))))
+            ok = -max_over_ranks(dist, -ok)
             cross = {"cameras": world, "queries_per_camera": len(dl0), "ms": round(cel * 1e3, 3),
                      "mmatches_s": round(nqm / cel / 1e6, 3),
-                     "exchange": "all_gather (%s)" % ("RCCL, device-resident" if device_path else dist.get_backend())}
+                     "device_matches_equal_host_matcher": bool(ok == 1.0) if device_path else None,
+                     "exchange": "all_gather (%s%s)" % (dist.get_backend(), ", device-resident rows"
+                                                        if device_path else ", host rows")}
         except Exception as e:  # reported, never fatal to the headline line
             cross = {"error": repr(e)[:200]}
 
@@ -755,7 +840,10 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": "synthetic seeded stereo frames (SURVEY §8d generator), resident in HBM",
+            "data": ("stub (CPU test of the multi-rank path, no GPU work)" if args.stub_gpu else
+                     "synthetic seeded stereo frames (SURVEY §8d generator), resident in HBM"),
+            "ranks": [{"rank": r_, "device": d_, "pid": p_} for r_, d_, p_ in placement],
+            "backend": dist.get_backend() if dist is not None else None,
             "config": {"workload": "C2 640x480 stereo, 8 levels x1.2, 2000 feat/frame, FAST 20/7, "
                                    "+ per-pair 2000x2000 Hamming kNN2 (left->right, all rows)",
                        "pairs_per_gpu_per_step": P, "images_per_gpu_per_step": 2 * P,
@@ -785,7 +873,8 @@ def main():
         print(json.dumps(out))
     if dist is not None:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

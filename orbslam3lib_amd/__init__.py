@@ -118,6 +118,14 @@ def load_library(path: str = LIB_PATH):
     return lib
 
 
+def hip_function(name: str):
+    """A HIP runtime entry point (e.g. "hipMemcpy2D") from the runtime liborbgpu.so is bound to.
+    ctypes looks the name up with dlsym on the library's handle, which searches liborbgpu.so and
+    then its dependencies in load order, i.e. the libamdhip64 it actually mapped (torch's bundled
+    copy when torch was imported first) -- no soname is hard-coded.  Test / bench plumbing."""
+    return getattr(load_library(), name)
+
+
 def _check(code):
     if code < 0:
         raise OrbGpuError(code, _lib.orbgpu_last_error().decode())
@@ -300,19 +308,44 @@ class BatchExtractor:
     upload(images[n,h,w]) -> run(laps) -> results stay in HBM; match_stereo() pairs 2p/2p+1.
     """
 
+    device_resident = True  # results live in HBM (dist.cross_camera_match_device)
+
     def __init__(self, nfeatures=2000, scaleFactor=1.2, nlevels=8, iniThFAST=20, minThFAST=7,
                  device=0, width=640, height=480, max_images=128):
         self.ctx = _Context(nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST, device, width,
                             height, max_images)
         self.width, self.height = int(width), int(height)
         self.n = 0
+        self._staged = None  # (n, h, w) of the batch upload_async staged for the next run()
+        self._pinned = []
+
+    def close(self):
+        """Frees the pinned host buffers of pinned() and the device context."""
+        self.free_pinned()
+        self.ctx.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
     def upload(self, images):
         imgs = np.ascontiguousarray(images, dtype=np.uint8)
         n, h, w = imgs.shape
         _check(_lib.orbgpu_upload_images(self.ctx.handle, _p(imgs), n, w, h, w))
         self.n, self.height, self.width = n, h, w
+        self._staged = None  # the synchronous upload replaces a staged one (orbgpu_upload_images)
         _check(_lib.orbgpu_synchronize(self.ctx.handle))
+
+    def knn_match(self, query, train):
+        """BFMatcher(NORM_HAMMING).knnMatch(query, train, 2) on this context's device, host arrays
+        in and out: (idx1, dist1, idx2, dist2) int32."""
+        q = np.ascontiguousarray(query, dtype=np.uint8).reshape(-1, 32)
+        t = np.ascontiguousarray(train, dtype=np.uint8).reshape(-1, 32)
+        out = [np.zeros(q.shape[0], np.int32) for _ in range(4)]
+        _check(_lib.orbgpu_match_knn2(self.ctx.handle, _p(q), q.shape[0], _p(t), t.shape[0], *[_p(o) for o in out]))
+        return tuple(out)
 
     def export_descriptors(self, image, device_ptr, cap_rows, row0=0, stream=None):
         """Rows [row0, n) of image's descriptors into device memory (device-to-device);
@@ -335,23 +368,32 @@ class BatchExtractor:
         imgs = np.ascontiguousarray(images, dtype=np.uint8)
         n, h, w = imgs.shape
         _check(_lib.orbgpu_upload_images_async(self.ctx.handle, _p(imgs), n, w, h, w))
-        self.n, self.height, self.width = n, h, w
+        # the current batch keeps its size until run() switches to the staged one: counts(),
+        # match_stereo() etc. issued before that still refer to the current batch
+        self._staged = (n, h, w)
 
     def pinned(self, shape):
-        """A uint8 numpy array over page-locked host memory (freed with the extractor)."""
+        """A uint8 numpy array over page-locked host memory.  The memory is freed by free_pinned()
+        or close() (or when the extractor is collected); the array must not be used after that."""
         nbytes = int(np.prod(shape))
         ptr = C.c_void_p()
         _check(_lib.orbgpu_host_alloc(nbytes, C.byref(ptr)))
-        self._pinned = getattr(self, "_pinned", []) + [ptr]
+        self._pinned.append(ptr)
         buf = (C.c_uint8 * nbytes).from_address(ptr.value)
         return np.frombuffer(buf, np.uint8).reshape(shape)
 
     def free_pinned(self):
-        for ptr in getattr(self, "_pinned", []):
+        """Frees every pinned() buffer (after the staged uploads that read them have landed)."""
+        if self._pinned and self.ctx.handle:
+            _check(_lib.orbgpu_synchronize(self.ctx.handle))
+        for ptr in self._pinned:
             _lib.orbgpu_host_free(ptr)
         self._pinned = []
 
     def run(self, laps=None, stream=None):
+        if self._staged is not None:  # the batch upload_async staged becomes the current one
+            self.n, self.height, self.width = self._staged
+            self._staged = None
         n = self.n
         lp = None
         if laps is not None:
@@ -438,12 +480,14 @@ class BatchExtractor:
         w = stride // 2 if width is None else int(width)
         _check(_lib.orbgpu_upload_sbs(self.ctx.handle, _p(frames), n, w, h, stride))
         self.n, self.height, self.width = 2 * n, h, w
+        self._staged = None
 
     def ingest_sbs(self, device_ptr, n_frames, stride, stream=None):
         """Split side-by-side frames already in device memory (zero-copy ingest)."""
         _check(_lib.orbgpu_ingest_sbs(self.ctx.handle, C.c_void_p(device_ptr), int(n_frames), self.width,
                                       self.height, int(stride), C.c_void_p(stream) if stream else None))
         self.n = 2 * int(n_frames)
+        self._staged = None
 
     def pack_soa(self, n_pairs=None, stream=None):
         """The orbslam3.idl SoA layout for every image (and n_pairs stereo pairs' matches)."""

@@ -85,11 +85,7 @@ struct BatchArgs {
     int oct2_lds_nodes, oct2_lds_bytes, oct2_nq_off, oct2_lds_keys;
     int oct_may_retry;               // some level can exceed the LDS instantiation of k_octree
     int oct_force_retry;             // diagnostics: every level through the generic instantiation
-    // k_pyramid stripe tables in rtab, one per stripe count 2^i (i < kPyrStripeKinds):
-    // entry [l * S + k] = {need_lo, need_hi, own_lo, own_hi} rows of level l for stripe k
-    int stripe_tab_off[5];
 };
-constexpr int kPyrStripeKinds = 5;  // 1, 2, 4, 8, 16 stripes per image
 
 struct MatchArgs {
     const uint8_t* desc;      // out_desc
@@ -200,17 +196,12 @@ __host__ __device__ inline OctLayout oct_layout(int n_cap, int C) {
 }
 
 // Kernel launchers (orb_kernels.hip).  Each returns hipGetLastError() of its launch.
-hipError_t launch_resize(const BatchArgs& a, int level, hipStream_t s);
-hipError_t launch_blur(const BatchArgs& a, hipStream_t s);
 constexpr int kBrMaxQuads = 40;  // k_blur_resize: level-l column quads / rows one blur tile owns
 constexpr int kBrMaxRows = 34;
 // The blur of level l - 1 and the resize to level l in one launch (every level except the last
 // blur, which launch_blur_level does).
 hipError_t launch_blur_resize(const BatchArgs& a, int level, hipStream_t s);
 hipError_t launch_blur_level(const BatchArgs& a, int level, hipStream_t s);
-// the whole pyramid (levels 1..L-1) and every blurred level in one launch: one workgroup per
-// (image, row stripe), 2^stripe_log2 stripes per image
-hipError_t launch_pyramid(const BatchArgs& a, int stripe_log2, hipStream_t s);
 // FAST cells of the levels that run the `tile`-byte LDS tile (48, 64 or kCellMax = 80):
 // fast_cell_range gives their flattened cell range, launch_fast_cells launches nothing if empty
 void fast_cell_range(const BatchArgs& a, int tile, int* c0, int* c1);
@@ -218,8 +209,7 @@ hipError_t launch_fast_cells(const BatchArgs& a, int tile, hipStream_t s);
 hipError_t launch_octree(const BatchArgs& a, hipStream_t s);
 hipError_t launch_orient_desc(const BatchArgs& a, hipStream_t s);
 hipError_t launch_finalize(const BatchArgs& a, hipStream_t s);
-hipError_t launch_knn2_pairs(const MatchArgs& m, int npairs, int qblocks, void* scratch, hipStream_t s);
-size_t knn2_scratch_bytes(int npairs, int out_cap);
+hipError_t launch_knn2_pairs(const MatchArgs& m, int npairs, hipStream_t s);
 hipError_t launch_stereo(const StereoArgs& s, int npairs, hipStream_t st);  // orb_stereo.hip
 hipError_t launch_undistort_grid(const GridArgs& g, int nimages, hipStream_t st);  // orb_frame.hip
 void grid_dist_table(const float* dist, int ndist, double k[14]);

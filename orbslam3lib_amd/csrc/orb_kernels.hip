@@ -1,23 +1,25 @@
 // orb_kernels.hip -- gfx950 kernels of the ORB front-end.  Integer/byte work: no MFMA.
 //
-// Pipeline for a batch of B images (all on one stream):
-//   k_resize      x (L-1)  cascaded bilinear pyramid, OpenCV INTER_LINEAR fixed point
-//   k_blur        x 1      7x7 Gaussian (sigma 2, fixed point, REFLECT_101) on every level
-//   k_fast_cells  x 1      one workgroup per (image, level, 35-px cell): FAST-9 strength,
-//                          3x3 nonmax at iniTh / minTh fallback, ordered compaction
+// Pipeline for a batch of B images (one launch per stage, or per sub-batch stream and stage):
+//   k_blur_resize x (L-1)  level l-1's 7x7 Gaussian (sigma 2, fixed point, REFLECT_101) and the
+//                          cascaded INTER_LINEAR resize to level l from one read of level l-1
+//   k_blur        x 1      the last level's blur
+//   k_fast_cells  x 1-3    one workgroup per (image, level, 35-px cell): FAST-9 strength,
+//                          3x3 nonmax at iniTh / minTh fallback, ordered compaction (one launch
+//                          per LDS tile size)
 //   k_octree      x 1      one workgroup per (image, level): DistributeOctTree
-//   k_orient_desc x 1      one wave per keypoint: IC_Angle + rBRIEF 256 bit
+//   k_orient_desc x 1      32 lanes per keypoint: IC_Angle + rBRIEF 256 bit
 //   k_finalize    x 1      one workgroup per image: scale + mono/stereo partition
-//   k_knn2        x 1      Hamming k=2 brute force, query-in-registers / train-in-LDS
+//   k_knn2_mfma   x 1      Hamming k=2 brute force on the i8 matrix cores
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include <algorithm>
+#include <atomic>
 
 #include "orb_kernels.h"
 #include "orb_math.h"
 #include "orb_fast_cell.h"
-#include "orb_fast_wave.h"
 #include "orb_octree.h"
 #include "orb_pattern_data.h"
 #include "orb_policy.h"
@@ -78,20 +80,11 @@ constexpr MomentWeights make_moment_weights() {
 __constant__ MomentWeights c_mw = make_moment_weights();
 
 // ---------------------------------------------------------------------------------------------
-// k_resize: level l from level l-1 (canonical ComputePyramid, ORBextractor_old.cc:1342-1344 ->
-// cv::resize INTER_LINEAR).  Horizontal: D = S[sx]*a0 + S[sx1]*a1 (int); vertical: OpenCV's
-// 128-bit SIMD body for x < simd_end, FixedPtCast tail after.  A block makes a 256 x 16 output
-// tile: its x-table slice and the source window (dword loads) are staged in LDS first.
-constexpr int kRsTW = 256, kRsTH = 16;
-// source window (rows, bytes) for scale factors up to 2 and, smaller (more workgroups per CU),
-// up to 1.25: tile * scale + the second tap + 2 px margin each side, rounded to 16 bytes
-constexpr int kRsSrcRows = 2 * kRsTH + 2, kRsSrcCols = 2 * kRsTW + 16;
-constexpr int kRsSrcRowsS = 24, kRsSrcColsS = 336;
-static_assert(kRsSrcCols % 16 == 0 && kRsSrcColsS % 16 == 0, "window rows are written in 16-byte chunks");
-
-// Four output pixels dx0 .. dx0+3 of one output row from source rows r0 / r1 (LDS window or
-// GlobalRow), x coefficients xt[0..3] (entries past the tile edge may be stale: their bytes are
-// padding or the next tile's, rewritten there), y coefficients b0 / b1.  Every product fits 24
+// ---------------------------------------------------------------------------------------------
+// cv::resize INTER_LINEAR (canonical ComputePyramid, ORBextractor_old.cc:1342-1344), fixed point.
+// Four output pixels dx0 .. dx0+3 of one output row from source rows r0 / r1 (LDS window rows), x
+// coefficients xt[0..3] (entries past the tile edge may be stale: their bytes are padding or the
+// next tile's, rewritten there), y coefficients b0 / b1.  Every product fits 24
 // bits (pixel <= 255, coefficients <= 2048, (D >> 4) < 2^15), so all multiplies are full-rate
 // v_mul_u32_u24 / v_mad_u32_u24.  Vertical rounding: OpenCV's SIMD body below simd_end,
 // FixedPtCast after it (only the last quads of a row take that branch).
@@ -126,102 +119,6 @@ __device__ inline uint32_t rs_quad(const Row& r0, const Row& r1, const int4* xt,
         }
     }
     return packed;
-}
-
-// Source bytes of a plane through bounds-checked byte loads (kAux: cache policy).
-template <int kAux>
-struct GlobalRow {
-    __amdgpu_buffer_rsrc_t rs;
-    int off;
-    __device__ int operator[](int x) const { return __builtin_amdgcn_raw_buffer_load_b8(rs, off + x, 0, kAux); }
-};
-
-// One 256 x 16 output tile of level l, output rows limited to [ty0, rhi).  xt_s / yt_s / win
-// are the caller's LDS; the caller synchronizes before the next tile reuses them.  kAux is the
-// cache policy of every source load (sc1 where the source was written by this launch).
-template <int kRsSrcRows, int kRsSrcCols, int kAux>
-__device__ inline void resize_tile(const BatchArgs& a, int img, int l, int tx0, int ty0, int rhi,
-                                   int4* xt_s, int4* yt_s, uint32_t (*win)[kRsSrcCols / 4]) {
-    const LevelGeom& G = a.lv[l];
-    const LevelGeom& S = a.lv[l - 1];
-    const uint8_t* src = a.lvl_base[l - 1] + (long long)img * S.img_stride;
-    uint8_t* dst = a.lvl_base[l] + (long long)img * G.img_stride;
-    const __amdgpu_buffer_rsrc_t srs = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)src, (short)0, (int)min(S.img_stride, 0x7fffffffLL), 0x00020000);
-    const int tw = min(kRsTW, G.w - tx0), th = min(min(kRsTH, G.h - ty0), rhi - ty0);
-    if (G.area2) {  // resize.cpp: INTER_LINEAR at exactly 2x is serviced by INTER_AREA fast
-        for (int i = threadIdx.x; i < kRsTW / 4 * kRsTH; i += 256) {
-            const int rr = i / (kRsTW / 4), dx0 = tx0 + 4 * (i % (kRsTW / 4));
-            if (rr >= th || dx0 >= G.w) continue;
-            const int dy = ty0 + rr;
-            const GlobalRow<kAux> s0{srs, 2 * dy * S.pitch}, s1{srs, (2 * dy + 1) * S.pitch};
-            uint32_t pk = 0;
-            for (int k = 0; k < 4; ++k) {
-                const int dx = min(dx0 + k, G.w - 1);
-                const int o = (s0[2 * dx] + s0[2 * dx + 1] + s1[2 * dx] + s1[2 * dx + 1] + 2) >> 2;
-                pk |= (uint32_t)o << (8 * k);
-            }
-            *reinterpret_cast<uint32_t*>(dst + (long long)dy * G.pitch + dx0) = pk;
-        }
-        return;
-    }
-    // the tables and the source window load together: the window origin is estimated from the
-    // scale (2 px margin), the tables decide below whether the window covers the tile exactly
-    for (int i = threadIdx.x; i < tw; i += 256) xt_s[i] = a.rtab[G.xtab_off + tx0 + i];
-    if (threadIdx.x < th) yt_s[threadIdx.x] = a.rtab[G.ytab_off + ty0 + threadIdx.x];
-    const float sxf = (float)S.w / (float)G.w, syf = (float)S.h / (float)G.h;
-    const int sx_lo = max(0, (int)floorf(((float)tx0 + 0.5f) * sxf - 0.5f) - 2) & ~3;
-    const int sy_lo = max(0, (int)floorf(((float)ty0 + 0.5f) * syf - 0.5f) - 2);
-    const int nrows = min(kRsSrcRows, S.h - sy_lo);
-    const int nq4 = min(kRsSrcCols / 16, (S.w - sx_lo + 15) >> 4);  // 16-byte chunks per row
-    const bool aligned = (S.pitch & 3) == 0;
-    if (aligned) {
-        // 16-byte buffer loads (bounds-checked: bytes past the plane read as 0 and are never
-        // used); half a wave per source row, no integer division
-        const int half = threadIdx.x >> 5, hl = threadIdx.x & 31;
-        for (int r = half; r < nrows; r += 8) {
-            const int rowofs = (sy_lo + r) * S.pitch + sx_lo;
-            for (int c = hl; c < nq4; c += 32) {
-                const auto v = __builtin_amdgcn_raw_buffer_load_b128(srs, rowofs + 16 * c, 0, kAux);
-                *reinterpret_cast<uint4*>(&win[r][4 * c]) = make_uint4(v[0], v[1], v[2], v[3]);
-            }
-        }
-    }
-    __syncthreads();
-    const bool staged = aligned && xt_s[0].x >= sx_lo && xt_s[tw - 1].y < sx_lo + 16 * nq4 &&
-                        yt_s[0].x >= sy_lo && yt_s[th - 1].y < sy_lo + nrows;
-    const uint8_t* wb = reinterpret_cast<const uint8_t*>(&win[0][0]);
-    const int q = threadIdx.x & 63;
-    // one body per source (LDS window / global plane): a merged body would take flat loads
-    auto body = [&](auto row_ptr) __attribute__((always_inline)) {
-        for (int rr = threadIdx.x >> 6; rr < th; rr += 4) {
-            const int dy = ty0 + rr;
-            const int dx0 = tx0 + 4 * q;
-            if (4 * q >= tw) continue;
-            const int4 yt = yt_s[rr];
-            const auto r0 = row_ptr(yt.x), r1 = row_ptr(yt.y);
-            const uint32_t packed = rs_quad(r0, r1, xt_s + 4 * q, yt.z, yt.w, dx0, G.simd_end);
-            *reinterpret_cast<uint32_t*>(dst + (long long)dy * G.pitch + dx0) = packed;
-        }
-    };
-    if (staged) {
-        body([&](int sy) { return wb + (sy - sy_lo) * kRsSrcCols - sx_lo; });
-    } else {
-        body([&](int sy) { return GlobalRow<kAux>{srs, sy * S.pitch}; });
-    }
-}
-
-template <int kRsSrcRows, int kRsSrcCols>
-__global__ __launch_bounds__(256) void k_resize(BatchArgs a, int l) {
-    __shared__ int4 xt_s[kRsTW];
-    __shared__ int4 yt_s[kRsTH];
-    __shared__ __attribute__((aligned(16))) uint32_t win[kRsSrcRows][kRsSrcCols / 4];
-    const LevelGeom& G = a.lv[l];
-    const int nxy = gridDim.x * gridDim.y;
-    const int wg = xcd_remap(blockIdx.x + blockIdx.y * gridDim.x + blockIdx.z * nxy, nxy * gridDim.z);
-    const int img = a.img0 + wg / nxy;
-    const int tx0 = (wg % nxy % gridDim.x) * kRsTW, ty0 = (wg % nxy / gridDim.x) * kRsTH;
-    resize_tile<kRsSrcRows, kRsSrcCols, 0>(a, img, l, tx0, ty0, G.h, xt_s, yt_s, win);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -429,7 +326,6 @@ __global__ __launch_bounds__(256) void k_blur(BatchArgs a, int tile0, int ntile)
 // columns <= tx0+134 for scales <= 2) all lie in the window's real pixels, so level l needs no
 // second read of level l - 1 and the blur of level l - 1 none of its own.  Ownership tables
 // (band_row / tile_quad) come from the host with the resize coefficients.
-constexpr int kSc1 = 16;  // buffer-load aux bit: sc1
 static_assert(kBrMaxQuads >= kBlurTW / 4 + 1 && kBrMaxRows >= kBlurTH + 1, "ownership caps");
 
 struct BrSmem {
@@ -537,210 +433,6 @@ hipError_t launch_blur_resize(const BatchArgs& a, int l, hipStream_t s) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// k_pyramid: ComputePyramid (ORBextractor_old.cc:1331-1356) and the per-level GaussianBlur
-// (:1146-1147) of one row stripe of one image in one workgroup, all levels in one launch.
-// Phase l blurs the stripe's own rows of level l and resizes the rows of level l+1 the stripe
-// needs; both only read level l.  The needed rows (host table) are the stripe's own rows, the
-// 3-row blur halo and the source-row cone of every later level, so each workgroup reads only
-// rows it wrote itself: the phases are separated by a vmcnt drain + workgroup barrier, and
-// every load of a level written in this launch is an sc1 load (from L2, never a stale L1
-// line).  Rows in the overlap of two stripes are computed by both, with identical values.
-
-union PyrSmem {
-    struct {
-        int4 xt[kRsTW];
-        int4 yt[kRsTH];
-        uint32_t win[kRsSrcRows][kRsSrcCols / 4];
-    } r;
-    struct {
-        uint4 tin4[kBlurTH + 8][(kBlurTW + 32) / 16];
-        uint4 hp[(kBlurTH + 8) / 2][kBlurTW / 4];
-    } b;
-};
-
-// One resize tile of k_pyramid: columns [tx0, tx0 + tw) (balanced tiles of at most 256 columns,
-// tw a multiple of 4 except at the right edge), rows [ty0, ty0 + th), and its source window.
-struct RsTile {
-    int tx0, ty0, tw, th;
-    int sx_lo, sy_lo, nrows, nq4;
-};
-
-__device__ inline RsTile rs_tile(const LevelGeom& G, const LevelGeom& S, int j, int tw_nom, int ty0, int rhi) {
-    RsTile t;
-    t.tx0 = j * tw_nom;
-    t.tw = min(tw_nom, G.w - t.tx0);
-    t.ty0 = ty0;
-    t.th = min(min(kRsTH, G.h - ty0), rhi - ty0);
-    const float sxf = (float)S.w / (float)G.w, syf = (float)S.h / (float)G.h;
-    t.sx_lo = max(0, (int)floorf(((float)t.tx0 + 0.5f) * sxf - 0.5f) - 2) & ~3;
-    t.sy_lo = max(0, (int)floorf(((float)ty0 + 0.5f) * syf - 0.5f) - 2);
-    t.nrows = min(kRsSrcRows, S.h - t.sy_lo);
-    t.nq4 = min(kRsSrcCols / 16, (S.w - t.sx_lo + 15) >> 4);
-    return t;
-}
-
-// Output quads of a resize tile flattened over the workgroup (row = item / quads per row), so a
-// narrow level keeps every lane busy.  Source from the staged window when it covers every tap,
-// else from the plane through byte loads (cache policy kAux).
-template <int kAux>
-__device__ inline void rs_compute(const BatchArgs& a, int img, int l, const RsTile& t, bool aligned,
-                                  const int4* xt_s, const int4* yt_s, const uint32_t (*win)[kRsSrcCols / 4]) {
-    const LevelGeom& G = a.lv[l];
-    const LevelGeom& S = a.lv[l - 1];
-    const uint8_t* src = a.lvl_base[l - 1] + (long long)img * S.img_stride;
-    uint8_t* dst = a.lvl_base[l] + (long long)img * G.img_stride;
-    const __amdgpu_buffer_rsrc_t srs = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)src, (short)0, (int)min(S.img_stride, 0x7fffffffLL), 0x00020000);
-    if (G.area2) {  // resize.cpp: INTER_LINEAR at exactly 2x is serviced by INTER_AREA fast
-        const int nq = (t.tw + 3) >> 2;
-        for (int it = threadIdx.x; it < t.th * nq; it += 256) {
-            const int rr = it / nq, dx0 = t.tx0 + 4 * (it - rr * nq);
-            const int dy = t.ty0 + rr;
-            const GlobalRow<kAux> s0{srs, 2 * dy * S.pitch}, s1{srs, (2 * dy + 1) * S.pitch};
-            uint32_t pk = 0;
-            for (int k = 0; k < 4; ++k) {
-                const int dx = min(dx0 + k, G.w - 1);
-                const int o = (s0[2 * dx] + s0[2 * dx + 1] + s1[2 * dx] + s1[2 * dx + 1] + 2) >> 2;
-                pk |= (uint32_t)o << (8 * k);
-            }
-            *reinterpret_cast<uint32_t*>(dst + (long long)dy * G.pitch + dx0) = pk;
-        }
-        return;
-    }
-    const bool staged = aligned && xt_s[0].x >= t.sx_lo && xt_s[t.tw - 1].y < t.sx_lo + 16 * t.nq4 &&
-                        yt_s[0].x >= t.sy_lo && yt_s[t.th - 1].y < t.sy_lo + t.nrows;
-    const uint8_t* wb = reinterpret_cast<const uint8_t*>(&win[0][0]);
-    const int nq = (t.tw + 3) >> 2;
-    const float inv_nq = 1.f / (float)nq;
-    auto body = [&](auto row_ptr) __attribute__((always_inline)) {
-        for (int it = threadIdx.x; it < t.th * nq; it += 256) {
-            const int rr = (int)(((float)it + 0.5f) * inv_nq);  // exact: it < 4096, nq <= 64
-            const int q = it - rr * nq;
-            const int dy = t.ty0 + rr, dx0 = t.tx0 + 4 * q;
-            const int4 yt = yt_s[rr];
-            const auto r0 = row_ptr(yt.x), r1 = row_ptr(yt.y);
-            const uint32_t packed = rs_quad(r0, r1, xt_s + 4 * q, yt.z, yt.w, dx0, G.simd_end);
-            *reinterpret_cast<uint32_t*>(dst + (long long)dy * G.pitch + dx0) = packed;
-        }
-    };
-    if (staged) {
-        body([&](int sy) { return wb + (sy - t.sy_lo) * kRsSrcCols - t.sx_lo; });
-    } else {
-        body([&](int sy) { return GlobalRow<kAux>{srs, sy * S.pitch}; });
-    }
-}
-
-// Phase l runs T = (blur tiles of level l) + (resize tiles of level l+1) tiles in order with a
-// one-tile software pipeline: tile t+1's window (and resize tables) is loaded into registers
-// while tile t is computed from LDS.
-__global__ __launch_bounds__(256) void k_pyramid(BatchArgs a, int S, int tab) {
-    constexpr int IWQ = (kBlurTW + 32) / 16, IH = kBlurTH + 8;
-    constexpr int kBlCh = IH * IWQ;                 // 16-byte chunks of a blur window
-    constexpr int kRsQ = kRsSrcCols / 16;
-    constexpr int kRsCh = kRsSrcRows * kRsQ;        // 16-byte chunks of a resize window
-    constexpr int kPre = (kRsCh + 255) / 256;
-    constexpr int kBlPre = (kBlCh + 255) / 256;
-    static_assert(kBlPre <= kPre, "prefetch registers");
-    __shared__ PyrSmem sm;
-    const int wg = xcd_remap(blockIdx.x, gridDim.x);  // the stripes of an image share an XCD
-    const int img = a.img0 + wg / S, k = wg % S;
-    const int tid = threadIdx.x;
-    for (int l = 0; l < a.nlevels; ++l) {
-        const LevelGeom& G = a.lv[l];
-        const int4 e = a.rtab[tab + l * S + k];  // own rows [e.z, e.w)
-        const int nbx = (G.w + kBlurTW - 1) / kBlurTW;
-        const int nb = e.w > e.z ? nbx * ((e.w - e.z + kBlurTH - 1) / kBlurTH) : 0;
-        const bool has_next = l + 1 < a.nlevels;
-        const LevelGeom& D = a.lv[has_next ? l + 1 : l];
-        const int4 n = has_next ? a.rtab[tab + (l + 1) * S + k] : make_int4(0, 0, 0, 0);  // needed rows
-        const int rtx = (D.w + kRsTW - 1) / kRsTW;
-        const int tw_nom = ((D.w + rtx - 1) / rtx + 3) & ~3;
-        const int nr = n.y > n.x ? rtx * ((n.y - n.x + kRsTH - 1) / kRsTH) : 0;
-        const int T = nb + nr;
-        const bool aligned = (G.pitch & 3) == 0;  // level l is the source of level l+1
-        BlurTile bt;
-        bt.l = l;
-        bt.src = a.lvl_base[l] + (long long)img * G.img_stride;
-        bt.dst = a.blur_base[l] + (long long)img * G.bimg_stride;
-        const __amdgpu_buffer_rsrc_t srs = __builtin_amdgcn_make_buffer_rsrc(
-            (void*)bt.src, (short)0, (int)min(G.img_stride, 0x7fffffffLL), 0x00020000);
-        auto blur_xy = [&](int t, int& tx0, int& ty0) {
-            const int by = t / nbx;
-            ty0 = e.z + kBlurTH * by;
-            tx0 = kBlurTW * (t - by * nbx);
-        };
-        auto rs_of = [&](int t) {
-            const int r = t - nb, ry = r / rtx;
-            return rs_tile(D, G, r - ry * rtx, tw_nom, n.x + kRsTH * ry, n.y);
-        };
-        uint4 pre[kPre];
-        int4 pxt = make_int4(0, 0, 0, 0), pyt = make_int4(0, 0, 0, 0);
-        auto issue = [&](int t) {
-            if (t < nb) {
-                blur_xy(t, bt.tx0, bt.ty0);
-#pragma unroll
-                for (int c = 0; c < kBlPre; ++c) {
-                    const int i = tid + 256 * c;
-                    if (i < kBlCh) pre[c] = l == 0 ? blur_chunk<0>(a, bt, i, IWQ) : blur_chunk<kSc1>(a, bt, i, IWQ);
-                }
-            } else if (!D.area2) {
-                const RsTile rt = rs_of(t);
-#pragma unroll
-                for (int c = 0; c < kPre; ++c) {
-                    const int i = tid + 256 * c;
-                    const int row = i / kRsQ, q = i - row * kRsQ;
-                    pre[c] = make_uint4(0, 0, 0, 0);
-                    if (aligned && i < kRsCh && row < rt.nrows && q < rt.nq4) {
-                        const int off = (rt.sy_lo + row) * G.pitch + rt.sx_lo + 16 * q;
-                        const auto v = l == 0 ? __builtin_amdgcn_raw_buffer_load_b128(srs, off, 0, 0)
-                                              : __builtin_amdgcn_raw_buffer_load_b128(srs, off, 0, kSc1);
-                        pre[c] = make_uint4(v[0], v[1], v[2], v[3]);
-                    }
-                }
-                if (tid < rt.tw) pxt = a.rtab[D.xtab_off + rt.tx0 + tid];
-                if (tid < rt.th) pyt = a.rtab[D.ytab_off + rt.ty0 + tid];
-            }
-        };
-        if (T > 0) issue(0);
-        for (int t = 0; t < T; ++t) {
-            if (t < nb) {
-#pragma unroll
-                for (int c = 0; c < kBlPre; ++c) {
-                    const int i = tid + 256 * c;
-                    if (i < kBlCh) (&sm.b.tin4[0][0])[i] = pre[c];
-                }
-            } else if (!D.area2) {
-#pragma unroll
-                for (int c = 0; c < kPre; ++c) {
-                    const int i = tid + 256 * c;
-                    const int row = i / kRsQ, q = i - row * kRsQ;
-                    if (i < kRsCh) *reinterpret_cast<uint4*>(&sm.r.win[row][4 * q]) = pre[c];
-                }
-                sm.r.xt[tid] = pxt;
-                if (tid < kRsTH) sm.r.yt[tid] = pyt;
-            }
-            if (t + 1 < T) issue(t + 1);
-            __syncthreads();
-            if (t < nb) {
-                int tx0, ty0;
-                blur_xy(t, tx0, ty0);
-                blur_tile_compute(G, tx0, ty0, bt.dst, sm.b.tin4, sm.b.hp, e.z, e.w);
-            } else {
-                const RsTile rt = rs_of(t);
-                if (l == 0) rs_compute<0>(a, img, l + 1, rt, aligned, sm.r.xt, sm.r.yt, sm.r.win);
-                else rs_compute<kSc1>(a, img, l + 1, rt, aligned, sm.r.xt, sm.r.yt, sm.r.win);
-            }
-            __syncthreads();
-        }
-        if (has_next) {
-            // level l+1 complete in L2 before any wave of this workgroup reads it
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
-        }
-    }
-}
-
-// ---------------------------------------------------------------------------------------------
 // k_fast_cells: one workgroup per (level, cell), image = blockIdx.y.  Restates the cell loop of
 // ComputeKeyPointsOctTree (ORBextractor_old.cc:807-871) with cv::FAST(cell, kps, th, true):
 // detection on [3,rows-3)x[3,cols-3) of the cell ROI, 3x3 nonmax inside the cell only, iniTh
@@ -792,81 +484,6 @@ __global__ __launch_bounds__(kFastThreads) void k_fast_cells(BatchArgs a, int ce
     CellScratch cs{T, M, list, wcnt};
     const int n = fast_cell_run<CP>(p, src, G.pitch, sh, dword_ok, g, a.ini_th, a.min_th, cs, key_out, ld16);
     if (threadIdx.x == 0) *cnt_out = n;
-}
-
-// k_fast_wave: the same cells, one wave per cell (orb_fast_wave.h: 4 pixels per lane in the
-// compass pre-test), kFastWaveCells<CP> cells per workgroup, each wave with its own LDS tile, so
-// the waves never wait for each other.  Work item = (image, cell of the tile's levels), walked in
-// XCD order so neighbouring cells of one image share an L2.
-template <int CP>
-constexpr int kFastWaveCells = CP == kCellPitchTiny ? 2 : 1;  // LDS: 8 KB per 48-byte-tile cell
-
-template <int CP>
-__global__ __launch_bounds__(64 * kFastWaveCells<CP>) void k_fast_wave(BatchArgs a, int cell0, int ncell) {
-    constexpr int NW = kFastWaveCells<CP>;
-    constexpr int kList = cell_list_cap<CP>();
-    constexpr int RQ = CP / 16;
-    static_assert(CP % 16 == 0, "16-byte LDS rows");
-    __shared__ __attribute__((aligned(16))) uint8_t Ts[NW][CP * CP];
-    __shared__ __attribute__((aligned(16))) uint8_t Ms[NW][CP * CP];
-    __shared__ uint16_t Ls[NW][kList];
-    const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const int lane = (int)(threadIdx.x & 63);
-    const int item = xcd_remap(blockIdx.x, gridDim.x) * NW + w;
-    if (item >= ncell * a.nimages) return;  // wave-uniform; no barrier in this kernel
-    const int img = a.img0 + item / ncell;
-    const int gcell = cell0 + item % ncell;  // flattened over the levels
-    int l = 0;
-    while (l + 1 < a.nlevels && gcell >= a.lv[l + 1].cell_first) ++l;
-    const LevelGeom& G = a.lv[l];
-    const int cell = gcell - G.cell_first;
-    const int ci = cell / G.nCols, cj = cell % G.nCols;
-    int32_t* cnt_out = a.cellcnt + (long long)img * a.cellcnt_img_stride + G.cellcnt_off + cell;
-    uint32_t* key_out = a.cellkeys + (long long)img * a.cellkeys_img_stride + G.cellkey_off +
-                        (long long)cell * G.cell_cap;
-    CellGeom g;
-    g.iniY = kMinBorder + ci * G.hCell;
-    g.iniX = kMinBorder + cj * G.wCell;
-    g.minBorder = kMinBorder;
-    if (g.iniY >= G.maxBY - 3 || g.iniX >= G.maxBX - 6) {  // :812, :821
-        if (lane == 0) *cnt_out = 0;
-        return;
-    }
-    g.rows = min(g.iniY + G.hCell + 6, G.maxBY) - g.iniY;
-    g.cols = min(g.iniX + G.wCell + 6, G.maxBX) - g.iniX;
-    const bool dword_ok = ((G.pitch | G.img_stride) & 3) == 0;
-    const int sh = dword_ok ? (g.iniX & 3) : 0;
-    const uint8_t* base = a.lvl_base[l] + (long long)img * G.img_stride;
-    const long long roi = (long long)g.iniY * G.pitch + (g.iniX - sh);
-    uint8_t* T = Ts[w];
-    uint8_t* M = Ms[w];
-    uint4* T128 = reinterpret_cast<uint4*>(T);
-    uint4* M128 = reinterpret_cast<uint4*>(M);
-    // stage the ROI (16-byte bounds-checked buffer loads) and clear the strength plane
-    const int rows = g.rows;
-    if (dword_ok) {
-        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-            (void*)base, (short)0, (int)min(G.img_stride, 0x7fffffffLL), 0x00020000);
-        const int nq = (sh + g.cols + 15) >> 4;
-        for (int i = lane; i < rows * RQ; i += 64) {
-            const int r = i / RQ, q = i - r * RQ;
-            if (q < nq) {
-                const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(roi + (long long)r * G.pitch + 16 * q), 0, 0);
-                T128[i] = make_uint4(v[0], v[1], v[2], v[3]);
-            }
-            M128[i] = make_uint4(0, 0, 0, 0);
-        }
-    } else {  // rows not dword aligned (odd input widths): byte path, sh = 0
-        const uint8_t* src = base + roi;
-        for (int i = lane; i < rows * CP; i += 64) {
-            const int r = i / CP, c = i - r * CP;
-            if (c < g.cols) T[i] = src[(long long)r * G.pitch + c];
-        }
-        for (int i = lane; i < rows * RQ; i += 64) M128[i] = make_uint4(0, 0, 0, 0);
-    }
-    fw_wave_sync();
-    const int n = fast_cell_wave<CP>(T, M, Ls[w], sh, g, a.ini_th, a.min_th, key_out);
-    if (lane == 0) *cnt_out = n;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1273,69 +890,8 @@ __global__ __launch_bounds__(256) void k_finalize(BatchArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// Hamming k=2 brute force (cv::BFMatcher NORM_HAMMING knnMatch k=2, batchDistance insertion:
-// a candidate enters if d < dist[1], shifts past entries only while they are > d -> the two
-// lexicographically smallest (distance, train index)).  One query per thread in 8 VGPRs, train
-// descriptors staged through LDS 512 at a time and read as broadcasts.
-constexpr int kTrainChunk = 512;
-
-// Top-2 by packed key (distance << 16 | train index): integer order == lexicographic
-// (distance, index) order, so the insertion rule becomes k1' = min(k1, k), k2' = med3(k1, k2, k)
-// with no branches.  Requires nt < 65536 (checked on the host).  The train set is split over
-// kKnnSplit workgroups per query block (occupancy); a merge kernel folds the partial pairs.
-constexpr int kKnnSplit = 4;
-
 __device__ inline uint32_t med3_u32(uint32_t a, uint32_t b, uint32_t c) {
     return max(min(a, b), min(max(a, b), c));  // lowers to v_med3_u32
-}
-
-__device__ inline uint32_t hamming256(const uint4& qa, const uint4& qb, const uint4& ta, const uint4& tb) {
-    const uint32_t s0 = __popc(qa.x ^ ta.x) + __popc(qa.y ^ ta.y);
-    const uint32_t s1 = __popc(qa.z ^ ta.z) + __popc(qa.w ^ ta.w);
-    const uint32_t s2 = __popc(qb.x ^ tb.x) + __popc(qb.y ^ tb.y);
-    const uint32_t s3 = __popc(qb.z ^ tb.z) + __popc(qb.w ^ tb.w);
-    return (s0 + s1) + (s2 + s3);
-}
-
-// Partial top-2 of query qi over train rows [t0, t1) -> packed keys.
-__device__ inline void knn2_partial(const uint8_t* q, int nq, const uint8_t* t, int t0, int t1, int qi,
-                                    uint4 (*tl)[2], uint32_t* k1o, uint32_t* k2o) {
-    uint4 qa = make_uint4(0, 0, 0, 0), qb = qa;
-    if (qi < nq) {
-        const uint4* qp = reinterpret_cast<const uint4*>(q + (long long)qi * 32);
-        qa = qp[0];
-        qb = qp[1];
-    }
-    uint32_t k1 = 0xFFFFFFFFu, k2 = 0xFFFFFFFFu;
-    for (int base = t0; base < t1; base += kTrainChunk) {
-        const int m = min(kTrainChunk, t1 - base);
-        __syncthreads();
-        for (int i = threadIdx.x; i < m; i += blockDim.x) {
-            const uint4* tp = reinterpret_cast<const uint4*>(t + (long long)(base + i) * 32);
-            tl[i][0] = tp[0];
-            tl[i][1] = tp[1];
-        }
-        __syncthreads();
-        int j = 0;
-        for (; j + 4 <= m; j += 4) {
-            uint32_t kk[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-                kk[u] = (hamming256(qa, qb, tl[j + u][0], tl[j + u][1]) << 16) | (uint32_t)(base + j + u);
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                k2 = med3_u32(k1, k2, kk[u]);
-                k1 = min(k1, kk[u]);
-            }
-        }
-        for (; j < m; ++j) {
-            const uint32_t key = (hamming256(qa, qb, tl[j][0], tl[j][1]) << 16) | (uint32_t)(base + j);
-            k2 = med3_u32(k1, k2, key);
-            k1 = min(k1, key);
-        }
-    }
-    *k1o = k1;
-    *k2o = k2;
 }
 
 __device__ inline void knn2_store(uint32_t k1, uint32_t k2, int qi, int32_t* i1, int32_t* d1,
@@ -1344,68 +900,6 @@ __device__ inline void knn2_store(uint32_t k1, uint32_t k2, int qi, int32_t* i1,
     d1[qi] = k1 == 0xFFFFFFFFu ? 0x7fffffff : (int32_t)(k1 >> 16);
     i2[qi] = k2 == 0xFFFFFFFFu ? -1 : (int32_t)(k2 & 0xFFFF);
     d2[qi] = k2 == 0xFFFFFFFFu ? 0x7fffffff : (int32_t)(k2 >> 16);
-}
-
-struct KnnPart {
-    uint32_t* keys;  // [pair][split][out_cap][2]
-};
-
-__global__ __launch_bounds__(256) void k_knn2_pairs(MatchArgs m, KnnPart part) {
-    __shared__ uint4 tl[kTrainChunk][2];
-    const int pair = m.pair0 + blockIdx.z, split = blockIdx.y;
-    const int qimg = 2 * pair, timg = 2 * pair + 1;
-    const int qn = m.out_n[qimg], tn = m.out_n[timg];
-    const int q0 = m.stereo_only ? m.out_mono[qimg] : 0;
-    const int tq0 = m.stereo_only ? m.out_mono[timg] : 0;
-    const int nq = qn > q0 ? qn - q0 : 0, nt = tn > tq0 ? tn - tq0 : 0;
-    if ((int)(blockIdx.x * blockDim.x) >= nq) return;
-    const int per = (nt + kKnnSplit - 1) / kKnnSplit;
-    const int t0 = min(nt, split * per), t1 = min(nt, t0 + per);
-    const uint8_t* q = m.desc + ((long long)qimg * m.out_cap + q0) * 32;
-    const uint8_t* t = m.desc + ((long long)timg * m.out_cap + tq0) * 32;
-    const int qi = blockIdx.x * blockDim.x + threadIdx.x;
-    uint32_t k1, k2;
-    knn2_partial(q, nq, t, t0, t1, qi, tl, &k1, &k2);
-    if (qi < nq) {
-        uint2* o = reinterpret_cast<uint2*>(part.keys) + ((long long)pair * kKnnSplit + split) * m.out_cap + qi;
-        *o = make_uint2(k1, k2);
-    }
-}
-
-__global__ __launch_bounds__(256) void k_knn2_merge(MatchArgs m, KnnPart part) {
-    const int pair = m.pair0 + blockIdx.y;
-    const int qimg = 2 * pair, timg = 2 * pair + 1;
-    const int qn = m.out_n[qimg];
-    const int q0 = m.stereo_only ? m.out_mono[qimg] : 0;
-    const int nq = qn > q0 ? qn - q0 : 0;
-    const int tn = m.out_n[timg];
-    const int tq0 = m.stereo_only ? m.out_mono[timg] : 0;
-    const int nt = tn > tq0 ? tn - tq0 : 0;
-    if (blockIdx.x == 0 && threadIdx.x == 0) m.nq[pair] = nq;
-    const int qi = blockIdx.x * blockDim.x + threadIdx.x;
-    if (qi >= nq) return;
-    const int per = (nt + kKnnSplit - 1) / kKnnSplit;
-    uint32_t k1 = 0xFFFFFFFFu, k2 = 0xFFFFFFFFu;
-    for (int sp = 0; sp < kKnnSplit; ++sp) {
-        if (sp * per >= nt) break;
-        const uint2 v = reinterpret_cast<const uint2*>(part.keys)[((long long)pair * kKnnSplit + sp) * m.out_cap + qi];
-        k2 = med3_u32(k1, k2, v.x);
-        k1 = min(k1, v.x);
-        k2 = med3_u32(k1, k2, v.y);
-        k1 = min(k1, v.y);
-    }
-    const long long o = (long long)pair * m.out_cap;
-    knn2_store(k1, k2, qi, m.idx1 + o, m.dist1 + o, m.idx2 + o, m.dist2 + o);
-}
-
-__global__ __launch_bounds__(256) void k_knn2_plain(const uint8_t* q, int nq, const uint8_t* t,
-                                                    int nt, int32_t* i1, int32_t* d1, int32_t* i2,
-                                                    int32_t* d2) {
-    __shared__ uint4 tl[kTrainChunk][2];
-    const int qi = blockIdx.x * blockDim.x + threadIdx.x;
-    uint32_t k1, k2;
-    knn2_partial(q, nq, t, 0, nt, qi, tl, &k1, &k2);
-    if (qi < nq) knn2_store(k1, k2, qi, i1, d1, i2, d2);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1601,31 +1095,10 @@ __global__ __launch_bounds__(256) void k_knn2_mfma_plain(const uint8_t* q, int n
 }
 
 // ---------------------------------------------------------------------------------------------
-hipError_t launch_resize(const BatchArgs& a, int level, hipStream_t s) {
-    const LevelGeom& G = a.lv[level];
-    const LevelGeom& S = a.lv[level - 1];
-    dim3 grid((G.w + kRsTW - 1) / kRsTW, (G.h + kRsTH - 1) / kRsTH, a.nimages);
-    if (4 * S.w <= 5 * G.w && 4 * S.h <= 5 * G.h)  // scale <= 1.25: the small window
-        hipLaunchKernelGGL((k_resize<kRsSrcRowsS, kRsSrcColsS>), grid, dim3(256), 0, s, a, level);
-    else
-        hipLaunchKernelGGL((k_resize<kRsSrcRows, kRsSrcCols>), grid, dim3(256), 0, s, a, level);
-    return hipGetLastError();
-}
-hipError_t launch_blur(const BatchArgs& a, hipStream_t s) {
-    // persistent: 8192 workgroups (32 per CU, about 4 resident at a time) loop over the tiles
-    const int total = a.total_tiles * a.nimages;
-    hipLaunchKernelGGL(k_blur, dim3(std::min(total, 8192)), dim3(256), 0, s, a, 0, a.total_tiles);
-    return hipGetLastError();
-}
 hipError_t launch_blur_level(const BatchArgs& a, int l, hipStream_t s) {
     const LevelGeom& G = a.lv[l];
     const int n = G.tiles_x * G.tiles_y;
     hipLaunchKernelGGL(k_blur, dim3(std::min(n * a.nimages, 8192)), dim3(256), 0, s, a, G.tile_first, n);
-    return hipGetLastError();
-}
-hipError_t launch_pyramid(const BatchArgs& a, int stripe_log2, hipStream_t s) {
-    const int S = 1 << stripe_log2;
-    hipLaunchKernelGGL(k_pyramid, dim3(a.nimages * S), dim3(256), 0, s, a, S, a.stripe_tab_off[stripe_log2]);
     return hipGetLastError();
 }
 void fast_cell_range(const BatchArgs& a, int tile, int* c0, int* c1) {
@@ -1638,21 +1111,6 @@ hipError_t launch_fast_cells(const BatchArgs& a, int tile, hipStream_t s) {
     int c0, c1;
     fast_cell_range(a, tile, &c0, &c1);
     if (c1 <= c0) return hipSuccess;
-    static const bool one_wave = getenv("ORBGPU_FAST_WAVE") != nullptr;  // one wave per cell
-    if (one_wave) {
-        const long long items = (long long)(c1 - c0) * a.nimages;
-        auto wgs = [&](int nw) { return dim3((unsigned)((items + nw - 1) / nw)); };
-        if (tile == kCellPitchTiny)
-            hipLaunchKernelGGL(k_fast_wave<kCellPitchTiny>, wgs(kFastWaveCells<kCellPitchTiny>),
-                               dim3(64 * kFastWaveCells<kCellPitchTiny>), 0, s, a, c0, c1 - c0);
-        else if (tile == kCellPitchSmall)
-            hipLaunchKernelGGL(k_fast_wave<kCellPitchSmall>, wgs(kFastWaveCells<kCellPitchSmall>),
-                               dim3(64 * kFastWaveCells<kCellPitchSmall>), 0, s, a, c0, c1 - c0);
-        else
-            hipLaunchKernelGGL(k_fast_wave<kCellMax>, wgs(kFastWaveCells<kCellMax>),
-                               dim3(64 * kFastWaveCells<kCellMax>), 0, s, a, c0, c1 - c0);
-        return hipGetLastError();
-    }
     const dim3 grid(c1 - c0, a.nimages), block(kFastThreads);
     const uint32_t d = (uint32_t)(c1 - c0);
     const uint32_t magic = d > 1 ? 0xFFFFFFFFu / d + 1u : 0u;  // ceil(2^32 / d) for d >= 2
@@ -1662,12 +1120,17 @@ hipError_t launch_fast_cells(const BatchArgs& a, int tile, hipStream_t s) {
     return hipGetLastError();
 }
 hipError_t launch_octree(const BatchArgs& a, hipStream_t s) {
-    if (a.oct_lds_bytes > 65536) {
+    // the dynamic-LDS limit is raised once per size (not on every launch: the launch sequence may
+    // be captured into a hipGraph, orb_runtime.cpp run_batch)
+    static std::atomic<int> lds_set{65536};
+    if (a.oct_lds_bytes > lds_set.load()) {
         for (const void* f : {reinterpret_cast<const void*>(k_octree<512>),
                               reinterpret_cast<const void*>(k_octree_retry)}) {
             hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, a.oct_lds_bytes);
             if (e != hipSuccess) return e;
         }
+        int cur = lds_set.load();
+        while (a.oct_lds_bytes > cur && !lds_set.compare_exchange_weak(cur, a.oct_lds_bytes)) {}
     }
     const int split = a.nimages < a.oct_split_min_images ? a.nlevels : std::min(a.oct_split, a.nlevels);
     if (split > 0)
@@ -1698,30 +1161,15 @@ hipError_t launch_finalize(const BatchArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_finalize, dim3(a.nimages), dim3(256), 0, s, a);
     return hipGetLastError();
 }
-static bool knn_valu() {  // diagnostics: the VALU popcount matcher
-    static const bool v = getenv("ORBGPU_KNN_VALU") != nullptr;
-    return v;
-}
-hipError_t launch_knn2_pairs(const MatchArgs& m, int npairs, int qblocks, void* scratch, hipStream_t s) {
-    if (!knn_valu()) {
-        hipLaunchKernelGGL(k_knn2_mfma_pairs, dim3((m.out_cap + kKnnQ - 1) / kKnnQ, npairs), dim3(256), 0, s, m);
-        return hipGetLastError();
-    }
-    KnnPart part{reinterpret_cast<uint32_t*>(scratch)};
-    hipLaunchKernelGGL(k_knn2_pairs, dim3(qblocks, kKnnSplit, npairs), dim3(256), 0, s, m, part);
-    hipLaunchKernelGGL(k_knn2_merge, dim3(qblocks, npairs), dim3(256), 0, s, m, part);
+hipError_t launch_knn2_pairs(const MatchArgs& m, int npairs, hipStream_t s) {
+    hipLaunchKernelGGL(k_knn2_mfma_pairs, dim3((m.out_cap + kKnnQ - 1) / kKnnQ, npairs), dim3(256), 0, s, m);
     return hipGetLastError();
 }
-size_t knn2_scratch_bytes(int npairs, int out_cap) { return (size_t)npairs * kKnnSplit * out_cap * 8 + 256; }
 hipError_t launch_knn2_plain(const uint8_t* q, int nq, const uint8_t* t, int nt, int32_t* i1,
                              int32_t* d1, int32_t* i2, int32_t* d2, hipStream_t s) {
     if (nq == 0) return hipSuccess;
-    if (!knn_valu()) {
-        hipLaunchKernelGGL(k_knn2_mfma_plain, dim3((nq + kKnnQ - 1) / kKnnQ), dim3(256), 0, s, q, nq, t, nt, i1,
-                           d1, i2, d2);
-        return hipGetLastError();
-    }
-    hipLaunchKernelGGL(k_knn2_plain, dim3((nq + 255) / 256), dim3(256), 0, s, q, nq, t, nt, i1, d1, i2, d2);
+    hipLaunchKernelGGL(k_knn2_mfma_plain, dim3((nq + kKnnQ - 1) / kKnnQ), dim3(256), 0, s, q, nq, t, nt, i1,
+                       d1, i2, d2);
     return hipGetLastError();
 }
 

@@ -40,11 +40,11 @@ int fail(int code, const std::string& msg) {
     } while (0)
 
 enum Stage { ST_RESIZE, ST_BLUR, ST_FAST48, ST_FAST, ST_FAST_TOP, ST_OCTREE, ST_ORIENT, ST_FINAL, ST_KNN,
-             ST_PYRAMID, ST_STEREO, ST_GRID, ST_SBS, ST_SOA, ST_SBP, ST_FISHEYE, ST_COUNT };
+             ST_STEREO, ST_GRID, ST_SBS, ST_SOA, ST_SBP, ST_FISHEYE, ST_COUNT };
 // names as rocprofv3 shows the kernels (templates with their argument)
 const char* kStageNames[ST_COUNT] = {"k_blur_resize",    "k_blur",   "k_fast_cells<48>", "k_fast_cells<64>",
                                      "k_fast_cells<80>", "k_octree", "k_orient_desc",    "k_finalize",
-                                     "k_knn2",           "k_pyramid", "k_stereo",         "k_undistort_grid",
+                                     "k_knn2",           "k_stereo",  "k_undistort_grid",
                                      "k_sbs_split",      "k_pack_soa",       "k_sbp",
                                      "k_fisheye_stereo"};
 
@@ -84,6 +84,15 @@ struct Pending {
     hipEvent_t a, b;
 };
 
+// Device-to-host copy on the context's own stream, waited for before the call returns (the
+// callers ran ctx_sync first, so the stream is idle and the copy sees every result).  Never a
+// null-stream hipMemcpy: that would also order against other contexts' and torch's work.
+#define D2H(dst, src, bytes)                                                               \
+    do {                                                                                   \
+        HIP_TRY(hipMemcpyAsync((dst), (src), (bytes), hipMemcpyDeviceToHost, c->stream));  \
+        HIP_TRY(hipStreamSynchronize(c->stream));                                          \
+    } while (0)
+
 }  // namespace
 
 struct orbgpu_ctx {
@@ -104,7 +113,7 @@ struct orbgpu_ctx {
     // device buffers
     DevBuf input, pyr, blur, rtab, cellkeys, cellcnt, octws, lvlkey, lvlangle, lvldesc, lvlcnt,
         status, outkps, outdesc, outn, outmono, laps, midx1, mdist1, midx2, mdist2, mnq, scratch,
-        octdbg, knnpart, strow, stidx, stur, stdepth, stsad, gxy, gcell, gstart, gidx, sbs, soa, m16,
+        octdbg, strow, stidx, stur, stdepth, stsad, gxy, gcell, gstart, gidx, sbs, soa, m16,
         sbpmp, sbpoff, sbpcand, sbpblk, sbpmatch, sbpnm, sbplr, fel2r, fer2l, fedepth, fep3d, fecnt;
     float grid_bounds[4] = {0, 0, 0, 0}, grid_inv[2] = {0, 0};  // of the last undistort_grid
     int sbp_frames = 0, sbp_step = 1, sbp_two_cam = 0;
@@ -129,16 +138,15 @@ struct orbgpu_ctx {
     // idle GPU per step (ORBGPU_ISOLATE=<stage bit mask> turns it on)
     unsigned isolate_mask = 0;
     bool serialize = false;  // profiling: every stage isolated
+    bool oct_stamps = false; // ORBGPU_OCT_STAMPS (read once at create): octree phase clocks
+    // the captured launch sequence of a one-stream batch (run_batch), keyed by {n, w, h, slot}
+    bool use_graph = true;   // ORBGPU_GRAPH=0 launches every kernel directly (A/B)
+    hipGraphExec_t graph_exec = nullptr;
+    int graph_key[4] = {-1, -1, -1, -1};
     std::vector<int32_t> laps_host;  // lapping areas currently in `laps` (device), per image
     bool need_fork = true;           // the main stream holds work the sub streams must wait for
     bool stagger = true;             // ORBGPU_STAGGER=0: the chunks start every layout in lockstep
     std::vector<hipEvent_t> stagger_ev;
-    // pyramid + blur as the per-level k_resize launches and k_blur (default) or as one k_pyramid
-    // launch (ORBGPU_PYR=1; measured slower on the 128-pair bench: 618 vs ~530 us per step, its
-    // stripes recompute the halo rows and each workgroup walks its tiles serially);
-    // ORBGPU_PYR_STRIPES=<log2> fixes the stripes per image
-    bool pyr_mode = false;
-    int pyr_stripes_log2 = -1;
     struct ChunkRec { int img0, n; hipStream_t st; };
     std::vector<ChunkRec> last_chunks;
     int last_images = 0, last_w = 0, last_h = 0, last_pairs = 0;
@@ -247,9 +255,20 @@ int alloc_all(orbgpu_ctx* c, int n_images) {
     return r ? fail(ORBGPU_ERR_HIP, "hipMalloc failed (device memory)") : 0;
 }
 
+int ctx_sync(orbgpu_ctx* c, bool with_copy = false);
+
+void drop_graph(orbgpu_ctx* c) {
+    if (c->graph_exec) hipGraphExecDestroy(c->graph_exec);
+    c->graph_exec = nullptr;
+    c->graph_key[0] = -1;
+}
+
 // Level geometry for a w x h image (input row stride = w in the batch buffer).
 int set_geometry(orbgpu_ctx* c, int w, int h) {
     if (c->gw == w && c->gh == h) return 0;
+    if (c->gw >= 0)  // the tables and buffers below are still read by the last batch's kernels
+        if (int e = ctx_sync(c, true)) return e;
+    drop_graph(c);  // its launches carry the old geometry and buffers
     const int L = c->prm.nlevels;
     BatchArgs& A = c->A;
     A = BatchArgs{};
@@ -359,41 +378,6 @@ int set_geometry(orbgpu_ctx* c, int w, int h) {
             G.tile_quad_off = push_ints(tq);
         }
     }
-    // k_pyramid stripe tables (1, 2, 4, 8, 16 stripes per image): own rows k*h/S .. (k+1)*h/S of
-    // every level; needed rows of level l = own rows +- 3 (blur halo, REFLECT_101 stays inside)
-    // joined with the source rows of the rows needed at level l+1, from the top level down
-    for (int si = 0; si < kPyrStripeKinds; ++si) {
-        const int S = 1 << si;
-        A.stripe_tab_off[si] = (int)c->rtab_host.size();
-        std::vector<int4> tab((size_t)L * S);
-        for (int k = 0; k < S; ++k) {
-            int nlo = 0, nhi = 0;
-            for (int l = L - 1; l >= 0; --l) {
-                const LevelGeom& G = A.lv[l];
-                const int own_lo = (int)((long long)k * G.h / S), own_hi = (int)((long long)(k + 1) * G.h / S);
-                int lo = std::max(0, own_lo - 3), hi = std::min(G.h, own_hi + 3);
-                if (l + 1 < L && nhi > nlo) {
-                    const LevelGeom& U = A.lv[l + 1];
-                    int slo, shi;
-                    if (U.area2) {
-                        slo = 2 * nlo;
-                        shi = 2 * nhi;
-                    } else {
-                        slo = c->rtab_host[U.ytab_off + nlo].x;
-                        shi = c->rtab_host[U.ytab_off + nhi - 1].y + 1;
-                    }
-                    lo = std::min(lo, slo);
-                    hi = std::max(hi, shi);
-                }
-                lo = std::max(lo, 0);
-                hi = std::min(hi, G.h);
-                tab[(size_t)l * S + k] = make_int4(lo, hi, own_lo, own_hi);
-                nlo = lo;
-                nhi = hi;
-            }
-        }
-        c->rtab_host.insert(c->rtab_host.end(), tab.begin(), tab.end());
-    }
     c->pyr_img = round_up_ll(pyr, 256);
     c->blur_img = round_up_ll(blr, 256);
     c->cellkeys_img = ck;
@@ -462,21 +446,17 @@ int set_geometry(orbgpu_ctx* c, int w, int h) {
     // FAST LDS tiles: each level takes the smallest tile its cell ROIs (+3 alignment bytes) fit:
     // 48 bytes, else 64, else 80.  Cells grow as the levels shrink (fewer, wider cells) but not
     // monotonically in both directions (640x480: level 6's cells are 51 rows tall, level 7's 42),
-    // so the tiers are chosen per level.  The one-wave FAST kernel finds a cell's level from the
-    // flattened index, so under ORBGPU_FAST_WAVE the tiers stay level prefixes.
+    // so the tiers are chosen per level.
     auto fits = [&](int l, int P) { return A.lv[l].wCell + 9 <= P && A.lv[l].hCell + 6 <= P; };
     int tier[kMaxLevels];
-    const bool prefix_tiers = getenv("ORBGPU_FAST_WAVE") != nullptr;
     int min_tier = 0;
     if (const char* fp = getenv("ORBGPU_FAST_PITCH")) {  // diagnostics: force the larger tiles
         const int P = atoi(fp);
         min_tier = P == kCellMax ? 2 : P == kCellPitchSmall ? 1 : 0;
     }
-    for (int l = 0, floor_t = min_tier; l < L; ++l) {
-        int t = fits(l, kCellPitchTiny) ? 0 : fits(l, kCellPitchSmall) ? 1 : 2;
-        t = std::max(t, prefix_tiers ? floor_t : min_tier);
-        floor_t = t;
-        tier[l] = t;
+    for (int l = 0; l < L; ++l) {
+        const int t = fits(l, kCellPitchTiny) ? 0 : fits(l, kCellPitchSmall) ? 1 : 2;
+        tier[l] = std::max(t, min_tier);
     }
     // k_fast_cells per-cell records, two int4 per cell: {level, iniX, iniY, rows | cols << 16} and
     // {cell-count index, cell-key index, skip, 0} (the cell loop's :807-821 geometry), grouped by
@@ -514,8 +494,10 @@ int set_geometry(orbgpu_ctx* c, int w, int h) {
     }
     int r = alloc_all(c, c->max_images);
     if (r) return r;
-    HIP_TRY(hipMemcpy(c->rtab.p, c->rtab_host.data(), sizeof(int4) * c->rtab_host.size(),
-                      hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpyAsync(c->rtab.p, c->rtab_host.data(), sizeof(int4) * c->rtab_host.size(),
+                           hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));  // pageable source
+    c->need_fork = true;
     for (int l = 0; l < L; ++l) {
         A.lvl_base[l] = l == 0 ? nullptr : c->pyr.as<uint8_t>() + pyr_off[l];
         A.blur_base[l] = c->blur.as<uint8_t>() + blur_off[l];
@@ -593,6 +575,29 @@ int rejoin(orbgpu_ctx* c, hipStream_t s) {
     HIP_TRY(hipStreamWaitEvent(c->stream, c->ext_done, 0));
     c->need_fork = true;
     return 0;
+}
+
+// Waits for the work of this context's own streams (the chunk streams, and the copy stream when
+// with_copy) -- never the whole device: two contexts driven from two threads (one extractor per
+// eye, Frame.cc:142-145) or torch work beside them do not wait for each other.  Work enqueued on
+// a caller's stream is covered through rejoin(), which every such entry point calls.
+int ctx_sync(orbgpu_ctx* c, bool with_copy) {
+    HIP_TRY(hipSetDevice(c->device));
+    for (hipStream_t s : c->sub) HIP_TRY(hipStreamSynchronize(s));
+    if (with_copy && c->copy) HIP_TRY(hipStreamSynchronize(c->copy));
+    return 0;
+}
+
+// True when p points into device memory (hipMalloc / torch CUDA tensors): the device entry
+// points refuse host pointers instead of faulting on them.  A failed query leaves a sticky
+// error for hipGetLastError, which the launchers read: clear it.
+bool device_ptr(const void* p) {
+    hipPointerAttribute_t at{};
+    if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return at.type == hipMemoryTypeDevice || at.type == hipMemoryTypeManaged;
 }
 
 // A per-image count the device wrote: k_finalize stores -5 (octree workspace overflow) or -2
@@ -702,10 +707,8 @@ int orbgpu_create(const orbgpu_params* p, int device, int max_width, int max_hei
         if (iso) c->isolate_mask = (unsigned)strtoul(iso, nullptr, 0);
         const char* sg = getenv("ORBGPU_STAGGER");
         if (sg) c->stagger = atoi(sg) != 0;
-        const char* pm = getenv("ORBGPU_PYR");
-        if (pm) c->pyr_mode = atoi(pm) != 0;
-        const char* ps = getenv("ORBGPU_PYR_STRIPES");
-        if (ps) c->pyr_stripes_log2 = std::max(0, std::min(kPyrStripeKinds - 1, atoi(ps)));
+        c->oct_stamps = getenv("ORBGPU_OCT_STAMPS") != nullptr;
+        if (const char* g = getenv("ORBGPU_GRAPH")) c->use_graph = atoi(g) != 0;
     }
     int r = ensure_input(c, 1, max_width, max_height);
     if (!r) r = set_geometry(c, max_width, max_height);
@@ -728,12 +731,13 @@ int orbgpu_destroy(orbgpu_ctx* c) {
                       &c->octws,   &c->lvlkey,  &c->lvlangle, &c->lvldesc, &c->lvlcnt, &c->status,
                       &c->outkps,  &c->outdesc, &c->outn,   &c->outmono, &c->laps,     &c->midx1,
                       &c->mdist1,  &c->midx2,   &c->mdist2, &c->mnq,     &c->scratch, &c->octdbg,
-                      &c->knnpart, &c->strow,  &c->stidx, &c->stur,    &c->stdepth,  &c->stsad,
+                      &c->strow,  &c->stidx, &c->stur,    &c->stdepth,  &c->stsad,
                       &c->gxy,     &c->gcell,  &c->gstart, &c->gidx,    &c->sbs,      &c->soa,
                       &c->m16,     &c->sbpmp,  &c->sbpoff, &c->sbpcand, &c->sbpblk,  &c->sbpmatch,
                       &c->sbpnm,   &c->sbplr,  &c->fel2r,  &c->fer2l,   &c->fedepth, &c->fep3d,
                       &c->fecnt};
     for (DevBuf* b : bufs) b->release();
+    drop_graph(c);
     for (size_t k = 1; k < c->sub.size(); ++k) hipStreamDestroy(c->sub[k]);
     if (c->fork) hipEventDestroy(c->fork);
     if (c->ext_done) hipEventDestroy(c->ext_done);
@@ -844,7 +848,7 @@ int orbgpu_run_batch(orbgpu_ctx* c, int n, int w, int h, const int32_t* laps, vo
     A.nimages = n;
     A.img0 = 0;
     A.octdbg = nullptr;
-    if (getenv("ORBGPU_OCT_STAMPS")) {  // diagnostic build of the octree phase clocks
+    if (c->oct_stamps) {  // diagnostic build of the octree phase clocks
         const size_t bytes = (size_t)n * kMaxLevels * 8 * 8;
         if (!c->octdbg.ensure(bytes)) {
             hipMemsetAsync(c->octdbg.p, 0, bytes, s);
@@ -871,7 +875,7 @@ int orbgpu_run_batch(orbgpu_ctx* c, int n, int w, int h, const int32_t* laps, vo
     const int K = (!stream && (n % 2) == 0) ? std::min((int)c->sub.size(), n / 2) : 1;
     // a different sub-batch layout than last time may put an image on another stream: drain first
     if (!c->last_chunks.empty() && ((int)c->last_chunks.size() != K || c->last_images != n))
-        HIP_TRY(hipDeviceSynchronize());
+        if (int e_ = ctx_sync(c)) return e_;
     const bool relayout = c->last_chunks.empty() || (int)c->last_chunks.size() != K || c->last_images != n;
     if (K > 1) {
         // sub stream k > 0 waits for the main stream only when the main stream holds work it
@@ -923,99 +927,120 @@ int orbgpu_run_batch(orbgpu_ctx* c, int n, int w, int h, const int32_t* laps, vo
         }
         return 0;
     };
-    // the whole pyramid + blur in one k_pyramid launch per chunk: 2^sl row stripes per image,
-    // enough workgroups for the batch to cover the chip (about 1024), at most 16 per image
-    int sl = 0;
-    if (c->pyr_stripes_log2 >= 0) {
-        sl = c->pyr_stripes_log2;
-    } else {
-        while (sl + 1 < kPyrStripeKinds && (n << sl) < 1024) ++sl;
-    }
-    if (stagger) {
-        // chunk-major: chunk k's first kernel waits for chunk k-1's pyramid + blur
-        for (size_t k = 0; k < chunks.size(); ++k) {
-            const Chunk& ch = chunks[k];
-            BatchArgs B = A;
-            B.img0 = ch.img0;
-            B.nimages = ch.n;
-            if (k > 0) HIP_TRY(hipStreamWaitEvent(ch.st, c->stagger_ev[k - 1], 0));
-            if (c->pyr_mode) {
-                if ((r = timed(c, ST_PYRAMID, ch.st, [&] { return launch_pyramid(B, sl, ch.st); }))) return r;
-            } else {
+    // the kernel sequence of this batch (every launch goes to the chunk streams)
+    auto launch_all = [&]() -> int {
+        int r = 0;
+        if (stagger) {
+            // chunk-major: chunk k's first kernel waits for chunk k-1's pyramid + blur
+            for (size_t k = 0; k < chunks.size(); ++k) {
+                const Chunk& ch = chunks[k];
+                BatchArgs B = A;
+                B.img0 = ch.img0;
+                B.nimages = ch.n;
+                if (k > 0) HIP_TRY(hipStreamWaitEvent(ch.st, c->stagger_ev[k - 1], 0));
                 for (int l = 1; l < A.nlevels; ++l)
                     if ((r = timed(c, ST_RESIZE, ch.st, [&] { return launch_blur_resize(B, l, ch.st); }))) return r;
                 const int lt = A.nlevels - 1;
                 if ((r = timed(c, ST_BLUR, ch.st, [&] { return launch_blur_level(B, lt, ch.st); }))) return r;
+                HIP_TRY(hipEventRecord(c->stagger_ev[k], ch.st));
             }
-            HIP_TRY(hipEventRecord(c->stagger_ev[k], ch.st));
-        }
-    } else if (c->pyr_mode) {
-        r = each(ST_PYRAMID, [&](const BatchArgs& B, hipStream_t st) { return launch_pyramid(B, sl, st); });
-        if (r) return r;
-    } else {
-        // level l - 1's blur and level l in one pass over level l - 1, then the last level's blur
-        for (int l = 1; l < A.nlevels; ++l) {
-            r = each(ST_RESIZE, [&](const BatchArgs& B, hipStream_t st) { return launch_blur_resize(B, l, st); });
-            if (r) return r;
-        }
-        const int lt = A.nlevels - 1;
-        if ((r = each(ST_BLUR, [&](const BatchArgs& B, hipStream_t st) { return launch_blur_level(B, lt, st); }))) return r;
-    }
-    {   // the FAST tiles as one group: one join / fork around all of them when isolated
-        const int tiles[3] = {kCellPitchTiny, kCellPitchSmall, kCellMax};
-        const int stages[3] = {ST_FAST48, ST_FAST, ST_FAST_TOP};
-        bool any[3], iso = false;
-        for (int t = 0; t < 3; ++t) {
-            int c0, c1;
-            fast_cell_range(A, tiles[t], &c0, &c1);
-            any[t] = c1 > c0;
-            iso = iso || (any[t] && chunks.size() > 1 && (c->serialize || ((c->isolate_mask >> stages[t]) & 1u)));
-        }
-        if (iso) {
-            for (size_t k = 1; k < chunks.size(); ++k) {
-                HIP_TRY(hipEventRecord(c->join[k], chunks[k].st));
-                HIP_TRY(hipStreamWaitEvent(chunks[0].st, c->join[k], 0));
+        } else {
+            // level l - 1's blur and level l in one pass over level l - 1, then the last level's blur
+            for (int l = 1; l < A.nlevels; ++l) {
+                r = each(ST_RESIZE, [&](const BatchArgs& B, hipStream_t st) { return launch_blur_resize(B, l, st); });
+                if (r) return r;
             }
+            const int lt = A.nlevels - 1;
+            if ((r = each(ST_BLUR, [&](const BatchArgs& B, hipStream_t st) { return launch_blur_level(B, lt, st); }))) return r;
         }
-        for (int t = 0; t < 3; ++t) {
-            if (!any[t]) continue;
-            for (const Chunk& ch : chunks) {
-                BatchArgs B = A;
-                if (!iso) {
-                    B.img0 = ch.img0;
-                    B.nimages = ch.n;
+        {   // the FAST tiles as one group: one join / fork around all of them when isolated
+            const int tiles[3] = {kCellPitchTiny, kCellPitchSmall, kCellMax};
+            const int stages[3] = {ST_FAST48, ST_FAST, ST_FAST_TOP};
+            bool any[3], iso = false;
+            for (int t = 0; t < 3; ++t) {
+                int c0, c1;
+                fast_cell_range(A, tiles[t], &c0, &c1);
+                any[t] = c1 > c0;
+                iso = iso || (any[t] && chunks.size() > 1 && (c->serialize || ((c->isolate_mask >> stages[t]) & 1u)));
+            }
+            if (iso) {
+                for (size_t k = 1; k < chunks.size(); ++k) {
+                    HIP_TRY(hipEventRecord(c->join[k], chunks[k].st));
+                    HIP_TRY(hipStreamWaitEvent(chunks[0].st, c->join[k], 0));
                 }
-                const hipStream_t st = ch.st;
-                const int tile = tiles[t];
-                if ((r = timed(c, stages[t], st, [&] { return launch_fast_cells(B, tile, st); }))) return r;
-                if (iso) break;  // whole batch on the main stream
+            }
+            for (int t = 0; t < 3; ++t) {
+                if (!any[t]) continue;
+                for (const Chunk& ch : chunks) {
+                    BatchArgs B = A;
+                    if (!iso) {
+                        B.img0 = ch.img0;
+                        B.nimages = ch.n;
+                    }
+                    const hipStream_t st = ch.st;
+                    const int tile = tiles[t];
+                    if ((r = timed(c, stages[t], st, [&] { return launch_fast_cells(B, tile, st); }))) return r;
+                    if (iso) break;  // whole batch on the main stream
+                }
+            }
+            if (iso) {
+                HIP_TRY(hipEventRecord(c->fork, chunks[0].st));
+                for (size_t k = 1; k < chunks.size(); ++k) HIP_TRY(hipStreamWaitEvent(chunks[k].st, c->fork, 0));
             }
         }
-        if (iso) {
-            HIP_TRY(hipEventRecord(c->fork, chunks[0].st));
-            for (size_t k = 1; k < chunks.size(); ++k) HIP_TRY(hipStreamWaitEvent(chunks[k].st, c->fork, 0));
+        if ((r = each(ST_OCTREE, [](const BatchArgs& B, hipStream_t st) { return launch_octree(B, st); }))) return r;
+        if ((r = each(ST_ORIENT, [](const BatchArgs& B, hipStream_t st) { return launch_orient_desc(B, st); }))) return r;
+        if ((r = each(ST_FINAL, [](const BatchArgs& B, hipStream_t st) { return launch_finalize(B, st); }))) return r;
+        return 0;
+    };
+    // One stream, no caller stream, no instrumentation (the single-pair / latency shape, e.g.
+    // orbgpu_extract_stereo): the ~15 launches are captured once into a hipGraph and replayed
+    // while the batch shape and input slot stay the same -- one submission instead of ~15.
+    const bool graphable = chunks.size() == 1 && !stream && c->prof_mask == 0 && c->use_graph &&
+                           !c->oct_stamps;
+    if (graphable) {
+        const int key[4] = {n, w, h, c->in_slot};
+        if (!c->graph_exec || std::memcmp(key, c->graph_key, sizeof key) != 0) {
+            drop_graph(c);
+            HIP_TRY(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+            const int rr = launch_all();
+            hipGraph_t g = nullptr;
+            const hipError_t ec = hipStreamEndCapture(s, &g);
+            if (rr || ec != hipSuccess) {
+                if (g) hipGraphDestroy(g);
+                return rr ? rr : fail(ORBGPU_ERR_HIP, std::string("hipStreamEndCapture: ") + hipGetErrorString(ec));
+            }
+            const hipError_t ei = hipGraphInstantiate(&c->graph_exec, g, nullptr, nullptr, 0);
+            hipGraphDestroy(g);
+            if (ei != hipSuccess) {
+                c->graph_exec = nullptr;
+                return fail(ORBGPU_ERR_HIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(ei));
+            }
+            std::memcpy(c->graph_key, key, sizeof key);
         }
+        HIP_TRY(hipGraphLaunch(c->graph_exec, s));
+    } else if ((r = launch_all())) {
+        return r;
     }
-    if ((r = each(ST_OCTREE, [](const BatchArgs& B, hipStream_t st) { return launch_octree(B, st); }))) return r;
-    if ((r = each(ST_ORIENT, [](const BatchArgs& B, hipStream_t st) { return launch_orient_desc(B, st); }))) return r;
-    if ((r = each(ST_FINAL, [](const BatchArgs& B, hipStream_t st) { return launch_finalize(B, st); }))) return r;
     c->last_chunks.clear();
     for (const Chunk& ch : chunks) c->last_chunks.push_back({ch.img0, ch.n, ch.st});
     c->last_images = n;
     c->last_w = w;
     c->last_h = h;
+    // a caller's stream: the context's streams wait for it before they touch this batch's
+    // buffers again (the next async upload overwrites the input slot this batch read)
+    if (stream && (r = rejoin(c, s))) return r;
     return ORBGPU_OK;
 }
 
 int orbgpu_synchronize(orbgpu_ctx* c) {
     if (!c) return fail(ORBGPU_ERR_INVALID, "null ctx");
-    HIP_TRY(hipSetDevice(c->device));
-    HIP_TRY(hipDeviceSynchronize());
+    if (int e_ = ctx_sync(c, true)) return e_;
     resolve_pending(c);
-    if (getenv("ORBGPU_OCT_STAMPS") && c->octdbg.p && c->last_images > 0) {
+    if (c->oct_stamps && c->octdbg.p && c->last_images > 0) {
         const int n = c->last_images, L = c->prm.nlevels;
         std::vector<unsigned long long> d((size_t)n * kMaxLevels * 8);
-        HIP_TRY(hipMemcpy(d.data(), c->octdbg.p, d.size() * 8, hipMemcpyDeviceToHost));
+        D2H(d.data(), c->octdbg.p, d.size() * 8);
         for (int l = 0; l < L; ++l) {
             double acc[8] = {};
             for (int i = 0; i < n; ++i)
@@ -1032,9 +1057,9 @@ int orbgpu_download_counts(orbgpu_ctx* c, int n, int32_t* nk, int32_t* nm) {
     if (!c) return fail(ORBGPU_ERR_INVALID, "null ctx");
     if (n > c->last_images) return fail(ORBGPU_ERR_INVALID, "more images than the last batch");
     HIP_TRY(hipStreamSynchronize(c->stream));
-    HIP_TRY(hipDeviceSynchronize());
-    if (nk) HIP_TRY(hipMemcpy(nk, c->outn.p, (size_t)n * 4, hipMemcpyDeviceToHost));
-    if (nm) HIP_TRY(hipMemcpy(nm, c->outmono.p, (size_t)n * 4, hipMemcpyDeviceToHost));
+    if (int e_ = ctx_sync(c)) return e_;
+    if (nk) D2H(nk, c->outn.p, (size_t)n * 4);
+    if (nm) D2H(nm, c->outmono.p, (size_t)n * 4);
     return ORBGPU_OK;
 }
 
@@ -1042,10 +1067,10 @@ int orbgpu_candidate_counts(orbgpu_ctx* c, int n, int32_t* counts) {
     if (!c || !counts) return fail(ORBGPU_ERR_INVALID, "null argument");
     if (n > c->last_images) return fail(ORBGPU_ERR_INVALID, "more images than the last batch");
     HIP_TRY(hipSetDevice(c->device));
-    HIP_TRY(hipDeviceSynchronize());
+    if (int e_ = ctx_sync(c)) return e_;
     std::vector<int32_t> cc((size_t)n * c->cellcnt_img);
     if (!cc.empty())
-        HIP_TRY(hipMemcpy(cc.data(), c->cellcnt.p, cc.size() * 4, hipMemcpyDeviceToHost));
+        D2H(cc.data(), c->cellcnt.p, cc.size() * 4);
     const BatchArgs& A = c->A;
     for (int i = 0; i < n; ++i) {
         long long s = 0;
@@ -1059,20 +1084,19 @@ int orbgpu_candidate_counts(orbgpu_ctx* c, int n, int32_t* counts) {
 int orbgpu_download_result(orbgpu_ctx* c, int img, orbgpu_keypoint* kps, uint8_t* desc, int cap,
                            int* n, int* n_mono) {
     if (!c || img < 0 || img >= c->last_images) return fail(ORBGPU_ERR_INVALID, "bad image index");
-    HIP_TRY(hipDeviceSynchronize());
+    if (int e_ = ctx_sync(c)) return e_;
     int32_t nk = 0, nm = 0;
-    HIP_TRY(hipMemcpy(&nk, c->outn.as<int32_t>() + img, 4, hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(&nm, c->outmono.as<int32_t>() + img, 4, hipMemcpyDeviceToHost));
+    D2H(&nk, c->outn.as<int32_t>() + img, 4);
+    D2H(&nm, c->outmono.as<int32_t>() + img, 4);
     if (int e = count_status(nk)) return e;
     if (n) *n = nk;
     if (n_mono) *n_mono = nm;
     if (nk > cap) return fail(ORBGPU_ERR_CAPACITY, "caller capacity too small");
     if (kps && nk)
-        HIP_TRY(hipMemcpy(kps, c->outkps.as<orbgpu_keypoint>() + (size_t)img * c->out_cap,
-                          sizeof(orbgpu_keypoint) * nk, hipMemcpyDeviceToHost));
+        D2H(kps, c->outkps.as<orbgpu_keypoint>() + (size_t)img * c->out_cap,
+                          sizeof(orbgpu_keypoint) * nk);
     if (desc && nk)
-        HIP_TRY(hipMemcpy(desc, c->outdesc.as<uint8_t>() + (size_t)img * c->out_cap * 32, 32 * (size_t)nk,
-                          hipMemcpyDeviceToHost));
+        D2H(desc, c->outdesc.as<uint8_t>() + (size_t)img * c->out_cap * 32, 32 * (size_t)nk);
     return ORBGPU_OK;
 }
 
@@ -1118,7 +1142,7 @@ int orbgpu_get_pyramid_level(orbgpu_ctx* c, int img, int level, int blurred, uin
                              int dst_stride, int* width, int* height) {
     if (!c || img < 0 || img >= c->last_images || level < 0 || level >= c->prm.nlevels)
         return fail(ORBGPU_ERR_INVALID, "bad image/level");
-    HIP_TRY(hipDeviceSynchronize());
+    if (int e_ = ctx_sync(c)) return e_;
     const LevelGeom& G = c->A.lv[level];
     if (width) *width = G.w;
     if (height) *height = G.h;
@@ -1136,20 +1160,19 @@ int orbgpu_get_pyramid_level(orbgpu_ctx* c, int img, int level, int blurred, uin
         src = c->A.lvl_base[level] + (size_t)img * c->pyr_img;
         pitch = G.pitch;
     }
-    HIP_TRY(hipMemcpy2D(dst, dst_stride, src, pitch, G.w, G.h, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy2DAsync(dst, dst_stride, src, pitch, G.w, G.h, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
     return ORBGPU_OK;
 }
 
 int orbgpu_get_level_keypoints(orbgpu_ctx* c, int img, orbgpu_keypoint* kps, uint8_t* desc, int cap,
                                int32_t* counts) {
     if (!c || img < 0 || img >= c->last_images) return fail(ORBGPU_ERR_INVALID, "bad image index");
-    HIP_TRY(hipDeviceSynchronize());
+    if (int e_ = ctx_sync(c)) return e_;
     const int L = c->prm.nlevels;
     std::vector<int32_t> cnt(kMaxLevels), st(kMaxLevels);
-    HIP_TRY(hipMemcpy(cnt.data(), c->lvlcnt.as<int32_t>() + img * kMaxLevels, 4 * kMaxLevels,
-                      hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(st.data(), c->status.as<int32_t>() + img * kMaxLevels, 4 * kMaxLevels,
-                      hipMemcpyDeviceToHost));
+    D2H(cnt.data(), c->lvlcnt.as<int32_t>() + img * kMaxLevels, 4 * kMaxLevels);
+    D2H(st.data(), c->status.as<int32_t>() + img * kMaxLevels, 4 * kMaxLevels);
     int off = 0;
     for (int l = 0; l < L; ++l) {
         if (st[l]) return fail(ORBGPU_ERR_OVERFLOW, "octree status " + std::to_string(st[l]));
@@ -1161,11 +1184,10 @@ int orbgpu_get_level_keypoints(orbgpu_ctx* c, int img, orbgpu_keypoint* kps, uin
         std::vector<float> ang(m);
         const size_t base = (size_t)img * c->lvlkp_img + G.kp_off;
         if (m) {
-            HIP_TRY(hipMemcpy(keys.data(), c->lvlkey.as<uint32_t>() + base, 4 * m, hipMemcpyDeviceToHost));
-            HIP_TRY(hipMemcpy(ang.data(), c->lvlangle.as<float>() + base, 4 * m, hipMemcpyDeviceToHost));
+            D2H(keys.data(), c->lvlkey.as<uint32_t>() + base, 4 * m);
+            D2H(ang.data(), c->lvlangle.as<float>() + base, 4 * m);
             if (desc)
-                HIP_TRY(hipMemcpy(desc + 32 * (size_t)off, c->lvldesc.as<uint8_t>() + base * 32, 32 * (size_t)m,
-                                  hipMemcpyDeviceToHost));
+                D2H(desc + 32 * (size_t)off, c->lvldesc.as<uint8_t>() + base * 32, 32 * (size_t)m);
         }
         for (int i = 0; i < m; ++i) {
             orbgpu_keypoint& k = kps[off + i];
@@ -1215,6 +1237,7 @@ int orbgpu_export_descriptors(orbgpu_ctx* c, int img, int row0, uint8_t* dst, in
     if (!c || img < 0 || img >= c->last_images || row0 < 0 || (cap > 0 && !dst))
         return fail(ORBGPU_ERR_INVALID, "bad arguments");
     HIP_TRY(hipSetDevice(c->device));
+    if (cap > 0 && !device_ptr(dst)) return fail(ORBGPU_ERR_INVALID, "device_dst is not device memory");
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
     int r = join_all(c, s);  // the descriptors come from the chunk streams
     if (r) return r;
@@ -1238,6 +1261,9 @@ int orbgpu_match_knn2_device(orbgpu_ctx* c, const uint8_t* q, int nq, const uint
     if (nt > 65535) return fail(ORBGPU_ERR_INVALID, "train set larger than 65535 rows");
     if (nq == 0) return ORBGPU_OK;
     HIP_TRY(hipSetDevice(c->device));
+    for (const void* p : {(const void*)q, (const void*)i1, (const void*)d1, (const void*)i2, (const void*)d2})
+        if (!device_ptr(p)) return fail(ORBGPU_ERR_INVALID, "query / outputs must be device memory");
+    if (nt && !device_ptr(t)) return fail(ORBGPU_ERR_INVALID, "train must be device memory");
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
     int r = timed(c, ST_KNN, s, [&] { return launch_knn2_plain(q, nq, t, nt, i1, d1, i2, d2, s); });
     if (r) return r;
@@ -1259,10 +1285,7 @@ int orbgpu_match_stereo_batch(orbgpu_ctx* c, int n_pairs, int stereo_only, void*
     m.idx2 = c->midx2.as<int32_t>();
     m.dist2 = c->mdist2.as<int32_t>();
     m.nq = c->mnq.as<int32_t>();
-    const int qblocks = (c->out_cap + 255) / 256;
     if (c->out_cap > 65535) return fail(ORBGPU_ERR_INVALID, "matcher supports < 65536 rows per image");
-    if (c->knnpart.ensure(knn2_scratch_bytes(n_pairs, c->out_cap)))
-        return fail(ORBGPU_ERR_HIP, "hipMalloc failed (knn scratch)");
     // follow the extraction's sub-batches so each chunk matches right after it is extracted
     bool chunked = !stream && !c->last_chunks.empty();
     for (const auto& ch : c->last_chunks) chunked &= (ch.img0 % 2) == 0 && (ch.n % 2) == 0;
@@ -1274,7 +1297,7 @@ int orbgpu_match_stereo_batch(orbgpu_ctx* c, int n_pairs, int stereo_only, void*
             HIP_TRY(hipStreamWaitEvent(s0, c->join[k], 0));
         }
         m.pair0 = 0;
-        int r = timed(c, ST_KNN, s0, [&] { return launch_knn2_pairs(m, n_pairs, qblocks, c->knnpart.p, s0); });
+        int r = timed(c, ST_KNN, s0, [&] { return launch_knn2_pairs(m, n_pairs, s0); });
         if (r) return r;
         HIP_TRY(hipEventRecord(c->fork, s0));
         for (size_t k = 1; k < c->last_chunks.size(); ++k)
@@ -1285,14 +1308,14 @@ int orbgpu_match_stereo_batch(orbgpu_ctx* c, int n_pairs, int stereo_only, void*
             if (np <= 0) continue;
             MatchArgs mm = m;
             mm.pair0 = p0;
-            int r = timed(c, ST_KNN, ch.st, [&] { return launch_knn2_pairs(mm, np, qblocks, c->knnpart.p, ch.st); });
+            int r = timed(c, ST_KNN, ch.st, [&] { return launch_knn2_pairs(mm, np, ch.st); });
             if (r) return r;
         }
     } else {
         m.pair0 = 0;
         int r = join_all(c, s);  // the extraction may have run on the chunk streams
         if (r) return r;
-        r = timed(c, ST_KNN, s, [&] { return launch_knn2_pairs(m, n_pairs, qblocks, c->knnpart.p, s); });
+        r = timed(c, ST_KNN, s, [&] { return launch_knn2_pairs(m, n_pairs, s); });
         if (r) return r;
         if ((r = rejoin(c, s))) return r;
     }
@@ -1303,17 +1326,17 @@ int orbgpu_match_stereo_batch(orbgpu_ctx* c, int n_pairs, int stereo_only, void*
 int orbgpu_download_matches(orbgpu_ctx* c, int pair, int32_t* i1, int32_t* d1, int32_t* i2,
                             int32_t* d2, int cap, int* nq) {
     if (!c || pair < 0 || pair >= c->last_pairs) return fail(ORBGPU_ERR_INVALID, "bad pair");
-    HIP_TRY(hipDeviceSynchronize());
+    if (int e_ = ctx_sync(c)) return e_;
     int32_t n = 0;
-    HIP_TRY(hipMemcpy(&n, c->mnq.as<int32_t>() + pair, 4, hipMemcpyDeviceToHost));
+    D2H(&n, c->mnq.as<int32_t>() + pair, 4);
     if (nq) *nq = n;
     if (n > cap) return fail(ORBGPU_ERR_CAPACITY, "caller capacity too small");
     const size_t o = (size_t)pair * c->out_cap;
     if (n) {
-        if (i1) HIP_TRY(hipMemcpy(i1, c->midx1.as<int32_t>() + o, 4 * (size_t)n, hipMemcpyDeviceToHost));
-        if (d1) HIP_TRY(hipMemcpy(d1, c->mdist1.as<int32_t>() + o, 4 * (size_t)n, hipMemcpyDeviceToHost));
-        if (i2) HIP_TRY(hipMemcpy(i2, c->midx2.as<int32_t>() + o, 4 * (size_t)n, hipMemcpyDeviceToHost));
-        if (d2) HIP_TRY(hipMemcpy(d2, c->mdist2.as<int32_t>() + o, 4 * (size_t)n, hipMemcpyDeviceToHost));
+        if (i1) D2H(i1, c->midx1.as<int32_t>() + o, 4 * (size_t)n);
+        if (d1) D2H(d1, c->mdist1.as<int32_t>() + o, 4 * (size_t)n);
+        if (i2) D2H(i2, c->midx2.as<int32_t>() + o, 4 * (size_t)n);
+        if (d2) D2H(d2, c->mdist2.as<int32_t>() + o, 4 * (size_t)n);
     }
     return ORBGPU_OK;
 }
@@ -1381,17 +1404,17 @@ int orbgpu_download_stereo(orbgpu_ctx* c, int pair, float* u_right, float* depth
                            int* n) {
     if (!c || pair < 0 || pair >= c->stereo_pairs) return fail(ORBGPU_ERR_INVALID, "bad pair");
     HIP_TRY(hipSetDevice(c->device));
-    HIP_TRY(hipDeviceSynchronize());
+    if (int e_ = ctx_sync(c)) return e_;
     int32_t nl = 0;
-    HIP_TRY(hipMemcpy(&nl, c->outn.as<int32_t>() + 2 * pair, 4, hipMemcpyDeviceToHost));
+    D2H(&nl, c->outn.as<int32_t>() + 2 * pair, 4);
     if (int e = count_status(nl)) return e;
     if (n) *n = nl;
     if (nl > cap) return fail(ORBGPU_ERR_CAPACITY, "caller capacity too small");
     const size_t o = (size_t)pair * c->out_cap;
     if (nl) {
-        if (u_right) HIP_TRY(hipMemcpy(u_right, c->stur.as<float>() + o, 4 * (size_t)nl, hipMemcpyDeviceToHost));
-        if (depth) HIP_TRY(hipMemcpy(depth, c->stdepth.as<float>() + o, 4 * (size_t)nl, hipMemcpyDeviceToHost));
-        if (sad) HIP_TRY(hipMemcpy(sad, c->stsad.as<int32_t>() + o, 4 * (size_t)nl, hipMemcpyDeviceToHost));
+        if (u_right) D2H(u_right, c->stur.as<float>() + o, 4 * (size_t)nl);
+        if (depth) D2H(depth, c->stdepth.as<float>() + o, 4 * (size_t)nl);
+        if (sad) D2H(sad, c->stsad.as<int32_t>() + o, 4 * (size_t)nl);
     }
     return ORBGPU_OK;
 }
@@ -1460,10 +1483,10 @@ int orbgpu_download_fisheye(orbgpu_ctx* c, int pair, int32_t* l2r, int32_t* r2l,
                             int* n_left, int* n_right, int* n_matches) {
     if (!c || pair < 0 || pair >= c->fisheye_pairs) return fail(ORBGPU_ERR_INVALID, "bad pair");
     HIP_TRY(hipSetDevice(c->device));
-    HIP_TRY(hipDeviceSynchronize());
+    if (int e_ = ctx_sync(c)) return e_;
     int32_t n[2] = {0, 0}, cnt[2] = {0, 0};
-    HIP_TRY(hipMemcpy(n, c->outn.as<int32_t>() + 2 * pair, 8, hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(cnt, c->fecnt.as<int32_t>() + 2 * pair, 8, hipMemcpyDeviceToHost));
+    D2H(n, c->outn.as<int32_t>() + 2 * pair, 8);
+    D2H(cnt, c->fecnt.as<int32_t>() + 2 * pair, 8);
     if (int e = count_status(n[0])) return e;
     if (int e = count_status(n[1])) return e;
     if (n_left) *n_left = n[0];
@@ -1472,11 +1495,11 @@ int orbgpu_download_fisheye(orbgpu_ctx* c, int pair, int32_t* l2r, int32_t* r2l,
     if (n[0] > cap || n[1] > cap) return fail(ORBGPU_ERR_CAPACITY, "caller capacity too small");
     const size_t o = (size_t)pair * c->out_cap;
     if (n[0]) {
-        if (l2r) HIP_TRY(hipMemcpy(l2r, c->fel2r.as<int32_t>() + o, 4 * (size_t)n[0], hipMemcpyDeviceToHost));
-        if (depth) HIP_TRY(hipMemcpy(depth, c->fedepth.as<float>() + o, 4 * (size_t)n[0], hipMemcpyDeviceToHost));
-        if (p3d) HIP_TRY(hipMemcpy(p3d, c->fep3d.as<float>() + 3 * o, 12 * (size_t)n[0], hipMemcpyDeviceToHost));
+        if (l2r) D2H(l2r, c->fel2r.as<int32_t>() + o, 4 * (size_t)n[0]);
+        if (depth) D2H(depth, c->fedepth.as<float>() + o, 4 * (size_t)n[0]);
+        if (p3d) D2H(p3d, c->fep3d.as<float>() + 3 * o, 12 * (size_t)n[0]);
     }
-    if (n[1] && r2l) HIP_TRY(hipMemcpy(r2l, c->fer2l.as<int32_t>() + o, 4 * (size_t)n[1], hipMemcpyDeviceToHost));
+    if (n[1] && r2l) D2H(r2l, c->fer2l.as<int32_t>() + o, 4 * (size_t)n[1]);
     return ORBGPU_OK;
 }
 
@@ -1512,7 +1535,8 @@ int orbgpu_ingest_sbs(orbgpu_ctx* c, const uint8_t* frames, int n, int w, int h,
     r = timed(c, ST_SBS, s, [&] { return launch_sbs_split(a, s); });
     if (r) return r;
     c->need_fork = true;
-    return ORBGPU_OK;
+    // a caller's stream: the next batch (forked from the context's stream) waits for the split
+    return rejoin(c, s);
 }
 
 int orbgpu_upload_sbs(orbgpu_ctx* c, const uint8_t* frames, int n, int w, int h, int stride) {
@@ -1572,10 +1596,10 @@ int orbgpu_download_soa(orbgpu_ctx* c, int image, int32_t* x, int32_t* y, int32_
                         uint8_t* orb, int cap, int* count, int* mono) {
     if (!c || image < 0 || image >= c->soa_images) return fail(ORBGPU_ERR_INVALID, "bad image");
     HIP_TRY(hipSetDevice(c->device));
-    HIP_TRY(hipDeviceSynchronize());
+    if (int e_ = ctx_sync(c)) return e_;
     int32_t nm[2] = {0, 0};
-    HIP_TRY(hipMemcpy(&nm[0], c->outn.as<int32_t>() + image, 4, hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(&nm[1], c->outmono.as<int32_t>() + image, 4, hipMemcpyDeviceToHost));
+    D2H(&nm[0], c->outn.as<int32_t>() + image, 4);
+    D2H(&nm[1], c->outmono.as<int32_t>() + image, 4);
     if (int e = count_status(nm[0])) return e;
     if (count) *count = nm[0];
     if (mono) *mono = nm[1];
@@ -1585,8 +1609,8 @@ int orbgpu_download_soa(orbgpu_ctx* c, int image, int32_t* x, int32_t* y, int32_
     const size_t plane = (size_t)c->max_images * c->out_cap, o = (size_t)image * c->out_cap;
     int32_t* dst[4] = {x, y, angle, level};
     for (int k = 0; k < 4; ++k)
-        if (dst[k]) HIP_TRY(hipMemcpy(dst[k], c->soa.as<int32_t>() + k * plane + o, 4 * n, hipMemcpyDeviceToHost));
-    if (orb) HIP_TRY(hipMemcpy(orb, c->outdesc.as<uint8_t>() + o * 32, 32 * n, hipMemcpyDeviceToHost));
+        if (dst[k]) D2H(dst[k], c->soa.as<int32_t>() + k * plane + o, 4 * n);
+    if (orb) D2H(orb, c->outdesc.as<uint8_t>() + o * 32, 32 * n);
     return ORBGPU_OK;
 }
 
@@ -1594,16 +1618,16 @@ int orbgpu_download_matches16(orbgpu_ctx* c, int pair, int16_t* indices, int16_t
                               int cap, int* nq) {
     if (!c || pair < 0 || pair >= c->soa_pairs) return fail(ORBGPU_ERR_INVALID, "bad pair");
     HIP_TRY(hipSetDevice(c->device));
-    HIP_TRY(hipDeviceSynchronize());
+    if (int e_ = ctx_sync(c)) return e_;
     int32_t n = 0;
-    HIP_TRY(hipMemcpy(&n, c->mnq.as<int32_t>() + pair, 4, hipMemcpyDeviceToHost));
+    D2H(&n, c->mnq.as<int32_t>() + pair, 4);
     if (nq) *nq = n;
     if (n > cap) return fail(ORBGPU_ERR_CAPACITY, "caller capacity too small");
     if (!n) return ORBGPU_OK;
     const size_t mplane = (size_t)(c->max_images / 2 + 1) * c->out_cap, o = (size_t)pair * c->out_cap;
     int16_t* dst[3] = {indices, dist1, dist2};
     for (int k = 0; k < 3; ++k)
-        if (dst[k]) HIP_TRY(hipMemcpy(dst[k], c->m16.as<int16_t>() + k * mplane + o, 2 * (size_t)n, hipMemcpyDeviceToHost));
+        if (dst[k]) D2H(dst[k], c->m16.as<int16_t>() + k * mplane + o, 2 * (size_t)n);
     return ORBGPU_OK;
 }
 
@@ -1748,11 +1772,11 @@ int orbgpu_download_projection_matches(orbgpu_ctx* c, int frame, int32_t* match,
                                        int* nmatches) {
     if (!c || frame < 0 || frame >= c->sbp_frames) return fail(ORBGPU_ERR_INVALID, "bad frame");
     HIP_TRY(hipSetDevice(c->device));
-    HIP_TRY(hipDeviceSynchronize());
+    if (int e_ = ctx_sync(c)) return e_;
     int32_t nk[2] = {0, 0}, nm = 0;
     const size_t img = (size_t)frame * c->sbp_step;
-    HIP_TRY(hipMemcpy(nk, c->outn.as<int32_t>() + img, c->sbp_two_cam ? 8 : 4, hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(&nm, c->sbpnm.as<int32_t>() + frame, 4, hipMemcpyDeviceToHost));
+    D2H(nk, c->outn.as<int32_t>() + img, c->sbp_two_cam ? 8 : 4);
+    D2H(&nm, c->sbpnm.as<int32_t>() + frame, 4);
     if (int e = count_status(nk[0])) return e;
     if (c->sbp_two_cam)
         if (int e = count_status(nk[1])) return e;
@@ -1763,8 +1787,7 @@ int orbgpu_download_projection_matches(orbgpu_ctx* c, int frame, int32_t* match,
     if (n > cap) return fail(ORBGPU_ERR_CAPACITY, "caller capacity too small");
     const size_t ncap = c->sbp_two_cam ? 2 * (size_t)c->out_cap : (size_t)c->out_cap;
     if (match && n)
-        HIP_TRY(hipMemcpy(match, c->sbpmatch.as<int32_t>() + (size_t)frame * ncap, 4 * (size_t)n,
-                          hipMemcpyDeviceToHost));
+        D2H(match, c->sbpmatch.as<int32_t>() + (size_t)frame * ncap, 4 * (size_t)n);
     return ORBGPU_OK;
 }
 
@@ -1827,18 +1850,18 @@ int orbgpu_download_grid(orbgpu_ctx* c, int image, float* xy_un, int32_t* cell, 
                          int32_t* cell_idx, int cap, int* n) {
     if (!c || image < 0 || image >= c->grid_images) return fail(ORBGPU_ERR_INVALID, "bad image");
     HIP_TRY(hipSetDevice(c->device));
-    HIP_TRY(hipDeviceSynchronize());
+    if (int e_ = ctx_sync(c)) return e_;
     int32_t nk = 0;
-    HIP_TRY(hipMemcpy(&nk, c->outn.as<int32_t>() + image, 4, hipMemcpyDeviceToHost));
+    D2H(&nk, c->outn.as<int32_t>() + image, 4);
     nk = std::max(nk, 0);
     if (n) *n = nk;
     if (nk > cap) return fail(ORBGPU_ERR_CAPACITY, "caller capacity too small");
     const size_t o = (size_t)image * c->out_cap;
     const size_t G = kGridCols * kGridRows + 1;
-    if (xy_un && nk) HIP_TRY(hipMemcpy(xy_un, c->gxy.as<float>() + 2 * o, 8 * (size_t)nk, hipMemcpyDeviceToHost));
-    if (cell && nk) HIP_TRY(hipMemcpy(cell, c->gcell.as<int32_t>() + o, 4 * (size_t)nk, hipMemcpyDeviceToHost));
-    if (cell_start) HIP_TRY(hipMemcpy(cell_start, c->gstart.as<int32_t>() + (size_t)image * G, 4 * G, hipMemcpyDeviceToHost));
-    if (cell_idx && nk) HIP_TRY(hipMemcpy(cell_idx, c->gidx.as<int32_t>() + o, 4 * (size_t)nk, hipMemcpyDeviceToHost));
+    if (xy_un && nk) D2H(xy_un, c->gxy.as<float>() + 2 * o, 8 * (size_t)nk);
+    if (cell && nk) D2H(cell, c->gcell.as<int32_t>() + o, 4 * (size_t)nk);
+    if (cell_start) D2H(cell_start, c->gstart.as<int32_t>() + (size_t)image * G, 4 * G);
+    if (cell_idx && nk) D2H(cell_idx, c->gidx.as<int32_t>() + o, 4 * (size_t)nk);
     return ORBGPU_OK;
 }
 

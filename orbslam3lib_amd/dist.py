@@ -47,25 +47,41 @@ def cross_camera_match_device(dist, be, image=0, row0=0):
     one RCCL all_gather moves every camera's rows over xGMI, and every other camera is matched on
     this GPU from device memory (orbgpu_match_knn2_device) on torch's current stream.  Only the
     per-camera row counts (one int each) pass through the host.  Returns {rank: int32 device
-    tensor [4, n] (idx1, dist1, idx2, dist2)} for the other ranks."""
+    tensor [4, n] (idx1, dist1, idx2, dist2)} for the other ranks.
+
+    Under gloo (the ranks share fewer GPUs than there are ranks, e.g. the one-GPU rehearsal) the
+    export and the matcher still run on device buffers; only the all_gather is staged through
+    host tensors.  An extractor that is not device-resident (the CPU tests' stand-in) gets host
+    buffers throughout; liborbgpu refuses host pointers in its device entry points."""
     import torch
     world, rank = dist.get_world_size(), dist.get_rank()
-    if dist.get_backend() == "nccl":
+    nccl = dist.get_backend() == "nccl"
+    on_device = nccl or (bool(getattr(be, "device_resident", False)) and torch.cuda.is_available())
+    if on_device:
         dev = torch.device("cuda", torch.cuda.current_device())
         stream = torch.cuda.current_stream().cuda_stream
-    else:  # gloo rehearsal: host tensors, `be` then works on host addresses (tests)
+    else:  # host stand-in (tests): `be` works on host addresses
         dev, stream = torch.device("cpu"), None
+    comm = dev if nccl else torch.device("cpu")  # where the collectives' tensors live
     nk, _ = be.counts()
     n_local = max(int(nk[image]) - int(row0), 0)
-    n = torch.tensor([n_local], dtype=torch.int64, device=dev)
+    n = torch.tensor([n_local], dtype=torch.int64, device=comm)
     counts = [torch.zeros_like(n) for _ in range(world)]
     dist.all_gather(counts, n)
     counts = [int(c.item()) for c in counts]
     maxn = max(max(counts), 1)
     buf = torch.zeros((maxn, 32), dtype=torch.uint8, device=dev)
     be.export_descriptors(image, buf.data_ptr(), maxn, row0, stream)
-    rows = [torch.empty_like(buf) for _ in range(world)]
-    dist.all_gather(rows, buf)
+    if comm == dev:
+        rows = [torch.empty_like(buf) for _ in range(world)]
+        dist.all_gather(rows, buf)
+    else:  # gloo between device buffers: host staging around the collective only
+        if dev.type == "cuda":
+            torch.cuda.current_stream().synchronize()
+        hb = buf.cpu()
+        hrows = [torch.empty_like(hb) for _ in range(world)]
+        dist.all_gather(hrows, hb)
+        rows = [h.to(dev) for h in hrows]
     out = {}
     for r in range(world):
         if r == rank:

@@ -152,8 +152,18 @@ def test_bench_batch_pairs(oracle, P):
             _same_knn(be.matches(p), oracle.knn2(ref[2 * u][1], ref[2 * u + 1][1]), "step %d pair %d" % (step, p))
 
 
+class _Hip:
+    """HIP runtime entry points from the runtime liborbgpu.so is bound to (og.hip_function)."""
+
+    def __getattr__(self, name):
+        import orbslam3lib_amd as og
+        f = og.hip_function(name)
+        setattr(self, name, f)
+        return f
+
+
 def _hip():
-    lib = C.CDLL("libamdhip64.so.7")  # the runtime liborbgpu.so is linked against
+    lib = _Hip()
     lib.hipStreamCreate.argtypes = [C.POINTER(C.c_void_p)]
     lib.hipStreamDestroy.argtypes = [C.c_void_p]
     return lib
@@ -332,3 +342,100 @@ def test_device_descriptor_export_and_knn2(oracle):
         be.synchronize()
         for p in bufs:
             hip.hipFree(p)
+
+
+def test_device_entry_points_refuse_host_pointers():
+    """orbgpu_export_descriptors / orbgpu_match_knn2_device take device memory only: a host
+    address is refused with ORBGPU_ERR_INVALID instead of being written by a device copy or
+    read by a kernel (the gloo branch of the C5 exchange once passed host tensors)."""
+    import orbslam3lib_amd as og
+    imgs = np.stack(synth.stereo_pair(480, 640, 71))
+    be = og.BatchExtractor(2000, 1.2, 8, 20, 7, width=640, height=480, max_images=2)
+    be.upload(imgs)
+    be.run()
+    host = np.zeros((4096, 32), np.uint8)
+    with pytest.raises(og.OrbGpuError) as e:
+        be.export_descriptors(0, host.ctypes.data, 4096)
+    assert e.value.code == -3
+    out = np.zeros((4, 16), np.int32)
+    with pytest.raises(og.OrbGpuError) as e:
+        be.match_knn2_device(host.ctypes.data, 16, host.ctypes.data, 16, out.ctypes.data)
+    assert e.value.code == -3
+    # the context stays usable, and no stale HIP error leaks into the next launch
+    be.run()
+    be.synchronize()
+    assert be.counts()[0].min() > 0
+
+
+def test_caller_stream_batches_with_async_upload(oracle):
+    """orbgpu_run_batch on a caller's stream interleaved with orbgpu_upload_images_async through
+    both input slots: the batch on the caller's stream is rejoined into the
+    context's streams, so the copy that refills its input slot two batches later waits for it.
+    Every batch's results equal the oracle's for its own frames."""
+    import orbslam3lib_amd as og
+    P, W, H = 16, 640, 480
+    sets = [np.stack([x for i in range(P) for x in synth.stereo_pair(H, W, 1300 + 40 * b + i)]) for b in range(4)]
+    refs = {}
+    be = og.BatchExtractor(2000, 1.2, 8, 20, 7, width=W, height=H, max_images=2 * P)
+    pin = [be.pinned(s_.shape) for s_ in sets]
+    for p_, s_ in zip(pin, sets):
+        p_[:] = s_
+    hip = _hip()
+    s = C.c_void_p()
+    assert hip.hipStreamCreate(C.byref(s)) == 0
+    try:
+        be.upload(sets[0])
+        for b in range(4):
+            be.run(stream=s.value)
+            be.match_stereo(False, stream=s.value)
+            if b + 1 < 4:
+                be.upload_async(pin[b + 1])  # slot of batch b - 1, which ran on the caller's stream
+            be.synchronize()
+            for i in (0, 2 * P - 1):
+                key = (b, i)
+                if key not in refs:
+                    refs[key] = oracle.extract(sets[b][i], nfeatures=2000)
+                k, d, m = be.result(i)
+                rk, rd, rm = refs[key]
+                _same_kps(k, rk)
+                np.testing.assert_array_equal(d, rd, err_msg="batch %d image %d" % (b, i))
+            _, dl, _ = be.result(2 * P - 2)
+            _, dr, _ = be.result(2 * P - 1)
+            _same_knn(be.matches(P - 1), oracle.knn2(dl, dr), "batch %d" % b)
+    finally:
+        be.synchronize()
+        be.close()
+        hip.hipStreamDestroy(s)
+
+
+def test_two_contexts_do_not_wait_for_each_other():
+    """One extractor per eye from two threads (Frame.cc:142-145): a context's synchronous calls
+    wait for its own streams only.  Context A queues ~20 large batches without synchronising;
+    context B's blocking single-pair extraction must return long before A's queue drains (with a
+    device-wide synchronize it would wait for all of A's work)."""
+    import time
+
+    import orbslam3lib_amd as og
+    P, W, H = 64, 640, 480
+    L, R = synth.stereo_pair(H, W, 77)
+    big = np.stack([L, R] * P)
+    a = og.BatchExtractor(2000, 1.2, 8, 20, 7, width=W, height=H, max_images=2 * P)
+    a.upload(big)
+    ex = og.ORBextractor(2000, 1.2, 8, 20, 7, max_width=W, max_height=H, max_images=2)
+    ex.extract_stereo(L, R)  # warm: code objects loaded, buffers sized
+    t0 = time.perf_counter()
+    a.run()
+    a.synchronize()
+    t_one = time.perf_counter() - t0
+    nb = max(8, int(0.08 / max(t_one, 1e-4)))  # >= ~80 ms of queued work
+    t0 = time.perf_counter()
+    for _ in range(nb):
+        a.run()
+    tb0 = time.perf_counter()
+    (kl, dl, ml), _ = ex.extract_stereo(L, R)
+    t_b = time.perf_counter() - tb0
+    a.synchronize()
+    t_a = time.perf_counter() - t0
+    assert len(kl) > 0
+    assert t_b < 0.5 * t_a, (t_b, t_a, nb)
+

@@ -301,46 +301,22 @@ def _check_pyramid(ex, oracle, imgs, sf=1.2, L=8):
                                           err_msg="img %d blur level %d" % (i, l))
 
 
-@pytest.mark.parametrize("mode", ["per-level", "1", "2", "4", "8", "16"])
-def test_pyramid_stripes_and_per_level_path(oracle, monkeypatch, mode):
-    """k_pyramid (one launch, 2^k row stripes per image, each stripe recomputing the rows its
-    blur halo and its later levels' source cones need) at every stripe count, and the per-level
-    k_blur_resize + last-level k_blur path (ORBGPU_PYR=0): pyramid and blurred levels of a stereo pair."""
-    if mode == "per-level":
-        monkeypatch.setenv("ORBGPU_PYR", "0")
-    else:
-        monkeypatch.setenv("ORBGPU_PYR", "1")
-        monkeypatch.setenv("ORBGPU_PYR_STRIPES", str(int(mode).bit_length() - 1))
+def test_pyramid_per_level_path(oracle):
+    """The per-level k_blur_resize launches + the last level's k_blur: pyramid and blurred levels
+    of a stereo pair."""
     L, R = synth.stereo_pair(480, 640, 3)
     ex = _extractor()
     ex.extract_stereo(L, R)
     _check_pyramid(ex, oracle, [L, R])
 
 
-@pytest.mark.parametrize("pyr", ["0", "1"])
-def test_pyramid_exact_2x_area_path(oracle, monkeypatch, pyr):
+def test_pyramid_exact_2x_area_path(oracle):
     """Scale factor 2 on a 640x480 frame: every level is an exact 2x downscale, which OpenCV
-    serves with INTER_AREA (2x2 mean) instead of INTER_LINEAR -- k_blur_resize and k_pyramid."""
-    monkeypatch.setenv("ORBGPU_PYR", pyr)
+    serves with INTER_AREA (2x2 mean) instead of INTER_LINEAR (k_blur_resize's area path)."""
     img = synth.frame(480, 640, 6)
     ex = _extractor(nf=500, L=3, sf=2.0)
     k, d, m = ex(img)
     _check_pyramid(ex, oracle, [img], sf=2.0, L=3)
     rk, rd, rm = oracle.extract(img, nfeatures=500, scale_factor=2.0, nlevels=3)
-    _same_kps(k, rk)
-    np.testing.assert_array_equal(d, rd)
-
-
-@pytest.mark.parametrize("pitch", [None, "80"])
-def test_one_wave_fast_cells(oracle, frame0, monkeypatch, pitch):
-    """The one-wave-per-cell FAST kernel (ORBGPU_FAST_WAVE=1, k_fast_wave) on the 640x480 frame,
-    with the runtime's tiles and with every level forced through the 80-byte tile."""
-    L, _ = frame0
-    monkeypatch.setenv("ORBGPU_FAST_WAVE", "1")
-    if pitch:
-        monkeypatch.setenv("ORBGPU_FAST_PITCH", pitch)
-    ex = _extractor()
-    k, d, m = ex(L)
-    rk, rd, rm = oracle.extract(L, nfeatures=2000)
     _same_kps(k, rk)
     np.testing.assert_array_equal(d, rd)

@@ -7,13 +7,13 @@
 set -e
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
-R=${ROUND:-r02}
+R=${ROUND:-r03}
 O=gpurun_out/refresh
 mkdir -p $O
 timeout -k 10 500 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1
 echo pytest-done
 bash tools/pmc_traffic.sh $O/pmct
-python3 tools/traffic.py $O/pmct $O/traffic.json > /dev/null
+python3 tools/traffic.py $O/pmct $O/traffic.json --images $((2 * ${PAIRS:-256})) --steps ${STEPS:-3} > /dev/null
 cp $O/traffic.json profiles/traffic_$R.json
 echo traffic-done
 timeout -k 10 300 python bench.py > $O/bench.json 2> $O/bench.err

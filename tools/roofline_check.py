@@ -1,32 +1,30 @@
-"""Cross-check of bench.py's roofline kernel time against the rocprofv3 kernel trace of the same
-bench command (tools/refresh_profiles.sh): the mean duration of the dominant kernel's launches in
-the timed region (the first steps x chunks chunk-grid launches after the serialized pass), over
-the whole chunk-grid run, and in the serialized pass.
-Usage: python tools/roofline_check.py BENCH_JSON KERNEL_TRACE_CSV [steps] [chunks]
-BENCH_JSON is best the line the profiled process itself printed: the concurrent launch time
-depends on how the chunk streams' stages happen to line up in that run (a FAST launch that
-meets another chunk's FAST takes ~2x as long as one beside the octree or descriptor stage)."""
+"""Cross-check of bench.py's roofline against the rocprofv3 kernel trace of the same bench command
+(tools/refresh_profiles.sh).  The bench line's `roofline` is the dominant kernel alone on the GPU:
+its launches in the bench's serialized pass (one whole-batch launch per step, per level for
+k_blur_resize), timed with HIP events on the kernel's stream.  Here the same launches are located
+in the trace and their mean duration gives frac = bytes_per_launch / mean / peak, which must agree
+with the line's frac (within 10%).  The timed region's concurrent launches (chunk
+grids, other chunks' stages beside them) are reported beside it.
+Usage: python tools/roofline_check.py BENCH_JSON KERNEL_TRACE_CSV [chunks]
+BENCH_JSON: the line the profiled process itself printed."""
 import csv
 import json
 import sys
 
 bench = json.load(open(sys.argv[1]))
-steps = int(sys.argv[3]) if len(sys.argv) > 3 else bench["steps"]
-chunks = int(sys.argv[4]) if len(sys.argv) > 4 else 3  # ORBGPU_STREAMS default
-name = bench["roofline"]["kernel"]
+chunks = int(sys.argv[3]) if len(sys.argv) > 3 else 3  # ORBGPU_STREAMS default
+roof = bench["roofline"]
+name = roof["kernel"]
+steps, warmup = bench["steps"], bench.get("warmup", 3)
 rows = [r for r in csv.DictReader(open(sys.argv[2])) if name in r["Kernel_Name"].replace("void ", "")]
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-# the headline steps launch the kernel on the chunk streams with the chunk grids (one grid per
-# level and chunk size for a per-level kernel); the bench's serialized profiling pass uses
-# whole-batch grids
 grid = lambda r: (r["Grid_Size_X"], r["Grid_Size_Y"], r["Grid_Size_Z"])
-n_timed = bench["roofline"].get("timed_launches") or steps * chunks
-per_chunk_step = max(1, n_timed // (steps * chunks))  # launches per chunk per step (levels)
-first = {grid(r) for r in rows[:bench.get("warmup", 3) * chunks * per_chunk_step]}  # warm-up steps
-# launch order: warm-up steps (chunk grids), the serialized profiled pass (whole-batch grids, the
-# kernel alone on the GPU), then the timed region (chunk grids again).  The streaming-ingest loop
-# that follows reuses the chunk grids, so the timed region is the first n_timed chunk-grid
-# launches after the serialized pass -- not the last ones of the run.
+dur = lambda r: (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+n_ser = roof.get("launches") or 3  # serialized launches (3 steps x launches per step)
+per_step = max(1, n_ser // 3)
+# launch order: warm-up steps (chunk grids), the serialized pass (whole-batch grids, the kernel
+# alone on the GPU), then the timed region (chunk grids again)
+first = {grid(r) for r in rows[:warmup * chunks * per_step]}
 i = 0
 while i < len(rows) and grid(rows[i]) in first:
     i += 1
@@ -38,13 +36,19 @@ head = []
 while i < len(rows) and grid(rows[i]) in first:
     head.append(rows[i])
     i += 1
-d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in head]
-timed = d[:n_timed]
-ds = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in ser]
-print(json.dumps({"kernel": name, "bench_avg_us": bench["roofline"]["avg_us"],
-                  "rocprof_timed_region_avg_us": round(sum(timed) / len(timed), 2),
-                  "rocprof_chunk_grid_run_avg_us": round(sum(d) / len(d), 2), "launches": len(d),
-                  "timed_launches": len(timed),
-                  "bench_serialized_avg_us": bench["roofline"].get("serialized_avg_us"),
-                  "rocprof_serialized_avg_us": round(sum(ds) / len(ds), 2) if ds else None,
-                  "serialized_launches": len(ds)}))
+ds = [dur(r) for r in ser]
+dt = [dur(r) for r in head][:steps * chunks * per_step]
+ser_avg = sum(ds) / len(ds) if ds else None
+out = {"kernel": name, "peak_GBps": roof["peak"], "bytes_per_launch": roof.get("bytes_per_launch"),
+       "bench_avg_us": roof["avg_us"], "rocprof_serialized_avg_us": round(ser_avg, 2) if ser_avg else None,
+       "serialized_launches": len(ds), "bench_frac": roof["frac"]}
+if ser_avg and roof.get("bytes_per_launch"):
+    fr = roof["bytes_per_launch"] / (ser_avg * 1e-6) / 1e9 / roof["peak"]
+    out["rocprof_frac"] = round(fr, 4)
+    out["frac_agreement"] = round(fr / roof["frac"], 3) if roof["frac"] else None
+    out["within_10pct"] = abs(fr / roof["frac"] - 1) <= 0.10 if roof["frac"] else None
+conc = roof.get("concurrent") or {}
+out["concurrent"] = {"bench_avg_us": conc.get("avg_us"),
+                     "rocprof_timed_region_avg_us": round(sum(dt) / len(dt), 2) if dt else None,
+                     "timed_launches": len(dt)}
+print(json.dumps(out))
