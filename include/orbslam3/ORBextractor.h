@@ -5,18 +5,35 @@
 // monoIndex, the scale getters and the public mvImagePyramid; plus the stereo entry point of the
 // DSP-backed extractor (cpp/include/ORBextractor.h:52-57), which returns the frame id whose
 // matches LynxHardwareAccelerator::BFMatchORB fetches (Frame.cc:1164).  The stereo form takes
-// the side-by-side Y8 frame the AHardwareBuffer holds as a cv::Mat (2W x H), or two images.
+// the AHardwareBuffer itself (as FrameAHB.cc:176 passes it), the side-by-side Y8 frame as a
+// cv::Mat (2W x H), or two images.
 // ORBmatcher stays the reference's own class (cpp/include/ORBmatcher.h:37-44); its
 // DescriptorDistance body can call orbgpu::DescriptorDistance below.
 // Everything computes on the GPU through include/orbgpu.h.
 #pragma once
+#include <cstdint>
 #include <vector>
 
 #include "../orbgpu.h"
 #include "LynxHardwareAcceleration/LynxHardwareAccelerator.h"
 #include "cv_shim.h"
 
+// <android/hardware_buffer.h>'s opaque buffer type: only pointers to it cross this header.
+struct AHardwareBuffer;
+
 namespace ORB_SLAM3 {
+
+// How the AHardwareBuffer form of operator() reads a buffer (ORBextractor.cc:133-147 does
+// AHardwareBuffer_describe + AHardwareBuffer_lock(CPU_READ_OFTEN), then unlocks once the frame is
+// copied): lock maps the side-by-side Y8 frame for reading and reports its full width (both eyes),
+// height and row stride in bytes, returning 0 on success; unlock releases it.  Under __ANDROID__
+// the default is exactly those NDK calls; elsewhere there is no default and the caller installs one
+// (a camera SDK's buffer type, a test double).
+struct AHardwareBufferAccess {
+    int (*lock)(AHardwareBuffer* buffer, const uint8_t** data, int* width, int* height, int* stride);
+    void (*unlock)(AHardwareBuffer* buffer);
+};
+void SetAHardwareBufferAccess(const AHardwareBufferAccess& access);
 
 class ORBextractor {
 public:
@@ -34,10 +51,18 @@ public:
     int operator()(cv::InputArray _image, cv::InputArray _mask, std::vector<cv::KeyPoint>& _keypoints,
                    cv::OutputArray _descriptors, std::vector<int>& vLappingArea);
 
-    // Stereo form (ORBextractor.h:52-57, ORBextractor.cc:118-165): _image is one side-by-side Y8
-    // frame, left eye in columns [0, W), right eye in [W, 2W).  Both eyes and the stereo-row kNN2
-    // in one device pass; returns the frame id (for LynxHardwareAccelerator::BFMatchORB), -1 on
-    // an error.
+    // Stereo form of the headset (ORBextractor.h:52-57, ORBextractor.cc:118-165; called by
+    // FrameAHB::ExtractORB, FrameAHB.cc:176): the AHardwareBuffer holds one side-by-side Y8 frame,
+    // left eye in columns [0, W), right eye in [W, 2W).  It is locked (SetAHardwareBufferAccess),
+    // copied to the device and unlocked, then both eyes and the stereo-row kNN2 run in one device
+    // pass; returns the frame id (for LynxHardwareAccelerator::BFMatchORB), -1 on an error (no
+    // lock function, lock failure, odd width, device error: lastStatus()).
+    int operator()(AHardwareBuffer* _image, std::vector<cv::KeyPoint>& _keypointsLeft,
+                   cv::OutputArray _descriptorsLeft, std::vector<int>& vLappingAreaLeft,
+                   std::vector<cv::KeyPoint>& _keypointsRight, cv::OutputArray _descriptorsRight,
+                   std::vector<int>& vLappingAreaRight, int& monoLeft, int& monoRight);
+
+    // Same with the side-by-side frame as an image (2W x H).
     int operator()(cv::InputArray _image, std::vector<cv::KeyPoint>& _keypointsLeft,
                    cv::OutputArray _descriptorsLeft, std::vector<int>& vLappingAreaLeft,
                    std::vector<cv::KeyPoint>& _keypointsRight, cv::OutputArray _descriptorsRight,
@@ -68,6 +93,9 @@ protected:
     int ensureContext(int width, int height);
     void exportPyramid(int image);
     LynxHardwareAccelerator* accelerator(int width, int height);
+    int extractStored(LynxHardwareAccelerator* acc, std::vector<cv::KeyPoint>& kl, cv::OutputArray dl,
+                      std::vector<int>& lapL, std::vector<cv::KeyPoint>& kr, cv::OutputArray dr,
+                      std::vector<int>& lapR, int& monoLeft, int& monoRight);
 
     int nfeatures;
     double scaleFactor;

@@ -51,7 +51,7 @@ __device__ inline void kb8_unproject(const float* P, float precision, float u, f
             theta = theta - theta_fix;
             if (fabsf(theta_fix) < precision) break;
         }
-        scale = tanf(theta) / theta_d;
+        scale = libm_tanf(theta) / theta_d;
     }
     r[0] = pwx * scale;
     r[1] = pwy * scale;
@@ -61,8 +61,8 @@ __device__ inline void kb8_unproject(const float* P, float precision, float u, f
 // KannalaBrandt8::project(const Eigen::Vector3f&) (KannalaBrandt8.cpp:61-78)
 __device__ inline void kb8_project(const float* P, const float x[3], float uv[2]) {
     const float x2_plus_y2 = x[0] * x[0] + x[1] * x[1];
-    const float theta = atan2f(sqrtf(x2_plus_y2), x[2]);
-    const float psi = atan2f(x[1], x[0]);
+    const float theta = libm_atan2f(sqrtf(x2_plus_y2), x[2]);
+    const float psi = libm_atan2f(x[1], x[0]);
     const float theta2 = theta * theta;
     const float theta3 = theta * theta2;
     const float theta5 = theta3 * theta2;

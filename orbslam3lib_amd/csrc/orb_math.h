@@ -72,6 +72,150 @@ __host__ __device__ inline void libm_sincosf(float y, float* sn, float* cs) {
     *cs = libm_poly(xs, x2, f * C0, f * C1, f * C2, f * C3, f * C4, (n ^ 1) & 1);
 }
 
+// atanf / atan2f / tanf of the host libm the oracle links (glibc 2.35, this image and the GPU
+// box), for Frame::ComputeStereoFishEyeMatches' KannalaBrandt8 camera model (project:
+// atan2f(sqrt(x^2 + y^2), z) and atan2f(y, x), CameraModels/KannalaBrandt8.cpp:61-78; unproject:
+// std::tan(float theta) = tanf, :110-137).  glibc's single-precision atanf / atan2f are the
+// fdlibm float algorithm (11-term odd/even polynomial after the 7/16, 11/16, 19/16, 39/16
+// argument split; atan2f's quadrant and pi_lo corrections); its tanf is the fdlibm float kernel
+// (13-term polynomial, the |x| >= 0.6744 pi/4 - x transform and the -1/(x + r) refinement) after a
+// double-precision reduction by pi/2.  Checked against the host libm: atanf on every positive
+// float (2,139,095,040 values, odd function), tanf on every float of [-2.35, 2.35] (the domain of
+// the restated reduction, |x| < 3 pi / 4), atan2f on 4e8 random pairs (bit patterns, [-3, 3]^2,
+// the near-diagonal band) -- tools/libm_fisheye_exhaustive.py, tests/test_host_harness.py.  No
+// FMA contraction (-ffp-contract=off): every expression is rounded as written.
+__host__ __device__ inline float libm_atanf(float x) {
+    const float atanhi[4] = {4.6364760399e-01f, 7.8539812565e-01f, 9.8279368877e-01f, 1.5707962513e+00f};
+    const float atanlo[4] = {5.0121582440e-09f, 3.7748947079e-08f, 3.4473217170e-08f, 7.5497894159e-08f};
+    const float aT[11] = {3.3333334327e-01f,  -2.0000000298e-01f, 1.4285714924e-01f, -1.1111110449e-01f,
+                          9.0908870101e-02f,  -7.6918758452e-02f, 6.6610731184e-02f, -5.8335702866e-02f,
+                          4.9768779427e-02f,  -3.6531571299e-02f, 1.6285819933e-02f};
+    const int32_t hx = __builtin_bit_cast(int32_t, x), ix = hx & 0x7fffffff;
+    int id;
+    if (ix >= 0x4c000000) {  // |x| >= 2^25
+        if (ix > 0x7f800000) return x + x;
+        return hx > 0 ? atanhi[3] + atanlo[3] : -atanhi[3] - atanlo[3];
+    }
+    if (ix < 0x3ee00000) {  // |x| < 0.4375
+        if (ix < 0x31000000) return x;  // |x| < 2^-29
+        id = -1;
+    } else {
+        x = __builtin_fabsf(x);
+        if (ix < 0x3f980000) {      // |x| < 1.1875
+            if (ix < 0x3f300000) {  // 7/16 <= |x| < 11/16
+                id = 0;
+                x = (2.0f * x - 1.0f) / (2.0f + x);
+            } else {
+                id = 1;
+                x = (x - 1.0f) / (x + 1.0f);
+            }
+        } else if (ix < 0x401c0000) {  // |x| < 2.4375
+            id = 2;
+            x = (x - 1.5f) / (1.0f + 1.5f * x);
+        } else {
+            id = 3;
+            x = -1.0f / x;
+        }
+    }
+    float z = x * x;
+    const float w = z * z;
+    const float s1 = z * (aT[0] + w * (aT[2] + w * (aT[4] + w * (aT[6] + w * (aT[8] + w * aT[10])))));
+    const float s2 = w * (aT[1] + w * (aT[3] + w * (aT[5] + w * (aT[7] + w * aT[9]))));
+    if (id < 0) return x - x * (s1 + s2);
+    z = atanhi[id] - ((x * (s1 + s2) - atanlo[id]) - x);
+    return hx < 0 ? -z : z;
+}
+
+__host__ __device__ inline float libm_atan2f(float y, float x) {
+    const float tiny = 1.0e-30f, pi_o_4 = 7.8539818525e-01f, pi_o_2 = 1.5707963705e+00f,
+                pi = 3.1415927410e+00f, pi_lo = -8.7422776573e-08f;
+    const int32_t hx = __builtin_bit_cast(int32_t, x), ix = hx & 0x7fffffff;
+    const int32_t hy = __builtin_bit_cast(int32_t, y), iy = hy & 0x7fffffff;
+    if (ix > 0x7f800000 || iy > 0x7f800000) return x + y;  // NaN
+    if (hx == 0x3f800000) return libm_atanf(y);             // x = 1
+    const int m = ((hy >> 31) & 1) | ((hx >> 30) & 2);       // 2 sign(x) + sign(y)
+    if (iy == 0) return m <= 1 ? y : m == 2 ? pi + tiny : -pi - tiny;
+    if (ix == 0) return hy < 0 ? -pi_o_2 - tiny : pi_o_2 + tiny;
+    if (ix == 0x7f800000) {
+        if (iy == 0x7f800000) {
+            const float r[4] = {pi_o_4 + tiny, -pi_o_4 - tiny, 3.0f * pi_o_4 + tiny, -3.0f * pi_o_4 - tiny};
+            return r[m];
+        }
+        const float r[4] = {0.0f, -0.0f, pi + tiny, -pi - tiny};
+        return r[m];
+    }
+    if (iy == 0x7f800000) return hy < 0 ? -pi_o_2 - tiny : pi_o_2 + tiny;
+    const int k = (iy - ix) >> 23;
+    float z;
+    if (k > 60) z = pi_o_2 + 0.5f * pi_lo;  // |y / x| > 2^60
+    else if (hx < 0 && k < -60) z = 0.0f;   // |y| / x < -2^60
+    else z = libm_atanf(__builtin_fabsf(y / x));
+    switch (m) {
+        case 0: return z;
+        case 1: return -z;
+        case 2: return pi - (z - pi_lo);
+        default: return (z - pi_lo) - pi;
+    }
+}
+
+// __kernel_tanf(x, y, iy): tan(x + y) for |x + y| <= pi/4 (iy = 1), -1 / tan(x + y) (iy = -1).
+__host__ __device__ inline float libm_kernel_tanf(float x, float y, int iy) {
+    const float T[13] = {3.3333334327e-01f, 1.3333334029e-01f, 5.3968254477e-02f, 2.1869488060e-02f,
+                         8.8632395491e-03f, 3.5920790397e-03f, 1.4562094584e-03f, 5.8804126456e-04f,
+                         2.4646313977e-04f, 7.8179444245e-05f, 7.1407252108e-05f, -1.8558637748e-05f,
+                         2.5907305826e-05f};
+    const float pio4 = 7.8539812565e-01f, pio4lo = 3.7748947079e-08f;
+    const int32_t hx = __builtin_bit_cast(int32_t, x), ix = hx & 0x7fffffff;
+    if (ix < 0x39000000 && (int)x == 0) {  // |x| < 2^-13
+        if ((ix | (iy + 1)) == 0) return 1.0f / __builtin_fabsf(x);
+        return iy == 1 ? x : -1.0f / x;
+    }
+    if (ix >= 0x3f2ca140) {  // |x| >= 0.6744
+        if (hx < 0) {
+            x = -x;
+            y = -y;
+        }
+        const float zz = pio4 - x, ww = pio4lo - y;
+        x = zz + ww;
+        y = 0.0f;
+        if (__builtin_fabsf(x) < 0x1p-13f) return (float)((1 - ((hx >> 30) & 2)) * iy) * (1.0f - (float)(2 * iy) * x);
+    }
+    const float z = x * x;
+    float w = z * z;
+    float r = T[1] + w * (T[3] + w * (T[5] + w * (T[7] + w * (T[9] + w * T[11]))));
+    float v = z * (T[2] + w * (T[4] + w * (T[6] + w * (T[8] + w * (T[10] + w * T[12])))));
+    float s = z * x;
+    r = y + z * (s * (r + v) + y);
+    r += T[0] * s;
+    w = x + r;
+    if (ix >= 0x3f2ca140) {
+        v = (float)iy;
+        return (float)(1 - ((hx >> 30) & 2)) * (v - 2.0f * (x - (w * w / (w + v) - r)));
+    }
+    if (iy == 1) return w;
+    // -1 / (x + r) refined: z + v = r + x with z the high 12 bits of w
+    const float zh = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, w) & 0xfffff000u);
+    v = r - (zh - x);
+    const float a = -1.0f / w;
+    const float t = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, a) & 0xfffff000u);
+    s = 1.0f + t * zh;
+    return t + a * (s + t * v);
+}
+
+// tanf(x) for |x| < 3 pi / 4 (the restated reduction's domain; the fisheye unprojection's theta
+// lies in [0, pi / 2]): |x| <= pi/4 straight to the kernel, else x - n pi/2 (n = +-1) in double,
+// split into a float head and tail, and the kernel's -1 / tan form.
+__host__ __device__ inline float libm_tanf(float x) {
+    const int32_t ix = __builtin_bit_cast(int32_t, x) & 0x7fffffff;
+    if (ix <= 0x3f490fda) return libm_kernel_tanf(x, 0.0f, 1);
+    if (ix >= 0x7f800000) return x - x;
+    const double xd = (double)x;
+    const int n = xd > 0.0 ? 1 : -1;
+    const double yd = xd - (double)n * 1.57079632679489661923;
+    const float y0 = (float)yd, y1 = (float)(yd - (double)y0);
+    return libm_kernel_tanf(y0, y1, -1);
+}
+
 // cv::fastAtan2 (OpenCV 4.2 core mathfuncs atanImpl<float>), degrees in [0, 360).
 // Called by IC_Angle, cpp/src/ORBextractor_old.cc:104.
 __host__ __device__ inline float fast_atan2_deg(float y, float x) {

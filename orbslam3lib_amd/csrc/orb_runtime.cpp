@@ -685,8 +685,12 @@ int orbgpu_create(const orbgpu_params* p, int device, int max_width, int max_hei
         // hardware queues a process gets (GPU_MAX_HW_QUEUES = 4); a 5th stream shares a queue
         // and the ingest copy then serialises with the kernels (measured: 3.16 vs 1.75 ms per
         // 128-pair step with the upload beside it; 3 and 4 chunk streams compute equally fast)
+        // A context that can never hold more than one stereo pair (the single-pair / one-eye
+        // extractor) gets one stream: chunks are whole pairs, and every stream takes one of the
+        // process's hardware queues, which a second context (the other eye's thread) needs for its
+        // own work not to queue behind this one's.
         const char* e = getenv("ORBGPU_STREAMS");
-        const int ns = std::max(1, std::min(8, e ? atoi(e) : 3));
+        const int ns = std::max(1, std::min({8, e ? atoi(e) : 3, max_images / 2}));
         for (int k = 1; k < ns; ++k) {
             hipStream_t st;
             if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) break;

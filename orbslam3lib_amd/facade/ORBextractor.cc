@@ -8,12 +8,45 @@
 #include "../../include/orbslam3/ORBextractor.h"
 
 #include <cstring>
+#include <mutex>
 #include <stdexcept>
 #include <string>
+
+#if defined(__ANDROID__)
+#include <android/hardware_buffer.h>
+#endif
 
 namespace ORB_SLAM3 {
 
 static_assert(sizeof(orbgpu_keypoint) == 28, "cv::KeyPoint layout");
+
+namespace {
+#if defined(__ANDROID__)
+// ORBextractor.cc:133-147: describe, lock for CPU reads, unlock after the copy.  The frame is an
+// 8-bit format, so the stride in pixels is the stride in bytes.
+int ahb_lock_ndk(AHardwareBuffer* b, const uint8_t** data, int* w, int* h, int* stride) {
+    AHardwareBuffer_Desc d = {};
+    AHardwareBuffer_describe(b, &d);
+    void* p = nullptr;
+    if (AHardwareBuffer_lock(b, AHARDWAREBUFFER_USAGE_CPU_READ_OFTEN, -1, nullptr, &p) != 0 || !p) return -1;
+    *data = static_cast<const uint8_t*>(p);
+    *w = (int)d.width;
+    *h = (int)d.height;
+    *stride = (int)d.stride;
+    return 0;
+}
+void ahb_unlock_ndk(AHardwareBuffer* b) { AHardwareBuffer_unlock(b, nullptr); }
+AHardwareBufferAccess g_ahb{ahb_lock_ndk, ahb_unlock_ndk};
+#else
+AHardwareBufferAccess g_ahb{nullptr, nullptr};
+#endif
+std::mutex g_ahb_mutex;
+}  // namespace
+
+void SetAHardwareBufferAccess(const AHardwareBufferAccess& access) {
+    std::lock_guard<std::mutex> g(g_ahb_mutex);
+    g_ahb = access;
+}
 
 ORBextractor::ORBextractor(int _nfeatures, float _scaleFactor, int _nlevels, int _iniThFAST,
                            int _minThFAST)
@@ -108,6 +141,59 @@ LynxHardwareAccelerator* ORBextractor::accelerator(int width, int height) {
     return LynxHardwareAccelerator::lynxHardwareAccelerator.get();
 }
 
+// Both eyes of the frame the accelerator holds, the stereo-row kNN2, the pyramid export.
+int ORBextractor::extractStored(LynxHardwareAccelerator* acc, std::vector<cv::KeyPoint>& kl, cv::OutputArray dl,
+                                std::vector<int>& lapL, std::vector<cv::KeyPoint>& kr, cv::OutputArray dr,
+                                std::vector<int>& lapR, int& monoLeft, int& monoRight) {
+    int nl = 0, nr = 0;
+    const int id = acc->ExtractORB(nl, nr, kl, kr, dl, dr, lapL.size() > 0 ? lapL[0] : 0,
+                                   lapL.size() > 1 ? lapL[1] : 0, lapR.size() > 0 ? lapR[0] : 0,
+                                   lapR.size() > 1 ? lapR[1] : 0, monoLeft, monoRight);
+    if (id < 0) return -1;
+    if (mbExportPyramid) acc->ExportPyramid(0, mvImagePyramid);
+    return id;
+}
+
+int ORBextractor::operator()(AHardwareBuffer* _image, std::vector<cv::KeyPoint>& kl, cv::OutputArray dl,
+                             std::vector<int>& lapL, std::vector<cv::KeyPoint>& kr, cv::OutputArray dr,
+                             std::vector<int>& lapR, int& monoLeft, int& monoRight) {
+    AHardwareBufferAccess access;
+    {
+        std::lock_guard<std::mutex> g(g_ahb_mutex);
+        access = g_ahb;
+    }
+    if (!_image || !access.lock || !access.unlock) {
+        mStatus = ORBGPU_ERR_INVALID;
+        return -1;
+    }
+    const uint8_t* data = nullptr;
+    int width = 0, height = 0, stride = 0;
+    if (access.lock(_image, &data, &width, &height, &stride) != 0 || !data) {
+        mStatus = ORBGPU_ERR_INVALID;
+        return -1;
+    }
+    // :136-137: each eye is half the buffer's width
+    if (width < 2 || (width & 1) || height < 1 || stride < width) {
+        access.unlock(_image);
+        mStatus = ORBGPU_ERR_INVALID;
+        return -1;
+    }
+    // :143 copies the frame to the accelerator and :146-148 unlock; the copy here may still be in
+    // flight on the device queue when StoreInputBuffer returns, so the buffer stays locked until
+    // the extraction (which waits for it) has returned
+    int id = -1;
+    try {
+        LynxHardwareAccelerator* acc = accelerator(width / 2, height);
+        acc->StoreInputBuffer(data, width / 2, height, stride);
+        id = extractStored(acc, kl, dl, lapL, kr, dr, lapR, monoLeft, monoRight);
+    } catch (const std::exception&) {
+        mStatus = ORBGPU_ERR_HIP;
+        id = -1;
+    }
+    access.unlock(_image);
+    return id;
+}
+
 int ORBextractor::operator()(cv::InputArray _image, std::vector<cv::KeyPoint>& kl, cv::OutputArray dl,
                              std::vector<int>& lapL, std::vector<cv::KeyPoint>& kr, cv::OutputArray dr,
                              std::vector<int>& lapR, int& monoLeft, int& monoRight) {
@@ -118,13 +204,7 @@ int ORBextractor::operator()(cv::InputArray _image, std::vector<cv::KeyPoint>& k
     try {
         LynxHardwareAccelerator* acc = accelerator(W, H);
         acc->StoreInputBuffer(sbs.ptr<unsigned char>(0), W, H, (int)sbs.step[0]);
-        int nl = 0, nr = 0;
-        const int id = acc->ExtractORB(nl, nr, kl, kr, dl, dr, lapL.size() > 0 ? lapL[0] : 0,
-                                       lapL.size() > 1 ? lapL[1] : 0, lapR.size() > 0 ? lapR[0] : 0,
-                                       lapR.size() > 1 ? lapR[1] : 0, monoLeft, monoRight);
-        if (id < 0) return -1;
-        if (mbExportPyramid) acc->ExportPyramid(0, mvImagePyramid);
-        return id;
+        return extractStored(acc, kl, dl, lapL, kr, dr, lapR, monoLeft, monoRight);
     } catch (const std::exception&) {
         mStatus = ORBGPU_ERR_HIP;
         return -1;

@@ -68,6 +68,30 @@ static int compare_knn(const char* tag, const std::vector<uint16_t>& idx, const 
     return 0;
 }
 
+// A test double of the headset's buffer: the facade only sees AHardwareBuffer* and calls the
+// installed lock / unlock (ORB_SLAM3::SetAHardwareBufferAccess).
+struct AHardwareBuffer {
+    std::vector<uint8_t> pixels;
+    int width = 0, height = 0, stride = 0;
+    int locks = 0, unlocks = 0;
+    bool locked = false;
+};
+static AHardwareBuffer g_buf;
+static int test_ahb_lock(AHardwareBuffer* b, const uint8_t** data, int* w, int* h, int* stride) {
+    if (b->locked) return -1;
+    b->locked = true;
+    ++b->locks;
+    *data = b->pixels.data();
+    *w = b->width;
+    *h = b->height;
+    *stride = b->stride;
+    return 0;
+}
+static void test_ahb_unlock(AHardwareBuffer* b) {
+    b->locked = false;
+    ++b->unlocks;
+}
+
 int main(int argc, char** argv) {
     const char* oracle_path = argc > 1 ? argv[1] : "oracle/build/liborb_oracle.so";
     void* h = dlopen(oracle_path, RTLD_NOW);
@@ -128,6 +152,36 @@ int main(int argc, char** argv) {
         if (ex.mvImagePyramid[0].cols != W) { printf("%s: pyramid\n", tag); bad = 1; }
     }
     if (ids[1] != ids[0] + 1) { printf("frame ids %d %d\n", ids[0], ids[1]); bad = 1; }
+    // the AHardwareBuffer form, called as FrameAHB::ExtractORB does (FrameAHB.cc:168-177), on a
+    // test double of the buffer with a padded row stride; locked once, unlocked once
+    {
+        const int stride = 2 * W + 64;
+        g_buf.pixels.assign((size_t)stride * H, 0xEE);
+        for (int y = 0; y < H; ++y) std::memcpy(g_buf.pixels.data() + (size_t)y * stride, sbs.data() + (size_t)y * 2 * W, 2 * W);
+        g_buf.width = 2 * W;
+        g_buf.height = H;
+        g_buf.stride = stride;
+        cv::Mat dl, dr;
+        std::vector<cv::KeyPoint> kl, kr;
+        int ml = -1, mr = -1;
+        if (ex((AHardwareBuffer*)&g_buf, kl, dl, lapL, kr, dr, lapR, ml, mr) != -1) {  // no access installed
+            printf("ahb: accepted without a lock function\n");
+            bad = 1;
+        }
+        ORB_SLAM3::SetAHardwareBufferAccess({test_ahb_lock, test_ahb_unlock});
+        const int id = ex((AHardwareBuffer*)&g_buf, kl, dl, lapL, kr, dr, lapR, ml, mr);
+        if (id <= 0 || g_buf.locks != 1 || g_buf.unlocks != 1 || g_buf.locked) {
+            printf("ahb: id %d locks %d unlocks %d\n", id, g_buf.locks, g_buf.unlocks);
+            bad = 1;
+        } else {
+            bad |= compare("ahb", kl, dl, ml, rkl.data(), rdl.data(), rnl, rml);
+            bad |= compare("ahb", kr, dr, mr, rkr.data(), rdr.data(), rnr, rmr);
+            std::vector<uint16_t> idx, d1, d2;
+            ORB_SLAM3::LynxHardwareAccelerator::lynxHardwareAccelerator->BFMatchORB(
+                id, dr.rowRange(mr, dr.rows), dl.rowRange(ml, dl.rows), idx, d1, d2);
+            bad |= compare_knn("ahb", idx, d1, d2, ri1.data(), rd1.data(), rd2.data(), nq);
+        }
+    }
     // a frame id that left the 3-frame cache: matched again on the device from the rows given
     {
         cv::Mat dl, dr;

@@ -4,7 +4,7 @@
 //   * Frame.cc:24,26 include ORBextractor.h and ORBmatcher.h together -- ORBmatcher stays the
 //     reference's own class (declared here with its shape from ORBmatcher.h:37-44);
 //   * the CPU extractor call of Frame::ExtractORB (ORBextractor_old.h:56-57) and the stereo call of
-//     FrameAHB::ExtractORB (FrameAHB.cc:176) returning mnIdMatchingData;
+//     FrameAHB::ExtractORB (FrameAHB.cc:168-177, AHardwareBuffer* in) returning mnIdMatchingData;
 //   * Frame::ComputeStereoFishEyeMatches' fetch of the matches (Frame.cc:1161-1164);
 //   * ComputeStereoMatches' read of mvImagePyramid (Frame.cc:834).
 #include <opencv2/opencv.hpp>
@@ -36,6 +36,15 @@ struct FrameLike {
     void ExtractORB(int flag, const cv::Mat& im, const int x0, const int x1) {
         std::vector<int> vLapping = {x0, x1};
         if (flag == 0) monoLeft = (*mpORBextractorLeft)(im, cv::Mat(), mvKeys, mDescriptors, vLapping);
+    }
+    // FrameAHB::ExtractORB (FrameAHB.cc:168-177) as the reference writes it
+    void ExtractORB(AHardwareBuffer* imagesBuffer, const int x0, const int x1, const int x0_1, const int x0_2) {
+        std::vector<int> vLapping_left = {x0, x1};
+        std::vector<int> vLapping_right = {x0_1, x0_2};
+        monoLeft = 0;
+        monoRight = 0;
+        mnIdMatchingData = (*mpORBextractorLeft)(imagesBuffer, mvKeys, mDescriptors, vLapping_left, mvKeysRight,
+                                                 mDescriptorsRight, vLapping_right, monoLeft, monoRight);
     }
     void ExtractORBStereo(const cv::Mat& sideBySide, int x0, int x1, int x0_1, int x0_2) {
         std::vector<int> vLapping_left = {x0, x1};

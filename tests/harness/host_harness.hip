@@ -34,6 +34,52 @@ long long harness_libm_sincosf_mismatches(float lo, float hi, int stride, long l
     return bad;
 }
 
+// libm_atanf / libm_tanf (orb_math.h) against the host's atanf / tanf on every `stride`-th float
+// of [lo, hi) (lo >= 0, or both negative: floats are walked by bit pattern).
+long long harness_libm_atanf_tanf_mismatches(float lo, float hi, int stride, int which, long long* checked) {
+    uint32_t u = __builtin_bit_cast(uint32_t, lo);
+    const uint32_t end = __builtin_bit_cast(uint32_t, hi);
+    long long bad = 0, n = 0;
+    for (; u < end; u += (uint32_t)stride) {
+        volatile float y = __builtin_bit_cast(float, u);
+        const float ref = which ? tanf(y) : atanf(y);
+        const float got = which ? libm_tanf(y) : libm_atanf(y);
+        bad += __builtin_bit_cast(uint32_t, ref) != __builtin_bit_cast(uint32_t, got);
+        ++n;
+    }
+    if (checked) *checked = n;
+    return bad;
+}
+
+// libm_atan2f against the host's atan2f on n pseudo-random pairs (xorshift from seed): raw bit
+// patterns, [-3, 3]^2 and the |y| ~ |x| band, one quarter each.
+long long harness_libm_atan2f_random(long long n, unsigned long long seed) {
+    unsigned long long s = seed | 1;
+    auto rnd = [&]() {
+        s ^= s << 13;
+        s ^= s >> 7;
+        s ^= s << 17;
+        return (uint32_t)s;
+    };
+    long long bad = 0;
+    for (long long i = 0; i < n; ++i) {
+        const uint32_t a = rnd(), b = rnd();
+        float y, x;
+        switch (i & 3) {
+            case 0: y = __builtin_bit_cast(float, a); x = __builtin_bit_cast(float, b); break;
+            case 1: y = (float)(int32_t)a / 2147483648.0f * 3.0f; x = (float)(int32_t)b / 2147483648.0f * 3.0f; break;
+            case 2: y = __builtin_bit_cast(float, a & 0x3fffffffu); x = __builtin_bit_cast(float, b & 0x3fffffffu) * ((b >> 31) ? -1.f : 1.f); break;
+            default:
+                y = __builtin_bit_cast(float, 0x3f000000u + (a & 0x00ffffffu));
+                x = y * (0.5f + (float)(b & 0xffff) / 65536.0f) * ((a >> 31) ? -1.f : 1.f);
+        }
+        volatile float vy = y, vx = x;
+        const float ref = atan2f(vy, vx), got = libm_atan2f(vy, vx);
+        bad += __builtin_bit_cast(uint32_t, ref) != __builtin_bit_cast(uint32_t, got) && !(ref != ref && got != got);
+    }
+    return bad;
+}
+
 int harness_octree(const uint32_t* keys, int n, int W, int H, int N, uint32_t* out, int out_cap) {
     const int nIni = std::max(1, (int)std::round((float)W / (float)H));
     const int cap = std::max(N + 3, 4 * nIni) + 8;

@@ -194,3 +194,31 @@ def test_libm_sincosf_restatement_equals_host_libm(harness):
         assert f(float(lo), float(hi), 1, C.byref(n)) == 0, e
         total += n.value
     assert total > 300_000
+
+
+def test_libm_fisheye_restatements_equal_host_libm(harness):
+    """orb_math.h libm_atanf / libm_atan2f / libm_tanf (the KannalaBrandt8 model's atan2f and
+    tanf in k_fisheye_stereo, CameraModels/KannalaBrandt8.cpp:61-78, 110-137) equal the host libm
+    the oracle calls: every 97th positive float for atanf, every 31st float of [-2.35, 2.35] for
+    tanf (the restated reduction's domain) plus every float within 2^14 ulps of the branch points
+    pi/4 and 0.6744, and 2e6 random atan2f pairs.  The exhaustive passes (every positive float;
+    every float of [-2.35, 2.35]; 4e8 pairs) are tools/libm_fisheye_exhaustive.py."""
+    import math
+    f = harness.harness_libm_atanf_tanf_mismatches
+    f.restype = C.c_longlong
+    f.argtypes = [C.c_float, C.c_float, C.c_int, C.c_int, C.POINTER(C.c_longlong)]
+    n = C.c_longlong(0)
+    inf = float(np.float32(np.inf))
+    assert f(0.0, inf, 97, 0, C.byref(n)) == 0 and n.value > 20_000_000
+    assert f(0.0, 2.35, 31, 1, C.byref(n)) == 0 and n.value > 30_000_000
+    assert f(-0.0, -2.35, 31, 1, C.byref(n)) == 0 and n.value > 30_000_000
+    for e in (math.pi / 4, 0.6744, 3 * math.pi / 8, math.pi / 2):
+        u = int(np.float32(e).view(np.uint32))
+        lo = np.uint32(u - (1 << 14)).view(np.float32)
+        hi = np.uint32(u + (1 << 14)).view(np.float32)
+        assert f(float(lo), float(hi), 1, 1, C.byref(n)) == 0, e
+    g = harness.harness_libm_atan2f_random
+    g.restype = C.c_longlong
+    g.argtypes = [C.c_longlong, C.c_ulonglong]
+    assert g(2_000_000, 12345) == 0
+
