@@ -58,33 +58,25 @@ def fast_tiers(w, h, sf=1.2, L=8):
     return out
 
 
-def algorithmic_bytes(w, h, L, nkp, sf=1.2, ncand=0.0, fused=True):
-    """Per-image bytes by stage: pyramid sum(A_{l-1}+A_l), FAST sum(A_l), blur
-    2*sum(A_l), 48 B per output keypoint (16 B keypoint + 32 B descriptor) for orientation +
-    descriptor; the octree reads its 4-byte candidate keys and writes 4 bytes per kept keypoint;
-    the assembly reads the level keypoint (key, angle, descriptor: 40 B) and writes the
-    cv::KeyPoint and the descriptor (60 B).
-    fused (the default path): FAST runs inside the pyramid kernels on the window they stage, so a
-    level's read serves blur, resize and FAST, and the kernel writes the level's KS plane (1 B per
-    pixel: the kept corners' strength) besides the blur and the next level; k_fast_gather reads KS
-    and writes the 4-byte cell keys.  Unfused (ORBGPU_FAST_FUSED=0): k_fast_cells reads every level
-    again (split between its 48-, 64- and 80-byte tile launches)."""
+def algorithmic_bytes(w, h, L, nkp, sf=1.2, ncand=0.0):
+    """Per-image bytes by stage: pyramid sum(A_{l-1}+A_l), FAST sum(A_l) (split
+    between the 48-, 64- and 80-byte tile launches), blur 2*sum(A_l), 48 B per output keypoint
+    (16 B keypoint + 32 B descriptor) for orientation + descriptor; the octree reads its 4-byte
+    candidate keys and writes 4 bytes per kept keypoint; the assembly reads the level keypoint
+    (key, angle, descriptor: 40 B) and writes the cv::KeyPoint and the descriptor (60 B)."""
     A = [a * b for a, b in level_sizes(w, h, sf, L)]
     tier = fast_tiers(w, h, sf, L)
-    k = 1 if fused else 0
-    out = {
-        # one pass over level l-1 per launch: read it, write its blur and level l (and its KS)
-        "k_blur_resize": sum((2 + k) * A[l - 1] + A[l] for l in range(1, L)),
-        "k_blur": (2 + k) * A[L - 1],  # the last level (the others ride in k_blur_resize)
+    return {
+        # one pass over level l-1 per launch: read it, write its blur and level l
+        "k_blur_resize": sum(2 * A[l - 1] + A[l] for l in range(1, L)),
+        "k_fast_cells<48>": sum(a for a, t in zip(A, tier) if t == 48),
+        "k_fast_cells<64>": sum(a for a, t in zip(A, tier) if t == 64),
+        "k_fast_cells<80>": sum(a for a, t in zip(A, tier) if t == 80),
+        "k_blur": 2 * A[L - 1],  # the last level's blur (the others ride in k_blur_resize)
         "k_orient_desc": 48 * nkp,
         "k_octree": 4 * ncand + 4 * nkp,
         "k_finalize": 100 * nkp,
     }
-    if fused:
-        out["k_fast_gather"] = sum(A) + 4 * ncand
-    else:
-        out.update({"k_fast_cells<%d>" % t: sum(a for a, tt in zip(A, tier) if tt == t) for t in (48, 64, 80)})
-    return out
 
 
 def fast_pyramid_bytes(w, h, L, sf=1.2):
@@ -424,8 +416,7 @@ def main():
     # launch of the same whole-batch launch (profiles/traffic_r*.json, per image and step there)
     n_img = 2 * P
     nser = 3
-    fused = "k_fast_gather" in stages_all and stages_all["k_fast_gather"][1] > 0
-    per_img = algorithmic_bytes(W, H, args.nlevels, feats_per_step / n_img, ncand=cand_per_img, fused=fused)
+    per_img = algorithmic_bytes(W, H, args.nlevels, feats_per_step / n_img, ncand=cand_per_img)
     traffic_tab, traffic_src = {}, None
     tps = sorted(glob.glob(os.path.join(ROOT, "profiles", "traffic_r*.json")))
     if tps:
@@ -498,8 +489,7 @@ def main():
     # the serialized pass.  The pyramid kernel also writes each level's blur (k_blur_resize reads
     # level l-1 once for both), so its time carries the blur: the bytes are SURVEY §8d's B_fp plus
     # the blur's 2 sum(A_l) (B_extract without the 48 B per keypoint)
-    fp_names = [k for k in stages_all if (k in ("k_blur_resize", "k_blur", "k_fast_gather") or
-                                          k.startswith("k_fast_cells")) and stages_all[k][1] > 0]
+    fp_names = [k for k in stages_all if k in ("k_blur_resize", "k_blur") or k.startswith("k_fast_cells")]
     fp_ms = sum(stages_all[k][0] for k in fp_names) / 3.0  # 3 serialized steps
     roof_fp = None
     if fp_ms > 0:
@@ -508,8 +498,7 @@ def main():
         ach = fp_bytes / (fp_ms * 1e-3) / 1e9
         roof_fp = {"kernels": fp_names, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
                    "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "bytes_per_step": int(fp_bytes),
-                   "includes": "pyramid + blur + FAST (%s); bytes = B_fp + 2 sum(A_l)" % (
-                       "FAST in the pyramid kernels + k_fast_gather + minTh reruns" if fused else "per-cell FAST"),
+                   "includes": "pyramid + blur (fused) + FAST; bytes = B_fp + 2 sum(A_l)",
                    "us_per_step": round(fp_ms * 1e3, 1)}
 
     # the matcher's own roofline (north_star: "Hamming BFMatch"): it runs on the int8 matrix cores
