@@ -73,9 +73,6 @@ struct BatchArgs {
     int fast_n48;  // k_fast_cells records [0, fast_n48) run the 48-byte FAST tile,
     int fast_n64;  // [fast_n48, fast_n64) the 64-byte one, the rest the 80-byte one (records are
                    // grouped by tile, levels in order inside each group)
-    long long ks_delta;              // KS plane of (image, level) = its blurred plane + ks_delta
-                                     // (fast_tile: kept FAST strength at iniThFAST, 0 elsewhere)
-    int fused_fast;                  // FAST in the pyramid kernels + k_fast_gather (else k_fast_cells)
     unsigned long long* octdbg;      // diagnostic: [img][kMaxLevels][8] phase clocks, or null
     int oct_lds_nodes;               // node capacity of k_octree's dynamic LDS (0: all global)
     int oct_lds_bytes;
@@ -208,10 +205,7 @@ hipError_t launch_blur_level(const BatchArgs& a, int level, hipStream_t s);
 // FAST cells of the levels that run the `tile`-byte LDS tile (48, 64 or kCellMax = 80):
 // fast_cell_range gives their flattened cell range, launch_fast_cells launches nothing if empty
 void fast_cell_range(const BatchArgs& a, int tile, int* c0, int* c1);
-// rerun = 1: only the cells k_fast_gather left with kFastRerun, at minThFAST
-hipError_t launch_fast_cells(const BatchArgs& a, int tile, int rerun, hipStream_t s);
-// every cell's keys from the KS planes the pyramid kernels wrote (a.fused_fast)
-hipError_t launch_fast_gather(const BatchArgs& a, hipStream_t s);
+hipError_t launch_fast_cells(const BatchArgs& a, int tile, hipStream_t s);
 hipError_t launch_octree(const BatchArgs& a, hipStream_t s);
 hipError_t launch_orient_desc(const BatchArgs& a, hipStream_t s);
 hipError_t launch_finalize(const BatchArgs& a, hipStream_t s);

@@ -20,7 +20,6 @@
 #include "orb_kernels.h"
 #include "orb_math.h"
 #include "orb_fast_cell.h"
-#include "orb_fast_tile.h"
 #include "orb_octree.h"
 #include "orb_pattern_data.h"
 #include "orb_policy.h"
@@ -278,9 +277,6 @@ __global__ __launch_bounds__(256) void k_blur(BatchArgs a, int tile0, int ntile)
     constexpr int NCH = (IH * IWQ + 255) / 256;  // window chunks per thread
     __shared__ uint4 tin4[IH][IWQ];
     __shared__ uint4 hp[NRP][kBlurTW / 4];  // [row pair][column quad]: 4 columns x (row0,row1)
-    __shared__ FastTileSmem fs;             // FAST of the tile (a.fused_fast), orb_fast_tile.h
-    static_assert(sizeof(hp) >= kFtListBytes && IW == kFtPitch && IH >= kFtRow0 + kFtH + 4, "fast_tile LDS");
-    const int fast_t = min(max(a.ini_th, 0), 255);
     // tiles [tile0, tile0 + ntile) of every image (all levels: 0, total_tiles)
     auto tile_of = [&](int t) { return (t / ntile) * a.total_tiles + tile0 + t % ntile; };
     const int total = ntile * a.nimages;
@@ -318,9 +314,6 @@ __global__ __launch_bounds__(256) void k_blur(BatchArgs a, int tile0, int ntile)
         }
         __syncthreads();
         blur_tile_compute(G, tx0, ty0, dst, tin4, hp, 0, G.h);
-        if (a.fused_fast)
-            fast_tile(G, tx0, ty0, fast_t, reinterpret_cast<uint8_t*>(&tin4[0][0]), reinterpret_cast<uint16_t*>(&hp[0][0]),
-                      fs, dst + a.ks_delta);
     }
 }
 
@@ -345,8 +338,7 @@ struct BrSmem {
 // Blur tile k of level s = l - 1 of image img, and (resize) the level-l outputs it owns.  kAux:
 // cache policy of the window loads (sc1 where level s was written by this launch).
 template <int kAux>
-__device__ inline void br_tile(const BatchArgs& a, int l, bool resize, int img, int by, int bx, BrSmem& sm,
-                               FastTileSmem& fs) {
+__device__ inline void br_tile(const BatchArgs& a, int l, bool resize, int img, int by, int bx, BrSmem& sm) {
     constexpr int IW = kBlurTW + 32, IH = kBlurTH + 8, IWQ = IW / 16;
     constexpr int NCH = (IH * IWQ + 255) / 256;
     const LevelGeom& S = a.lv[l - 1];
@@ -384,12 +376,13 @@ __device__ inline void br_tile(const BatchArgs& a, int l, bool resize, int img, 
     }
     __syncthreads();
     blur_tile_compute(S, bt.tx0, bt.ty0, bt.dst, sm.tin4, sm.hp, 0, S.h);  // fixes only off-plane columns
+    if (!resize) return;
     // resize from the window: window row r = source row ty0 - 4 + r, column c = tx0 - 16 + c
     const uint8_t* wb = reinterpret_cast<const uint8_t*>(&sm.tin4[0][0]);
     const int wy0 = bt.ty0 - 4, wx0 = bt.tx0 - 16;
     uint8_t* dst = a.lvl_base[l] + (long long)img * G.img_stride;
     const float inv_nq = nq > 0 ? 1.f / (float)nq : 0.f;
-    for (int it = threadIdx.x; resize && it < nr * nq; it += 256) {
+    for (int it = threadIdx.x; it < nr * nq; it += 256) {
         const int rr = (int)(((float)it + 0.5f) * inv_nq);  // exact: it < 34 * 40
         const int q = it - rr * nq;
         const int dy = r0 + rr, dx0 = 4 * (q0 + q);
@@ -411,13 +404,7 @@ __device__ inline void br_tile(const BatchArgs& a, int l, bool resize, int img, 
         }
         *reinterpret_cast<uint32_t*>(dst + (long long)dy * G.pitch + dx0) = packed;
     }
-    // FAST of level l - 1 on the same window (orb_fast_tile.h); the blur's row-pair buffer holds
-    // the candidate lists, the window the KS tile once the strengths are in
-    if (a.fused_fast)
-        fast_tile(S, bt.tx0, bt.ty0, min(max(a.ini_th, 0), 255), reinterpret_cast<uint8_t*>(&sm.tin4[0][0]),
-                  reinterpret_cast<uint16_t*>(&sm.hp[0][0]), fs, bt.dst + a.ks_delta);
 }
-static_assert(sizeof(BrSmem::hp) >= kFtListBytes && kBlurTW + 32 == kFtPitch, "fast_tile LDS");
 
 // n / d for a launch constant d by a mul-high with the host's magic ceil(2^32 / d) (d >= 2;
 // magic 0 stands for d == 1); exact for 0 <= n < 2^32 / d
@@ -427,14 +414,13 @@ __device__ inline int div_magic(int n, uint32_t magic) {
 
 __global__ __launch_bounds__(256) void k_blur_resize(BatchArgs a, int l, uint32_t per_magic, uint32_t tx_magic) {
     __shared__ BrSmem sm;
-    __shared__ FastTileSmem fs;
     const LevelGeom& S = a.lv[l - 1];
     const int per = S.tiles_x * S.tiles_y;
     const int wg = xcd_remap(blockIdx.x, gridDim.x);  // an image's tiles on one XCD
     const int irel = div_magic(wg, per_magic);
     const int k = wg - irel * per;
     const int by = div_magic(k, tx_magic), bx = k - by * S.tiles_x;
-    br_tile<0>(a, l, true, a.img0 + irel, by, bx, sm, fs);
+    br_tile<0>(a, l, true, a.img0 + irel, by, bx, sm);
 }
 
 
@@ -452,10 +438,9 @@ hipError_t launch_blur_resize(const BatchArgs& a, int l, hipStream_t s) {
 // detection on [3,rows-3)x[3,cols-3) of the cell ROI, 3x3 nonmax inside the cell only, iniTh
 // then minTh if the cell yields nothing, keys emitted in row-major order.
 constexpr int kFastThreads = 128;  // one workgroup (2 waves) per cell
-constexpr int kFastRerun = -1;     // k_fast_gather: the cell kept nothing at iniThFAST
 
 template <int CP>
-__global__ __launch_bounds__(kFastThreads) void k_fast_cells(BatchArgs a, int cell0, uint32_t ncell_magic, int rerun) {
+__global__ __launch_bounds__(kFastThreads) void k_fast_cells(BatchArgs a, int cell0, uint32_t ncell_magic) {
     constexpr int kList = cell_list_cap<CP>();
     __shared__ __attribute__((aligned(16))) uint8_t T[CP * CP];
     __shared__ __attribute__((aligned(16))) uint8_t M[CP * CP];  // 16-byte rows when CP % 16 == 0
@@ -478,8 +463,6 @@ __global__ __launch_bounds__(kFastThreads) void k_fast_cells(BatchArgs a, int ce
     g.iniX = e0.y;
     g.iniY = e0.z;
     g.minBorder = kMinBorder;
-    // rerun: only the cells k_fast_gather found empty at iniThFAST, straight at minThFAST
-    if (rerun && *cnt_out != kFastRerun) return;
     if (e1.z) {  // :812, :821
         if (threadIdx.x == 0) *cnt_out = 0;
         return;
@@ -499,68 +482,8 @@ __global__ __launch_bounds__(kFastThreads) void k_fast_cells(BatchArgs a, int ce
     };
     DevPolicy p{scratch};
     CellScratch cs{T, M, list, wcnt};
-    const int n = fast_cell_run<CP>(p, src, G.pitch, sh, dword_ok, g, rerun ? a.min_th : a.ini_th, a.min_th, cs,
-                                    key_out, ld16);
+    const int n = fast_cell_run<CP>(p, src, G.pitch, sh, dword_ok, g, a.ini_th, a.min_th, cs, key_out, ld16);
     if (threadIdx.x == 0) *cnt_out = n;
-}
-
-// k_fast_gather: one wave per cell (4 per workgroup), records in the order of k_fast_cells'
-// table.  The cell's detection region [iniX + 3, iniX + cols - 3) x [iniY + 3, iniY + rows - 3) of
-// the level's KS plane (fast_tile: m of the corners kept at iniThFAST, 0 elsewhere) is walked in
-// row-major order, the order cv::FAST emits (ORBextractor_old.cc:828), one dword (4 pixels) per
-// lane; the keys go to the cell's list exactly as k_fast_cells writes them (x, y relative to
-// minBorder, response = cornerScore = m - 1).  A cell that kept nothing is marked kFastRerun when
-// minThFAST < iniThFAST (:845-861): k_fast_cells(rerun) redoes it.  No barriers: waves are
-// independent.
-__global__ __launch_bounds__(256) void k_fast_gather(BatchArgs a, uint32_t ngrp_magic) {
-    const int wg = xcd_remap(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * gridDim.y);
-    const int irel = gridDim.x == 1 ? wg : (int)__umulhi((uint32_t)wg, ngrp_magic);
-    const int img = a.img0 + irel;
-    const int lane = (int)(threadIdx.x & 63);
-    const int gcell = (wg - irel * (int)gridDim.x) * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    if (gcell >= a.total_cells) return;
-    const int4 e0 = a.rtab[a.fast_tab_off + 2 * gcell];
-    const int4 e1 = a.rtab[a.fast_tab_off + 2 * gcell + 1];
-    const LevelGeom& G = a.lv[e0.x];
-    int32_t* cnt_out = a.cellcnt + (long long)img * a.cellcnt_img_stride + e1.x;
-    uint32_t* key_out = a.cellkeys + (long long)img * a.cellkeys_img_stride + e1.y;
-    const int rows = e0.w & 0xFFFF, cols = e0.w >> 16;
-    const int x0 = e0.y + 3, x1 = e0.y + cols - 3, y0 = e0.z + 3, y1 = e0.z + rows - 3;
-    if (e1.z || x1 <= x0 || y1 <= y0) {  // :812, :821; an empty detection region keeps nothing
-        if (lane == 0) *cnt_out = 0;
-        return;
-    }
-    const uint8_t* ks = a.blur_base[e0.x] + a.ks_delta + (long long)img * G.bimg_stride;
-    const int a0 = x0 & ~3, ndw = (x1 - a0 + 3) >> 2, items = (y1 - y0) * ndw;
-    const float inv = 1.f / (float)ndw;
-    auto rank = [](uint64_t b) {
-        return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
-    };
-    int total = 0;
-    for (int base = 0; base < items; base += 64) {
-        const int i = base + lane;
-        uint32_t D = 0, mask = 0;
-        int x = 0, y = 0;
-        if (i < items) {
-            const int r = (int)(((float)i + 0.5f) * inv);  // exact: i < 69 * 19
-            x = a0 + 4 * (i - r * ndw);
-            y = y0 + r;
-            D = *reinterpret_cast<const uint32_t*>(ks + (long long)y * G.bpitch + x);
-            const int lo = max(x0 - x, 0), hi = min(x1 - x, 4);
-#pragma unroll
-            for (int k = 0; k < 4; ++k) mask |= (((D >> (8 * k)) & 0xFFu) != 0u ? 1u : 0u) << k;
-            mask &= ((1u << hi) - 1u) & ~((1u << lo) - 1u);
-        }
-        const int c = __builtin_popcount(mask);
-        const uint64_t b0 = __ballot(c & 1), b1 = __ballot(c & 2), b2 = __ballot(c & 4);
-        int pos = total + rank(b0) + 2 * rank(b1) + 4 * rank(b2);
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-            if ((mask >> k) & 1u)
-                key_out[pos++] = make_key(x + k - kMinBorder, y - kMinBorder, (int)((D >> (8 * k)) & 0xFFu) - 1);
-        total += __popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2);
-    }
-    if (lane == 0) *cnt_out = (total == 0 && a.min_th < a.ini_th) ? kFastRerun : total;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1183,13 +1106,7 @@ void fast_cell_range(const BatchArgs& a, int tile, int* c0, int* c1) {
     *c0 = tile == kCellPitchTiny ? 0 : tile == kCellPitchSmall ? s48 : s64;
     *c1 = tile == kCellPitchTiny ? s48 : tile == kCellPitchSmall ? s64 : a.total_cells;
 }
-hipError_t launch_fast_gather(const BatchArgs& a, hipStream_t s) {
-    const uint32_t d = (uint32_t)((a.total_cells + 3) / 4);
-    const uint32_t magic = d > 1 ? 0xFFFFFFFFu / d + 1u : 0u;  // ceil(2^32 / d) for d >= 2
-    hipLaunchKernelGGL(k_fast_gather, dim3(d, a.nimages), dim3(256), 0, s, a, magic);
-    return hipGetLastError();
-}
-hipError_t launch_fast_cells(const BatchArgs& a, int tile, int rerun, hipStream_t s) {
+hipError_t launch_fast_cells(const BatchArgs& a, int tile, hipStream_t s) {
     // smaller tiles = less LDS per workgroup = more cells resident per CU
     int c0, c1;
     fast_cell_range(a, tile, &c0, &c1);
@@ -1197,9 +1114,9 @@ hipError_t launch_fast_cells(const BatchArgs& a, int tile, int rerun, hipStream_
     const dim3 grid(c1 - c0, a.nimages), block(kFastThreads);
     const uint32_t d = (uint32_t)(c1 - c0);
     const uint32_t magic = d > 1 ? 0xFFFFFFFFu / d + 1u : 0u;  // ceil(2^32 / d) for d >= 2
-    if (tile == kCellPitchTiny) hipLaunchKernelGGL(k_fast_cells<kCellPitchTiny>, grid, block, 0, s, a, c0, magic, rerun);
-    else if (tile == kCellPitchSmall) hipLaunchKernelGGL(k_fast_cells<kCellPitchSmall>, grid, block, 0, s, a, c0, magic, rerun);
-    else hipLaunchKernelGGL(k_fast_cells<kCellMax>, grid, block, 0, s, a, c0, magic, rerun);
+    if (tile == kCellPitchTiny) hipLaunchKernelGGL(k_fast_cells<kCellPitchTiny>, grid, block, 0, s, a, c0, magic);
+    else if (tile == kCellPitchSmall) hipLaunchKernelGGL(k_fast_cells<kCellPitchSmall>, grid, block, 0, s, a, c0, magic);
+    else hipLaunchKernelGGL(k_fast_cells<kCellMax>, grid, block, 0, s, a, c0, magic);
     return hipGetLastError();
 }
 hipError_t launch_octree(const BatchArgs& a, hipStream_t s) {

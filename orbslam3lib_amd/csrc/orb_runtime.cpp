@@ -40,13 +40,13 @@ int fail(int code, const std::string& msg) {
     } while (0)
 
 enum Stage { ST_RESIZE, ST_BLUR, ST_FAST48, ST_FAST, ST_FAST_TOP, ST_OCTREE, ST_ORIENT, ST_FINAL, ST_KNN,
-             ST_STEREO, ST_GRID, ST_SBS, ST_SOA, ST_SBP, ST_FISHEYE, ST_FAST_GATHER, ST_COUNT };
+             ST_STEREO, ST_GRID, ST_SBS, ST_SOA, ST_SBP, ST_FISHEYE, ST_COUNT };
 // names as rocprofv3 shows the kernels (templates with their argument)
 const char* kStageNames[ST_COUNT] = {"k_blur_resize",    "k_blur",   "k_fast_cells<48>", "k_fast_cells<64>",
                                      "k_fast_cells<80>", "k_octree", "k_orient_desc",    "k_finalize",
                                      "k_knn2",           "k_stereo",  "k_undistort_grid",
                                      "k_sbs_split",      "k_pack_soa",       "k_sbp",
-                                     "k_fisheye_stereo", "k_fast_gather"};
+                                     "k_fisheye_stereo"};
 
 struct DevBuf {
     void* p = nullptr;
@@ -111,7 +111,7 @@ struct orbgpu_ctx {
     long long pyr_img = 0, blur_img = 0, cellkeys_img = 0, octws_img = 0;
     int cellcnt_img = 0, lvlkp_img = 0, out_cap = 0;
     // device buffers
-    DevBuf input, pyr, blur, ks, rtab, cellkeys, cellcnt, octws, lvlkey, lvlangle, lvldesc, lvlcnt,
+    DevBuf input, pyr, blur, rtab, cellkeys, cellcnt, octws, lvlkey, lvlangle, lvldesc, lvlcnt,
         status, outkps, outdesc, outn, outmono, laps, midx1, mdist1, midx2, mdist2, mnq, scratch,
         octdbg, strow, stidx, stur, stdepth, stsad, gxy, gcell, gstart, gidx, sbs, soa, m16,
         sbpmp, sbpoff, sbpcand, sbpblk, sbpmatch, sbpnm, sbplr, fel2r, fer2l, fedepth, fep3d, fecnt;
@@ -139,9 +139,6 @@ struct orbgpu_ctx {
     unsigned isolate_mask = 0;
     bool serialize = false;  // profiling: every stage isolated
     bool oct_stamps = false; // ORBGPU_OCT_STAMPS (read once at create): octree phase clocks
-    // FAST inside the pyramid kernels + k_fast_gather (default); ORBGPU_FAST_FUSED=0: the per-cell
-    // k_fast_cells path for every cell (A/B)
-    bool fused_fast = true;
     // the captured launch sequence of a one-stream batch (run_batch), keyed by {n, w, h, slot}
     bool use_graph = true;   // ORBGPU_GRAPH=0 launches every kernel directly (A/B)
     hipGraphExec_t graph_exec = nullptr;
@@ -235,7 +232,6 @@ int alloc_all(orbgpu_ctx* c, int n_images) {
     int r = 0;
     r |= c->pyr.ensure(ni * c->pyr_img + 256);
     r |= c->blur.ensure(ni * c->blur_img + 256);
-    r |= c->ks.ensure(ni * c->blur_img + 256);  // KS planes: the blurred planes' layout
     r |= c->rtab.ensure(sizeof(int4) * (c->rtab_host.size() + 1));
     r |= c->cellkeys.ensure(ni * c->cellkeys_img * 4 + 256);
     r |= c->cellcnt.ensure(ni * c->cellcnt_img * 4 + 256);
@@ -507,8 +503,6 @@ int set_geometry(orbgpu_ctx* c, int w, int h) {
         A.blur_base[l] = c->blur.as<uint8_t>() + blur_off[l];
     }
     A.rtab = c->rtab.as<int4>();
-    A.ks_delta = c->ks.as<uint8_t>() - c->blur.as<uint8_t>();
-    A.fused_fast = c->fused_fast ? 1 : 0;
     A.cellkeys = c->cellkeys.as<uint32_t>();
     A.cellkeys_img_stride = c->cellkeys_img;
     A.cellcnt = c->cellcnt.as<int32_t>();
@@ -719,7 +713,6 @@ int orbgpu_create(const orbgpu_params* p, int device, int max_width, int max_hei
         if (sg) c->stagger = atoi(sg) != 0;
         c->oct_stamps = getenv("ORBGPU_OCT_STAMPS") != nullptr;
         if (const char* g = getenv("ORBGPU_GRAPH")) c->use_graph = atoi(g) != 0;
-        if (const char* f = getenv("ORBGPU_FAST_FUSED")) c->fused_fast = atoi(f) != 0;
     }
     int r = ensure_input(c, 1, max_width, max_height);
     if (!r) r = set_geometry(c, max_width, max_height);
@@ -738,7 +731,7 @@ int orbgpu_destroy(orbgpu_ctx* c) {
     resolve_pending(c);
     for (auto e : c->event_pool) hipEventDestroy(e);
     if (c->copy) hipStreamSynchronize(c->copy);
-    DevBuf* bufs[] = {&c->input, &c->input2, &c->pyr,     &c->blur,   &c->ks,   &c->rtab,    &c->cellkeys, &c->cellcnt,
+    DevBuf* bufs[] = {&c->input, &c->input2, &c->pyr,     &c->blur,   &c->rtab,    &c->cellkeys, &c->cellcnt,
                       &c->octws,   &c->lvlkey,  &c->lvlangle, &c->lvldesc, &c->lvlcnt, &c->status,
                       &c->outkps,  &c->outdesc, &c->outn,   &c->outmono, &c->laps,     &c->midx1,
                       &c->mdist1,  &c->midx2,   &c->mdist2, &c->mnq,     &c->scratch, &c->octdbg,
@@ -964,11 +957,6 @@ int orbgpu_run_batch(orbgpu_ctx* c, int n, int w, int h, const int32_t* laps, vo
             const int lt = A.nlevels - 1;
             if ((r = each(ST_BLUR, [&](const BatchArgs& B, hipStream_t st) { return launch_blur_level(B, lt, st); }))) return r;
         }
-        // fused FAST: the pyramid kernels left each level's KS plane; every cell's keys come from
-        // it, the cells empty at iniThFAST are redone at minThFAST by k_fast_cells (rerun)
-        const int rerun = c->fused_fast ? 1 : 0;
-        if (rerun && (r = each(ST_FAST_GATHER, [](const BatchArgs& B, hipStream_t st) { return launch_fast_gather(B, st); })))
-            return r;
         {   // the FAST tiles as one group: one join / fork around all of them when isolated
             const int tiles[3] = {kCellPitchTiny, kCellPitchSmall, kCellMax};
             const int stages[3] = {ST_FAST48, ST_FAST, ST_FAST_TOP};
@@ -995,7 +983,7 @@ int orbgpu_run_batch(orbgpu_ctx* c, int n, int w, int h, const int32_t* laps, vo
                     }
                     const hipStream_t st = ch.st;
                     const int tile = tiles[t];
-                    if ((r = timed(c, stages[t], st, [&] { return launch_fast_cells(B, tile, rerun, st); }))) return r;
+                    if ((r = timed(c, stages[t], st, [&] { return launch_fast_cells(B, tile, st); }))) return r;
                     if (iso) break;  // whole batch on the main stream
                 }
             }
