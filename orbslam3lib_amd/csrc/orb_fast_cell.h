@@ -94,7 +94,8 @@ __device__ inline uint32_t fw_compass4(uint32_t C, uint32_t Cm, uint32_t Cp, uin
 struct CellScratch {
     uint8_t* T;        // [P * P], 4-byte aligned
     uint8_t* M;        // [P * P], 4-byte aligned
-    uint16_t* list;    // [cell_list_cap<P>()] wave-private candidate lists (offsets into T/M)
+    uint16_t* list;    // [cell_list_cap<P>() + 1] wave-private candidate lists (offsets into
+                       // T/M) and a sink entry
     int32_t* wcnt;     // [waves]
 };
 
@@ -183,6 +184,8 @@ __host__ __device__ int fast_cell_detect(Pol& p, int sh, const CellGeom& g, int 
     const int i0 = w * nd / W, i1 = (w + 1) * nd / W;  // nd <= 4900, W <= 16: no overflow
 #endif
     uint16_t* list = cs.list + i0;
+    uint16_t* sink = cs.list + cell_list_cap<CP>();  // one entry past the list (CellScratch)
+    (void)sink;
 #if !defined(__HIP_DEVICE_COMPILE__)
     const float inv_dc = dc > 0 ? 1.f / (float)dc : 0.f;
     auto off_of = [&](int i) {
@@ -220,9 +223,14 @@ __host__ __device__ int fast_cell_detect(Pol& p, int sh, const CellGeom& g, int 
                 const int c = __builtin_popcount(m4);
                 const uint64_t b0 = p.ballot(c & 1), b1 = p.ballot(c & 2), b2 = p.ballot(c & 4);
                 int pos = na + rank(b0) + 2 * rank(b1) + 4 * rank(b2);
+                // unconditional stores: a lane's slots past its candidates go to the sink entry
+                // after the list (no exec-mask juggling per pixel)
 #pragma unroll
-                for (int k = 0; k < 4; ++k)
-                    if ((m4 >> k) & 1u) list[pos++] = (uint16_t)(o + k);
+                for (int k = 0; k < 4; ++k) {
+                    const bool on = (m4 >> k) & 1u;
+                    *(on ? list + pos : sink) = (uint16_t)(o + k);
+                    pos += on ? 1 : 0;
+                }
                 na += p.popc64(b0) + 2 * p.popc64(b1) + 4 * p.popc64(b2);
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the list is read by other lanes
@@ -246,11 +254,15 @@ __host__ __device__ int fast_cell_detect(Pol& p, int sh, const CellGeom& g, int 
             na += p.popc64(m);
         }
 #endif
-        // exact strength of every candidate (m > t <=> corner at t), corners kept in order
+        // exact strength of every candidate (m > t <=> corner at t), corners kept in order; the
+        // next batch's list entries are read one batch ahead (the in-place writes of a batch
+        // land below its own start, never on entries not yet read)
         int nb = 0;
+        int o_next = na > 0 ? list[lane < na ? lane : na - 1] : 0;
         for (int base = 0; base < na; base += L) {
             const int j = base + lane;
-            const int o = list[j < na ? j : 0];
+            const int o = o_next;
+            if (base + L < na) o_next = list[base + L + lane < na ? base + L + lane : na - 1];
             const int sm = fast_strength_packed<CP>(&T[o]);
             const bool f = j < na && sm > t;
             const uint64_t m = p.ballot(f);

@@ -444,7 +444,7 @@ __global__ __launch_bounds__(kFastThreads) void k_fast_cells(BatchArgs a, int ce
     constexpr int kList = cell_list_cap<CP>();
     __shared__ __attribute__((aligned(16))) uint8_t T[CP * CP];
     __shared__ __attribute__((aligned(16))) uint8_t M[CP * CP];  // 16-byte rows when CP % 16 == 0
-    __shared__ uint16_t list[kList];
+    __shared__ uint16_t list[kList + 2];  // + the sink entry of the compass compaction
     __shared__ int32_t wcnt[kFastThreads / 64];
     __shared__ int scratch[16];
     const int wg = xcd_remap(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * gridDim.y);

@@ -161,7 +161,7 @@ int harness_level_candidates(const uint8_t* lvl, int w, int h, int ini, int mn, 
     std::vector<uint32_t> T32(kCellMax * kCellMax / 4), M32(kCellMax * kCellMax / 4);
     uint8_t* T = reinterpret_cast<uint8_t*>(T32.data());
     uint8_t* M = reinterpret_cast<uint8_t*>(M32.data());
-    std::vector<uint16_t> list(cell_list_cap<kCellMax>());
+    std::vector<uint16_t> list(cell_list_cap<kCellMax>() + 1);
     std::vector<int32_t> wcnt(4);
     std::vector<uint32_t> tmp(kCellMax * kCellMax);
     int total = 0, cnt = 0;
