@@ -83,8 +83,8 @@ __constant__ MomentWeights c_mw = make_moment_weights();
 // ---------------------------------------------------------------------------------------------
 // cv::resize INTER_LINEAR (canonical ComputePyramid, ORBextractor_old.cc:1342-1344), fixed point.
 // Four output pixels dx0 .. dx0+3 of one output row from source rows r0 / r1 (LDS window rows), x
-// coefficients xt[0..3] (entries past the tile edge may be stale: their bytes are padding or the
-// next tile's, rewritten there), y coefficients b0 / b1.  Every product fits 24
+// coefficients xt[k * kBrMaxQuads] (k = 0..3; entries past the tile edge may be stale: their
+// bytes are padding or the next tile's, rewritten there), y coefficients b0 / b1.  Every product fits 24
 // bits (pixel <= 255, coefficients <= 2048, (D >> 4) < 2^15), so all multiplies are full-rate
 // v_mul_u32_u24 / v_mad_u32_u24.  Vertical rounding: OpenCV's SIMD body below simd_end,
 // FixedPtCast after it (only the last quads of a row take that branch).
@@ -94,7 +94,7 @@ __device__ inline uint32_t rs_quad(const Row& r0, const Row& r1, const int4* xt,
     int D0[4], D1[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-        const int4 x = xt[k];
+        const int4 x = xt[k * kBrMaxQuads];
         D0[k] = __umul24(r0[x.x], x.z) + __umul24(r0[x.y], x.w);
         D1[k] = __umul24(r1[x.x], x.z) + __umul24(r1[x.y], x.w);
     }
@@ -331,7 +331,7 @@ static_assert(kBrMaxQuads >= kBlurTW / 4 + 1 && kBrMaxRows >= kBlurTH + 1, "owne
 struct BrSmem {
     uint4 tin4[kBlurTH + 8][(kBlurTW + 32) / 16];
     uint4 hp[(kBlurTH + 8) / 2][kBlurTW / 4];
-    int4 xts[4 * kBrMaxQuads];
+    int4 xts[4 * kBrMaxQuads];  // [k][quad]: a wave's consecutive quads read consecutive entries
     int4 yts[kBrMaxRows];
 };
 
@@ -365,7 +365,8 @@ __device__ inline void br_tile(const BatchArgs& a, int l, bool resize, int img, 
         nr = min(band_row[by + 1] - r0, kBrMaxRows);
         nq = min(tile_quad[bx + 1] - q0, kBrMaxQuads);
         if (!G.area2) {
-            for (int i = threadIdx.x; i < 4 * nq; i += 256) sm.xts[i] = a.rtab[G.xtab_off + min(4 * q0 + i, G.w - 1)];
+            for (int i = threadIdx.x; i < 4 * nq; i += 256)
+                sm.xts[(i & 3) * kBrMaxQuads + (i >> 2)] = a.rtab[G.xtab_off + min(4 * q0 + i, G.w - 1)];
             if (threadIdx.x < nr) sm.yts[threadIdx.x] = a.rtab[G.ytab_off + r0 + threadIdx.x];
         }
     }
@@ -400,7 +401,7 @@ __device__ inline void br_tile(const BatchArgs& a, int l, bool resize, int img, 
             const int4 yt = sm.yts[rr];
             const uint8_t* row0 = wb + (yt.x - wy0) * IW - wx0;
             const uint8_t* row1 = wb + (yt.y - wy0) * IW - wx0;
-            packed = rs_quad(row0, row1, sm.xts + 4 * q, yt.z, yt.w, dx0, G.simd_end);
+            packed = rs_quad(row0, row1, sm.xts + q, yt.z, yt.w, dx0, G.simd_end);
         }
         *reinterpret_cast<uint32_t*>(dst + (long long)dy * G.pitch + dx0) = packed;
     }
@@ -593,7 +594,13 @@ __global__ __launch_bounds__(NT) void k_octree(BatchArgs a, int l0, OctCfg q) {
     extern __shared__ __attribute__((aligned(16))) uint8_t nodemem_lds[];  // per-launch size
     __shared__ int scratch[16];
     __shared__ OctShared sh;
+#ifdef OCT_IMAGE_MAJOR
+    const int nl = gridDim.y, tot = gridDim.x * gridDim.y;
+    const int lg = xcd_remap(blockIdx.x + blockIdx.y * gridDim.x, tot);
+    octree_level<true>(a, a.img0 + lg / nl, l0 + lg % nl, nodemem_lds, scratch, sh, q);
+#else
     octree_level<true>(a, a.img0 + blockIdx.x, l0 + blockIdx.y, nodemem_lds, scratch, sh, q);
+#endif
 }
 
 // The levels k_octree left with kOctRetry, redone with generic pointers: a small persistent
@@ -664,10 +671,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
     // per disc row v = s - 15 (s = 0..31): byte masks of the 32-byte window u = -15..16 restricted
     // to |u| <= umax[|v|] (rows past v = 15 are empty), and the packed test pairs (x0,y0,x1,y1
     // int8): both in LDS tables shared by the workgroup instead of 16 VGPRs per lane
+    // Both tables are stored index-major ([i][sub], [b][sub]): the 32 lanes of a keypoint read 32
+    // consecutive entries per instruction, conflict-free (a [sub][i] layout puts every lane of a
+    // b128 read on the same 4 banks: 32-way conflicts, measured as half the kernel's LDS time)
     static_assert(kOdRows == 1 && kOdLanes * 8 == 256 && kOdLanes * kOdPairs == 256, "LDS table shapes");
-    __shared__ __attribute__((aligned(16))) uint32_t s_msk[kOdLanes][8];
-    // test pair j as floats {x0, x1, y0, y1}: the two samples of a pair rotate as one packed pair
-    __shared__ __attribute__((aligned(16))) uint4 s_pat[kOdLanes * kOdPairs];
+    __shared__ __attribute__((aligned(16))) uint32_t s_msk[8][kOdLanes];
+    // test pair j = sub * kOdPairs + b as floats {x0, x1, y0, y1} at s_pat[b][sub]: the two samples
+    // of a pair rotate as one packed pair
+    __shared__ __attribute__((aligned(16))) uint4 s_pat[kOdPairs][kOdLanes];
     {
         const int ts = threadIdx.x / 8, ti = threadIdx.x % 8;
         const int v = ts - 15;
@@ -678,9 +689,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
             const int u = 4 * ti + j - 15;
             m |= ((u < 0 ? -u : u) <= d ? 0xFFu : 0u) << (8 * j);
         }
-        s_msk[ts][ti] = m;
-        const int8_t* pv = c_pattern.v + 4 * threadIdx.x;  // x0, y0, x1, y1
-        s_pat[threadIdx.x] = make_uint4(__float_as_uint((float)pv[0]), __float_as_uint((float)pv[2]),
+        s_msk[ti][ts] = m;
+        const int8_t* pv = c_pattern.v + 4 * threadIdx.x;  // x0, y0, x1, y1 of pair threadIdx.x
+        s_pat[threadIdx.x % kOdPairs][threadIdx.x / kOdPairs] = make_uint4(__float_as_uint((float)pv[0]), __float_as_uint((float)pv[2]),
                                         __float_as_uint((float)pv[1]), __float_as_uint((float)pv[3]));
     }
     __syncthreads();
@@ -751,7 +762,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
             uint32_t sacc = 0, uacc = 0;
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
-                const uint32_t b = __builtin_amdgcn_alignbyte(w[i + 1], w[i], shf) & s_msk[sub][i];
+                const uint32_t b = __builtin_amdgcn_alignbyte(w[i + 1], w[i], shf) & s_msk[i][sub];
                 sacc = __builtin_amdgcn_sad_u8(b, 0u, sacc);
                 const uint32_t wu = (uint32_t)(4 * i) * 0x01010101u + 0x03020100u;
                 uacc = __builtin_amdgcn_udot4(b, wu, uacc, false);
@@ -792,7 +803,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
         uint32_t bits = 0;
 #pragma unroll
         for (int b = 0; b < kOdPairs; ++b) {
-            uint4 pw = s_pat[sub * kOdPairs + b];  // float bit patterns {x0, x1, y0, y1}
+            uint4 pw = s_pat[b][sub];  // float bit patterns {x0, x1, y0, y1}
             asm volatile("" : "+v"(pw.x), "+v"(pw.y), "+v"(pw.z), "+v"(pw.w));  // not hoisted
             const float x0 = __uint_as_float(pw.x), x1 = __uint_as_float(pw.y);
             const float y0 = __uint_as_float(pw.z), y1 = __uint_as_float(pw.w);
