@@ -921,7 +921,7 @@ __device__ inline void knn2_store(uint32_t k1, uint32_t k2, int qi, int32_t* i1,
 // train rows are the two largest accumulators (no popcount, no per-pair VALU beyond the top-2
 // update).  Train rows are walked in 4096-row segments (12-bit local index); each segment's
 // winners are folded into (H << 16 | t) keys, the layout of the VALU matcher.
-//   workgroup = 4 waves x 32 queries; per 32-row train tile each wave issues 8
+//   workgroup = kKnnWaves waves x 32 queries; per 32-row train tile each wave issues 8
 //   v_mfma_i32_32x32x32_i8 (K = 256 bits): A = train tile (expanded once per workgroup into
 //   LDS, double-buffered), B = the wave's queries (expanded once into registers).
 // C/D layout (cdna_hip_programming.md §3): lane l holds column l & 31 (its query) and rows
@@ -929,9 +929,15 @@ __device__ inline void knn2_store(uint32_t k1, uint32_t k2, int qi, int32_t* i1,
 // fragment is the same map for A and B, so any consistent bit -> element assignment is exact.
 typedef int knn_v4i __attribute__((ext_vector_type(4)));
 typedef int knn_v16i __attribute__((ext_vector_type(16)));
-constexpr int kKnnQ = 128;       // queries per workgroup
-constexpr int kKnnPitch = 272;   // bytes per expanded train row in LDS (256 + 16: no bank conflicts)
-constexpr int kKnnSeg = 4096;    // train rows per key segment
+#ifndef KNN_WAVES
+#define KNN_WAVES 8
+#endif
+constexpr int kKnnWaves = KNN_WAVES;     // waves per workgroup, 32 queries each
+constexpr int kKnnThreads = 64 * kKnnWaves;
+constexpr int kKnnQ = 32 * kKnnWaves;    // queries per workgroup
+constexpr int kKnnPitch = 272;           // bytes per expanded train row in LDS (256 + 16: no bank conflicts)
+constexpr int kKnnSeg = 4096;            // train rows per key segment
+static_assert(kKnnWaves == 4 || kKnnWaves == 8, "expansion roles");
 
 // 4 descriptor bits -> 4 int8 (+64 for a set bit, -64 otherwise), bit k -> byte k
 __device__ inline uint32_t knn_expand4(uint32_t n) {
@@ -962,7 +968,7 @@ __device__ inline int knn_max3_i32(int a, int b, int c) {
     return r;
 }
 
-// One workgroup: queries [qb * 128, +128) of q against all nt train rows of t.
+// One workgroup: queries [qb * kKnnQ, +kKnnQ) of q against all nt train rows of t.
 __device__ __attribute__((always_inline)) inline void knn2_mfma_block(
     const uint8_t* q, int nq, const uint8_t* t, int nt, int qb, int32_t* i1, int32_t* d1, int32_t* i2,
     int32_t* d2, uint8_t* lds) {
@@ -980,22 +986,31 @@ __device__ __attribute__((always_inline)) inline void knn2_mfma_block(
     }
     uint32_t g1 = 0xFFFFFFFFu, g2 = 0xFFFFFFFFu;  // (H << 16 | t), lexicographic min
     const int ntiles_all = (nt + 31) >> 5;
-    // expansion role: thread -> (row tid >> 3, dword tid & 7) of a tile
-    const int er = tid >> 3, ed = tid & 7;
+    // expansion role.  4 waves: thread -> (row tid >> 3, dword tid & 7) of a tile, two 16-byte
+    // stores (threads ed >= 4 store their upper half first, so each store instruction's 8 chunks
+    // start on 8 distinct 4-bank boundaries).  8 waves: thread -> (row tid >> 4, 16-bit piece
+    // tid & 15), one 16-byte store (8 lanes write 128 contiguous bytes: conflict-free).
+    constexpr int kPieces = kKnnThreads / 32;  // pieces per train row
+    const int er = tid / kPieces, ed = tid % kPieces;
     auto load_packed = [&](int tile) __attribute__((always_inline)) {
         const int row = min(tile * 32 + er, nt - 1);
-        return *reinterpret_cast<const uint32_t*>(t + (long long)row * 32 + 4 * ed);
+        if constexpr (kKnnWaves == 4)
+            return *reinterpret_cast<const uint32_t*>(t + (long long)row * 32 + 4 * ed);
+        else
+            return (uint32_t)*reinterpret_cast<const uint16_t*>(t + (long long)row * 32 + 2 * ed);
     };
-    // the 8 threads of a row write 256 contiguous bytes as two 16-byte stores each; threads
-    // ed >= 4 store their upper half first, so each store instruction's 8 chunks start on 8
-    // distinct 4-bank boundaries (ds_write_b128 banks: (a / 4) mod 32) instead of 4 twice
-    const bool kswap = ed >= 4;
     auto store_expanded = [&](int buf, uint32_t w) __attribute__((always_inline)) {
-        uint8_t* dst = lds + buf * (32 * kKnnPitch) + er * kKnnPitch + 32 * ed;
-        const uint32_t ws = kswap ? __builtin_amdgcn_alignbit(w, w, 16) : w;  // halves swapped
-        const knn_v4i first = knn_expand16(ws & 0xFFFFu), second = knn_expand16(ws >> 16);
-        *reinterpret_cast<knn_v4i*>(dst + (kswap ? 16 : 0)) = first;
-        *reinterpret_cast<knn_v4i*>(dst + (kswap ? 0 : 16)) = second;
+        if constexpr (kKnnWaves == 4) {
+            uint8_t* dst = lds + buf * (32 * kKnnPitch) + er * kKnnPitch + 32 * ed;
+            const bool kswap = ed >= 4;
+            const uint32_t ws = kswap ? __builtin_amdgcn_alignbit(w, w, 16) : w;  // halves swapped
+            const knn_v4i first = knn_expand16(ws & 0xFFFFu), second = knn_expand16(ws >> 16);
+            *reinterpret_cast<knn_v4i*>(dst + (kswap ? 16 : 0)) = first;
+            *reinterpret_cast<knn_v4i*>(dst + (kswap ? 0 : 16)) = second;
+        } else {
+            uint8_t* dst = lds + buf * (32 * kKnnPitch) + er * kKnnPitch + 16 * ed;
+            *reinterpret_cast<knn_v4i*>(dst) = knn_expand16(w);
+        }
     };
     // packed train words run two tiles ahead of the MFMAs (one in LDS, one in flight): the word
     // of tile u lives in pk[u & 1]; loads are unconditional (clamped rows) so waits stay counted
@@ -1004,17 +1019,30 @@ __device__ __attribute__((always_inline)) inline void knn2_mfma_block(
         store_expanded(0, load_packed(0));
         pk1 = load_packed(1);
     }
-    // accumulator preload: row(g) = (g & 3) + 8 (g >> 2) + 4 h, so 4095 - local row index is
-    // (4095 - 4 h - 32 (tile - tile0)) - rowc(g) with a compile-time rowc
+    // accumulator preload, the same for every tile: row(g) = (g & 3) + 8 (g >> 2) + 4 h, so
+    // C0[g] = 4095 - 4 h - rowc(g) is 4095 - (tile-local row) and tile k of a segment yields
+    // acc = key + 32 k, key = 4096 (256 - 2H) + 4095 - (segment-local row).  The running top-2
+    // keys are kept in the frame of the tile being selected (+32 per tile) instead of
+    // re-preloading 16 accumulators per tile.
     auto rowc = [](int g) { return (g & 3) + 8 * (g >> 2); };
+    knn_v16i C0;
+#pragma unroll
+    for (int g = 0; g < 16; ++g) C0[g] = 4095 - 4 * h - rowc(g);
+    constexpr int kNone = -(1 << 30);  // below every key, and stays below after +32 per tile
     for (int seg0 = 0; seg0 < nt; seg0 += kKnnSeg) {
         const int tile0 = seg0 >> 5, tile1 = min(ntiles_all, (seg0 + kKnnSeg) >> 5);  // tile0 even
-        // two independent top-2 chains (even / odd accumulator rows), segment-local keys,
-        // lexicographic max; the selection of tile ti - 1 runs while tile ti's MFMAs are in flight
-        int ka1 = INT_MIN, ka2 = INT_MIN, kb1 = INT_MIN, kb2 = INT_MIN;
+        // two independent top-2 chains (even / odd accumulator rows), lexicographic max; the
+        // selection of tile ti - 1 runs while tile ti's MFMAs are in flight
+        int ka1 = kNone, ka2 = kNone, kb1 = kNone, kb2 = kNone;
         // two candidates per step and chain (keys are distinct): the new best is max3(k1, x, y),
         // the new second max(k2, med3(k1, x, y)) -- 3 VALU per 2 candidates instead of 4
-        auto select = [&](const knn_v16i& v) __attribute__((always_inline)) {
+        auto select = [&](const knn_v16i& v, bool shift) __attribute__((always_inline)) {
+            if (shift) {  // previous tile's frame -> this tile's frame
+                ka1 += 32;
+                ka2 += 32;
+                kb1 += 32;
+                kb2 += 32;
+            }
 #pragma unroll
             for (int g = 0; g < 16; g += 4) {
                 const int x0 = v[g], y0 = v[g + 1], x1 = v[g + 2], y1 = v[g + 3];
@@ -1031,21 +1059,22 @@ __device__ __attribute__((always_inline)) inline void knn2_mfma_block(
             __syncthreads();  // tile ti expanded; the other buffer is free
             pk_load = load_packed(ti + 2);  // word of tile ti + 2 (pk[ti & 1] is free)
             const uint8_t* ab = lds + PAR * (32 * kKnnPitch) + r * kKnnPitch + 16 * h;
-            const int base = 4095 - 4 * h - 32 * (ti - tile0);
-#pragma unroll
-            for (int g = 0; g < 16; ++g) acc[g] = base - rowc(g);
-            if (ti * 32 + 32 > nt) {  // partial last tile: padding rows never win
-#pragma unroll
-                for (int g = 0; g < 16; ++g)
-                    if (ti * 32 + rowc(g) + 4 * h >= nt) acc[g] = -(1 << 30);
+            {
+                const knn_v4i a = *reinterpret_cast<const knn_v4i*>(ab);
+                acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, qf[0], C0, 0, 0, 0);
             }
 #pragma unroll
-            for (int s = 0; s < 8; ++s) {
+            for (int s = 1; s < 8; ++s) {
                 const knn_v4i a = *reinterpret_cast<const knn_v4i*>(ab + 32 * s);
                 acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, qf[s], acc, 0, 0, 0);
             }
-            if (ti > tile0) select(prev);
+            if (ti > tile0) select(prev, ti - 1 > tile0);
             if (ti + 1 < ntiles_all) store_expanded(PAR ^ 1, pk_use);  // word of tile ti + 1
+            if (ti * 32 + 32 > nt) {  // partial last tile: padding rows never win
+#pragma unroll
+                for (int g = 0; g < 16; ++g)
+                    if (ti * 32 + rowc(g) + 4 * h >= nt) acc[g] = kNone;
+            }
         };
         using P0 = std::integral_constant<int, 0>;
         using P1 = std::integral_constant<int, 1>;
@@ -1057,12 +1086,14 @@ __device__ __attribute__((always_inline)) inline void knn2_mfma_block(
         }
         if (ti < tile1) {
             body(ti, P0{}, acc0, acc1, pk1, pk0);
-            select(acc0);
+            select(acc0, ti > tile0);
         } else if (tile1 > tile0) {
-            select(acc1);
+            select(acc1, tile1 - 1 > tile0);
         }
-        int k1 = max(ka1, kb1);
-        int k2 = max(min(ka1, kb1), max(ka2, kb2));
+        // back to segment keys: the last selected tile is tile1 - 1
+        const int unbias = 32 * (tile1 - 1 - tile0);
+        int k1 = max(ka1, kb1) - unbias;
+        int k2 = max(min(ka1, kb1), max(ka2, kb2)) - unbias;
         // fold the segment's two winners into global (H << 16 | t) keys
         auto fold = [&](int k) __attribute__((always_inline)) {
             if (k < -(1 << 24)) return;  // padding rows only
@@ -1083,7 +1114,7 @@ __device__ __attribute__((always_inline)) inline void knn2_mfma_block(
     if (h == 0 && qi < nq) knn2_store(g1, g2, qi, i1, d1, i2, d2);
 }
 
-__global__ __launch_bounds__(256) void k_knn2_mfma_pairs(MatchArgs m) {
+__global__ __launch_bounds__(kKnnThreads) void k_knn2_mfma_pairs(MatchArgs m) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[2 * 32 * kKnnPitch];
     const int pair = m.pair0 + blockIdx.y;
     const int qimg = 2 * pair, timg = 2 * pair + 1;
@@ -1099,7 +1130,7 @@ __global__ __launch_bounds__(256) void k_knn2_mfma_pairs(MatchArgs m) {
     knn2_mfma_block(q, nq, t, nt, blockIdx.x, m.idx1 + o, m.dist1 + o, m.idx2 + o, m.dist2 + o, lds);
 }
 
-__global__ __launch_bounds__(256) void k_knn2_mfma_plain(const uint8_t* q, int nq, const uint8_t* t, int nt,
+__global__ __launch_bounds__(kKnnThreads) void k_knn2_mfma_plain(const uint8_t* q, int nq, const uint8_t* t, int nt,
                                                          int32_t* i1, int32_t* d1, int32_t* i2, int32_t* d2) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[2 * 32 * kKnnPitch];
     knn2_mfma_block(q, nq, t, nt, blockIdx.x, i1, d1, i2, d2, lds);
@@ -1173,13 +1204,13 @@ hipError_t launch_finalize(const BatchArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 hipError_t launch_knn2_pairs(const MatchArgs& m, int npairs, hipStream_t s) {
-    hipLaunchKernelGGL(k_knn2_mfma_pairs, dim3((m.out_cap + kKnnQ - 1) / kKnnQ, npairs), dim3(256), 0, s, m);
+    hipLaunchKernelGGL(k_knn2_mfma_pairs, dim3((m.out_cap + kKnnQ - 1) / kKnnQ, npairs), dim3(kKnnThreads), 0, s, m);
     return hipGetLastError();
 }
 hipError_t launch_knn2_plain(const uint8_t* q, int nq, const uint8_t* t, int nt, int32_t* i1,
                              int32_t* d1, int32_t* i2, int32_t* d2, hipStream_t s) {
     if (nq == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_knn2_mfma_plain, dim3((nq + kKnnQ - 1) / kKnnQ), dim3(256), 0, s, q, nq, t, nt, i1,
+    hipLaunchKernelGGL(k_knn2_mfma_plain, dim3((nq + kKnnQ - 1) / kKnnQ), dim3(kKnnThreads), 0, s, q, nq, t, nt, i1,
                        d1, i2, d2);
     return hipGetLastError();
 }
