@@ -113,7 +113,8 @@ __device__ inline uint32_t rs_quad(const Row& r0, const Row& r1, const int4* xt,
                 const int sv = (__umul24(D0[k] >> 4, b0) >> 16) + (__umul24(D1[k] >> 4, b1) >> 16);
                 o = (sv + 2) >> 2;
             } else {
-                o = (int)(((unsigned)D0[k] * (unsigned)b0 + (unsigned)D1[k] * (unsigned)b1 + (1u << 21)) >> 22);
+                // D < 2^19, b <= 2048: both 24-bit, products < 2^30 (full-rate multiplies)
+                o = (int)((__umul24((unsigned)D0[k], (unsigned)b0) + __umul24((unsigned)D1[k], (unsigned)b1) + (1u << 21)) >> 22);
             }
             packed |= (uint32_t)min(o, 255) << (8 * k);
         }
@@ -125,6 +126,15 @@ __device__ inline uint32_t rs_quad(const Row& r0, const Row& r1, const int4* xt,
 // k_blur: cv::GaussianBlur(Size(7,7), 2, 2, BORDER_REFLECT_101) on each level
 // (ORBextractor_old.cc:1146-1147), bit-exact fixed point: kernel {18,34,48,56,48,34,18}/256,
 // out = (sum_v w_v sum_h w_h p + 2^15) >> 16 with the horizontal sums exact (<= 65280, u16).
+// Byte offset of (row y, column x) inside one plane: planes are < 16 M rows of < 16 MB pitch
+// and < 2^32 bytes, so the row product is one full-rate 24-bit multiply (no 64-bit multiply
+// per access).
+__device__ inline size_t plane_off(int y, int pitch, int x) {
+    uint32_t o;  // v_mad_u32_u24 kept as such (not re-associated into a 64-bit multiply-add)
+    asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(o) : "v"(y), "v"(pitch), "v"(x));
+    return (size_t)o;
+}
+
 __device__ inline int refl101(int p, int n) {
     p = p < 0 ? -p : p;
     return p >= n ? 2 * n - p - 2 : p;
@@ -265,7 +275,7 @@ __device__ inline void blur_tile_compute(const LevelGeom& G, int tx0, int ty0, u
         const uint32_t lo = __builtin_amdgcn_perm(sv[1], sv[0], 0x0c0c0602u);
         const uint32_t hi = __builtin_amdgcn_perm(sv[3], sv[2], 0x0c0c0602u);
         const uint32_t packed = lo | (hi << 16);
-        if (y >= rlo && y < rhi && y < G.h && x < G.w) *reinterpret_cast<uint32_t*>(dst + (long long)y * G.bpitch + x) = packed;
+        if (y >= rlo && y < rhi && y < G.h && x < G.w) *reinterpret_cast<uint32_t*>(dst + plane_off(y, G.bpitch, x)) = packed;
     }
 }
 
@@ -385,11 +395,11 @@ __device__ inline void br_tile(const BatchArgs& a, int l, bool resize, int img, 
     const float inv_nq = nq > 0 ? 1.f / (float)nq : 0.f;
     for (int it = threadIdx.x; it < nr * nq; it += 256) {
         const int rr = (int)(((float)it + 0.5f) * inv_nq);  // exact: it < 34 * 40
-        const int q = it - rr * nq;
+        const int q = it - __mul24(rr, nq);
         const int dy = r0 + rr, dx0 = 4 * (q0 + q);
         uint32_t packed = 0;
         if (G.area2) {
-            const uint8_t* s0 = wb + (2 * dy - wy0) * IW - wx0;
+            const uint8_t* s0 = wb + __mul24(2 * dy - wy0, IW) - wx0;
             const uint8_t* s1 = s0 + IW;
 #pragma unroll
             for (int kk = 0; kk < 4; ++kk) {
@@ -399,11 +409,11 @@ __device__ inline void br_tile(const BatchArgs& a, int l, bool resize, int img, 
             }
         } else {
             const int4 yt = sm.yts[rr];
-            const uint8_t* row0 = wb + (yt.x - wy0) * IW - wx0;
-            const uint8_t* row1 = wb + (yt.y - wy0) * IW - wx0;
+            const uint8_t* row0 = wb + __mul24(yt.x - wy0, IW) - wx0;
+            const uint8_t* row1 = wb + __mul24(yt.y - wy0, IW) - wx0;
             packed = rs_quad(row0, row1, sm.xts + q, yt.z, yt.w, dx0, G.simd_end);
         }
-        *reinterpret_cast<uint32_t*>(dst + (long long)dy * G.pitch + dx0) = packed;
+        *reinterpret_cast<uint32_t*>(dst + plane_off(dy, G.pitch, dx0)) = packed;
     }
 }
 
@@ -726,7 +736,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
         // the moment row (round trip 1) and the 37 x 37 blurred patch (rows y-18..y+18 from the
         // dword at or below x-18, 16-byte buffer loads, out-of-range bytes read as 0 and never
         // sampled) are both requested before either is used, so the two round trips overlap
-        const uint8_t* row = lvl + (long long)(y + vrow[0]) * G.pitch;
+        const uint8_t* row = lvl + plane_off(y + vrow[0], G.pitch, 0);
         uint32_t w[9];
         if (raw_dw) {  // 2 x dwordx4 + 1 dword (global loads need only dword alignment)
             const uint4 A = *reinterpret_cast<const uint4*>(row + xa);
