@@ -64,7 +64,9 @@ typedef struct orbgpu_ctx orbgpu_ctx;
 
 /* Build a context for images up to max_width x max_height and batches of up to max_images
  * images.  Allocates all device memory once (nothing is allocated per call).  device = HIP
- * ordinal.  Replaces the ORBextractor ctor + LynxHardwareAccelerator ctor (orbslam3_open). */
+ * ordinal.  Replaces the ORBextractor ctor + LynxHardwareAccelerator ctor (orbslam3_open).
+ * ORBGPU_ERR_INVALID for nlevels outside [1, 16], scale_factor not in (1, 2], negative
+ * nfeatures or sizes outside (0, 4112); ORBGPU_ERR_NO_DEVICE without a HIP device. */
 int orbgpu_create(const orbgpu_params* params, int device, int max_width, int max_height,
                   int max_images, orbgpu_ctx** out_ctx);
 int orbgpu_destroy(orbgpu_ctx* ctx); /* orbslam3_close */

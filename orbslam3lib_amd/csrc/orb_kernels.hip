@@ -81,22 +81,39 @@ __constant__ MomentWeights c_mw = make_moment_weights();
 
 // ---------------------------------------------------------------------------------------------
 // ---------------------------------------------------------------------------------------------
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+__device__ inline u16x2 as_u16x2(uint32_t x) { return __builtin_bit_cast(u16x2, x); }
+__device__ inline uint32_t as_u32(u16x2 x) { return __builtin_bit_cast(uint32_t, x); }
+
 // cv::resize INTER_LINEAR (canonical ComputePyramid, ORBextractor_old.cc:1342-1344), fixed point.
-// Four output pixels dx0 .. dx0+3 of one output row from source rows r0 / r1 (LDS window rows), x
-// coefficients xt[k * kBrMaxQuads] (k = 0..3; entries past the tile edge may be stale: their
-// bytes are padding or the next tile's, rewritten there), y coefficients b0 / b1.  Every product fits 24
-// bits (pixel <= 255, coefficients <= 2048, (D >> 4) < 2^15), so all multiplies are full-rate
-// v_mul_u32_u24 / v_mad_u32_u24.  Vertical rounding: OpenCV's SIMD body below simd_end,
-// FixedPtCast after it (only the last quads of a row take that branch).
-template <class Row>
-__device__ inline uint32_t rs_quad(const Row& r0, const Row& r1, const int4* xt, int b0, int b1, int dx0,
-                                   int simd_end) {
+// Four output pixels dx0 .. dx0+3 of one output row from source rows r0 / r1 (LDS window rows,
+// indexed by source column).  The quad's taps lie in the 8 source bytes from its first left tap
+// `base` (scale <= 2: the last right tap is at most base + 7), read as three aligned dwords per
+// row and byte-aligned with v_alignbyte; sel[k] picks output k's two taps as a u16 pair (v_perm)
+// and cw[k] holds its two x coefficients as a u16 pair, so each horizontal sum is one
+// v_dot2_u32_u16 (exact: taps <= 255, coefficients <= 2048).  Vertical rounding: OpenCV's SIMD
+// body below simd_end, FixedPtCast after it (only the last quads of a row take that branch);
+// every product fits 24 bits (D < 2^19, b <= 2048), so all multiplies are full-rate
+// v_mul_u32_u24.
+__device__ inline uint32_t rs_quad(const uint8_t* r0, const uint8_t* r1, int base, int4 sel, int4 cw, int b0,
+                                   int b1, int dx0, int simd_end) {
+    const uint32_t* p0 = reinterpret_cast<const uint32_t*>(r0 + (base & ~3));
+    const uint32_t* p1 = reinterpret_cast<const uint32_t*>(r1 + (base & ~3));
+    const uint32_t sh = (uint32_t)(base & 3);
+    const uint32_t a0 = p0[0], a1 = p0[1], a2 = p0[2];
+    const uint32_t c0 = p1[0], c1 = p1[1], c2 = p1[2];
+    const uint32_t lo0 = __builtin_amdgcn_alignbyte(a1, a0, sh), hi0 = __builtin_amdgcn_alignbyte(a2, a1, sh);
+    const uint32_t lo1 = __builtin_amdgcn_alignbyte(c1, c0, sh), hi1 = __builtin_amdgcn_alignbyte(c2, c1, sh);
+    const int sl[4] = {sel.x, sel.y, sel.z, sel.w};
+    const int cl[4] = {cw.x, cw.y, cw.z, cw.w};
     int D0[4], D1[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-        const int4 x = xt[k * kBrMaxQuads];
-        D0[k] = __umul24(r0[x.x], x.z) + __umul24(r0[x.y], x.w);
-        D1[k] = __umul24(r1[x.x], x.z) + __umul24(r1[x.y], x.w);
+        const uint32_t t0 = __builtin_amdgcn_perm(hi0, lo0, (uint32_t)sl[k]);
+        const uint32_t t1 = __builtin_amdgcn_perm(hi1, lo1, (uint32_t)sl[k]);
+        D0[k] = (int)__builtin_amdgcn_udot2(as_u16x2(t0), as_u16x2((uint32_t)cl[k]), 0u, false);
+        D1[k] = (int)__builtin_amdgcn_udot2(as_u16x2(t1), as_u16x2((uint32_t)cl[k]), 0u, false);
     }
     uint32_t packed = 0;
     if (dx0 + 3 < simd_end) {
@@ -148,10 +165,6 @@ __device__ inline int refl101(int p, int n) {
 // {0,18}{34,48}{56,48}{34,18} (even rows) or {18,34}{48,56}{48,34}{18,0} (odd rows), the
 // accumulator seeded with the 2^15 rounding term.
 constexpr int kBlurTW = 128, kBlurTH = 32;
-typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-
-__device__ inline u16x2 as_u16x2(uint32_t x) { return __builtin_bit_cast(u16x2, x); }
-__device__ inline uint32_t as_u32(u16x2 x) { return __builtin_bit_cast(uint32_t, x); }
 
 struct BlurTile {
     int l, ty0, tx0;
@@ -341,7 +354,11 @@ static_assert(kBrMaxQuads >= kBlurTW / 4 + 1 && kBrMaxRows >= kBlurTH + 1, "owne
 struct BrSmem {
     uint4 tin4[kBlurTH + 8][(kBlurTW + 32) / 16];
     uint4 hp[(kBlurTH + 8) / 2][kBlurTW / 4];
-    int4 xts[4 * kBrMaxQuads];  // [k][quad]: a wave's consecutive quads read consecutive entries
+    // per owned output quad (rs_quad): tap selectors, coefficient pairs, first left tap; one
+    // array per field so a wave's consecutive quads read consecutive entries
+    int4 xsel[kBrMaxQuads];
+    int4 xcw[kBrMaxQuads];
+    int xbase[kBrMaxQuads];
     int4 yts[kBrMaxRows];
 };
 
@@ -375,8 +392,22 @@ __device__ inline void br_tile(const BatchArgs& a, int l, bool resize, int img, 
         nr = min(band_row[by + 1] - r0, kBrMaxRows);
         nq = min(tile_quad[bx + 1] - q0, kBrMaxQuads);
         if (!G.area2) {
-            for (int i = threadIdx.x; i < 4 * nq; i += 256)
-                sm.xts[(i & 3) * kBrMaxQuads + (i >> 2)] = a.rtab[G.xtab_off + min(4 * q0 + i, G.w - 1)];
+            if (threadIdx.x < nq) {
+                const int q = threadIdx.x;
+                int4 x[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) x[k] = a.rtab[G.xtab_off + min(4 * (q0 + q) + k, G.w - 1)];
+                const int base = x[0].x;
+                int sl[4], cl[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {  // taps relative to base: 0 .. 7 (scale <= 2)
+                    sl[k] = (x[k].x - base) | 0x0c00 | ((x[k].y - base) << 16) | 0x0c000000;
+                    cl[k] = x[k].z | (x[k].w << 16);
+                }
+                sm.xsel[q] = make_int4(sl[0], sl[1], sl[2], sl[3]);
+                sm.xcw[q] = make_int4(cl[0], cl[1], cl[2], cl[3]);
+                sm.xbase[q] = base;
+            }
             if (threadIdx.x < nr) sm.yts[threadIdx.x] = a.rtab[G.ytab_off + r0 + threadIdx.x];
         }
     }
@@ -411,7 +442,7 @@ __device__ inline void br_tile(const BatchArgs& a, int l, bool resize, int img, 
             const int4 yt = sm.yts[rr];
             const uint8_t* row0 = wb + __mul24(yt.x - wy0, IW) - wx0;
             const uint8_t* row1 = wb + __mul24(yt.y - wy0, IW) - wx0;
-            packed = rs_quad(row0, row1, sm.xts + q, yt.z, yt.w, dx0, G.simd_end);
+            packed = rs_quad(row0, row1, sm.xbase[q], sm.xsel[q], sm.xcw[q], yt.z, yt.w, dx0, G.simd_end);
         }
         *reinterpret_cast<uint32_t*>(dst + plane_off(dy, G.pitch, dx0)) = packed;
     }
@@ -844,64 +875,123 @@ struct KP28 {
     int32_t octave, class_id;
 };
 
-__global__ __launch_bounds__(256) void k_finalize(BatchArgs a) {
-    __shared__ int scratch[16];
+// The image's keypoints are walked as one sequence (level l's keypoint j at off[l] + j), in
+// batches of kFinU chunks of kFinThreads whose loads are all issued before the first chunk's partition,
+// so a batch costs one memory round trip instead of one per level and chunk.  The mono / stereo
+// ranks come from per-wave ballots and one barrier per chunk.
+constexpr int kFinU = 2;
+#ifndef FIN_WIDE_MAX
+#define FIN_WIDE_MAX 8
+#endif
+constexpr int kFinWideMaxImages = FIN_WIDE_MAX;
+
+template <int kFinThreads>  // a chunk is one keypoint per thread
+__global__ __launch_bounds__(kFinThreads) void k_finalize(BatchArgs a) {
+    __shared__ int4 s_lv[kMaxLevels];  // {level key base (image-relative), off[l], scale bits, patch}
+    __shared__ int s_wave[2][kFinThreads / 64];  // per-wave stereo counts, double-buffered over chunks
     const int img = a.img0 + blockIdx.x;
-    DevPolicy p{scratch};
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int L = a.nlevels;
+    int off[kMaxLevels];  // uniform: first sequence index of each level
     int total = 0;
     bool bad = false;
-    for (int l = 0; l < a.nlevels; ++l) {
-        total += a.lvlcnt[img * kMaxLevels + l];
-        bad |= a.status[img * kMaxLevels + l] != 0;
+#pragma unroll
+    for (int l = 0; l < kMaxLevels; ++l) {
+        off[l] = total;
+        if (l < L) {
+            total += a.lvlcnt[img * kMaxLevels + l];
+            bad |= a.status[img * kMaxLevels + l] != 0;
+        }
     }
     if (bad || total > a.out_cap) {
-        if (threadIdx.x == 0) {
+        if (tid == 0) {
             a.out_n[img] = bad ? -5 : -2;
             a.out_mono[img] = 0;
         }
         return;
     }
+    if (tid == 0) {  // uniform level loop: the level records are read with scalar loads
+#pragma unroll
+        for (int l = 0; l < kMaxLevels; ++l)
+            if (l < L) s_lv[l] = make_int4(a.lv[l].kp_off, off[l], __float_as_int(l == 0 ? 1.f : a.lv[l].scale), a.lv[l].patch);
+    }
+    __syncthreads();
     const float lap0 = (float)a.laps[2 * img], lap1 = (float)a.laps[2 * img + 1];
     KP28* out = reinterpret_cast<KP28*>(a.out_kps) + (long long)img * a.out_cap;
     uint8_t* od = a.out_desc + (long long)img * a.out_cap * 32;
-    int mono = 0, stereo = 0;
-    for (int l = 0; l < a.nlevels; ++l) {
-        const LevelGeom& G = a.lv[l];
-        const int cnt = a.lvlcnt[img * kMaxLevels + l];
-        const long long kbase = (long long)img * a.lvlkp_img_stride + G.kp_off;
-        for (int base = 0; base < cnt; base += 256) {
-            const int i = base + threadIdx.x;
+    const long long ibase = (long long)img * a.lvlkp_img_stride;
+    const uint64_t lt = (1ull << lane) - 1ull;
+    int mono = 0, stereo = 0, chunk_no = 0;
+    for (int base = 0; base < total; base += kFinThreads * kFinU) {
+        uint32_t key[kFinU];
+        float ang[kFinU];
+        uint4 d0[kFinU], d1[kFinU];
+        int lev[kFinU];
+#pragma unroll
+        for (int u = 0; u < kFinU; ++u) {
+            const int i = base + u * kFinThreads + tid;
+            int l = 0;
+#pragma unroll
+            for (int k = 1; k < kMaxLevels; ++k) l += (k < L && i >= off[k]) ? 1 : 0;
+            lev[u] = l;
+            if (i < total) {
+                const int4 info = s_lv[l];
+                const long long kb = ibase + info.x + (i - info.y);
+                key[u] = a.lvlkey[kb];
+                ang[u] = a.lvlangle[kb];
+                const uint4* s4 = reinterpret_cast<const uint4*>(a.lvldesc + kb * 32);
+                d0[u] = s4[0];
+                d1[u] = s4[1];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kFinU; ++u) {
+            const int cb = base + u * kFinThreads;
+            if (cb >= total) continue;  // uniform (the batch's last chunks)
+            const int i = cb + tid;
+            const bool valid = i < total;
             KP28 k;
             bool st = false;
-            if (i < cnt) {
-                const uint32_t key = a.lvlkey[kbase + i];
-                k.x = (float)(key_x(key) + kMinBorder);
-                k.y = (float)(key_y(key) + kMinBorder);
+            if (valid) {
+                const int l = lev[u];
+                const int4 info = s_lv[l];
+                k.x = (float)(key_x(key[u]) + kMinBorder);
+                k.y = (float)(key_y(key[u]) + kMinBorder);
                 if (l != 0) {
-                    k.x = k.x * G.scale;
-                    k.y = k.y * G.scale;
+                    k.x = k.x * __int_as_float(info.z);
+                    k.y = k.y * __int_as_float(info.z);
                 }
-                k.size = (float)G.patch;
-                k.angle = a.lvlangle[kbase + i];
-                k.response = (float)key_resp(key);
+                k.size = (float)info.w;
+                k.angle = ang[u];
+                k.response = (float)key_resp(key[u]);
                 k.octave = l;
                 k.class_id = -1;
                 st = (k.x >= lap0 && k.x <= lap1);
             }
-            int tst;
-            const int exs = p.scan_excl(st ? 1 : 0, &tst);
-            const int exm = (int)threadIdx.x - exs;  // earlier lanes of this chunk are all valid
-            if (i < cnt) {
+            const uint64_t bal = __ballot(st);
+            const int buf = chunk_no & 1;
+            if (lane == 0) s_wave[buf][w] = __popcll(bal);
+            __syncthreads();
+            int before = 0, tst = 0;
+#pragma unroll
+            for (int v = 0; v < kFinThreads / 64; ++v) {
+                const int c = s_wave[buf][v];
+                tst += c;
+                before += v < w ? c : 0;
+            }
+            const int exs = before + __popcll(bal & lt);
+            const int exm = tid - exs;  // earlier lanes of this chunk are all valid
+            if (valid) {
                 const int dst = st ? (total - 1 - (stereo + exs)) : (mono + exm);
                 out[dst] = k;
-                const uint4* s4 = reinterpret_cast<const uint4*>(a.lvldesc + (kbase + i) * 32);
                 uint4* d4 = reinterpret_cast<uint4*>(od + (long long)dst * 32);
-                d4[0] = s4[0];
-                d4[1] = s4[1];
+                d4[0] = d0[u];
+                d4[1] = d1[u];
             }
-            const int chunk = min(256, cnt - base);
+            const int chunk = min(kFinThreads, total - cb);
             stereo += tst;
             mono += chunk - tst;
+            ++chunk_no;
         }
     }
     if (threadIdx.x == 0) {
@@ -1210,7 +1300,9 @@ hipError_t launch_orient_desc(const BatchArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 hipError_t launch_finalize(const BatchArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(k_finalize, dim3(a.nimages), dim3(256), 0, s, a);
+    // few images (the latency shape): 512 threads per image; full batches: 256
+    if (a.nimages <= kFinWideMaxImages) hipLaunchKernelGGL(k_finalize<512>, dim3(a.nimages), dim3(512), 0, s, a);
+    else hipLaunchKernelGGL(k_finalize<256>, dim3(a.nimages), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 hipError_t launch_knn2_pairs(const MatchArgs& m, int npairs, hipStream_t s) {

@@ -659,6 +659,10 @@ int orbgpu_create(const orbgpu_params* p, int device, int max_width, int max_hei
         max_width <= 0 || max_height <= 0 || max_images <= 0 || max_width >= 4096 + 16 ||
         max_height >= 4096 + 16)
         return fail(ORBGPU_ERR_INVALID, "invalid ORB parameters or sizes");
+    // k_blur_resize makes level l from the window of level l - 1 its tile has staged; the taps
+    // of a resize step stay inside that window only for scale steps up to 2
+    if (p->scale_factor > 2.0f)
+        return fail(ORBGPU_ERR_INVALID, "scale_factor above 2 is not supported");
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
         return fail(ORBGPU_ERR_NO_DEVICE, "no HIP device");

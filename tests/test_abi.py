@@ -5,6 +5,7 @@ import os
 import re
 
 import numpy as np
+import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -47,3 +48,14 @@ def test_host_entry_points():
     # null arguments are rejected with a status code, never a crash
     assert lib.orbgpu_create(None, 0, 640, 480, 1, None) == -3
     assert lib.orbgpu_destroy(None) == 0
+
+
+@pytest.mark.parametrize("scale", [1.0, 2.5])
+def test_create_rejects_unsupported_scale_factor(scale):
+    """orbgpu_create validates the parameters before it looks for a device: a scale step of 1 or
+    above 2 (k_blur_resize makes level l from the staged window of level l - 1, which holds the
+    taps only for steps up to 2) is ORBGPU_ERR_INVALID, with or without a GPU."""
+    import orbslam3lib_amd as og
+    with pytest.raises(og.OrbGpuError) as e:
+        og.ORBextractor(1000, scale, 8, 20, 7, max_width=640, max_height=480)
+    assert e.value.code == -3  # ORBGPU_ERR_INVALID (include/orbgpu.h)
