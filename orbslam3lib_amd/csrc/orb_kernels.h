@@ -99,7 +99,10 @@ struct MatchArgs {
     int32_t* dist2;           // [pair][out_cap]
     int32_t* nq;              // [pair]
     int pair0;                // first pair of this launch
+    uint2* part;              // [kKnnSplitSlots][out_cap] partial top-2 keys of split launches, or null
 };
+constexpr int kKnnMaxSplit = 8;     // train-row splits of a launch with few pairs
+constexpr int kKnnSplitSlots = 8;   // pairs x splits the partial buffer holds (1 pair: 8 splits)
 
 // Frame::ComputeStereoMatches over a batch's device-resident results (orb_stereo.hip).
 struct StereoArgs {

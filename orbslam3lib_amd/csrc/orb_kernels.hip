@@ -1068,10 +1068,12 @@ __device__ inline int knn_max3_i32(int a, int b, int c) {
     return r;
 }
 
-// One workgroup: queries [qb * kKnnQ, +kKnnQ) of q against all nt train rows of t.
+// One workgroup: queries [qb * kKnnQ, +kKnnQ) of q against train tiles [ts, te) of t (all of
+// them unless the launch splits the train rows, ts even).  Without `part` the two best keys go
+// to i1 / d1 / i2 / d2; with it, to part[qi] (a split's partial top-2, merged by k_knn2_merge).
 __device__ __attribute__((always_inline)) inline void knn2_mfma_block(
-    const uint8_t* q, int nq, const uint8_t* t, int nt, int qb, int32_t* i1, int32_t* d1, int32_t* i2,
-    int32_t* d2, uint8_t* lds) {
+    const uint8_t* q, int nq, const uint8_t* t, int nt, int qb, int ts, int te, int32_t* i1, int32_t* d1,
+    int32_t* i2, int32_t* d2, uint2* part, uint8_t* lds) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int r = lane & 31, h = lane >> 5;
     const int qi = qb * kKnnQ + wave * 32 + r;
@@ -1085,7 +1087,6 @@ __device__ __attribute__((always_inline)) inline void knn2_mfma_block(
         for (int s = 0; s < 8; ++s) qf[s] = knn_expand16(dw[s] >> (16 * h));
     }
     uint32_t g1 = 0xFFFFFFFFu, g2 = 0xFFFFFFFFu;  // (H << 16 | t), lexicographic min
-    const int ntiles_all = (nt + 31) >> 5;
     // expansion role.  4 waves: thread -> (row tid >> 3, dword tid & 7) of a tile, two 16-byte
     // stores (threads ed >= 4 store their upper half first, so each store instruction's 8 chunks
     // start on 8 distinct 4-bank boundaries).  8 waves: thread -> (row tid >> 4, 16-bit piece
@@ -1115,9 +1116,9 @@ __device__ __attribute__((always_inline)) inline void knn2_mfma_block(
     // packed train words run two tiles ahead of the MFMAs (one in LDS, one in flight): the word
     // of tile u lives in pk[u & 1]; loads are unconditional (clamped rows) so waits stay counted
     uint32_t pk0 = 0, pk1 = 0;
-    if (nt > 0) {
-        store_expanded(0, load_packed(0));
-        pk1 = load_packed(1);
+    if (te > ts) {
+        store_expanded(0, load_packed(ts));
+        pk1 = load_packed(ts + 1);
     }
     // accumulator preload, the same for every tile: row(g) = (g & 3) + 8 (g >> 2) + 4 h, so
     // C0[g] = 4095 - 4 h - rowc(g) is 4095 - (tile-local row) and tile k of a segment yields
@@ -1129,8 +1130,9 @@ __device__ __attribute__((always_inline)) inline void knn2_mfma_block(
 #pragma unroll
     for (int g = 0; g < 16; ++g) C0[g] = 4095 - 4 * h - rowc(g);
     constexpr int kNone = -(1 << 30);  // below every key, and stays below after +32 per tile
-    for (int seg0 = 0; seg0 < nt; seg0 += kKnnSeg) {
-        const int tile0 = seg0 >> 5, tile1 = min(ntiles_all, (seg0 + kKnnSeg) >> 5);  // tile0 even
+    for (int seg0 = (ts * 32 / kKnnSeg) * kKnnSeg; seg0 < te * 32; seg0 += kKnnSeg) {
+        // this segment's tiles; keys are local to tile0 (< 4096 rows), tile0 even
+        const int tile0 = max(seg0 >> 5, ts), tile1 = min(te, (seg0 + kKnnSeg) >> 5);
         // two independent top-2 chains (even / odd accumulator rows), lexicographic max; the
         // selection of tile ti - 1 runs while tile ti's MFMAs are in flight
         int ka1 = kNone, ka2 = kNone, kb1 = kNone, kb2 = kNone;
@@ -1169,7 +1171,7 @@ __device__ __attribute__((always_inline)) inline void knn2_mfma_block(
                 acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, qf[s], acc, 0, 0, 0);
             }
             if (ti > tile0) select(prev, ti - 1 > tile0);
-            if (ti + 1 < ntiles_all) store_expanded(PAR ^ 1, pk_use);  // word of tile ti + 1
+            if (ti + 1 < te) store_expanded(PAR ^ 1, pk_use);  // word of tile ti + 1
             if (ti * 32 + 32 > nt) {  // partial last tile: padding rows never win
 #pragma unroll
                 for (int g = 0; g < 16; ++g)
@@ -1198,7 +1200,7 @@ __device__ __attribute__((always_inline)) inline void knn2_mfma_block(
         auto fold = [&](int k) __attribute__((always_inline)) {
             if (k < -(1 << 24)) return;  // padding rows only
             const int tl = 4095 - (k & 4095), dotp = k >> 12;
-            const uint32_t key = ((uint32_t)((256 - dotp) >> 1) << 16) | (uint32_t)(seg0 + tl);
+            const uint32_t key = ((uint32_t)((256 - dotp) >> 1) << 16) | (uint32_t)(32 * tile0 + tl);
             g2 = med3_u32(g1, g2, key);
             g1 = min(g1, key);
         };
@@ -1211,7 +1213,10 @@ __device__ __attribute__((always_inline)) inline void knn2_mfma_block(
     g1 = min(g1, o1);
     g2 = med3_u32(g1, g2, o2);
     g1 = min(g1, o2);
-    if (h == 0 && qi < nq) knn2_store(g1, g2, qi, i1, d1, i2, d2);
+    if (h == 0 && qi < nq) {
+        if (part) part[qi] = make_uint2(g1, g2);
+        else knn2_store(g1, g2, qi, i1, d1, i2, d2);
+    }
 }
 
 __global__ __launch_bounds__(kKnnThreads) void k_knn2_mfma_pairs(MatchArgs m) {
@@ -1227,13 +1232,39 @@ __global__ __launch_bounds__(kKnnThreads) void k_knn2_mfma_pairs(MatchArgs m) {
     const uint8_t* q = m.desc + ((long long)qimg * m.out_cap + q0) * 32;
     const uint8_t* t = m.desc + ((long long)timg * m.out_cap + tq0) * 32;
     const long long o = (long long)pair * m.out_cap;
-    knn2_mfma_block(q, nq, t, nt, blockIdx.x, m.idx1 + o, m.dist1 + o, m.idx2 + o, m.dist2 + o, lds);
+    // train split blockIdx.z of gridDim.z: tile ranges on 2-tile boundaries
+    const int npt = (((nt + 31) >> 5) + 1) >> 1, S = gridDim.z, sp = blockIdx.z;  // tile pairs
+    const int ts = 2 * (npt * sp / S), te = min((nt + 31) >> 5, 2 * (npt * (sp + 1) / S));
+    uint2* part = m.part ? m.part + ((long long)(blockIdx.y * S + sp)) * m.out_cap : nullptr;
+    knn2_mfma_block(q, nq, t, nt, blockIdx.x, ts, te, m.idx1 + o, m.dist1 + o, m.idx2 + o, m.dist2 + o, part, lds);
+}
+
+// The split launch's partial top-2 lists of one query, merged (keys are distinct train rows).
+__global__ __launch_bounds__(256) void k_knn2_merge(MatchArgs m, int nsplit) {
+    const int pair = m.pair0 + blockIdx.y;
+    const int qimg = 2 * pair, timg = 2 * pair + 1;
+    const int qn = m.out_n[qimg], tn = m.out_n[timg];
+    const int q0 = m.stereo_only ? m.out_mono[qimg] : 0;
+    const int nq = qn > q0 ? qn - q0 : 0;
+    (void)tn;
+    const int qi = blockIdx.x * 256 + threadIdx.x;
+    if (qi >= nq) return;
+    uint32_t g1 = 0xFFFFFFFFu, g2 = 0xFFFFFFFFu;
+    for (int sp = 0; sp < nsplit; ++sp) {
+        const uint2 k = m.part[((long long)(blockIdx.y * nsplit + sp)) * m.out_cap + qi];
+        g2 = med3_u32(g1, g2, k.x);
+        g1 = min(g1, k.x);
+        g2 = med3_u32(g1, g2, k.y);
+        g1 = min(g1, k.y);
+    }
+    const long long o = (long long)pair * m.out_cap;
+    knn2_store(g1, g2, qi, m.idx1 + o, m.dist1 + o, m.idx2 + o, m.dist2 + o);
 }
 
 __global__ __launch_bounds__(kKnnThreads) void k_knn2_mfma_plain(const uint8_t* q, int nq, const uint8_t* t, int nt,
                                                          int32_t* i1, int32_t* d1, int32_t* i2, int32_t* d2) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[2 * 32 * kKnnPitch];
-    knn2_mfma_block(q, nq, t, nt, blockIdx.x, i1, d1, i2, d2, lds);
+    knn2_mfma_block(q, nq, t, nt, blockIdx.x, 0, (nt + 31) >> 5, i1, d1, i2, d2, nullptr, lds);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1306,7 +1337,17 @@ hipError_t launch_finalize(const BatchArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 hipError_t launch_knn2_pairs(const MatchArgs& m, int npairs, hipStream_t s) {
-    hipLaunchKernelGGL(k_knn2_mfma_pairs, dim3((m.out_cap + kKnnQ - 1) / kKnnQ, npairs), dim3(kKnnThreads), 0, s, m);
+    // few pairs (the latency shape): the train rows split over S workgroups per query block, so
+    // the launch has ~256 workgroups instead of 8 per pair, and k_knn2_merge combines the splits
+    const int S = m.part ? std::max(1, std::min(kKnnMaxSplit, kKnnSplitSlots / std::max(npairs, 1))) : 1;
+    if (S > 1) {
+        hipLaunchKernelGGL(k_knn2_mfma_pairs, dim3((m.out_cap + kKnnQ - 1) / kKnnQ, npairs, S), dim3(kKnnThreads), 0, s, m);
+        hipLaunchKernelGGL(k_knn2_merge, dim3((m.out_cap + 255) / 256, npairs), dim3(256), 0, s, m, S);
+        return hipGetLastError();
+    }
+    MatchArgs m1 = m;
+    m1.part = nullptr;
+    hipLaunchKernelGGL(k_knn2_mfma_pairs, dim3((m.out_cap + kKnnQ - 1) / kKnnQ, npairs), dim3(kKnnThreads), 0, s, m1);
     return hipGetLastError();
 }
 hipError_t launch_knn2_plain(const uint8_t* q, int nq, const uint8_t* t, int nt, int32_t* i1,

@@ -112,7 +112,7 @@ struct orbgpu_ctx {
     int cellcnt_img = 0, lvlkp_img = 0, out_cap = 0;
     // device buffers
     DevBuf input, pyr, blur, rtab, cellkeys, cellcnt, octws, lvlkey, lvlangle, lvldesc, lvlcnt,
-        status, outkps, outdesc, outn, outmono, laps, midx1, mdist1, midx2, mdist2, mnq, scratch,
+        status, outkps, outdesc, outn, outmono, laps, midx1, mdist1, midx2, mdist2, mnq, mpart, scratch,
         octdbg, strow, stidx, stur, stdepth, stsad, gxy, gcell, gstart, gidx, sbs, soa, m16,
         sbpmp, sbpoff, sbpcand, sbpblk, sbpmatch, sbpnm, sbplr, fel2r, fer2l, fedepth, fep3d, fecnt;
     float grid_bounds[4] = {0, 0, 0, 0}, grid_inv[2] = {0, 0};  // of the last undistort_grid
@@ -252,6 +252,7 @@ int alloc_all(orbgpu_ctx* c, int n_images) {
     r |= c->midx2.ensure(np * c->out_cap * 4 + 256);
     r |= c->mdist2.ensure(np * c->out_cap * 4 + 256);
     r |= c->mnq.ensure(np * 4 + 64);
+    r |= c->mpart.ensure((size_t)kKnnSplitSlots * c->out_cap * 8 + 256);
     return r ? fail(ORBGPU_ERR_HIP, "hipMalloc failed (device memory)") : 0;
 }
 
@@ -738,7 +739,7 @@ int orbgpu_destroy(orbgpu_ctx* c) {
     DevBuf* bufs[] = {&c->input, &c->input2, &c->pyr,     &c->blur,   &c->rtab,    &c->cellkeys, &c->cellcnt,
                       &c->octws,   &c->lvlkey,  &c->lvlangle, &c->lvldesc, &c->lvlcnt, &c->status,
                       &c->outkps,  &c->outdesc, &c->outn,   &c->outmono, &c->laps,     &c->midx1,
-                      &c->mdist1,  &c->midx2,   &c->mdist2, &c->mnq,     &c->scratch, &c->octdbg,
+                      &c->mdist1,  &c->midx2,   &c->mdist2, &c->mnq,     &c->mpart,   &c->scratch, &c->octdbg,
                       &c->strow,  &c->stidx, &c->stur,    &c->stdepth,  &c->stsad,
                       &c->gxy,     &c->gcell,  &c->gstart, &c->gidx,    &c->sbs,      &c->soa,
                       &c->m16,     &c->sbpmp,  &c->sbpoff, &c->sbpcand, &c->sbpblk,  &c->sbpmatch,
@@ -1293,6 +1294,8 @@ int orbgpu_match_stereo_batch(orbgpu_ctx* c, int n_pairs, int stereo_only, void*
     m.idx2 = c->midx2.as<int32_t>();
     m.dist2 = c->mdist2.as<int32_t>();
     m.nq = c->mnq.as<int32_t>();
+    m.part = nullptr;  // the split path (one launch over <= 4 pairs) sets it below
+    uint2* split_part = n_pairs * 2 <= kKnnSplitSlots && !getenv("ORBGPU_KNN_NOSPLIT") ? c->mpart.as<uint2>() : nullptr;
     if (c->out_cap > 65535) return fail(ORBGPU_ERR_INVALID, "matcher supports < 65536 rows per image");
     // follow the extraction's sub-batches so each chunk matches right after it is extracted
     bool chunked = !stream && !c->last_chunks.empty();
@@ -1305,6 +1308,7 @@ int orbgpu_match_stereo_batch(orbgpu_ctx* c, int n_pairs, int stereo_only, void*
             HIP_TRY(hipStreamWaitEvent(s0, c->join[k], 0));
         }
         m.pair0 = 0;
+        m.part = split_part;
         int r = timed(c, ST_KNN, s0, [&] { return launch_knn2_pairs(m, n_pairs, s0); });
         if (r) return r;
         HIP_TRY(hipEventRecord(c->fork, s0));
@@ -1316,11 +1320,13 @@ int orbgpu_match_stereo_batch(orbgpu_ctx* c, int n_pairs, int stereo_only, void*
             if (np <= 0) continue;
             MatchArgs mm = m;
             mm.pair0 = p0;
+            if (c->last_chunks.size() == 1) mm.part = split_part;  // one launch: the slots are its own
             int r = timed(c, ST_KNN, ch.st, [&] { return launch_knn2_pairs(mm, np, ch.st); });
             if (r) return r;
         }
     } else {
         m.pair0 = 0;
+        m.part = split_part;
         int r = join_all(c, s);  // the extraction may have run on the chunk streams
         if (r) return r;
         r = timed(c, ST_KNN, s, [&] { return launch_knn2_pairs(m, n_pairs, s); });

@@ -90,6 +90,28 @@ def test_batch_knn2_past_4096_train_rows(oracle):
     np.testing.assert_array_equal(d, rd)
 
 
+def test_split_knn2_one_pair_past_4096_rows(oracle, monkeypatch):
+    """A one-pair batch (the C4 shape) matches with the train rows split over 8 workgroups per
+    query block plus k_knn2_merge (orb_kernels.hip launch_knn2_pairs); at 1920x1080 with 8200
+    features the splits straddle the 4096-row key segments.  Equal to the oracle, and to the
+    unsplit launch (ORBGPU_KNN_NOSPLIT)."""
+    import orbslam3lib_amd as og
+    imgs = np.stack(synth.stereo_pair(1080, 1920, 61))
+    be = _batch(og, 1920, 1080, 12, 8200, imgs)
+    be.run()
+    be.match_stereo(False)
+    be.synchronize()
+    _, dl, _ = be.result(0)
+    _, dr, _ = be.result(1)
+    assert len(dr) > 4096 and len(dl) > 4096, (len(dl), len(dr))
+    split = be.matches(0)
+    _same_knn(split, oracle.knn2(dl, dr), "split")
+    monkeypatch.setenv("ORBGPU_KNN_NOSPLIT", "1")
+    be.match_stereo(False)
+    be.synchronize()
+    _same_knn(be.matches(0), split, "unsplit vs split")
+
+
 def test_c5_batch_16_pairs(oracle):
     """The C5 side line's batch (bench.py other_configs: 1920x1080, 12 levels, 5000 features,
     16 pairs tiled from 4 seeded pairs, 4 chunk streams): every pair's 5000 x 5000 kNN2 against
