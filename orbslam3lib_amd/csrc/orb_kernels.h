@@ -167,9 +167,13 @@ struct GridArgs {
 // Octree workspace layout for one (image, level) with n_cap keys and node capacity C.  The node
 // state lives in LDS when C <= kOctLdsNodes, otherwise in the `nodemem` part of this block.
 constexpr int kOctLdsNodes = 1024;
-constexpr int kOdKpBlock = 8;  // keypoints per k_orient_desc block (256 threads / 32 lanes)
+#ifndef OD_LANES
+#define OD_LANES 32
+#endif
+constexpr int kOdKpBlock = 256 / OD_LANES;  // keypoints per k_orient_desc pass (256 threads / lanes per keypoint)
 
 constexpr int kOctLdsKeys = 16384;  // per-key node labels (u16) kept in LDS up to this many keys
+constexpr int kFastMergeMaxImages = 4;  // launches this small run the 48/64 FAST cells as one launch
 constexpr int kOctSmallThreads = 256;  // default workgroup size of the short-level k_octree launch
 constexpr int kOctSmallMinImages = 32;  // launches with fewer images keep the 512-thread shape
 constexpr int kOctSmallLds = 36 * 1024;  // default dynamic LDS of that launch: 4 workgroups per CU with the static part

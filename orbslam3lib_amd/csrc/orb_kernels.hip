@@ -667,7 +667,7 @@ __global__ __launch_bounds__(512, 1) void k_octree_retry(BatchArgs a) {
 // test pairs, sampled from the keypoint's blurred patch staged in LDS.  The kernel waits on
 // three dependent memory round trips per keypoint (key, moment rows + patch, samples); few
 // vector-memory instructions and registers per lane keep many of them in flight.
-constexpr int kOdLanes = 32;                   // lanes per keypoint
+constexpr int kOdLanes = OD_LANES;             // lanes per keypoint (orb_kernels.h)
 constexpr int kOdRows = 32 / kOdLanes;         // disc rows per lane
 constexpr int kOdPairs = 256 / kOdLanes;       // test pairs per lane
 static_assert(kOdKpBlock == 256 / kOdLanes, "orb_kernels.h kOdKpBlock");
@@ -676,20 +676,20 @@ constexpr int kOdPatchR = 18;                    // |rotated pattern offset| <= 
 constexpr int kOdPatchRows = 2 * kOdPatchR + 1;  // 37
 constexpr int kOdPatchPitch = 48;                // 3 x 16 B: covers x-18..x+18 from the dword below
 
-// Sum of v over each 32-lane half of the wave, in every lane: DPP quad_perm xor 1 / xor 2, row
-// half-mirror (pairs the two quads of 8 lanes) and row mirror (the two halves of a 16-lane row),
-// then the other row of the 32 through ds_swizzle (xor mask 16).
-__device__ inline int od_sum32(int v) {
+// Sum of v over each kOdLanes-lane group of the wave, in every lane: DPP quad_perm xor 1 / xor 2,
+// row half-mirror (pairs the two quads of 8 lanes) and row mirror (the two halves of a 16-lane
+// row), then for 32-lane groups the other row of the 32 through ds_swizzle (xor mask 16).
+__device__ inline int od_sum(int v) {
     v += __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
     v += __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
     v += __builtin_amdgcn_update_dpp(0, v, 0x141, 0xF, 0xF, false);  // row_half_mirror
     v += __builtin_amdgcn_update_dpp(0, v, 0x140, 0xF, 0xF, false);  // row_mirror
-    v += __builtin_amdgcn_ds_swizzle(v, 0x401F);                     // lane ^ 16 within 32
+    if constexpr (kOdLanes == 32) v += __builtin_amdgcn_ds_swizzle(v, 0x401F);  // lane ^ 16 within 32
     return v;
 }
 
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k_orient_desc(BatchArgs a,
-                                                                                          uint32_t nblk_magic) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kOdLanes == 32 ? 6 : 5))) void k_orient_desc(
+    BatchArgs a, uint32_t nblk_magic) {
     // per keypoint group: the blurred patch around the keypoint, staged with 16-byte loads
     __shared__ __attribute__((aligned(16))) uint8_t patch[kOdKpBlock][kOdPatchRows * kOdPatchPitch];
     const int wg = xcd_remap(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * gridDim.y);
@@ -715,8 +715,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
     // Both tables are stored index-major ([i][sub], [b][sub]): the 32 lanes of a keypoint read 32
     // consecutive entries per instruction, conflict-free (a [sub][i] layout puts every lane of a
     // b128 read on the same 4 banks: 32-way conflicts, measured as half the kernel's LDS time)
-    static_assert(kOdRows == 1 && kOdLanes * 8 == 256 && kOdLanes * kOdPairs == 256, "LDS table shapes");
-    __shared__ __attribute__((aligned(16))) uint32_t s_msk[8][kOdLanes];
+    static_assert((kOdLanes == 16 || kOdLanes == 32) && kOdLanes * kOdRows == 32 && kOdLanes * kOdPairs == 256,
+                  "LDS table shapes");
+    __shared__ __attribute__((aligned(16))) uint32_t s_msk[8][32];  // [dword][disc row index v + 15]
     // test pair j = sub * kOdPairs + b as floats {x0, x1, y0, y1} at s_pat[b][sub]: the two samples
     // of a pair rotate as one packed pair
     __shared__ __attribute__((aligned(16))) uint4 s_pat[kOdPairs][kOdLanes];
@@ -767,19 +768,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
         // the moment row (round trip 1) and the 37 x 37 blurred patch (rows y-18..y+18 from the
         // dword at or below x-18, 16-byte buffer loads, out-of-range bytes read as 0 and never
         // sampled) are both requested before either is used, so the two round trips overlap
-        const uint8_t* row = lvl + plane_off(y + vrow[0], G.pitch, 0);
-        uint32_t w[9];
-        if (raw_dw) {  // 2 x dwordx4 + 1 dword (global loads need only dword alignment)
-            const uint4 A = *reinterpret_cast<const uint4*>(row + xa);
-            const uint4 B = *reinterpret_cast<const uint4*>(row + xa + 16);
-            w[0] = A.x; w[1] = A.y; w[2] = A.z; w[3] = A.w;
-            w[4] = B.x; w[5] = B.y; w[6] = B.z; w[7] = B.w;
-            w[8] = *reinterpret_cast<const uint32_t*>(row + xa + 32);
-        } else {
+        uint32_t w[kOdRows][9];
 #pragma unroll
-            for (int i = 0; i < 9; ++i) {
-                const uint8_t* q = row + xa + 4 * i;
-                w[i] = (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16) | ((uint32_t)q[3] << 24);
+        for (int h = 0; h < kOdRows; ++h) {
+            const uint8_t* row = lvl + plane_off(y + vrow[h], G.pitch, 0);
+            if (raw_dw) {  // 2 x dwordx4 + 1 dword (global loads need only dword alignment)
+                const uint4 A = *reinterpret_cast<const uint4*>(row + xa);
+                const uint4 B = *reinterpret_cast<const uint4*>(row + xa + 16);
+                w[h][0] = A.x; w[h][1] = A.y; w[h][2] = A.z; w[h][3] = A.w;
+                w[h][4] = B.x; w[h][5] = B.y; w[h][6] = B.z; w[h][7] = B.w;
+                w[h][8] = *reinterpret_cast<const uint32_t*>(row + xa + 32);
+            } else {
+#pragma unroll
+                for (int i = 0; i < 9; ++i) {
+                    const uint8_t* q = row + xa + 4 * i;
+                    w[h][i] = (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16) | ((uint32_t)q[3] << 24);
+                }
             }
         }
         const int pitch = G.bpitch;
@@ -799,22 +803,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
         // IC_Angle moments (ORBextractor_old.cc:78-105): the row window is byte-aligned with
         // v_alignbyte, masked to the disc, then
         //   s = sum of bytes (v_sad_u8), sum u*p = dot4(bytes, {4i..4i+3}) - 15 s
-        {
+#pragma unroll
+        for (int h = 0; h < kOdRows; ++h) {
             uint32_t sacc = 0, uacc = 0;
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
-                const uint32_t b = __builtin_amdgcn_alignbyte(w[i + 1], w[i], shf) & s_msk[i][sub];
+                const uint32_t b = __builtin_amdgcn_alignbyte(w[h][i + 1], w[h][i], shf) & s_msk[i][sub + h * kOdLanes];
                 sacc = __builtin_amdgcn_sad_u8(b, 0u, sacc);
                 const uint32_t wu = (uint32_t)(4 * i) * 0x01010101u + 0x03020100u;
                 uacc = __builtin_amdgcn_udot4(b, wu, uacc, false);
             }
-            m10 = (int)uacc - 15 * (int)sacc;
-            m01 = vrow[0] * (int)sacc;
+            m10 += (int)uacc - 15 * (int)sacc;
+            m01 += vrow[h] * (int)sacc;
         }
-        // sums over the keypoint's 32 lanes: xor 1, xor 2 (quad_perm), the 8- and 16-lane mirrors
-        // (DPP, no LDS round trip), then lane ^ 16 (ds_swizzle)
-        m10 = od_sum32(m10);
-        m01 = od_sum32(m01);
+        // sums over the keypoint's lanes: xor 1, xor 2 (quad_perm), the 8- and 16-lane mirrors
+        // (DPP, no LDS round trip), then for 32 lanes lane ^ 16 (ds_swizzle)
+        m10 = od_sum(m10);
+        m01 = od_sum(m01);
         const float angle = fast_atan2_deg((float)m01, (float)m10);
         // computeOrbDescriptor (:108-148): lane `sub` makes bits [sub * kOdPairs, + kOdPairs)
         const float factorPI = (float)(3.14159265358979323846 / 180.0);
@@ -1283,6 +1288,14 @@ hipError_t launch_fast_cells(const BatchArgs& a, int tile, hipStream_t s) {
     // smaller tiles = less LDS per workgroup = more cells resident per CU
     int c0, c1;
     fast_cell_range(a, tile, &c0, &c1);
+    // a launch of a few images (the latency shape) leaves the GPU mostly idle: the 48- and 64-byte
+    // cells go in ONE 64-byte launch instead of two back to back (every 48 cell fits 64)
+    const bool merge = a.nimages <= kFastMergeMaxImages && a.fast_n48 > 0 && a.fast_n64 > a.fast_n48;
+    if (merge && tile == kCellPitchSmall) return hipSuccess;  // done by the 48 launch
+    if (merge && tile == kCellPitchTiny) {
+        tile = kCellPitchSmall;
+        c1 = a.fast_n64;
+    }
     if (c1 <= c0) return hipSuccess;
     const dim3 grid(c1 - c0, a.nimages), block(kFastThreads);
     const uint32_t d = (uint32_t)(c1 - c0);
