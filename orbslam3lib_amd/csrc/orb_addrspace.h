@@ -21,4 +21,26 @@ using asp = typename asp_t<AS, T>::type;
 
 constexpr int kGeneric = -1, kGlobalAS = 1, kLdsAS = 3;
 
+// The 16-byte vector pointer in the same address space as P (whole-record ds_read_b128 /
+// ds_write_b128 accesses of 16-byte records).
+typedef unsigned int orb_u32x4 __attribute__((ext_vector_type(4)));
+template <class P>
+struct vec4_ptr;
+template <class T>
+struct vec4_ptr<T*> {
+    using type = orb_u32x4*;
+};
+template <class T>
+struct vec4_ptr<__attribute__((address_space(1))) T*> {
+    using type = __attribute__((address_space(1))) orb_u32x4*;
+};
+template <class T>
+struct vec4_ptr<__attribute__((address_space(3))) T*> {
+    using type = __attribute__((address_space(3))) orb_u32x4*;
+};
+template <class P>
+__host__ __device__ inline typename vec4_ptr<P>::type as_vec4(P p) {
+    return reinterpret_cast<typename vec4_ptr<P>::type>(p);
+}
+
 }  // namespace orbgpu

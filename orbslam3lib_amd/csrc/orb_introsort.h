@@ -18,10 +18,11 @@ namespace orbgpu {
 
 // Element sorted by the octree: key = (size << 16 | ulx) would NOT reproduce libstdc++ on
 // ties, so the comparator is kept separate and the payload (node index) travels with it.
-struct SortElem {
+struct alignas(16) SortElem {
     int32_t size;
     int32_t ulx;
     int32_t node;
+    int32_t pad;  // 16 bytes: one ds_read_b128 / ds_write_b128 per element
 };
 
 __host__ __device__ inline bool node_less(SortElem a, SortElem b) {
@@ -34,29 +35,30 @@ __host__ __device__ inline bool node_less(SortElem a, SortElem b) {
 // struct take generic references, which an LDS-qualified lvalue cannot bind to).
 template <class EP>
 __host__ __device__ inline SortElem se_ld(EP a, int i) {
+    const orb_u32x4 v = as_vec4(a)[i];
     SortElem e;
-    e.size = a[i].size;
-    e.ulx = a[i].ulx;
-    e.node = a[i].node;
+    e.size = (int32_t)v.x;
+    e.ulx = (int32_t)v.y;
+    e.node = (int32_t)v.z;
+    e.pad = 0;
     return e;
 }
 template <class EP>
 __host__ __device__ inline void se_st(EP a, int i, SortElem e) {
-    a[i].size = e.size;
-    a[i].ulx = e.ulx;
-    a[i].node = e.node;
+    orb_u32x4 v;
+    v.x = (uint32_t)e.size;
+    v.y = (uint32_t)e.ulx;
+    v.z = (uint32_t)e.node;
+    v.w = 0;
+    as_vec4(a)[i] = v;
 }
 
 template <class EP>
 __host__ __device__ inline void isort_swap(EP a, int i, int j) {
-    // field-wise (a 12-byte struct temporary would be placed in scratch memory by hipcc)
-    const int32_t s0 = a[i].size, u0 = a[i].ulx, n0 = a[i].node;
-    a[i].size = a[j].size;
-    a[i].ulx = a[j].ulx;
-    a[i].node = a[j].node;
-    a[j].size = s0;
-    a[j].ulx = u0;
-    a[j].node = n0;
+    // whole 16-byte elements (a struct temporary could be placed in scratch memory by hipcc)
+    const orb_u32x4 x = as_vec4(a)[i], y = as_vec4(a)[j];
+    as_vec4(a)[i] = y;
+    as_vec4(a)[j] = x;
 }
 
 __host__ __device__ inline int isort_lg(int n) {
@@ -274,30 +276,33 @@ __host__ __device__ __attribute__((always_inline)) inline void introsort_partiti
                 s.segK[g] = 0;
             }
         }
-        for (int i = tid; i < m; i += NT) s.segof[i] = 0xFFFF;
         p.sync();
-        for (int g = 0; g < nseg; ++g) {
-            if (s.segK[g] < 0) continue;
-            const int f = F[g], l = L[g];
-            for (int i = f + tid; i < l; i += NT) s.segof[i] = (uint16_t)g;
-        }
-        p.sync();
+        // the segment of every position (segments are disjoint and in position order: a
+        // binary search over their first positions), and the stopper scans of all segments
+        int top = 1;
+        while (2 * top <= nseg) top *= 2;
         int lc = 0, rc = 0;
         for (int base = 0; base <= m; base += NT) {
             const int i = base + tid;
             int lf = 0, rf = 0;
-            if (i < m && s.segof[i] != 0xFFFF) {
-                const int f = F[s.segof[i]];
-                const SortElem pv = se_ld(a, f);
-                lf = (i > f) && !node_less(se_ld(a, i), pv);
-                rf = !node_less(pv, se_ld(a, i));
+            if (i < m) {
+                int g = 0;
+                for (int h = top; h; h >>= 1)
+                    if (g + h < nseg && F[g + h] <= i) g += h;
+                const bool in = nseg > 0 && F[g] <= i && i < L[g] && s.segK[g] >= 0;
+                s.segof[i] = in ? (uint16_t)g : (uint16_t)0xFFFF;
+                if (in) {
+                    const int f = F[g];
+                    const SortElem pv = se_ld(a, f);
+                    lf = (i > f) && !node_less(se_ld(a, i), pv);
+                    rf = !node_less(pv, se_ld(a, i));
+                }
             }
             int tl, tr;
-            const int el = p.scan_small(lf, &tl);
-            const int er = p.scan_small(rf, &tr);
+            const int2 e = p.scan_pair(lf, rf, &tl, &tr);
             if (i <= m) {
-                s.lex[i] = (uint16_t)(lc + el);
-                s.rex[i] = (uint16_t)(rc + er);
+                s.lex[i] = (uint16_t)(lc + e.x);
+                s.rex[i] = (uint16_t)(rc + e.y);
             }
             lc += tl;
             rc += tr;
@@ -312,26 +317,19 @@ __host__ __device__ __attribute__((always_inline)) inline void introsort_partiti
             if (!node_less(pv, se_ld(a, i))) s.rpos[f + (s.rex[l] - s.rex[i] - 1)] = (uint16_t)i;
         }
         p.sync();
+        // the scan swaps (L'_k, R'_k) while L'_k < R'_k: a prefix of k (L' ascends, R' descends),
+        // so pair k swaps in place (no position is in two swapping pairs) and the last swapping
+        // pair (or k = 0 when none swaps) records K
         for (int j = tid; j < m; j += NT) {
             const int g = s.segof[j];
             if (g == 0xFFFF) continue;
             const int f = F[g], l = L[g], k = j - f;
             const int nl = s.lex[l] - s.lex[f], nr = s.rex[l] - s.rex[f];
-            if (k < nl && k < nr && s.lpos[j] < s.rpos[j]) p.atomic_add(&s.segK[g], 1);
-        }
-        p.sync();
-        for (int j = tid; j < m; j += NT) {
-            const int g = s.segof[j];
-            if (g == 0xFFFF || j - F[g] >= s.segK[g]) continue;
-            se_st(s.tmp, s.lpos[j], se_ld(a, s.rpos[j]));
-            se_st(s.tmp, s.rpos[j], se_ld(a, s.lpos[j]));
-        }
-        p.sync();
-        for (int j = tid; j < m; j += NT) {
-            const int g = s.segof[j];
-            if (g == 0xFFFF || j - F[g] >= s.segK[g]) continue;
-            se_st(a, s.lpos[j], se_ld(s.tmp, s.lpos[j]));
-            se_st(a, s.rpos[j], se_ld(s.tmp, s.rpos[j]));
+            const int np = nl < nr ? nl : nr;
+            const bool sw = k < np && s.lpos[j] < s.rpos[j];
+            const bool sw1 = k + 1 < np && s.lpos[j + 1] < s.rpos[j + 1];
+            if (sw) isort_swap(a, s.lpos[j], s.rpos[j]);
+            if (sw && !sw1) s.segK[g] = k + 1;
         }
         p.sync();
         // children segments, kept in position order (left child first)

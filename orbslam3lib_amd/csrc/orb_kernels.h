@@ -85,6 +85,7 @@ struct BatchArgs {
     int oct2_lds_nodes, oct2_lds_bytes, oct2_nq_off, oct2_lds_keys;
     int oct_may_retry;               // some level can exceed the LDS instantiation of k_octree
     int oct_force_retry;             // diagnostics: every level through the generic instantiation
+    int oct_pyr_max;                 // deepest count pyramid of k_octree (0: label passes only)
 };
 
 struct MatchArgs {
@@ -176,13 +177,16 @@ constexpr int kOctLdsKeys = 16384;  // per-key node labels (u16) kept in LDS up 
 constexpr int kFastMergeMaxImages = 4;  // launches this small run the 48/64 FAST cells as one launch
 constexpr int kOctSmallThreads = 256;  // default workgroup size of the short-level k_octree launch
 constexpr int kOctSmallMinImages = 32;  // launches with fewer images keep the 512-thread shape
-constexpr int kOctSmallLds = 36 * 1024;  // default dynamic LDS of that launch: 4 workgroups per CU with the static part
+// default dynamic LDS of that launch: a 640x480 level 0's node state (~38 KB) plus its depth-5
+// count pyramid (10.9 KB) and path tables (2.1 KB); 3 workgroups per CU with the static part
+constexpr int kOctSmallLds = 51 * 1024;
 
 // LDS layout of one k_octree launch
 struct OctCfg {
     int nq_off;     // byte offset of the per-key labels
     int lds_nodes;  // node capacity in LDS
     int lds_keys;   // labels kept in LDS up to this many keys (global workspace above)
+    int lds_bytes;  // dynamic LDS of the launch (the count pyramid takes what the level leaves)
 };
 
 struct OctLayout {

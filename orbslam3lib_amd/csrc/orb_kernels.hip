@@ -553,17 +553,20 @@ __device__ __attribute__((always_inline)) inline void octree_level(const BatchAr
     int32_t* cell_off = reinterpret_cast<int32_t*>(nodemem_lds);
     const bool off_in_lds = G.ncells <= q.nq_off / 4;
     if (!off_in_lds) cell_off = reinterpret_cast<int32_t*>(ws + L.nq);  // huge levels only
-    int carry = 0;
-    for (int base = 0; base < G.ncells; base += blockDim.x) {
-        const int i = base + threadIdx.x;
-        const int v = i < G.ncells ? cnt[i] : 0;
-        int tot;
-        const int ex = p.scan_excl(v, &tot);
-        if (i < G.ncells) cell_off[i] = carry + ex;
-        carry += tot;
-    }
-    const int n = carry;
-    __syncthreads();
+    auto scan_cells = [&]() {
+        int carry = 0;
+        for (int base = 0; base < G.ncells; base += blockDim.x) {
+            const int i = base + threadIdx.x;
+            const int v = i < G.ncells ? cnt[i] : 0;
+            int tot;
+            const int ex = p.scan_excl(v, &tot);
+            if (i < G.ncells) cell_off[i] = carry + ex;
+            carry += tot;
+        }
+        __syncthreads();
+        return carry;
+    };
+    const int n = scan_cells();
     uint32_t* out_keys = a.lvlkey + (long long)img * a.lvlkp_img_stride + G.kp_off;
     unsigned long long* dbg = a.octdbg ? a.octdbg + ((long long)img * kMaxLevels + l) * 8 : nullptr;
     int r = n > G.cand_cap ? -3 : 0;
@@ -571,6 +574,13 @@ __device__ __attribute__((always_inline)) inline void octree_level(const BatchAr
     // global workspace above that (dense levels of large frames: the label passes are parallel
     // and streaming, the serial node phases stay in LDS)
     const bool nodes_fit = off_in_lds && G.oct_cap <= q.lds_nodes && !a.oct_force_retry;
+    // the count pyramid takes the LDS the level's node state and cell offsets leave (orb_octree.h)
+    const int pyr_off = (int)((max(oct_nodemem_bytes(G.oct_cap), (size_t)(4 * G.ncells)) + 15) & ~(size_t)15);
+    // (the pyramid names keys by cell * cell_cap + slot in 24 bits)
+    const int pyrD = kLdsPath && q.lds_bytes > pyr_off && (long long)G.ncells * G.cell_cap < (1 << 24)
+                         ? oct_pyr_depth((size_t)(q.lds_bytes - pyr_off), G.W, G.H, a.oct_pyr_max)
+                         : 0;
+    uint16_t* xtbl = reinterpret_cast<uint16_t*>(nodemem_lds + pyr_off + oct_pyr_bytes(pyrD, oct_nini(G.W, G.H)));
     if (kLdsPath && r == 0 && !nodes_fit) r = kOctRetry;
     if (kLdsPath && r == 0 && n > q.lds_keys) {
         OctWST<kLdsAS, kGlobalAS, kGlobalAS> w;
@@ -586,7 +596,17 @@ __device__ __attribute__((always_inline)) inline void octree_level(const BatchAr
         w.cellkeys = (asp<kGlobalAS, const uint32_t>)ck;
         w.ncells = G.ncells;
         w.cell_cap = G.cell_cap;
+        w.pyr = (asp<kLdsAS, uint32_t>)(nodemem_lds + pyr_off);
+        w.pyrD = pyrD;
+        w.xcode = (asp<kLdsAS, uint16_t>)xtbl;
+        w.ycode = (asp<kLdsAS, uint16_t>)(xtbl + G.W + 1);
         r = octree_distribute(p, w, (asp<kLdsAS, OctShared>)&sh, G.W, G.H, G.N);
+        if (r == kOctDeep) {  // deeper than the pyramid: the label passes from the start
+            __syncthreads();
+            scan_cells();  // the node state overwrote the cell offsets
+            w.pyrD = 0;
+            r = octree_distribute(p, w, (asp<kLdsAS, OctShared>)&sh, G.W, G.H, G.N);
+        }
     } else if (kLdsPath && r == 0) {
         // everything node- and label-sized in LDS: ds_* accesses throughout
         OctWST<kLdsAS, kGlobalAS> w;
@@ -602,7 +622,17 @@ __device__ __attribute__((always_inline)) inline void octree_level(const BatchAr
         w.cellkeys = (asp<kGlobalAS, const uint32_t>)ck;
         w.ncells = G.ncells;
         w.cell_cap = G.cell_cap;
+        w.pyr = (asp<kLdsAS, uint32_t>)(nodemem_lds + pyr_off);
+        w.pyrD = pyrD;
+        w.xcode = (asp<kLdsAS, uint16_t>)xtbl;
+        w.ycode = (asp<kLdsAS, uint16_t>)(xtbl + G.W + 1);
         r = octree_distribute(p, w, (asp<kLdsAS, OctShared>)&sh, G.W, G.H, G.N);
+        if (r == kOctDeep) {  // deeper than the pyramid: the label passes from the start
+            __syncthreads();
+            scan_cells();  // the node state overwrote the cell offsets
+            w.pyrD = 0;
+            r = octree_distribute(p, w, (asp<kLdsAS, OctShared>)&sh, G.W, G.H, G.N);
+        }
     } else if (!kLdsPath && r == 0) {
         // huge levels: node state / labels / cell offsets in the global workspace where needed
         OctWST<kGeneric, kGeneric> w;
@@ -619,6 +649,9 @@ __device__ __attribute__((always_inline)) inline void octree_level(const BatchAr
         w.cellkeys = ck;
         w.ncells = G.ncells;
         w.cell_cap = G.cell_cap;
+        w.pyr = nullptr;
+        w.pyrD = 0;
+        w.xcode = w.ycode = nullptr;
         if (!off_in_lds && n > q.lds_keys) r = -3;  // cell offsets occupy L.nq
         else r = octree_distribute(p, w, &sh, G.W, G.H, G.N);
     }
@@ -653,7 +686,7 @@ __global__ __launch_bounds__(512, 1) void k_octree_retry(BatchArgs a) {
     for (int s = blockIdx.x; s < a.nimages * a.nlevels; s += gridDim.x) {
         const int img = a.img0 + s / a.nlevels, l = s % a.nlevels;
         if (a.status[img * kMaxLevels + l] != kOctRetry) continue;  // uniform per workgroup
-        octree_level<false>(a, img, l, nodemem_lds, scratch, sh, OctCfg{a.oct_nq_off, a.oct_lds_nodes, kOctLdsKeys});
+        octree_level<false>(a, img, l, nodemem_lds, scratch, sh, OctCfg{a.oct_nq_off, a.oct_lds_nodes, kOctLdsKeys, a.oct_lds_bytes});
         __syncthreads();
     }
 }
@@ -1321,9 +1354,9 @@ hipError_t launch_octree(const BatchArgs& a, hipStream_t s) {
     const int split = a.nimages < a.oct_split_min_images ? a.nlevels : std::min(a.oct_split, a.nlevels);
     if (split > 0)
         hipLaunchKernelGGL(k_octree<512>, dim3(a.nimages, split), dim3(512), a.oct_lds_bytes, s, a, 0,
-                           OctCfg{a.oct_nq_off, a.oct_lds_nodes, kOctLdsKeys});
+                           OctCfg{a.oct_nq_off, a.oct_lds_nodes, kOctLdsKeys, a.oct_lds_bytes});
     if (split < a.nlevels) {
-        const OctCfg q{a.oct2_nq_off, a.oct2_lds_nodes, a.oct2_lds_keys};
+        const OctCfg q{a.oct2_nq_off, a.oct2_lds_nodes, a.oct2_lds_keys, a.oct2_lds_bytes};
         if (a.oct2_threads == 128)
             hipLaunchKernelGGL(k_octree<128>, dim3(a.nimages, a.nlevels - split), dim3(128), a.oct2_lds_bytes, s, a,
                                split, q);

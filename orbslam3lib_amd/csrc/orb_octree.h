@@ -32,11 +32,44 @@
 
 namespace orbgpu {
 
-struct OctNode {
+struct alignas(16) OctNode {
     uint16_t x0, y0, x1, y1;  // UL = (x0,y0), BR = (x1,y1), relative to minBorder
     int32_t cnt;              // number of keys (bNoMore <=> cnt == 1)
+    uint32_t path;            // depth << 27 | quadrant-path index (count pyramid, see below)
 };
-static_assert(sizeof(OctNode) == 12, "OctNode: the count is int 3*i+2 of the node array");
+static_assert(sizeof(OctNode) == 16, "OctNode: 16 bytes");
+
+// ---- count pyramid ------------------------------------------------------------------------
+// Every node's bounds follow from its initial node and its quadrant path alone (oct_child), so a
+// key's node at depth d is fixed by its coordinates: path index = initial node * 4^d + the
+// quadrants of depths 1..d in base 4.  A histogram of the keys at depth D, summed up the levels,
+// gives the key count of EVERY node of depth <= D -- and therefore the child counts that the
+// label passes of the original formulation recount in every round -- plus, as a max over
+// (response, -input index), every node's retained key (:759-778).  Level d holds nIni * 4^d
+// entries from pyr_base(d): counts first, then the best values (same indexing).
+constexpr int kOctPyrMaxD = 7;
+constexpr int kOctDeep = -8;  // a node below depth D would be divided: rerun with label passes
+__host__ __device__ inline int pyr_base(int d, int nIni) { return nIni * (((1 << (2 * d)) - 1) / 3); }
+__host__ __device__ inline size_t oct_pyr_bytes(int D, int nIni) { return 8 * (size_t)pyr_base(D + 1, nIni); }
+__host__ __device__ inline uint32_t oct_path_code(int d, uint32_t idx) { return ((uint32_t)d << 27) | idx; }
+__host__ __device__ inline int oct_path_depth(uint32_t code) { return (int)(code >> 27); }
+__host__ __device__ inline uint32_t oct_path_idx(uint32_t code) { return code & 0x7FFFFFFu; }
+__host__ __device__ inline int oct_nini(int W, int H) {
+    const int nIni = (int)roundf((float)W / (float)H);
+    return nIni < 1 ? 1 : nIni;  // reference divides by zero here; never reached at sane sizes
+}
+// the per-axis path tables (u16 x codes for columns 0..W, y codes for rows 0..H)
+__host__ __device__ inline size_t oct_tbl_bytes(int W, int H) { return ((size_t)2 * (W + H + 2) + 15) & ~(size_t)15; }
+// deepest pyramid that fits `bytes` with the tables (0: none), at most Dmax
+__host__ __device__ inline int oct_pyr_depth(size_t bytes, int W, int H, int Dmax) {
+    const int nIni = oct_nini(W, H);
+    const size_t t = oct_tbl_bytes(W, H);
+    int D = 0;
+    while (D < Dmax && D < kOctPyrMaxD && oct_pyr_bytes(D + 1, nIni) + t <= bytes &&
+           ((size_t)nIni << (2 * (D + 1))) <= 65536)
+        ++D;
+    return D;
+}
 
 // Packed candidate key: x | y << 12 | response << 24 (relative coords < 4096, response < 256).
 __host__ __device__ inline int key_x(uint32_t k) { return (int)(k & 0xFFFu); }
@@ -103,13 +136,18 @@ struct OctWST {
     asp<LAS, const int32_t> cell_off;  // [ncells] exclusive scan of the cell counts, or null
     asp<GAS, const uint32_t> cellkeys;
     int ncells, cell_cap;
+    // count pyramid (LDS): depth pyrD > 0 runs the label-free formulation, 0 the label passes
+    asp<LAS, uint32_t> pyr;  // [oct_pyr_bytes(pyrD, nIni) / 4]
+    int pyrD;
+    asp<LAS, uint16_t> xcode;  // [W + 1] oct_xcode of every column (pyrD > 0)
+    asp<LAS, uint16_t> ycode;  // [H + 1] oct_ycode of every row
 };
 
 constexpr int kOctUnroll = 8;         // keys per thread per batch in the key passes
 constexpr int kOctWaveSortMax = 128;  // final-phase sorts up to this size partition on one wave
 
 struct OctShared {
-    int size, prev_size, nexp, ndiv, phase, done, nchild, nundiv, status, jstop;
+    int size, prev_size, nexp, ndiv, phase, done, nchild, nundiv, status, jstop, deep;
 };
 
 __host__ __device__ inline int oct_half(int a, int b) { return (b - a + 1) >> 1; }  // ceil((b-a)/2.f)
@@ -122,6 +160,32 @@ __host__ __device__ inline int oct_quadrant(uint32_t key, OctNode nd) {
     return (y < hy) ? 1 : 3;
 }
 
+// One axis of a key's path at depth D: bit d of the quadrant (x >= hx, or y >= hy) in base-4
+// digit D - d, with the bounds updated exactly as oct_child / oct_quadrant do.  A key's path
+// index is init * 4^D + code_x + 2 * code_y (init: its initial node, :585 kp.pt.x / hX).
+__host__ __device__ inline uint32_t oct_axis_code(int v, int lo, int hi, int D) {
+    uint32_t c = 0;
+    for (int d = 0; d < D; ++d) {
+        const int h = lo + oct_half(lo, hi);
+        const int b = v >= h;
+        c = 4 * c + (uint32_t)b;
+        lo = b ? h : lo;
+        hi = b ? hi : h;
+    }
+    return c;
+}
+__host__ __device__ inline int oct_init_node(int x, float hX, int nIni) {
+    const int i = (int)((float)x / hX);
+    return i >= nIni ? nIni - 1 : i;
+}
+// x part of the path index: init * 4^D + code_x
+__host__ __device__ inline uint32_t oct_xcode(int x, int D, float hX, int nIni) {
+    const int i = oct_init_node(x, hX, nIni);
+    const int x0 = (uint16_t)(int)(hX * (float)i), x1 = (uint16_t)(int)(hX * (float)(i + 1));
+    return ((uint32_t)i << (2 * D)) + oct_axis_code(x, x0, x1, D);
+}
+__host__ __device__ inline uint32_t oct_ycode(int y, int D, int H) { return 2 * oct_axis_code(y, 0, (uint16_t)H, D); }
+
 __host__ __device__ inline OctNode oct_child(OctNode nd, int q, int cnt) {
     const int hx = nd.x0 + oct_half(nd.x0, nd.x1);
     const int hy = nd.y0 + oct_half(nd.y0, nd.y1);
@@ -131,6 +195,7 @@ __host__ __device__ inline OctNode oct_child(OctNode nd, int q, int cnt) {
     c.y0 = (uint16_t)((q & 2) ? hy : nd.y0);
     c.y1 = (uint16_t)((q & 2) ? nd.y1 : hy);
     c.cnt = cnt;
+    c.path = oct_path_code(oct_path_depth(nd.path) + 1, 4 * oct_path_idx(nd.path) + (uint32_t)q);
     return c;
 }
 
@@ -142,23 +207,27 @@ __host__ __device__ inline OctNode oct_child(OctNode nd, int q, int cnt) {
 // p.node() -- wave 0 alone on the GPU, so their many scans need no workgroup barrier -- and
 // the key passes (relabel + child counts) run on every thread with the global key loads
 // software-pipelined; a phase-1 round costs two workgroup barriers.
+// whole nodes as one 16-byte access (the node phases run on one wave: fewer LDS instructions)
 template <class NP>
 __host__ __device__ inline OctNode on_ld(NP a, int i) {
+    const orb_u32x4 v = as_vec4(a)[i];
     OctNode n;
-    n.x0 = a[i].x0;
-    n.y0 = a[i].y0;
-    n.x1 = a[i].x1;
-    n.y1 = a[i].y1;
-    n.cnt = a[i].cnt;
+    n.x0 = (uint16_t)(v.x & 0xFFFFu);
+    n.y0 = (uint16_t)(v.x >> 16);
+    n.x1 = (uint16_t)(v.y & 0xFFFFu);
+    n.y1 = (uint16_t)(v.y >> 16);
+    n.cnt = (int32_t)v.z;
+    n.path = v.w;
     return n;
 }
 template <class NP>
 __host__ __device__ inline void on_st(NP a, int i, OctNode n) {
-    a[i].x0 = n.x0;
-    a[i].y0 = n.y0;
-    a[i].x1 = n.x1;
-    a[i].y1 = n.y1;
-    a[i].cnt = n.cnt;
+    orb_u32x4 v;
+    v.x = (uint32_t)n.x0 | ((uint32_t)n.y0 << 16);
+    v.y = (uint32_t)n.x1 | ((uint32_t)n.y1 << 16);
+    v.z = (uint32_t)n.cnt;
+    v.w = n.path;
+    as_vec4(a)[i] = v;
 }
 
 template <int LAS, int GAS, int NAS, class P>
@@ -184,13 +253,101 @@ __host__ __device__ __attribute__((always_inline)) inline int octree_distribute(
         }
     };
     if (ws.cap > 16383) return -3;  // node index must fit 14 bits of nq
+    const int nIni = oct_nini(W, H);
+    const float hX = (float)W / (float)nIni;
+    if (nIni + 4 > ws.cap) return -3;
+    // count-pyramid formulation (ws.pyrD > 0): one histogram of the keys replaces every label pass
+    const int D = ws.pyrD;
+    const bool fast = D > 0;
+    auto pcnt = ws.pyr;
+    auto pbest = ws.pyr + pyr_base(D + 1, nIni);
+    const int bD = pyr_base(D, nIni);
+    if (fast) {
+        for (int e = tid; e < (nIni << (2 * D)); e += NT) {
+            pcnt[bD + e] = 0;
+            pbest[bD + e] = 0;
+        }
+        p.sync();
+#ifdef OCT_DIAG
+        mark(1);
+#endif
+    }
+    // every key pass: f(base, key[kOctUnroll]) handles keys k = base + u * NT + tid (u <
+    // kOctUnroll; k >= n are padding) in stages across the batch so the LDS round trips of
+    // different keys overlap; the global key loads run one batch ahead
+    auto for_keys = [&](auto f) __attribute__((always_inline)) {
+        if (n <= 0) return;
+        uint32_t key[kOctUnroll], nkey[kOctUnroll];
+#pragma unroll
+        for (int u = 0; u < kOctUnroll; ++u) {
+            const int k = u * NT + tid;
+            key[u] = ws.keys[k < n ? k : n - 1];
+        }
+        for (int base = 0; base < n; base += kOctUnroll * NT) {
+            // the next batch's loads are in flight while this batch runs its LDS chains
+#pragma unroll
+            for (int u = 0; u < kOctUnroll; ++u) {
+                const int k = base + (kOctUnroll + u) * NT + tid;
+                nkey[u] = ws.keys[k < n ? k : n - 1];
+            }
+            f(base, key);
+#pragma unroll
+            for (int u = 0; u < kOctUnroll; ++u) key[u] = nkey[u];
+        }
+    };
 
-    // ---- keys: gather into vToDistributeKeys order (cell order) -------------------------
-    // kOctUnroll keys per thread advance through a fixed-length binary search in lockstep, so
-    // their LDS reads overlap; loads use clamped indices (unpredicated, countable waits)
-    if (ws.cell_off && n > 0) {
-        int steps = 0;
+    // ---- keys: the histogram (pyramid) or the gather into vToDistributeKeys order -------
+    // The pyramid reads the cell lists as they are and names a key by kid = cell * cell_cap +
+    // slot (monotone in the input index k, and the key's own address): no gathered copy.  The
+    // gather locates each k's cell by a fixed-length binary search over the cell offsets, many
+    // keys per thread in lockstep so their LDS reads and global loads overlap.
+    int steps = 0;
+    if (ws.cell_off)
         while ((1 << steps) < ws.ncells) ++steps;
+    if (fast) {
+        // the path index is init * 4^D + code_x + 2 * code_y: one table per axis
+        for (int x = tid; x <= W; x += NT) ws.xcode[x] = (uint16_t)oct_xcode(x, D, hX, nIni);
+        for (int y = tid; y <= H; y += NT) ws.ycode[y] = (uint16_t)oct_ycode(y, D, H);
+        p.sync();
+    }
+    auto pyr_add = [&](uint32_t key, int kid) __attribute__((always_inline)) {
+        const int x = key_x(key), y = key_y(key);
+        const int e = bD + (x <= W && y <= H ? (int)ws.xcode[x] + (int)ws.ycode[y]
+                                             : (int)(oct_xcode(x, D, hX, nIni) + oct_ycode(y, D, H)));
+        p.atomic_add(&pcnt[e], 1);
+        p.atomic_max(&pbest[e], ((uint32_t)key_resp(key) << 24) | (0xFFFFFFu - (uint32_t)kid));
+    };
+    if (fast && n > 0 && ws.cell_off) {
+        // cell lists as they are: wave w takes cells w, w + waves, ..., U of them at a time, its
+        // lanes their keys (no search for a key's cell; kid = cell * cell_cap + slot)
+        constexpr int U = 8;
+        const int Wv = p.nwaves(), wv = p.wave(), lane = p.lane(), Lw = p.wave_width();
+        for (int c0 = wv; c0 < ws.ncells; c0 += U * Wv) {
+            int cc[U], cn[U], mx = 0;
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int c = c0 + u * Wv;
+                cc[u] = c;
+                cn[u] = c < ws.ncells ? (c + 1 < ws.ncells ? ws.cell_off[c + 1] : n) - ws.cell_off[c] : 0;
+                mx = mx > cn[u] ? mx : cn[u];
+            }
+            for (int j0 = 0; j0 < mx; j0 += Lw) {
+                const int j = j0 + lane;
+                uint32_t key[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) key[u] = j < cn[u] ? ws.cellkeys[cc[u] * ws.cell_cap + j] : 0u;
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+                    if (j < cn[u]) pyr_add(key[u], cc[u] * ws.cell_cap + j);
+            }
+        }
+        p.sync();
+        mark(5);
+    } else if (fast && n > 0) {
+        for (int k = tid; k < n; k += NT) pyr_add(ws.keys[k], k);
+        p.sync();
+        mark(5);
+    } else if (ws.cell_off && n > 0) {
         for (int base = 0; base < n; base += kOctUnroll * NT) {
             int kk[kOctUnroll], lo[kOctUnroll];
 #pragma unroll
@@ -218,55 +375,45 @@ __host__ __device__ __attribute__((always_inline)) inline int octree_distribute(
         }
         p.sync();  // the cell offsets share memory with the node state written below
     }
-    // every key pass: f(base, key[kOctUnroll]) handles keys k = base + u * NT + tid (u <
-    // kOctUnroll; k >= n are padding) in stages across the batch so the LDS round trips of
-    // different keys overlap; the global key loads run one batch ahead
-    auto for_keys = [&](auto f) __attribute__((always_inline)) {
-        if (n <= 0) return;
-        uint32_t key[kOctUnroll], nkey[kOctUnroll];
-#pragma unroll
-        for (int u = 0; u < kOctUnroll; ++u) {
-            const int k = u * NT + tid;
-            key[u] = ws.keys[k < n ? k : n - 1];
-        }
-        for (int base = 0; base < n; base += kOctUnroll * NT) {
-            // the next batch's loads are in flight while this batch runs its LDS chains
-#pragma unroll
-            for (int u = 0; u < kOctUnroll; ++u) {
-                const int k = base + (kOctUnroll + u) * NT + tid;
-                nkey[u] = ws.keys[k < n ? k : n - 1];
+    if (fast) {  // the levels above D: sums and maxima of the four children
+        for (int d = D - 1; d >= 0; --d) {
+            const int b = pyr_base(d, nIni), b1 = pyr_base(d + 1, nIni);
+            for (int e = tid; e < (nIni << (2 * d)); e += NT) {
+                const int c = b1 + 4 * e;
+                pcnt[b + e] = pcnt[c] + pcnt[c + 1] + pcnt[c + 2] + pcnt[c + 3];
+                const uint32_t m0 = pbest[c] > pbest[c + 1] ? pbest[c] : pbest[c + 1];
+                const uint32_t m1 = pbest[c + 2] > pbest[c + 3] ? pbest[c + 2] : pbest[c + 3];
+                pbest[b + e] = m0 > m1 ? m0 : m1;
             }
-            f(base, key);
-#pragma unroll
-            for (int u = 0; u < kOctUnroll; ++u) key[u] = nkey[u];
+            p.sync();
         }
-    };
+        mark(6);
+    }
     // ---- initial nodes (:561-603) ------------------------------------------------------
-    int nIni = (int)roundf((float)W / (float)H);
-    if (nIni < 1) nIni = 1;  // reference divides by zero here; never reached at sane sizes
-    const float hX = (float)W / (float)nIni;
-    if (nIni + 4 > ws.cap) return -3;
     for (int i = tid; i < nIni; i += NT) {
         OctNode nd;
         nd.x0 = (uint16_t)(int)(hX * (float)i);
         nd.x1 = (uint16_t)(int)(hX * (float)(i + 1));
         nd.y0 = 0;
         nd.y1 = (uint16_t)H;
-        nd.cnt = 0;
+        nd.cnt = fast ? (int)pcnt[i] : 0;
+        nd.path = oct_path_code(0, (uint32_t)i);
         on_st(cur, i, nd);
     }
     p.sync();
-    for_keys([&](int base, const uint32_t* key) __attribute__((always_inline)) {
+    if (!fast) {
+        for_keys([&](int base, const uint32_t* key) __attribute__((always_inline)) {
 #pragma unroll
-        for (int u = 0; u < kOctUnroll; ++u) {
-            const int k = base + u * NT + tid;
-            int idx = (int)((float)key_x(key[u]) / hX);
-            if (idx >= nIni) idx = nIni - 1;  // unreachable for in-range keys; keeps memory safe
-            if (k < n) nq[k] = (uint16_t)(idx << 2);
-            p.run_add(&cur[idx].cnt, idx, k < n);
-        }
-    });
-    p.sync();
+            for (int u = 0; u < kOctUnroll; ++u) {
+                const int k = base + u * NT + tid;
+                int idx = (int)((float)key_x(key[u]) / hX);
+                if (idx >= nIni) idx = nIni - 1;  // unreachable for in-range keys; keeps memory safe
+                if (k < n) nq[k] = (uint16_t)(idx << 2);
+                p.run_add(&cur[idx].cnt, idx, k < n);
+            }
+        });
+        p.sync();
+    }
     if (nw) {  // drop the empty initial nodes (:594-603)
         auto np = p.node();
         const int ntid = np.tid(), NNT = np.nthreads();
@@ -277,9 +424,13 @@ __host__ __device__ __attribute__((always_inline)) inline int octree_distribute(
             int tot;
             const int ex = np.scan_small(v, &tot);
             if (v) {
-                on_st(nxt, carry + ex, on_ld(cur, i));
+                const OctNode nd = on_ld(cur, i);
+                on_st(nxt, carry + ex, nd);
                 M.undivpos[i] = (uint16_t)(carry + ex);
-                for (int q = 0; q < 4; ++q) ccur[4 * (carry + ex) + q] = 0;
+                // round 1's candidates (>1 key): their child counts from the pyramid
+                const int b1 = pyr_base(1, nIni) + 4 * i;
+                for (int q = 0; q < 4; ++q)
+                    ccur[4 * (carry + ex) + q] = (fast && nd.cnt > 1) ? (int)pcnt[b1 + q] : 0;
             }
             carry += tot;
         }
@@ -289,6 +440,7 @@ __host__ __device__ __attribute__((always_inline)) inline int octree_distribute(
             sh->phase = 1;
             sh->done = 0;
             sh->status = 0;
+            sh->deep = 0;
         }
     }
     {
@@ -298,26 +450,28 @@ __host__ __device__ __attribute__((always_inline)) inline int octree_distribute(
     }
     p.sync();
     // relabel to the compacted list + count round 1 (every node with >1 key is a candidate)
-    for_keys([&](int base, const uint32_t* key) __attribute__((always_inline)) {
-        int v[kOctUnroll];
-        OctNode nd[kOctUnroll];
+    if (!fast) {
+        for_keys([&](int base, const uint32_t* key) __attribute__((always_inline)) {
+            int v[kOctUnroll];
+            OctNode nd[kOctUnroll];
 #pragma unroll
-        for (int u = 0; u < kOctUnroll; ++u) {
-            const int k = base + u * NT + tid;
-            v[u] = M.undivpos[nq[k < n ? k : n - 1] >> 2];
-        }
+            for (int u = 0; u < kOctUnroll; ++u) {
+                const int k = base + u * NT + tid;
+                v[u] = M.undivpos[nq[k < n ? k : n - 1] >> 2];
+            }
 #pragma unroll
-        for (int u = 0; u < kOctUnroll; ++u) nd[u] = on_ld(cur, v[u]);
+            for (int u = 0; u < kOctUnroll; ++u) nd[u] = on_ld(cur, v[u]);
 #pragma unroll
-        for (int u = 0; u < kOctUnroll; ++u) {
-            const int k = base + u * NT + tid;
-            const bool split = k < n && nd[u].cnt > 1;
-            const int q = split ? oct_quadrant(key[u], nd[u]) : 0;
-            p.run_add(&ccur[4 * v[u] + q], 4 * v[u] + q, split);
-            if (k < n) nq[k] = (uint16_t)((v[u] << 2) | q);
-        }
-    });
-    p.sync();
+            for (int u = 0; u < kOctUnroll; ++u) {
+                const int k = base + u * NT + tid;
+                const bool split = k < n && nd[u].cnt > 1;
+                const int q = split ? oct_quadrant(key[u], nd[u]) : 0;
+                p.run_add(&ccur[4 * v[u] + q], 4 * v[u] + q, split);
+                if (k < n) nq[k] = (uint16_t)((v[u] << 2) | q);
+            }
+        });
+        p.sync();
+    }
     mark(0);
 
     // ---- rounds (:612-757) -----------------------------------------------------------
@@ -504,7 +658,8 @@ __host__ __device__ __attribute__((always_inline)) inline int octree_distribute(
                         const int pos = nchild + carry + ex;
                         M.undivpos[i] = (uint16_t)pos;
                         on_st(nxt, pos, on_ld(cur, i));
-                        for (int q = 0; q < 4; ++q) cnxt[4 * pos + q] = 0;
+                        if (!fast)
+                            for (int q = 0; q < 4; ++q) cnxt[4 * pos + q] = 0;
                     }
                     carry += tot;
                 }
@@ -518,8 +673,16 @@ __host__ __device__ __attribute__((always_inline)) inline int octree_distribute(
                 for (int q = 3; q >= 0; --q) {  // push_front n1..n4 => front reads n4,n3,n2,n1
                     const int c = ccur[4 * i + q];
                     if (c > 0) {
-                        on_st(nxt, pos, oct_child(nd, q, c));
-                        for (int qq = 0; qq < 4; ++qq) cnxt[4 * pos + qq] = 0;
+                        const OctNode ch = oct_child(nd, q, c);
+                        on_st(nxt, pos, ch);
+                        // a fresh child with >1 key is a candidate of the next round: with the
+                        // pyramid, its child counts are looked up after this phase (all threads),
+                        // which needs it above depth D
+                        if (fast) {
+                            if (c > 1 && oct_path_depth(ch.path) >= D) sh->deep = 1;
+                        } else {
+                            for (int qq = 0; qq < 4; ++qq) cnxt[4 * pos + qq] = 0;
+                        }
                         M.childpos[4 * i + q] = (uint16_t)pos;
                         ++pos;
                     }
@@ -540,14 +703,29 @@ __host__ __device__ __attribute__((always_inline)) inline int octree_distribute(
                 } else if (sh->phase == 1 && nsize + sh->nexp * 3 > N) {
                     sh->phase = 2;
                 }
+                // the next round would divide a node whose children lie below the pyramid
+                if (!sh->done && sh->deep) {
+                    sh->status = kOctDeep;
+                    sh->done = 1;
+                }
                 if (ws.dbg) ws.dbg[7] += 1;
             }
             mark(4);
         }
         p.sync();
         mark(2);
-        // 3. relabel keys, and count the next round's candidates (fresh children with >1 key)
-        for_keys([&](int base, const uint32_t* key) __attribute__((always_inline)) {
+        // 3. the next round's candidates (fresh children with >1 key): their child counts from
+        // the pyramid, or relabel the keys and count them
+        if (fast && !sh->done) {
+            const int ne = sh->nexp;
+            for (int j = tid; j < ne; j += NT) {
+                const int pos = vsz2[j];
+                const uint32_t path = nxt[pos].path;
+                const int b = pyr_base(oct_path_depth(path) + 1, nIni) + 4 * (int)oct_path_idx(path);
+                for (int qq = 0; qq < 4; ++qq) cnxt[4 * pos + qq] = (int)pcnt[b + qq];
+            }
+        }
+        if (!fast) for_keys([&](int base, const uint32_t* key) __attribute__((always_inline)) {
             int e[kOctUnroll], nv[kOctUnroll];
             bool dv[kOctUnroll];
             OctNode nd[kOctUnroll];
@@ -587,13 +765,24 @@ __host__ __device__ __attribute__((always_inline)) inline int octree_distribute(
             vsz2 = u;
         }
         p.sync();
-        mark(5);
+        mark(fast ? 2 : 5);  // diagnostics: with the pyramid, slot 5 = gather + histogram
     }
     if (sh->status) return sh->status;
 
     // ---- retain the best key per node (:759-778) ----------------------------------------
     const int size = sh->size;
     if (size > ws.out_cap) return -5;
+    if (fast) {  // every node lies at depth <= D: its retained key is its pyramid maximum
+        for (int i = tid; i < size; i += NT) {
+            const uint32_t path = cur[i].path;
+            const uint32_t v = pbest[pyr_base(oct_path_depth(path), nIni) + (int)oct_path_idx(path)];
+            const int kid = (int)(0xFFFFFFu - (v & 0xFFFFFFu));
+            ws.out_keys[i] = ws.cell_off ? ws.cellkeys[kid] : ws.keys[kid];
+        }
+        p.sync();
+        mark(2);  // diagnostics: with the pyramid, slot 6 = the pyramid's reduction
+        return size;
+    }
     auto best = reinterpret_cast<asp<LAS, uint32_t>>(cnxt);
     for (int i = tid; i < size; i += NT) best[i] = 0;
     p.sync();

@@ -55,6 +55,14 @@ struct WaveScanPolicy {
         *total = __popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2);
         return __popcll(b0 & lt) + 2 * __popcll(b1 & lt) + 4 * __popcll(b2 & lt);
     }
+    // exclusive scans of two 0/1 flags at once
+    __device__ int2 scan_pair(int a, int b, int* ta, int* tb) {
+        const uint64_t lt = (1ull << (threadIdx.x & 63)) - 1ull;
+        const uint64_t ba = __ballot(a), bb = __ballot(b);
+        *ta = __popcll(ba);
+        *tb = __popcll(bb);
+        return make_int2(__popcll(ba & lt), __popcll(bb & lt));
+    }
 };
 
 struct DevPolicy {
@@ -150,6 +158,30 @@ struct DevPolicy {
         *total = tot;
         return before + ex;
     }
+    // block-wide exclusive scans of two 0/1 flags with one pair of barriers (<= 8 waves)
+    __device__ int2 scan_pair(int a, int b, int* ta, int* tb) {
+        const int lane = (int)(threadIdx.x & 63), wid = (int)(threadIdx.x >> 6);
+        const int nw = (int)((blockDim.x + 63) >> 6);
+        const uint64_t lt = (1ull << lane) - 1ull;
+        const uint64_t ba = __ballot(a), bb = __ballot(b);
+        __syncthreads();  // scratch may still be read by the previous call
+        if (lane == 0) {
+            scratch[wid] = __popcll(ba);
+            scratch[8 + wid] = __popcll(bb);
+        }
+        __syncthreads();
+        int pa = 0, pb = 0, sa = 0, sb = 0;
+        for (int w = 0; w < nw; ++w) {
+            const int x = scratch[w], y = scratch[8 + w];
+            pa += (w < wid) ? x : 0;
+            pb += (w < wid) ? y : 0;
+            sa += x;
+            sb += y;
+        }
+        *ta = sa;
+        *tb = sb;
+        return make_int2(pa + __popcll(ba & lt), pb + __popcll(bb & lt));
+    }
 };
 
 // One wave on its own (64 lanes), e.g. one FAST cell per wave: "sync" is a wave-level memory
@@ -206,6 +238,11 @@ struct SerialPolicy {
     __host__ __device__ int scan_small(int v, int* total) {
         *total = v;
         return 0;
+    }
+    __host__ __device__ int2 scan_pair(int a, int b, int* ta, int* tb) {
+        *ta = a;
+        *tb = b;
+        return make_int2(0, 0);
     }
     __host__ __device__ unsigned long long now() const { return 0; }
     __host__ __device__ int popc64(uint64_t x) const {

@@ -442,6 +442,9 @@ int set_geometry(orbgpu_ctx* c, int w, int h) {
         if (l >= A.oct_split && (G.oct_cap > A.oct2_lds_nodes || G.ncells > A.oct2_nq_off / 4)) A.oct_may_retry = 1;
     }
     A.oct_force_retry = getenv("ORBGPU_OCT_GENERIC") ? 1 : 0;  // diagnostics / tests
+    // ORBGPU_OCT_PYR=<d>: cap the count pyramid's depth (0: the label-pass formulation only)
+    A.oct_pyr_max = kOctPyrMaxD;
+    if (const char* e = getenv("ORBGPU_OCT_PYR")) A.oct_pyr_max = std::max(0, std::min(kOctPyrMaxD, atoi(e)));
     if (A.oct_force_retry) A.oct_may_retry = 1;
     A.total_cells = cell_first;
     // FAST LDS tiles: each level takes the smallest tile its cell ROIs (+3 alignment bytes) fit:
@@ -1054,7 +1057,7 @@ int orbgpu_synchronize(orbgpu_ctx* c) {
             double acc[8] = {};
             for (int i = 0; i < n; ++i)
                 for (int k = 0; k < 8; ++k) acc[k] += (double)d[((size_t)i * kMaxLevels + l) * 8 + k];
-            fprintf(stderr, "octree L%d us: init %.1f choose %.1f barrier %.1f sort %.1f rebuild %.1f relabel %.1f best %.1f rounds %.1f\n",
+            fprintf(stderr, "octree L%d us: init %.1f choose %.1f barrier %.1f sort %.1f rebuild %.1f relabel(pyramid: gather+histogram) %.1f best(pyramid: sums) %.1f rounds %.1f\n",
                     l, acc[0] / n / 100, acc[1] / n / 100, acc[2] / n / 100, acc[3] / n / 100,
                     acc[4] / n / 100, acc[5] / n / 100, acc[6] / n / 100, acc[7] / n);
         }

@@ -98,9 +98,92 @@ int harness_octree(const uint32_t* keys, int n, int W, int H, int N, uint32_t* o
     w.out_keys = out;
     w.out_cap = out_cap;
     w.dbg = nullptr;
+    w.pyr = nullptr;
+    w.pyrD = 0;
+    w.xcode = w.ycode = nullptr;
     OctShared sh;
     SerialPolicy p;
     return octree_distribute(p, w, &sh, W, H, N);
+}
+
+// The count-pyramid formulation with a pyramid of depth D (orb_octree.h), rerun with the label
+// passes when a node below depth D must be divided, as the kernel does.  *deep = 1 when it was.
+// ncells > 0: the keys arrive as per-cell lists (cell c holds counts[c] keys at cells[c * cap]),
+// the kernel's layout, so the cell search and the pyramid's cell-slot key names are exercised.
+int harness_octree_cells(const uint32_t* cells, const int32_t* counts, int ncells, int cap, int W, int H, int N,
+                         uint32_t* out, int out_cap, int D, int* deep) {
+    const int nIni = oct_nini(W, H);
+    const int ocap = std::max(N + 3, 4 * nIni) + 8;
+    std::vector<int32_t> off(ncells + 1, 0);
+    for (int c = 0; c < ncells; ++c) off[c + 1] = off[c] + counts[c];
+    const int n = off[ncells];
+    std::vector<uint32_t> keys(n + 1);
+    std::vector<uint16_t> nq(n + 1);
+    std::vector<uint8_t> mem(oct_nodemem_bytes(ocap) + 64);
+    std::vector<uint32_t> pyr(oct_pyr_bytes(D, nIni) / 4 + 1);
+    std::vector<uint16_t> tbl(W + H + 2);
+    OctWST<kGeneric, kGeneric> w;
+    w.keys = keys.data();
+    w.n = n;
+    w.nq = nq.data();
+    w.cell_off = off.data();
+    w.cellkeys = cells;
+    w.ncells = ncells;
+    w.cell_cap = cap;
+    w.m = oct_nodemem_carve<kGeneric>(mem.data(), ocap);
+    w.cap = ocap;
+    w.out_keys = out;
+    w.out_cap = out_cap;
+    w.dbg = nullptr;
+    w.pyr = pyr.data();
+    w.pyrD = D;
+    w.xcode = tbl.data();
+    w.ycode = tbl.data() + W + 1;
+    OctShared sh;
+    SerialPolicy p;
+    int r = octree_distribute(p, w, &sh, W, H, N);
+    *deep = r == kOctDeep;
+    if (r == kOctDeep) {
+        w.pyrD = 0;
+        r = octree_distribute(p, w, &sh, W, H, N);
+    }
+    return r;
+}
+
+int harness_octree_pyr(const uint32_t* keys, int n, int W, int H, int N, uint32_t* out, int out_cap, int D,
+                       int* deep) {
+    const int nIni = oct_nini(W, H);
+    const int cap = std::max(N + 3, 4 * nIni) + 8;
+    std::vector<uint16_t> nq(n + 1);
+    std::vector<uint8_t> mem(oct_nodemem_bytes(cap) + 64);
+    std::vector<uint32_t> pyr(oct_pyr_bytes(D, nIni) / 4 + 1);
+    std::vector<uint16_t> tbl(W + H + 2);
+    OctWST<kGeneric, kGeneric> w;
+    w.keys = const_cast<uint32_t*>(keys);
+    w.n = n;
+    w.nq = nq.data();
+    w.cell_off = nullptr;
+    w.cellkeys = nullptr;
+    w.ncells = 0;
+    w.cell_cap = 0;
+    w.m = oct_nodemem_carve<kGeneric>(mem.data(), cap);
+    w.cap = cap;
+    w.out_keys = out;
+    w.out_cap = out_cap;
+    w.dbg = nullptr;
+    w.pyr = pyr.data();
+    w.pyrD = D;
+    w.xcode = tbl.data();
+    w.ycode = tbl.data() + W + 1;
+    OctShared sh;
+    SerialPolicy p;
+    int r = octree_distribute(p, w, &sh, W, H, N);
+    *deep = r == kOctDeep;
+    if (r == kOctDeep) {
+        w.pyrD = 0;
+        r = octree_distribute(p, w, &sh, W, H, N);
+    }
+    return r;
 }
 
 void harness_introsort(const int32_t* size, const int32_t* ulx, int n, int32_t* perm) {

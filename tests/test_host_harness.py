@@ -152,6 +152,103 @@ def test_octree_edge_cases(harness, oracle):
         np.testing.assert_array_equal(r2, ref["response"])
 
 
+def _octree_pyr(harness, packed, W, H, N, D):
+    out = np.zeros(len(packed) + 4 * max(N, 1) + 64, np.uint32)
+    deep = C.c_int(0)
+    m = harness.harness_octree_pyr(_p(packed), len(packed), W, H, N, _p(out), len(out), D, C.byref(deep))
+    return m, out[:max(m, 0)], deep.value
+
+
+def _check_keys(out, ref):
+    x2, y2, r2 = _unpack(out)
+    np.testing.assert_array_equal(x2, ref["x"])
+    np.testing.assert_array_equal(y2, ref["y"])
+    np.testing.assert_array_equal(r2, ref["response"])
+
+
+@pytest.mark.parametrize("frame", [0, 3])
+def test_octree_count_pyramid_all_levels(harness, oracle, frame):
+    """The count-pyramid formulation (one histogram instead of the per-round label passes) on
+    every level at several pyramid depths: shallow ones must hand over to the label passes
+    (kOctDeep) and still match the oracle; deep enough ones finish on their own."""
+    img = synth.stereo_pair(480, 640, frame)[frame % 2]
+    seen = set()
+    for li, lvl in enumerate(oracle.pyramid(img)):
+        h, w = lvl.shape
+        cand = _level_cands(harness, lvl, 20, 7)
+        oc = oracle.level_candidates(lvl, 20, 7)
+        for N in (oracle.features_per_level(2000)[li], 1, 0, 7, 5000):
+            ref = oracle.distribute_octree(oc, 16, w - 16, 16, h - 16, N)
+            for D in (1, 2, 4, 5, 7):
+                m, out, deep = _octree_pyr(harness, cand, w - 32, h - 32, N, D)
+                assert m == len(ref), (li, N, D)
+                _check_keys(out, ref)
+                seen.add(deep)
+    assert seen == {0, 1}  # both the pyramid-only and the handed-over runs were exercised
+
+
+def test_octree_count_pyramid_cell_lists(harness, oracle):
+    """The kernel's input layout: the level's keys as per-cell lists (cell order = input order),
+    located by the binary search over the cell offsets and named by cell * cap + slot."""
+    img = synth.stereo_pair(480, 640, 5)[1]
+    rng = np.random.default_rng(2)
+    for li, lvl in enumerate(oracle.pyramid(img)[:4]):
+        h, w = lvl.shape
+        cand = _level_cands(harness, lvl, 20, 7)
+        oc = oracle.level_candidates(lvl, 20, 7)
+        # random cell boundaries (empty cells included), capacity with slack
+        cuts = np.sort(rng.integers(0, len(cand) + 1, size=60))
+        counts = np.diff(np.concatenate([[0], cuts, [len(cand)]])).astype(np.int32)
+        cap = int(counts.max()) + 3
+        cells = np.zeros(len(counts) * cap, np.uint32)
+        o = 0
+        for c, k in enumerate(counts):
+            cells[c * cap:c * cap + k] = cand[o:o + k]
+            o += k
+        for N in (oracle.features_per_level(2000)[li], 7):
+            ref = oracle.distribute_octree(oc, 16, w - 16, 16, h - 16, N)
+            for D in (2, 5):
+                out = np.zeros(len(cand) + 4 * N + 64, np.uint32)
+                deep = C.c_int(0)
+                m = harness.harness_octree_cells(_p(cells), _p(counts), len(counts), cap, w - 32, h - 32, N,
+                                                 _p(out), len(out), D, C.byref(deep))
+                assert m == len(ref), (li, N, D)
+                _check_keys(out[:m], ref)
+
+
+def test_octree_count_pyramid_edge_cases(harness, oracle):
+    # empty, single key, one tight cluster (deep divisions), a wide frame (nIni = 2) and keys on
+    # the initial-node seam, each at a shallow and a deep pyramid
+    kd = oracle.KP_DTYPE
+    rng = np.random.default_rng(11)
+    cases = [(np.zeros(0, kd), 608, 448, 10)]
+    one = np.zeros(1, kd); one["x"] = 5; one["y"] = 9; one["response"] = 30
+    cases.append((one, 608, 448, 10))
+    pts = set()
+    while len(pts) < 400:
+        pts.add((int(rng.integers(300, 316)), int(rng.integers(200, 231))))
+    cl = np.zeros(len(pts), kd)
+    for i, (x, y) in enumerate(sorted(pts, key=lambda t: (t[1], t[0]))):
+        cl[i]["x"], cl[i]["y"], cl[i]["response"] = x, y, rng.integers(0, 60)
+    cases.append((cl, 608, 448, 120))
+    for W, H, N in ((1888, 1048, 939), (1245, 600, 300), (633, 211, 150)):
+        pts = set()
+        while len(pts) < 3000:
+            pts.add((int(rng.integers(0, W)), int(rng.integers(0, H))))
+        wide = np.zeros(len(pts), kd)
+        for i, (x, y) in enumerate(pts):
+            wide[i]["x"], wide[i]["y"], wide[i]["response"] = x, y, rng.integers(0, 9)
+        cases.append((wide, W, H, N))
+    for keys, W, H, N in cases:
+        ref = oracle.distribute_octree(keys, 16, 16 + W, 16, 16 + H, N)
+        packed = (keys["x"].astype(np.uint32) | (keys["y"].astype(np.uint32) << 12) |
+                  (keys["response"].astype(np.uint32) << 24)).astype(np.uint32)
+        for D in (1, 3, 7):
+            m, out, _ = _octree_pyr(harness, packed, W, H, N, D)
+            assert m == len(ref), (W, H, N, D)
+            _check_keys(out, ref)
+
+
 @pytest.mark.parametrize("ini,mn", [(20, 7), (7, 20), (0, 0), (40, 3), (255, 1)])
 def test_cells_thresholds_and_fallback(harness, oracle, ini, mn):
     # a low-texture frame (many cells fall back to minThFAST) and a textured one
