@@ -260,7 +260,7 @@ __host__ __device__ __attribute__((always_inline)) inline int octree_distribute(
     const int D = ws.pyrD;
     const bool fast = D > 0;
     auto pcnt = ws.pyr;
-    auto pbest = ws.pyr + pyr_base(D + 1, nIni);
+    auto pbest = fast ? ws.pyr + pyr_base(D + 1, nIni) : ws.pyr;  // (no offset on a null pyr)
     const int bD = pyr_base(D, nIni);
     if (fast) {
         for (int e = tid; e < (nIni << (2 * D)); e += NT) {

@@ -13,6 +13,9 @@
 
 using namespace orbgpu;
 
+// node state is read and written as 16-byte records (orb_octree.h on_ld / on_st)
+static uint8_t* align16(uint8_t* p) { return (uint8_t*)(((uintptr_t)p + 15) & ~(uintptr_t)15); }
+
 extern "C" {
 
 // libm_sincosf (orb_math.h) against the host's own sinf / cosf on every `stride`-th float of
@@ -93,7 +96,7 @@ int harness_octree(const uint32_t* keys, int n, int W, int H, int N, uint32_t* o
     w.cellkeys = nullptr;
     w.ncells = 0;
     w.cell_cap = 0;
-    w.m = oct_nodemem_carve<kGeneric>(mem.data(), cap);
+    w.m = oct_nodemem_carve<kGeneric>(align16(mem.data()), cap);
     w.cap = cap;
     w.out_keys = out;
     w.out_cap = out_cap;
@@ -130,7 +133,7 @@ int harness_octree_cells(const uint32_t* cells, const int32_t* counts, int ncell
     w.cellkeys = cells;
     w.ncells = ncells;
     w.cell_cap = cap;
-    w.m = oct_nodemem_carve<kGeneric>(mem.data(), ocap);
+    w.m = oct_nodemem_carve<kGeneric>(align16(mem.data()), ocap);
     w.cap = ocap;
     w.out_keys = out;
     w.out_cap = out_cap;
@@ -166,7 +169,7 @@ int harness_octree_pyr(const uint32_t* keys, int n, int W, int H, int N, uint32_
     w.cellkeys = nullptr;
     w.ncells = 0;
     w.cell_cap = 0;
-    w.m = oct_nodemem_carve<kGeneric>(mem.data(), cap);
+    w.m = oct_nodemem_carve<kGeneric>(align16(mem.data()), cap);
     w.cap = cap;
     w.out_keys = out;
     w.out_cap = out_cap;
