@@ -309,36 +309,47 @@ __host__ __device__ __attribute__((always_inline)) inline int octree_distribute(
         for (int x = tid; x <= W; x += NT) ws.xcode[x] = (uint16_t)oct_xcode(x, D, hX, nIni);
         for (int y = tid; y <= H; y += NT) ws.ycode[y] = (uint16_t)oct_ycode(y, D, H);
         p.sync();
+#ifdef OCT_DIAG
+        mark(1);
+#endif
     }
     auto pyr_add = [&](uint32_t key, int kid) __attribute__((always_inline)) {
         const int x = key_x(key), y = key_y(key);
         const int e = bD + (x <= W && y <= H ? (int)ws.xcode[x] + (int)ws.ycode[y]
                                              : (int)(oct_xcode(x, D, hX, nIni) + oct_ycode(y, D, H)));
+#ifndef OCT_NOATOM
         p.atomic_add(&pcnt[e], 1);
         p.atomic_max(&pbest[e], ((uint32_t)key_resp(key) << 24) | (0xFFFFFFu - (uint32_t)kid));
+#else
+        if (kid == -5) pcnt[e] = 1;
+#endif
     };
     if (fast && n > 0 && ws.cell_off) {
-        // cell lists as they are: wave w takes cells w, w + waves, ..., U of them at a time, its
-        // lanes their keys (no search for a key's cell; kid = cell * cell_cap + slot)
-        constexpr int U = 8;
-        const int Wv = p.nwaves(), wv = p.wave(), lane = p.lane(), Lw = p.wave_width();
-        for (int c0 = wv; c0 < ws.ncells; c0 += U * Wv) {
-            int cc[U], cn[U], mx = 0;
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int c = c0 + u * Wv;
-                cc[u] = c;
-                cn[u] = c < ws.ncells ? (c + 1 < ws.ncells ? ws.cell_off[c + 1] : n) - ws.cell_off[c] : 0;
-                mx = mx > cn[u] ? mx : cn[u];
-            }
-            for (int j0 = 0; j0 < mx; j0 += Lw) {
-                const int j = j0 + lane;
+        // cell lists as they are (no search for a key's cell; kid = cell * cell_cap + slot):
+        // consecutive threads take consecutive cells, K threads per cell interleaving its slots,
+        // so the lanes of one atomic instruction hit different pyramid entries (a cell's own
+        // keys share a few entries: lanes on one cell would serialize on them)
+        const int nc = ws.ncells;
+        int K = 1;
+        while (2 * K * nc <= NT) K *= 2;
+        const int slots = K * nc;
+        constexpr int U = 16;  // keys in flight per thread
+        for (int t = tid; t < slots; t += NT) {
+            const int c = t % nc, ph = t / nc;
+            const int cnt_c = (c + 1 < nc ? ws.cell_off[c + 1] : n) - ws.cell_off[c];
+            const int cb = c * ws.cell_cap;
+            for (int j0 = ph; j0 < cnt_c; j0 += U * K) {
                 uint32_t key[U];
 #pragma unroll
-                for (int u = 0; u < U; ++u) key[u] = j < cn[u] ? ws.cellkeys[cc[u] * ws.cell_cap + j] : 0u;
+                for (int u = 0; u < U; ++u) {  // clamped, unpredicated: all U loads in flight
+                    const int j = j0 + u * K;
+                    key[u] = ws.cellkeys[cb + (j < cnt_c ? j : cnt_c - 1)];
+                }
 #pragma unroll
-                for (int u = 0; u < U; ++u)
-                    if (j < cn[u]) pyr_add(key[u], cc[u] * ws.cell_cap + j);
+                for (int u = 0; u < U; ++u) {
+                    const int j = j0 + u * K;
+                    if (j < cnt_c) pyr_add(key[u], cb + j);
+                }
             }
         }
         p.sync();
