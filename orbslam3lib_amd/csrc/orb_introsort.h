@@ -237,142 +237,120 @@ struct SortScratchT {
 };
 using SortScratch = SortScratchT<kGeneric>;
 
-// Step 1 (partition phase) on policy p.
+// Step 1 (partition phase) on policy p: segments are independent, so each is partitioned by
+// ONE wave (wave w takes segments w, w + waves, ...) with ballot scans inside the wave, and a
+// round of the recursion costs a single workgroup barrier.  The next round's segments are
+// appended through a counter (their order does not matter: segments are disjoint).
 template <int AS, class P>
 __host__ __device__ __attribute__((always_inline)) inline void introsort_partition(
-    P& p, asp<AS, SortElem> a, int m, const SortScratchT<AS>& s, asp<AS, int> sh_nseg) {
+    P& p, asp<AS, SortElem> a, int m, const SortScratchT<AS>& s, asp<AS, int> /*unused*/) {
     const int tid = p.tid(), NT = p.nthreads();
+    const int lane = p.lane(), wv = p.wave(), Wv = p.nwaves(), Lw = p.wave_width();
+    const uint64_t lt = p.lanemask_lt();
     if (m <= 1) return;
-    int cur = 0;
+    // s.rank[i] = first index of the final segment holding i (a segment of <= 16 elements is
+    // never partitioned again), 0xFFFF inside a heap-sorted segment (step 2 reads it)
+    if (m <= 16) {
+        for (int i = tid; i < m; i += NT) s.rank[i] = 0;
+        p.sync();
+        return;
+    }
+    // s.segK[0..2]: segment counters of rounds r, r + 1, r + 2 (mod 3)
     if (tid == 0) {
         s.segF[0][0] = 0;
         s.segL[0][0] = (uint16_t)m;
         s.segD[0][0] = (uint16_t)(2 * isort_lg(m));
-        *sh_nseg = m > 16 ? 1 : 0;
+        s.segK[0] = 1;
+        s.segK[1] = 0;
+        s.segK[2] = 0;
     }
-    // s.rank[i] = first index of the final segment holding i (a segment of <= 16 elements is
-    // never partitioned again), 0xFFFF inside a heap-sorted segment (step 2 reads it)
-    if (m <= 16)
-        for (int i = tid; i < m; i += NT) s.rank[i] = 0;
     p.sync();
-    while (true) {
-        const int nseg = *sh_nseg;
+    int cur = 0;
+    for (int r = 0;; ++r) {
+        const int nseg = s.segK[r % 3];
         if (nseg == 0) break;
-        // (no runtime-indexed pointer arrays: they would live in scratch memory)
+        if (tid == 0) s.segK[(r + 2) % 3] = 0;  // last read in round r - 1, appended in r + 1
         const auto F = cur ? s.segF[1] : s.segF[0];
         const auto L = cur ? s.segL[1] : s.segL[0];
         const auto D = cur ? s.segD[1] : s.segD[0];
         const auto NF = cur ? s.segF[0] : s.segF[1];
         const auto NL = cur ? s.segL[0] : s.segL[1];
         const auto ND = cur ? s.segD[0] : s.segD[1];
-        for (int g = tid; g < nseg; g += NT) {
-            const int f = F[g], l = L[g];
-            if (D[g] == 0) {
-                isort_heapsort(a + f, l - f);
-                s.segK[g] = -1;
-                for (int i = f; i < l; ++i) s.rank[i] = 0xFFFF;
-            } else {
-                isort_median_to_first(a, f, f + 1, f + (l - f) / 2, l - 1);
-                s.segK[g] = 0;
+        const auto nxt_cnt = s.segK + (r + 1) % 3;
+        for (int g = wv; g < nseg; g += Wv) {  // wave-uniform
+            const int f = F[g], l = L[g], d = D[g];
+            if (d == 0) {  // depth exhausted: std::__partial_sort, in place
+                if (lane == 0) isort_heapsort(a + f, l - f);
+                for (int i = f + lane; i < l; i += Lw) s.rank[i] = 0xFFFF;
+                p.wave_sync();
+                continue;
             }
-        }
-        p.sync();
-        // the segment of every position (segments are disjoint and in position order: a
-        // binary search over their first positions), and the stopper scans of all segments
-        int top = 1;
-        while (2 * top <= nseg) top *= 2;
-        int lc = 0, rc = 0;
-        for (int base = 0; base <= m; base += NT) {
-            const int i = base + tid;
-            int lf = 0, rf = 0;
-            if (i < m) {
-                int g = 0;
-                for (int h = top; h; h >>= 1)
-                    if (g + h < nseg && F[g + h] <= i) g += h;
-                const bool in = nseg > 0 && F[g] <= i && i < L[g] && s.segK[g] >= 0;
-                s.segof[i] = in ? (uint16_t)g : (uint16_t)0xFFFF;
-                if (in) {
-                    const int f = F[g];
-                    const SortElem pv = se_ld(a, f);
-                    lf = (i > f) && !node_less(se_ld(a, i), pv);
-                    rf = !node_less(pv, se_ld(a, i));
-                }
-            }
-            int tl, tr;
-            const int2 e = p.scan_pair(lf, rf, &tl, &tr);
-            if (i <= m) {
-                s.lex[i] = (uint16_t)(lc + e.x);
-                s.rex[i] = (uint16_t)(rc + e.y);
-            }
-            lc += tl;
-            rc += tr;
-        }
-        p.sync();
-        for (int i = tid; i < m; i += NT) {
-            const int g = s.segof[i];
-            if (g == 0xFFFF) continue;
-            const int f = F[g], l = L[g];
+            if (lane == 0) isort_median_to_first(a, f, f + 1, f + (l - f) / 2, l - 1);
+            p.wave_sync();
             const SortElem pv = se_ld(a, f);
-            if (i > f && !node_less(se_ld(a, i), pv)) s.lpos[f + (s.lex[i] - s.lex[f])] = (uint16_t)i;
-            if (!node_less(pv, se_ld(a, i))) s.rpos[f + (s.rex[l] - s.rex[i] - 1)] = (uint16_t)i;
-        }
-        p.sync();
-        // the scan swaps (L'_k, R'_k) while L'_k < R'_k: a prefix of k (L' ascends, R' descends),
-        // so pair k swaps in place (no position is in two swapping pairs) and the last swapping
-        // pair (or k = 0 when none swaps) records K
-        for (int j = tid; j < m; j += NT) {
-            const int g = s.segof[j];
-            if (g == 0xFFFF) continue;
-            const int f = F[g], l = L[g], k = j - f;
-            const int nl = s.lex[l] - s.lex[f], nr = s.rex[l] - s.rex[f];
-            const int np = nl < nr ? nl : nr;
-            const bool sw = k < np && s.lpos[j] < s.rpos[j];
-            const bool sw1 = k + 1 < np && s.lpos[j + 1] < s.rpos[j + 1];
-            if (sw) isort_swap(a, s.lpos[j], s.rpos[j]);
-            if (sw && !sw1) s.segK[g] = k + 1;
-        }
-        p.sync();
-        // children segments, kept in position order (left child first)
-        int carry = 0;
-        for (int base = 0; base < nseg; base += NT) {
-            const int g = base + tid;
-            int c = 0, cut = 0, f = 0, l = 0, d = 0;
-            if (g < nseg && s.segK[g] >= 0) {
-                f = F[g];
-                l = L[g];
-                d = D[g] - 1;
-                const int K = s.segK[g];
-                const int nl = s.lex[l] - s.lex[f];
-                cut = K < nl ? s.lpos[f + K] : 0x7fffffff;
-                if (K > 0) cut = cut < s.rpos[f + K - 1] ? cut : s.rpos[f + K - 1];
-                c = (cut - f > 16) + (l - cut > 16);
-                if (cut - f <= 16)
-                    for (int i = f; i < cut; ++i) s.rank[i] = (uint16_t)f;
-                if (l - cut <= 16)
-                    for (int i = cut; i < l; ++i) s.rank[i] = (uint16_t)cut;
+            // left stoppers L'_k (i > f, !(a[i] < pivot)) ascending into lpos[f + k]; right
+            // stoppers (!(pivot < a[i])) counted from the left into rex[i], then placed
+            // descending into rpos[f + k]
+            int nl = 0, nr = 0;
+            for (int i0 = f; i0 < l; i0 += Lw) {
+                const int i = i0 + lane;
+                bool lf = false, rf = false;
+                if (i < l) {
+                    const SortElem x = se_ld(a, i);
+                    lf = i > f && !node_less(x, pv);
+                    rf = !node_less(pv, x);
+                }
+                const uint64_t bl = p.ballot(lf), br = p.ballot(rf);
+                if (lf) s.lpos[f + nl + p.popc64(bl & lt)] = (uint16_t)i;
+                if (i < l) s.rex[i] = rf ? (uint16_t)(nr + p.popc64(br & lt)) : (uint16_t)0xFFFF;
+                nl += p.popc64(bl);
+                nr += p.popc64(br);
             }
-            int tot;
-            const int ex = p.scan_small(c, &tot);
-            if (c) {
-                int o = carry + ex;
+            p.wave_sync();
+            for (int i = f + lane; i < l; i += Lw) {
+                const int k = s.rex[i];
+                if (k != 0xFFFF) s.rpos[f + nr - 1 - k] = (uint16_t)i;
+            }
+            p.wave_sync();
+            // the scan swaps (L'_k, R'_k) while L'_k < R'_k: a prefix of k (L' ascends, R'
+            // descends) of K pairs, no position in two of them, so every pair swaps in place
+            const int np = nl < nr ? nl : nr;
+            int K = 0;
+            for (int k0 = 0; k0 < np; k0 += Lw) {
+                const int k = k0 + lane;
+                const bool sw = k < np && s.lpos[f + k] < s.rpos[f + k];
+                if (sw) isort_swap(a, s.lpos[f + k], s.rpos[f + k]);
+                K += p.popc64(p.ballot(sw));
+            }
+            p.wave_sync();
+            int cut = K < nl ? s.lpos[f + K] : 0x7fffffff;
+            if (K > 0) {
+                const int rk = s.rpos[f + K - 1];
+                cut = cut < rk ? cut : rk;
+            }
+            // children: > 16 elements go to the next round, the others are final segments
+            if (lane == 0) {
                 if (cut - f > 16) {
+                    const int o = p.atomic_add(nxt_cnt, 1);
                     NF[o] = (uint16_t)f;
                     NL[o] = (uint16_t)cut;
-                    ND[o] = (uint16_t)d;
-                    ++o;
+                    ND[o] = (uint16_t)(d - 1);
                 }
                 if (l - cut > 16) {
+                    const int o = p.atomic_add(nxt_cnt, 1);
                     NF[o] = (uint16_t)cut;
                     NL[o] = (uint16_t)l;
-                    ND[o] = (uint16_t)d;
+                    ND[o] = (uint16_t)(d - 1);
                 }
             }
-            carry += tot;
+            if (cut - f <= 16)
+                for (int i = f + lane; i < cut; i += Lw) s.rank[i] = (uint16_t)f;
+            if (l - cut <= 16)
+                for (int i = cut + lane; i < l; i += Lw) s.rank[i] = (uint16_t)cut;
+            p.wave_sync();
         }
         p.sync();
-        if (tid == 0) *sh_nseg = carry;
         cur ^= 1;
-        p.sync();
     }
 }
 

@@ -144,7 +144,6 @@ struct OctWST {
 };
 
 constexpr int kOctUnroll = 8;         // keys per thread per batch in the key passes
-constexpr int kOctWaveSortMax = 128;  // final-phase sorts up to this size partition on one wave
 
 struct OctShared {
     int size, prev_size, nexp, ndiv, phase, done, nchild, nundiv, status, jstop, deep;
@@ -511,28 +510,20 @@ __host__ __device__ __attribute__((always_inline)) inline int octree_distribute(
     while (!sh->done) {
         if (++guard > 4096) return -4;
         if (sh->phase != 1) {  // final phase: libstdc++-ordered sort of vPrev
-            // partition rounds: wave 0 alone for small arrays (no workgroup barriers), the
-            // whole block for large ones (more segments and elements per round)
+            // partition rounds: one wave per segment, one workgroup barrier per round
             const int m = sh->nexp;
             auto sb = reinterpret_cast<asp<LAS, SortElem>>(nxt);  // nxt is free until the rebuild
-            auto fill = [&](auto& q) __attribute__((always_inline)) {
-                for (int j = q.tid(); j < m; j += q.nthreads()) {
-                    const int v = vsz[j];
-                    SortElem e;
-                    e.size = cur[v].cnt;
-                    e.ulx = cur[v].x0;
-                    e.node = v;
-                    se_st(sb, j, e);
-                }
-                q.sync();
-                introsort_partition<LAS>(q, sb, m, sort_scratch(cnxt), &sh->jstop);
-            };
-            if (m > kOctWaveSortMax) {
-                fill(p);
-            } else if (nw) {
-                auto np = p.node();
-                fill(np);
+            for (int j = tid; j < m; j += NT) {
+                const int v = vsz[j];
+                SortElem e;
+                e.size = cur[v].cnt;
+                e.ulx = cur[v].x0;
+                e.node = v;
+                e.pad = 0;
+                se_st(sb, j, e);
             }
+            p.sync();
+            introsort_partition<LAS>(p, sb, m, sort_scratch(cnxt), &sh->jstop);
         }
         if (sh->phase != 1) {  // the O(m^2) stable rank pass spreads over the whole block
             p.sync();

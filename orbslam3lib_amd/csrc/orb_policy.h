@@ -73,6 +73,12 @@ struct DevPolicy {
     __device__ int tid() const { return (int)threadIdx.x; }
     __device__ int nthreads() const { return (int)blockDim.x; }
     __device__ void sync() { __syncthreads(); }
+    // memory ordering among the lanes of the calling wave (LDS written by one lane, read by another)
+    __device__ void wave_sync() {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
     template <class T>
     __device__ int atomic_add(T p, int v) {
         return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -209,6 +215,7 @@ struct SerialPolicy {
     __host__ __device__ int tid() const { return 0; }
     __host__ __device__ int nthreads() const { return 1; }
     __host__ __device__ void sync() {}
+    __host__ __device__ void wave_sync() {}
     template <class T>
     __host__ __device__ int atomic_add(T p, int v) {
         const int o = *p;
