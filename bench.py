@@ -713,15 +713,13 @@ def main():
         c4 = og.BatchExtractor(args.nfeatures, 1.2, args.nlevels, 20, 7, device=local, width=W, height=H, max_images=2)
         c4.upload(np.stack(uniq[0]))
         for _ in range(5):
-            c4.run()
-            c4.match_stereo(stereo_rows_only=False)
+            c4.run_match(stereo_rows_only=False)
         c4.synchronize()
         barrier(dist)
         k0 = time.perf_counter()
         n4 = 50
         for _ in range(n4):
-            c4.run()
-            c4.match_stereo(stereo_rows_only=False)
+            c4.run_match(stereo_rows_only=False)  # extraction + kNN2 as one graph submission
         c4.synchronize()
         k_el = max_over_ranks(dist, time.perf_counter() - k0)
         c4n, _ = c4.counts()

@@ -157,6 +157,12 @@ int orbgpu_match_knn2_device(orbgpu_ctx* ctx, const uint8_t* d_query, int nq, co
  * stereo_rows_only != 0 (Frame::ComputeStereoFishEyeMatches, Frame.cc:1142-1148) or all rows.
  * Results stay in HBM; fetch with orbgpu_download_matches. */
 int orbgpu_match_stereo_batch(orbgpu_ctx* ctx, int n_pairs, int stereo_rows_only, void* stream);
+/* orbgpu_run_batch followed by orbgpu_match_stereo_batch over all n_images / 2 pairs, as ONE
+ * submission when the batch runs as one captured graph (the latency shape: the accelerator
+ * session's stereo frame, LynxHardwareAccelerator.cpp:133-204, which extracts both eyes and
+ * runs BFMatchORB's kNN2 in one device pass); otherwise exactly the two calls.  n_images even. */
+int orbgpu_run_batch_match(orbgpu_ctx* ctx, int n_images, int width, int height, const int32_t* laps,
+                           int stereo_rows_only, void* stream);
 int orbgpu_download_matches(orbgpu_ctx* ctx, int pair, int32_t* idx1, int32_t* dist1,
                             int32_t* idx2, int32_t* dist2, int cap, int* nq);
 

@@ -50,7 +50,7 @@ EXPORTED = [
     "orbgpu_host_free", "orbgpu_export_descriptors", "orbgpu_match_knn2_device",
     "orbgpu_set_profiling", "orbgpu_num_stages", "orbgpu_stage_name", "orbgpu_stage_times",
     "orbgpu_reset_stage_times", "orbgpu_last_error", "orbgpu_abi_version",
-    "orbgpu_fisheye_stereo_batch", "orbgpu_download_fisheye",
+    "orbgpu_fisheye_stereo_batch", "orbgpu_download_fisheye", "orbgpu_run_batch_match",
 ]
 
 
@@ -401,6 +401,20 @@ class BatchExtractor:
         _check(_lib.orbgpu_run_batch(self.ctx.handle, n, self.width, self.height,
                                      _p(lp) if lp is not None else None,
                                      C.c_void_p(stream) if stream else None))
+
+    def run_match(self, laps=None, stereo_rows_only=False, stream=None):
+        """run() then match_stereo() over every pair as one submission when the batch is one
+        captured graph (orbgpu_run_batch_match; the latency shape)."""
+        if self._staged is not None:
+            self.n, self.height, self.width = self._staged
+            self._staged = None
+        n = self.n
+        lp = None
+        if laps is not None:
+            lp = np.ascontiguousarray(laps, dtype=np.int32).reshape(n, 2)
+        _check(_lib.orbgpu_run_batch_match(self.ctx.handle, n, self.width, self.height,
+                                           _p(lp) if lp is not None else None, int(stereo_rows_only),
+                                           C.c_void_p(stream) if stream else None))
 
     def match_stereo(self, stereo_rows_only=False, stream=None):
         _check(_lib.orbgpu_match_stereo_batch(self.ctx.handle, self.n // 2, int(stereo_rows_only),

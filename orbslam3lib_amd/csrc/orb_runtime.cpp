@@ -142,7 +142,8 @@ struct orbgpu_ctx {
     // the captured launch sequence of a one-stream batch (run_batch), keyed by {n, w, h, slot}
     bool use_graph = true;   // ORBGPU_GRAPH=0 launches every kernel directly (A/B)
     hipGraphExec_t graph_exec = nullptr;
-    int graph_key[4] = {-1, -1, -1, -1};
+    int graph_key[6] = {-1, -1, -1, -1, -1, -1};  // images, width, height, input slot, match pairs, rows
+    bool knn_nosplit = false;  // ORBGPU_KNN_NOSPLIT (read once at create): no split kNN2 launches
     std::vector<int32_t> laps_host;  // lapping areas currently in `laps` (device), per image
     bool need_fork = true;           // the main stream holds work the sub streams must wait for
     bool stagger = true;             // ORBGPU_STAGGER=0: the chunks start every layout in lockstep
@@ -721,6 +722,7 @@ int orbgpu_create(const orbgpu_params* p, int device, int max_width, int max_hei
         if (sg) c->stagger = atoi(sg) != 0;
         c->oct_stamps = getenv("ORBGPU_OCT_STAMPS") != nullptr;
         if (const char* g = getenv("ORBGPU_GRAPH")) c->use_graph = atoi(g) != 0;
+        c->knn_nosplit = getenv("ORBGPU_KNN_NOSPLIT") != nullptr;
     }
     int r = ensure_input(c, 1, max_width, max_height);
     if (!r) r = set_geometry(c, max_width, max_height);
@@ -833,7 +835,29 @@ int orbgpu_host_free(void* ptr) {
     return ORBGPU_OK;
 }
 
-int orbgpu_run_batch(orbgpu_ctx* c, int n, int w, int h, const int32_t* laps, void* stream) {
+// MatchArgs over the context's last batch: pair p = images 2p (query) and 2p + 1 (train)
+static MatchArgs stereo_match_args(orbgpu_ctx* c, int stereo_only) {
+    MatchArgs m;
+    m.desc = c->outdesc.as<uint8_t>();
+    m.out_n = c->outn.as<int32_t>();
+    m.out_mono = c->outmono.as<int32_t>();
+    m.out_cap = c->out_cap;
+    m.stereo_only = stereo_only;
+    m.idx1 = c->midx1.as<int32_t>();
+    m.dist1 = c->mdist1.as<int32_t>();
+    m.idx2 = c->midx2.as<int32_t>();
+    m.dist2 = c->mdist2.as<int32_t>();
+    m.nq = c->mnq.as<int32_t>();
+    m.part = nullptr;
+    m.pair0 = 0;
+    return m;
+}
+
+// The batch's kernels; match_pairs > 0 appends the stereo kNN2 of pairs [0, match_pairs) when the
+// batch runs as one captured graph (*matched = true: one submission for extraction and match).
+static int run_batch_impl(orbgpu_ctx* c, int n, int w, int h, const int32_t* laps, void* stream,
+                          int match_pairs, int stereo_only, bool* matched) {
+    if (matched) *matched = false;
     if (!c) return fail(ORBGPU_ERR_INVALID, "null ctx");
     if (w <= 0 || h <= 0) return fail(ORBGPU_ERR_EMPTY_IMAGE, "empty image");
     int r = ensure_input(c, n, w, h);
@@ -1010,12 +1034,20 @@ int orbgpu_run_batch(orbgpu_ctx* c, int n, int w, int h, const int32_t* laps, vo
     // while the batch shape and input slot stay the same -- one submission instead of ~15.
     const bool graphable = chunks.size() == 1 && !stream && c->prof_mask == 0 && c->use_graph &&
                            !c->oct_stamps;
+    const bool with_match = graphable && match_pairs > 0 && 2 * match_pairs <= n && c->out_cap <= 65535;
+    auto launch_match = [&]() -> int {
+        MatchArgs m = stereo_match_args(c, stereo_only);
+        m.part = match_pairs * 2 <= kKnnSplitSlots && !c->knn_nosplit ? c->mpart.as<uint2>() : nullptr;
+        HIP_TRY(launch_knn2_pairs(m, match_pairs, s));
+        return 0;
+    };
     if (graphable) {
-        const int key[4] = {n, w, h, c->in_slot};
+        const int key[6] = {n, w, h, c->in_slot, with_match ? match_pairs : 0, with_match ? stereo_only : 0};
         if (!c->graph_exec || std::memcmp(key, c->graph_key, sizeof key) != 0) {
             drop_graph(c);
             HIP_TRY(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
-            const int rr = launch_all();
+            int rr = launch_all();
+            if (!rr && with_match) rr = launch_match();
             hipGraph_t g = nullptr;
             const hipError_t ec = hipStreamEndCapture(s, &g);
             if (rr || ec != hipSuccess) {
@@ -1039,10 +1071,28 @@ int orbgpu_run_batch(orbgpu_ctx* c, int n, int w, int h, const int32_t* laps, vo
     c->last_images = n;
     c->last_w = w;
     c->last_h = h;
+    if (with_match) {
+        c->last_pairs = match_pairs;
+        if (matched) *matched = true;
+    }
     // a caller's stream: the context's streams wait for it before they touch this batch's
     // buffers again (the next async upload overwrites the input slot this batch read)
     if (stream && (r = rejoin(c, s))) return r;
     return ORBGPU_OK;
+}
+
+int orbgpu_run_batch(orbgpu_ctx* c, int n, int w, int h, const int32_t* laps, void* stream) {
+    return run_batch_impl(c, n, w, h, laps, stream, 0, 0, nullptr);
+}
+
+int orbgpu_run_batch_match(orbgpu_ctx* c, int n, int w, int h, const int32_t* laps, int stereo_rows_only,
+                           void* stream) {
+    if (!c) return fail(ORBGPU_ERR_INVALID, "null ctx");
+    if (n < 2 || (n % 2) != 0) return fail(ORBGPU_ERR_INVALID, "run_batch_match needs whole stereo pairs");
+    bool matched = false;
+    int r = run_batch_impl(c, n, w, h, laps, stream, n / 2, stereo_rows_only ? 1 : 0, &matched);
+    if (r || matched) return r;
+    return orbgpu_match_stereo_batch(c, n / 2, stereo_rows_only, stream);
 }
 
 int orbgpu_synchronize(orbgpu_ctx* c) {
@@ -1286,19 +1336,8 @@ int orbgpu_match_stereo_batch(orbgpu_ctx* c, int n_pairs, int stereo_only, void*
     if (!c || n_pairs < 1 || 2 * n_pairs > c->last_images) return fail(ORBGPU_ERR_INVALID, "bad pair count");
     HIP_TRY(hipSetDevice(c->device));
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
-    MatchArgs m;
-    m.desc = c->outdesc.as<uint8_t>();
-    m.out_n = c->outn.as<int32_t>();
-    m.out_mono = c->outmono.as<int32_t>();
-    m.out_cap = c->out_cap;
-    m.stereo_only = stereo_only;
-    m.idx1 = c->midx1.as<int32_t>();
-    m.dist1 = c->mdist1.as<int32_t>();
-    m.idx2 = c->midx2.as<int32_t>();
-    m.dist2 = c->mdist2.as<int32_t>();
-    m.nq = c->mnq.as<int32_t>();
-    m.part = nullptr;  // the split path (one launch over <= 4 pairs) sets it below
-    uint2* split_part = n_pairs * 2 <= kKnnSplitSlots && !getenv("ORBGPU_KNN_NOSPLIT") ? c->mpart.as<uint2>() : nullptr;
+    MatchArgs m = stereo_match_args(c, stereo_only);  // the split path (<= 4 pairs) sets m.part below
+    uint2* split_part = n_pairs * 2 <= kKnnSplitSlots && !c->knn_nosplit ? c->mpart.as<uint2>() : nullptr;
     if (c->out_cap > 65535) return fail(ORBGPU_ERR_INVALID, "matcher supports < 65536 rows per image");
     // follow the extraction's sub-batches so each chunk matches right after it is extracted
     bool chunked = !stream && !c->last_chunks.empty();

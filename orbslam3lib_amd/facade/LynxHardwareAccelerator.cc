@@ -3,8 +3,8 @@
 // Replaces cpp/src/LynxHardwareAcceleration/LynxHardwareAccelerator.cpp (FastRPC session, rpcmem
 // buffers, 3-slot match cache).  One liborbgpu context (two images: the eyes of one frame) holds
 // the frame on the device; ExtractORB runs the extraction of both eyes and the stereo-row kNN2
-// (orbgpu_run_batch + orbgpu_match_stereo_batch) and keeps the matches in the slot of its frame
-// id, as :134-213 do with matchingCache*.
+// as one submission (orbgpu_run_batch_match) and keeps the matches in the slot of its frame id,
+// as :134-213 do with matchingCache*.
 #include "../../include/orbslam3/LynxHardwareAcceleration/LynxHardwareAccelerator.h"
 
 #include <cstring>
@@ -127,8 +127,7 @@ int LynxHardwareAccelerator::ExtractORB(int& nl, int& nr, std::vector<cv::KeyPoi
     std::lock_guard<std::mutex> g(mMutex);
     if (mFrameW <= 0) return -1;  // nothing stored
     const int32_t laps[4] = {l0, l1, r0, r1};
-    if (orbgpu_run_batch(mCtx, 2, mFrameW, mFrameH, laps, nullptr) != ORBGPU_OK) return -1;
-    if (orbgpu_match_stereo_batch(mCtx, 1, 1, nullptr) != ORBGPU_OK) return -1;
+    if (orbgpu_run_batch_match(mCtx, 2, mFrameW, mFrameH, laps, 1, nullptr) != ORBGPU_OK) return -1;
     return finish(nl, nr, kl, kr, dl, dr, monoLeft, monoRight);
 }
 
@@ -149,8 +148,7 @@ int LynxHardwareAccelerator::ExtractORBPair(const uint8_t* left, const uint8_t* 
     if (orbgpu_upload_images(mCtx, mStage.data(), 2, width, height, width) != ORBGPU_OK) return -1;
     mFrameW = width;
     mFrameH = height;
-    if (orbgpu_run_batch(mCtx, 2, width, height, laps, nullptr) != ORBGPU_OK) return -1;
-    if (orbgpu_match_stereo_batch(mCtx, 1, 1, nullptr) != ORBGPU_OK) return -1;
+    if (orbgpu_run_batch_match(mCtx, 2, width, height, laps, 1, nullptr) != ORBGPU_OK) return -1;
     return finish(nl, nr, kl, kr, dl, dr, monoLeft, monoRight);
 }
 

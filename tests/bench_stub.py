@@ -47,6 +47,10 @@ class BatchExtractor:
     def match_stereo(self, stereo_rows_only=False, stream=None):
         pass
 
+    def run_match(self, laps=None, stereo_rows_only=False, stream=None):
+        self.run(laps, stream)
+        self.match_stereo(stereo_rows_only, stream)
+
     def synchronize(self):
         pass
 

@@ -109,6 +109,38 @@ def test_batch_path_matches_oracle(oracle):
             np.testing.assert_array_equal(a, b)
 
 
+@pytest.mark.parametrize("pairs,rows_only", [(1, True), (1, False), (3, False)])
+def test_run_batch_match_one_submission(oracle, pairs, rows_only):
+    """orbgpu_run_batch_match: one pair runs extraction + kNN2 as ONE captured graph (replayed for
+    the next frames, the graph keyed on the match too); three pairs take the chunked path (the two
+    calls).  Keypoints, descriptors and every pair's kNN2 (all rows or the stereo rows [mono, n)
+    of both eyes, Frame.cc:1142-1148) against the oracle, over three different frames."""
+    import orbslam3lib_amd as og
+    be = og.BatchExtractor(2000, 1.2, 8, 20, 7, width=640, height=480, max_images=2 * pairs)
+    laps = np.array([[0, 0], [60, 600]] * pairs if not rows_only else [[120, 640], [0, 520]] * pairs, np.int32)
+    for f in range(3):
+        imgs = synth.stereo_batch(480, 640, pairs, first=20 + 7 * f)
+        be.upload(imgs)
+        be.run_match(laps=laps, stereo_rows_only=rows_only)
+        be.synchronize()
+        res = [be.result(i) for i in range(2 * pairs)]
+        for i in range(2 * pairs):
+            rk, rd, rm = oracle.extract(imgs[i], nfeatures=2000, lap=tuple(laps[i]))
+            k, d, m = res[i]
+            assert m == rm
+            _same_kps(k, rk)
+            np.testing.assert_array_equal(d, rd)
+        for p in range(pairs):
+            _, ql, ml = res[2 * p]
+            _, tr, mr = res[2 * p + 1]
+            q, t = (ql[ml:], tr[mr:]) if rows_only else (ql, tr)
+            assert len(q) > 0 and len(t) > 0
+            r = oracle.knn2(q, t)
+            got = be.matches(p)
+            for a, b in zip(got, r):
+                np.testing.assert_array_equal(a, b)
+
+
 def test_knn2_ties_and_edges(oracle):
     import orbslam3lib_amd as og
     ex = _extractor()

@@ -5,7 +5,7 @@ cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
 O=${1:-gpurun_out/c4}
 mkdir -p $O
-PAIRS=1 STEPS=30 timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $O -o run -- python3 tools/profile_batch.py > $O/log.txt 2>&1 || { tail $O/log.txt; exit 1; }
+STEPS=30 timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $O -o run -- python3 tools/c4_run.py > $O/log.txt 2>&1 || { tail $O/log.txt; exit 1; }
 python3 - $O <<'PY'
 import csv, glob, sys
 rows = list(csv.DictReader(open(glob.glob(sys.argv[1] + "/**/run_kernel_trace.csv", recursive=True)[0])))
