@@ -143,7 +143,18 @@ def dist_setup():
             torch.cuda.set_device(local)
         else:
             local = int(os.environ.get("ORBGPU_BENCH_DEVICE", local % max(ndev, 1)))
-        td.init_process_group(backend=backend)
+        # the process group's own connection messages (gloo prints to stdout) go to stderr:
+        # rank 0's stdout carries exactly one line, the JSON result
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            td.init_process_group(backend=backend)
+            td.barrier()
+        finally:
+            sys.stdout.flush()
+            os.dup2(saved, 1)
+            os.close(saved)
         dist = td
     return world, rank, local, dist
 

@@ -22,8 +22,9 @@ def _run_bench(n, extra=()):
            "--no-stereo", "--no-grid", "--no-wire", "--no-sbp", "--no-configs", "--no-cpu-baseline"] + list(extra)
     out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
     assert out.returncode == 0, out.stderr[-3000:]
-    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
-    assert len(lines) == 1, out.stdout[-2000:]  # rank 0 alone prints
+    lines = [l for l in out.stdout.splitlines() if l.strip()]
+    # rank 0 alone prints, and only the JSON line (gloo's connection messages go to stderr)
+    assert len(lines) == 1 and lines[0].startswith("{"), out.stdout[-2000:]
     return json.loads(lines[0])
 
 
