@@ -9,10 +9,10 @@
 // kCellMax = 80 otherwise).  On the GPU one wave runs one cell (no workgroup barriers); the
 // code also accepts several waves per cell: each wave owns one contiguous row-major range of
 // detection pixels and keeps a private candidate list, so the wave lists concatenated in wave
-// order are row-major and ordered output needs only a prefix over waves.  Per threshold t: (1) compass pre-test on 64 pixels at a time, evaluated as lane
-// masks (eight compares, the rest is scalar mask logic), compacted into the wave list;
-// (2) the exact segment test on the compacted list (both polarities in one word per ring
-// point, 9-arcs by OR-of-3 trees); (3) exact strength m (orb_math.h) for the corners.
+// order are row-major and ordered output needs only a prefix over waves.  Per threshold t:
+// (1) the antipodal-pair pre-test (fw_pretest4) on 4 pixels per lane, passing pixels compacted
+// into the wave list; (2) the exact strength m (orb_math.h fast_strength_packed) of every
+// candidate, m > t being the segment test itself; (3) the 3x3 nonmax over the corners.
 // Policy-templated like orb_octree.h so the host harness runs the same code on the CPU.
 #pragma once
 #include <hip/hip_runtime.h>
@@ -55,27 +55,40 @@ typedef unsigned short fw_u16x2 __attribute__((ext_vector_type(2)));
 __device__ inline fw_u16x2 fw_as16(uint32_t x) { return __builtin_bit_cast(fw_u16x2, x); }
 __device__ inline uint32_t fw_as32(fw_u16x2 x) { return __builtin_bit_cast(uint32_t, x); }
 
-// Compass pre-test of the 4 pixels of LDS dword C (Cm / Cp: the dwords left and right of it,
-// U / D: the dwords 3 rows up / down), device only: bit k set when pixel k has two cyclically
-// adjacent compass points of {0, 4, 8, 12} beyond threshold t (tt = t in both u16 halves) on the
-// same side -- one of {0,8} and one of {4,12} darker than v-t, or both brighter than v+t.  The
-// pixels go through packed u16 arithmetic in pairs (0, 2) and (1, 3) built with v_perm.
-__device__ inline uint32_t fw_compass4(uint32_t C, uint32_t Cm, uint32_t Cp, uint32_t U, uint32_t D,
-                                       uint32_t tt) {
-    const uint32_t Lf = __builtin_amdgcn_alignbyte(C, Cm, 1);  // pixels x-3 (ring 12)
-    const uint32_t Rt = __builtin_amdgcn_alignbyte(Cp, C, 3);  // pixels x+3 (ring 4)
+// Pre-test of the 4 pixels of LDS dword C, device only: bit k set when, for each of the four
+// antipodal pairs of ring points {0,8}, {2,10}, {4,12}, {6,14}, one point of the pair is darker
+// than v-t (or, for all four pairs, one point is brighter than v+t).  Any 9-arc of the 16-point
+// ring holds one point of every antipodal pair, so a FAST corner at t passes (a necessary
+// condition; the exact strength decides).  On the SURVEY 8d frames 26% of the detection pixels
+// pass at iniThFAST (the 4-point compass {0,8} x {4,12} of rounds 1-3 passed 43%; corners 14%).
+// Inputs: row 0 (C and the dwords left / right of it: Cm, Cp), rows -3 / +3 (U3, D3: the same
+// column only), rows -2 / +2 with both neighbours (U2m, U2, U2p; D2m, D2, D2p).  The pixels go
+// through packed 16-bit arithmetic in pairs (0, 2) and (1, 3) built with v_perm; the high byte
+// of every half is 0x04, so each half is a normal f16 of one exponent and the gfx950 3-input
+// v_pk_maximum3_f16 / v_pk_minimum3_f16 order them as integers (orb_math.h pk_max3).
+__device__ inline uint32_t fw_pretest4(uint32_t C, uint32_t Cm, uint32_t Cp, uint32_t U3, uint32_t D3,
+                                       uint32_t U2m, uint32_t U2, uint32_t U2p, uint32_t D2m, uint32_t D2,
+                                       uint32_t D2p, uint32_t tt) {
+    const uint32_t K = 0x04040404u;
+    const uint32_t L3 = __builtin_amdgcn_alignbyte(C, Cm, 1);    // (-3, 0): ring 12
+    const uint32_t R3 = __builtin_amdgcn_alignbyte(Cp, C, 3);    // (+3, 0): ring 4
+    const uint32_t UL = __builtin_amdgcn_alignbyte(U2, U2m, 2);  // (-2, -2): ring 10
+    const uint32_t UR = __builtin_amdgcn_alignbyte(U2p, U2, 2);  // (+2, -2): ring 6
+    const uint32_t DL = __builtin_amdgcn_alignbyte(D2, D2m, 2);  // (-2, +2): ring 14
+    const uint32_t DR = __builtin_amdgcn_alignbyte(D2p, D2, 2);  // (+2, +2): ring 2
     const fw_u16x2 T2 = fw_as16(tt);
     auto test = [&](uint32_t sel) {
-        const fw_u16x2 v = fw_as16(__builtin_amdgcn_perm(0u, C, sel));
-        const fw_u16x2 p0 = fw_as16(__builtin_amdgcn_perm(0u, D, sel));    // ring 0: (0, +3)
-        const fw_u16x2 p8 = fw_as16(__builtin_amdgcn_perm(0u, U, sel));    // ring 8: (0, -3)
-        const fw_u16x2 p4 = fw_as16(__builtin_amdgcn_perm(0u, Rt, sel));   // ring 4: (+3, 0)
-        const fw_u16x2 p12 = fw_as16(__builtin_amdgcn_perm(0u, Lf, sel));  // ring 12: (-3, 0)
+        auto px = [&](uint32_t x) { return fw_as16(__builtin_amdgcn_perm(K, x, sel)); };
+        const fw_u16x2 v = px(C);
+        const fw_u16x2 p0 = px(D3), p8 = px(U3), p4 = px(R3), p12 = px(L3);
+        const fw_u16x2 p2 = px(DR), p10 = px(UL), p6 = px(UR), p14 = px(DL);
         const fw_u16x2 lo = __builtin_elementwise_sub_sat(v, T2), hi = v + T2;
-        const fw_u16x2 dk = __builtin_elementwise_max(__builtin_elementwise_min(p0, p8),
-                                                      __builtin_elementwise_min(p4, p12));
-        const fw_u16x2 bk = __builtin_elementwise_min(__builtin_elementwise_max(p0, p8),
-                                                      __builtin_elementwise_max(p4, p12));
+        const fw_u16x2 dk = pk_max3(__builtin_elementwise_min(p0, p8), __builtin_elementwise_min(p4, p12),
+                                    __builtin_elementwise_max(__builtin_elementwise_min(p2, p10),
+                                                              __builtin_elementwise_min(p6, p14)));
+        const fw_u16x2 bk = pk_min3(__builtin_elementwise_max(p0, p8), __builtin_elementwise_max(p4, p12),
+                                    __builtin_elementwise_min(__builtin_elementwise_max(p2, p10),
+                                                              __builtin_elementwise_max(p6, p14)));
         // dk < v - t  <=>  sat(lo - dk) > 0;   bk > v + t  <=>  sat(bk - hi) > 0
         const fw_u16x2 r = __builtin_elementwise_sub_sat(lo, dk) | __builtin_elementwise_sub_sat(bk, hi);
         // min(r, 1) per half as one v_pk_min_u16 (left to itself the compiler rewrites it as two
@@ -85,7 +98,7 @@ __device__ inline uint32_t fw_compass4(uint32_t C, uint32_t Cm, uint32_t Cp, uin
         asm("v_pk_min_u16 %0, %1, %2" : "=v"(one) : "v"(fw_as32(r)), "s"(0x00010001u));
         return one;
     };
-    const uint32_t e = test(0x0c020c00u), o = test(0x0c030c01u);  // pixels (0, 2) and (1, 3)
+    const uint32_t e = test(0x04020400u), o = test(0x04030401u);  // pixels (0, 2) and (1, 3)
     const uint32_t comb = e | (o << 1);                           // halves: p0 | p1 << 1, p2 | p3 << 1
     return (comb & 3u) | ((comb >> 14) & 0xCu);
 }
@@ -163,7 +176,7 @@ __host__ __device__ int fast_cell_detect(Pol& p, int sh, const CellGeom& g, int 
     const int W = p.nwaves(), w = p.wave(), L = p.wave_width(), lane = p.lane();
     const uint64_t lt = p.lanemask_lt();
 #if defined(__HIP_DEVICE_COMPILE__)
-    // device: the pre-test takes 4 pixels per lane (fw_compass4); a wave owns a contiguous
+    // device: the pre-test takes 4 pixels per lane (fw_pretest4); a wave owns a contiguous
     // row-major range of (row, dword group) items, and its list starts after the detection
     // pixels of the items before it
     const int xs = 3 + sh, xe = 3 + sh + dc;
@@ -208,17 +221,34 @@ __host__ __device__ int fast_cell_detect(Pol& p, int sh, const CellGeom& g, int 
                 return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32),
                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
             };
+            // this lane's item (row r, dword group q) as (q, LDS dword dw), advanced by L items
+            // per iteration without a division: L = dr rows + dq groups (plus one row on wrap)
+            int q = 0, dw = 0, dq = 0, ddw = 0;
+            if (ng > 0) {
+                const int i = j0 + lane;
+                const int r = (int)(((float)i + 0.5f) * inv_ng);  // exact: i < 69 * 19 + 64
+                q = i - r * ng;
+                dw = (r + 3) * RW + g0 + q;
+                const int dr = (int)(((float)L + 0.5f) * inv_ng);
+                dq = L - dr * ng;
+                ddw = dr * RW + dq;
+            }
             for (int base = j0; base < j1; base += L) {
                 const int i = base + lane;
                 uint32_t m4 = 0;
                 int o = 0;
                 if (i < j1) {
-                    const int r = (int)(((float)i + 0.5f) * inv_ng);  // exact: i < 69 * 19
-                    const int q = i - r * ng;
-                    const int dw = (r + 3) * RW + g0 + q;
-                    m4 = fw_compass4(T32[dw], T32[dw - 1], T32[dw + 1], T32[dw - 3 * RW], T32[dw + 3 * RW], tt);
+                    m4 = fw_pretest4(T32[dw], T32[dw - 1], T32[dw + 1], T32[dw - 3 * RW], T32[dw + 3 * RW],
+                                     T32[dw - 2 * RW - 1], T32[dw - 2 * RW], T32[dw - 2 * RW + 1],
+                                     T32[dw + 2 * RW - 1], T32[dw + 2 * RW], T32[dw + 2 * RW + 1], tt);
                     m4 &= (q == 0 ? first4 : 0xFu) & (q == ng - 1 ? last4 : 0xFu);
                     o = 4 * dw;
+                }
+                q += dq;
+                dw += ddw;
+                if (q >= ng) {
+                    q -= ng;
+                    dw += RW - ng;
                 }
                 const int c = __builtin_popcount(m4);
                 const uint64_t b0 = p.ballot(c & 1), b1 = p.ballot(c & 2), b2 = p.ballot(c & 4);
@@ -245,9 +275,11 @@ __host__ __device__ int fast_cell_detect(Pol& p, int sh, const CellGeom& g, int 
             const uint8_t* c = &T[o];
             const int v = c[0], lo = v - t, hi = v + t;
             const int p0 = c[3 * CP], p4 = c[3], p8 = c[-3 * CP], p12 = c[-3];
-            // compass pre-test: two cyclically adjacent of {0,4,8,12} beyond t on one side <=>
-            // one of {0,8} and one of {4,12} beyond it <=> a min/max over the opposite pairs
-            const int dk = imax(imin(p0, p8), imin(p4, p12)), bk = imin(imax(p0, p8), imax(p4, p12));
+            const int p2 = c[2 + 2 * CP], p6 = c[2 - 2 * CP], p10 = c[-2 - 2 * CP], p14 = c[-2 + 2 * CP];
+            // the device's pre-test (fw_pretest4): for each antipodal pair {0,8}, {2,10}, {4,12},
+            // {6,14} one point beyond t on the same side <=> a min/max over the pairs
+            const int dk = imax(imax(imin(p0, p8), imin(p4, p12)), imax(imin(p2, p10), imin(p6, p14)));
+            const int bk = imin(imin(imax(p0, p8), imax(p4, p12)), imin(imax(p2, p10), imax(p6, p14)));
             const bool cand = in & ((dk < lo) | (bk > hi));
             const uint64_t m = p.ballot(cand);
             if (cand) list[na + p.popc64(m & lt)] = (uint16_t)o;

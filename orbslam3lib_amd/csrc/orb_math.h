@@ -297,15 +297,46 @@ __host__ __device__ inline int fast_strength_corner(const uint8_t* c, int stride
 }
 
 // The same strength with both polarities in one 32-bit word per ring point: low half
-// d + 256, high half -d + 256 (d = v - p, both halves in [1, 511], so one v_mad_u32_u24
-// builds the word), then 9-arc minima and the maximum over arcs with packed u16 min/max:
-// low = sdark + 256, high = -bmin + 256.  Exact for any pixel; m > t <=> FAST corner at t.
+// d + kFastBias, high half -d + kFastBias (d = v - p; both halves in [0x401, 0x5FF], so one
+// v_mad_u32_u24 builds the word), then 9-arc minima and the maximum over arcs with packed
+// 16-bit min/max: low = sdark + kFastBias, high = -bmin + kFastBias.  Exact for any pixel;
+// m > t <=> FAST corner at t.  The bias puts every half in the normal f16 range with one
+// exponent (0x0400 <= h <= 0x7BFF), where the f16 order of the bit patterns is their integer
+// order, so the 3-input gfx950 v_pk_minimum3_f16 / v_pk_maximum3_f16 are exact integer
+// min3 / max3 on them.
 typedef unsigned short orb_u16x2 __attribute__((ext_vector_type(2)));
+constexpr int kFastBias = 1280;  // 0x500
+
+__host__ __device__ inline orb_u16x2 pk_min3(orb_u16x2 a, orb_u16x2 b, orb_u16x2 c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    uint32_t r;
+    asm("v_pk_minimum3_f16 %0, %1, %2, %3"
+        : "=v"(r)
+        : "v"(__builtin_bit_cast(uint32_t, a)), "v"(__builtin_bit_cast(uint32_t, b)),
+          "v"(__builtin_bit_cast(uint32_t, c)));
+    return __builtin_bit_cast(orb_u16x2, r);
+#else
+    return __builtin_elementwise_min(__builtin_elementwise_min(a, b), c);
+#endif
+}
+
+__host__ __device__ inline orb_u16x2 pk_max3(orb_u16x2 a, orb_u16x2 b, orb_u16x2 c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    uint32_t r;
+    asm("v_pk_maximum3_f16 %0, %1, %2, %3"
+        : "=v"(r)
+        : "v"(__builtin_bit_cast(uint32_t, a)), "v"(__builtin_bit_cast(uint32_t, b)),
+          "v"(__builtin_bit_cast(uint32_t, c)));
+    return __builtin_bit_cast(orb_u16x2, r);
+#else
+    return __builtin_elementwise_max(__builtin_elementwise_max(a, b), c);
+#endif
+}
 
 template <int STRIDE>
 __host__ __device__ inline int fast_strength_packed(const uint8_t* c) {
     const int v = c[0];
-    const uint32_t cv = (uint32_t)(v + 256) + ((uint32_t)(256 - v) << 16);
+    const uint32_t cv = (uint32_t)(v + kFastBias) + ((uint32_t)(kFastBias - v) << 16);
     orb_u16x2 x[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
@@ -313,26 +344,21 @@ __host__ __device__ inline int fast_strength_packed(const uint8_t* c) {
         x[k] = __builtin_bit_cast(orb_u16x2, p * 65535u + cv);
     }
     // The 16 arcs pair up: arcs [2j, 2j+8] and [2j+1, 2j+9] share the 8 points [2j+1, 2j+8],
-    // so max(min(arc 2j), min(arc 2j+1)) = min(a8[2j+1], max(x[2j], x[2j+9])).  Only the
-    // odd-start minima a2/a4/a8 are needed: 8+8+8 mins, 8 max + 8 min for the pairs, 7 max over
-    // the pairs = 47 packed ops (79 for the 16 arcs taken one by one).
-    orb_u16x2 a2[8], a4[8], a8[8], pr[8];
+    // so max(min(arc 2j), min(arc 2j+1)) = min(a8[2j+1], max(x[2j], x[2j+9])), and
+    // a8[2j+1] = min(a4[j], a4[j+2]) with a4[j] = min over [2j+1, 2j+4]: 8 + 8 two-input mins,
+    // 8 max + 8 min3 for the pairs, 4 max3/max over the pairs = 36 packed ops (47 with
+    // two-input ops only, 79 for the 16 arcs taken one by one).
+    orb_u16x2 a2[8], a4[8], pr[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) a2[j] = __builtin_elementwise_min(x[2 * j + 1], x[(2 * j + 2) & 15]);
 #pragma unroll
     for (int j = 0; j < 8; ++j) a4[j] = __builtin_elementwise_min(a2[j], a2[(j + 1) & 7]);   // [2j+1, 2j+4]
 #pragma unroll
-    for (int j = 0; j < 8; ++j) a8[j] = __builtin_elementwise_min(a4[j], a4[(j + 2) & 7]);   // [2j+1, 2j+8]
-#pragma unroll
     for (int j = 0; j < 8; ++j)
-        pr[j] = __builtin_elementwise_min(a8[j], __builtin_elementwise_max(x[2 * j], x[(2 * j + 9) & 15]));
-    // max over the 8 arc pairs as a tree: independent packed ops, no dependent back-to-back chain
-#pragma unroll
-    for (int w = 4; w >= 1; w >>= 1)
-#pragma unroll
-        for (int k = 0; k < w; ++k) pr[k] = __builtin_elementwise_max(pr[k], pr[k + w]);
-    const orb_u16x2 best = pr[0];
-    int s = (int)(best.x > best.y ? best.x : best.y) - 256;
+        pr[j] = pk_min3(a4[j], a4[(j + 2) & 7], __builtin_elementwise_max(x[2 * j], x[(2 * j + 9) & 15]));
+    const orb_u16x2 best = __builtin_elementwise_max(pk_max3(pr[0], pr[1], pr[2]),
+                                                     pk_max3(pr[3], pr[4], pk_max3(pr[5], pr[6], pr[7])));
+    int s = (int)(best.x > best.y ? best.x : best.y) - kFastBias;
     s = s < 0 ? 0 : s;
     return s > 255 ? 255 : s;
 }
