@@ -15,6 +15,9 @@
 // candidate, m > t being the segment test itself; (3) the 3x3 nonmax over the corners.
 // Policy-templated like orb_octree.h so the host harness runs the same code on the CPU.
 #pragma once
+#ifndef FAST_VAR
+#define FAST_VAR 0
+#endif
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -107,10 +110,41 @@ __device__ inline uint32_t fw_pretest4(uint32_t C, uint32_t Cm, uint32_t Cp, uin
 struct CellScratch {
     uint8_t* T;        // [P * P], 4-byte aligned
     uint8_t* M;        // [P * P], 4-byte aligned
-    uint16_t* list;    // [cell_list_cap<P>() + 1] wave-private candidate lists (offsets into
-                       // T/M) and a sink entry
+    uint16_t* list;    // [cell_list_cap<P>() + fast_list_slack(waves)] wave-private candidate
+                       // lists (offsets into T/M) and the sink entries
     int32_t* wcnt;     // [waves]
+    // device only (fast_cell_tables): per 4-bit pre-test mask, the positions of its set bits as
+    // u16 pairs (p0 | p1 << 16, p2 | p3 << 16), and the detection-pixel mask of each dword group
+    const uint2* lut = nullptr;  // [16]
+    const uint8_t* emask = nullptr;  // [ng <= 20]
 };
+
+// List entries past cell_list_cap on the device: each wave's list is followed by 4 spare
+// entries (the compaction writes 4 slots per lane, the ones past the lane's candidates are
+// overwritten by later lanes or land in the spare entries), then 4 sink entries.
+__host__ __device__ constexpr int fast_list_slack(int waves) { return 4 * waves + 4; }
+
+// Builds CellScratch's lut / emask tables (threads < 16 and < ng); the caller syncs before
+// fast_cell_detect.
+template <int CP>
+__device__ inline void fast_cell_tables(const CellGeom& g, int sh, uint2* lut, uint8_t* emask) {
+    const int tid = threadIdx.x;
+    if (tid < 16) {
+        int pos[4] = {0, 0, 0, 0}, n = 0;
+        for (int k = 0; k < 4; ++k)
+            if ((tid >> k) & 1) pos[n++] = k;
+        lut[tid] = make_uint2((uint32_t)pos[0] | ((uint32_t)pos[1] << 16), (uint32_t)pos[2] | ((uint32_t)pos[3] << 16));
+    }
+    const int dc = g.cols - 6 > 0 ? g.cols - 6 : 0;
+    const int xs = 3 + sh, xe = 3 + sh + dc;
+    const int g0 = xs >> 2;
+    const int ng = dc > 0 ? ((xe - 1) >> 2) - g0 + 1 : 0;
+    if (tid < ng) {
+        const uint32_t first4 = 0xFu & ~((1u << (xs - 4 * g0)) - 1u);
+        const uint32_t last4 = (1u << (xe - 4 * (g0 + ng - 1))) - 1u;
+        emask[tid] = (uint8_t)((tid == 0 ? first4 : 0xFu) & (tid == ng - 1 ? last4 : 0xFu));
+    }
+}
 
 // Stages the cell ROI in LDS (T) and clears the strength plane (M); the caller syncs.
 template <int CP, class Pol, class Ld16>
@@ -196,9 +230,12 @@ __host__ __device__ int fast_cell_detect(Pol& p, int sh, const CellGeom& g, int 
 #else
     const int i0 = w * nd / W, i1 = (w + 1) * nd / W;  // nd <= 4900, W <= 16: no overflow
 #endif
+#if defined(__HIP_DEVICE_COMPILE__)
+    uint16_t* list = cs.list + i0 + 4 * w;  // 4 spare entries after each wave's list
+    uint16_t* sink = cs.list + cell_list_cap<CP>() + 4 * W;  // 4 entries (fast_list_slack)
+#else
     uint16_t* list = cs.list + i0;
-    uint16_t* sink = cs.list + cell_list_cap<CP>();  // one entry past the list (CellScratch)
-    (void)sink;
+#endif
 #if !defined(__HIP_DEVICE_COMPILE__)
     const float inv_dc = dc > 0 ? 1.f / (float)dc : 0.f;
     auto off_of = [&](int i) {
@@ -214,9 +251,6 @@ __host__ __device__ int fast_cell_detect(Pol& p, int sh, const CellGeom& g, int 
             constexpr int RW = CP / 4;
             const uint32_t* T32 = reinterpret_cast<const uint32_t*>(T);
             const uint32_t tt = (uint32_t)t * 0x00010001u;
-            // detection pixels of the first / last dword group of a row (wave-uniform masks)
-            const uint32_t first4 = 0xFu & ~((1u << (xs - 4 * g0)) - 1u);
-            const uint32_t last4 = (1u << (xe - 4 * (g0 + ng - 1))) - 1u;
             auto rank = [](uint64_t b) {  // set lanes of b below this lane
                 return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32),
                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
@@ -236,32 +270,38 @@ __host__ __device__ int fast_cell_detect(Pol& p, int sh, const CellGeom& g, int 
             for (int base = j0; base < j1; base += L) {
                 const int i = base + lane;
                 uint32_t m4 = 0;
-                int o = 0;
                 if (i < j1) {
                     m4 = fw_pretest4(T32[dw], T32[dw - 1], T32[dw + 1], T32[dw - 3 * RW], T32[dw + 3 * RW],
                                      T32[dw - 2 * RW - 1], T32[dw - 2 * RW], T32[dw - 2 * RW + 1],
                                      T32[dw + 2 * RW - 1], T32[dw + 2 * RW], T32[dw + 2 * RW + 1], tt);
-                    m4 &= (q == 0 ? first4 : 0xFu) & (q == ng - 1 ? last4 : 0xFu);
-                    o = 4 * dw;
+                    m4 &= cs.emask[q];  // detection pixels of the row's first / last group
                 }
+                const int c = __builtin_popcount(m4);
+                const uint64_t b0 = p.ballot(c & 1), b1 = p.ballot(c & 2), b2 = p.ballot(c & 4);
+                const int pos = na + rank(b0) + 2 * rank(b1) + 4 * rank(b2);
+                // the lane's c entries 4 dw + (set bit positions), as u16 pairs from the table,
+                // written to 4 consecutive slots from pos; slots past c hold garbage that a later
+                // lane's entry overwrites (its slot index k is smaller, and the slots are written
+                // in the order k = 3, 2, 1, 0) or that lands in the wave's spare entries; lanes
+                // without candidates write the sink
+                const uint2 lv = cs.lut[m4];
+                const uint32_t e01 = __umul24((uint32_t)(4 * dw), 0x10001u) + lv.x;  // v_mad_u32_u24
+                const uint32_t e23 = __umul24((uint32_t)(4 * dw), 0x10001u) + lv.y;
+                uint16_t* d = c ? list + pos : sink;
+                d[3] = (uint16_t)(e23 >> 16);
+                asm volatile("" ::: "memory");  // keep the slot order (k = 3 .. 0)
+                d[2] = (uint16_t)e23;
+                asm volatile("" ::: "memory");
+                d[1] = (uint16_t)(e01 >> 16);
+                asm volatile("" ::: "memory");
+                d[0] = (uint16_t)e01;
+                na += p.popc64(b0) + 2 * p.popc64(b1) + 4 * p.popc64(b2);
                 q += dq;
                 dw += ddw;
                 if (q >= ng) {
                     q -= ng;
                     dw += RW - ng;
                 }
-                const int c = __builtin_popcount(m4);
-                const uint64_t b0 = p.ballot(c & 1), b1 = p.ballot(c & 2), b2 = p.ballot(c & 4);
-                int pos = na + rank(b0) + 2 * rank(b1) + 4 * rank(b2);
-                // unconditional stores: a lane's slots past its candidates go to the sink entry
-                // after the list (no exec-mask juggling per pixel)
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const bool on = (m4 >> k) & 1u;
-                    *(on ? list + pos : sink) = (uint16_t)(o + k);
-                    pos += on ? 1 : 0;
-                }
-                na += p.popc64(b0) + 2 * p.popc64(b1) + 4 * p.popc64(b2);
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the list is read by other lanes
             __builtin_amdgcn_wave_barrier();
@@ -295,7 +335,11 @@ __host__ __device__ int fast_cell_detect(Pol& p, int sh, const CellGeom& g, int 
             const int j = base + lane;
             const int o = o_next;
             if (base + L < na) o_next = list[base + L + lane < na ? base + L + lane : na - 1];
+#if FAST_VAR == 1  // measurement variant: every candidate a corner of strength t + 1
+            const int sm = t + 1;
+#else
             const int sm = fast_strength_packed<CP>(&T[o]);
+#endif
             const bool f = j < na && sm > t;
             const uint64_t m = p.ballot(f);
             if (f) {

@@ -11,6 +11,9 @@
 //   k_orient_desc x 1      32 lanes per keypoint: IC_Angle + rBRIEF 256 bit
 //   k_finalize    x 1      one workgroup per image: scale + mono/stereo partition
 //   k_knn2_mfma   x 1      Hamming k=2 brute force on the i8 matrix cores
+#ifndef BR_VAR
+#define BR_VAR 0
+#endif
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -91,13 +94,22 @@ __device__ inline uint32_t as_u32(u16x2 x) { return __builtin_bit_cast(uint32_t,
 // indexed by source column).  The quad's taps lie in the 8 source bytes from its first left tap
 // `base` (scale <= 2: the last right tap is at most base + 7), read as three aligned dwords per
 // row and byte-aligned with v_alignbyte; sel[k] picks output k's two taps as a u16 pair (v_perm)
-// and cw[k] holds its two x coefficients as a u16 pair, so each horizontal sum is one
-// v_dot2_u32_u16 (exact: taps <= 255, coefficients <= 2048).  Vertical rounding: OpenCV's SIMD
-// body below simd_end, FixedPtCast after it (only the last quads of a row take that branch);
-// every product fits 24 bits (D < 2^19, b <= 2048), so all multiplies are full-rate
-// v_mul_u32_u24.
-__device__ inline uint32_t rs_quad(const uint8_t* r0, const uint8_t* r1, int base, int4 sel, int4 cw, int b0,
-                                   int b1, int dx0, int simd_end) {
+// and cw[k] holds its two x coefficients times 16 as a u16 pair (16 c <= 32768), so each
+// horizontal sum is one v_dot2_u32_u16 yielding 16 D (exact: < 2^23).  Vertical rounding:
+// OpenCV's SIMD body (VResizeLinearVec_32s8u) below simd_end,
+//   out = (((D0 >> 4) b0 >> 16) + ((D1 >> 4) b1 >> 16) + 2) >> 2,
+// where (D >> 4) << 8 = 16 D & ~0xFF and the row weights come as b << 8 (B0 / B1 <= 2^19), so
+// each ((D >> 4) b) >> 16 is one v_mul_hi_u32_u24 of two 24-bit operands (the 48-bit product
+// >> 32); the sum is <= 1022 (c0 + c1 = b0 + b1 = 2048), so no clamp is needed.  FixedPtCast
+// after simd_end (only the last quads of a row take that branch).
+// (a * b) >> 32 for 24-bit a, b: one v_mul_hi_u32_u24 (the masks tell the compiler the operand
+// widths; both are no-ops on rs_quad's operands)
+__device__ inline uint32_t mulhi_u24(uint32_t a, uint32_t b) {
+    return (uint32_t)(((uint64_t)(a & 0xFFFFFFu) * (uint64_t)(b & 0xFFFFFFu)) >> 32);
+}
+
+__device__ inline uint32_t rs_quad(const uint8_t* r0, const uint8_t* r1, int base, int4 sel, int4 cw, int B0,
+                                   int B1, int dx0, int simd_end) {
     const uint32_t* p0 = reinterpret_cast<const uint32_t*>(r0 + (base & ~3));
     const uint32_t* p1 = reinterpret_cast<const uint32_t*>(r1 + (base & ~3));
     const uint32_t sh = (uint32_t)(base & 3);
@@ -107,36 +119,30 @@ __device__ inline uint32_t rs_quad(const uint8_t* r0, const uint8_t* r1, int bas
     const uint32_t lo1 = __builtin_amdgcn_alignbyte(c1, c0, sh), hi1 = __builtin_amdgcn_alignbyte(c2, c1, sh);
     const int sl[4] = {sel.x, sel.y, sel.z, sel.w};
     const int cl[4] = {cw.x, cw.y, cw.z, cw.w};
-    int D0[4], D1[4];
+    uint32_t D0[4], D1[4];  // 16 D
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const uint32_t t0 = __builtin_amdgcn_perm(hi0, lo0, (uint32_t)sl[k]);
         const uint32_t t1 = __builtin_amdgcn_perm(hi1, lo1, (uint32_t)sl[k]);
-        D0[k] = (int)__builtin_amdgcn_udot2(as_u16x2(t0), as_u16x2((uint32_t)cl[k]), 0u, false);
-        D1[k] = (int)__builtin_amdgcn_udot2(as_u16x2(t1), as_u16x2((uint32_t)cl[k]), 0u, false);
+        D0[k] = __builtin_amdgcn_udot2(as_u16x2(t0), as_u16x2((uint32_t)cl[k]), 0u, false);
+        D1[k] = __builtin_amdgcn_udot2(as_u16x2(t1), as_u16x2((uint32_t)cl[k]), 0u, false);
     }
-    uint32_t packed = 0;
-    if (dx0 + 3 < simd_end) {
+    uint32_t o[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        o[k] = (mulhi_u24(D0[k] & 0x7FFF00u, (uint32_t)B0) + mulhi_u24(D1[k] & 0x7FFF00u, (uint32_t)B1) + 2u) >> 2;
+    if (dx0 + 3 >= simd_end) {
+        const unsigned b0 = (unsigned)B0 >> 8, b1 = (unsigned)B1 >> 8;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            const int sv = (__umul24(D0[k] >> 4, b0) >> 16) + (__umul24(D1[k] >> 4, b1) >> 16);
-            packed |= (uint32_t)min((sv + 2) >> 2, 255) << (8 * k);
-        }
-    } else {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            int o;
-            if (dx0 + k < simd_end) {
-                const int sv = (__umul24(D0[k] >> 4, b0) >> 16) + (__umul24(D1[k] >> 4, b1) >> 16);
-                o = (sv + 2) >> 2;
-            } else {
+            if (dx0 + k >= simd_end) {
                 // D < 2^19, b <= 2048: both 24-bit, products < 2^30 (full-rate multiplies)
-                o = (int)((__umul24((unsigned)D0[k], (unsigned)b0) + __umul24((unsigned)D1[k], (unsigned)b1) + (1u << 21)) >> 22);
+                const uint32_t v = (__umul24(D0[k] >> 4, b0) + __umul24(D1[k] >> 4, b1) + (1u << 21)) >> 22;
+                o[k] = v < 255u ? v : 255u;
             }
-            packed |= (uint32_t)min(o, 255) << (8 * k);
         }
     }
-    return packed;
+    return o[0] | (o[1] << 8) | (o[2] << 16) | (o[3] << 24);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -402,13 +408,16 @@ __device__ inline void br_tile(const BatchArgs& a, int l, bool resize, int img, 
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {  // taps relative to base: 0 .. 7 (scale <= 2)
                     sl[k] = (x[k].x - base) | 0x0c00 | ((x[k].y - base) << 16) | 0x0c000000;
-                    cl[k] = x[k].z | (x[k].w << 16);
+                    cl[k] = (x[k].z << 4) | (x[k].w << 20);  // 16 c (rs_quad)
                 }
                 sm.xsel[q] = make_int4(sl[0], sl[1], sl[2], sl[3]);
                 sm.xcw[q] = make_int4(cl[0], cl[1], cl[2], cl[3]);
                 sm.xbase[q] = base;
             }
-            if (threadIdx.x < nr) sm.yts[threadIdx.x] = a.rtab[G.ytab_off + r0 + threadIdx.x];
+            if (threadIdx.x < nr) {  // (y0, y1, b0 << 8, b1 << 8): rs_quad's v_mul_hi_u32_u24 operands
+                const int4 y = a.rtab[G.ytab_off + r0 + threadIdx.x];
+                sm.yts[threadIdx.x] = make_int4(y.x, y.y, y.z << 8, y.w << 8);
+            }
         }
     }
 #pragma unroll
@@ -417,7 +426,12 @@ __device__ inline void br_tile(const BatchArgs& a, int l, bool resize, int img, 
         if (i < IH * IWQ) (&sm.tin4[0][0])[i] = pre[c];
     }
     __syncthreads();
+#if BR_VAR != 2 && BR_VAR != 3  // measurement variants (tools/build_variants.sh): 2, 3 skip the blur
     blur_tile_compute(S, bt.tx0, bt.ty0, bt.dst, sm.tin4, sm.hp, 0, S.h);  // fixes only off-plane columns
+#endif
+#if BR_VAR == 1 || BR_VAR == 3  // 1, 3 skip the resize
+    return;
+#endif
     if (!resize) return;
     // resize from the window: window row r = source row ty0 - 4 + r, column c = tx0 - 16 + c
     const uint8_t* wb = reinterpret_cast<const uint8_t*>(&sm.tin4[0][0]);
@@ -486,7 +500,9 @@ __global__ __launch_bounds__(kFastThreads) void k_fast_cells(BatchArgs a, int ce
     constexpr int kList = cell_list_cap<CP>();
     __shared__ __attribute__((aligned(16))) uint8_t T[CP * CP];
     __shared__ __attribute__((aligned(16))) uint8_t M[CP * CP];  // 16-byte rows when CP % 16 == 0
-    __shared__ uint16_t list[kList + 2];  // + the sink entry of the compass compaction
+    __shared__ __attribute__((aligned(8))) uint16_t list[kList + fast_list_slack(kFastThreads / 64)];
+    __shared__ uint2 lut[16];
+    __shared__ uint8_t emask[32];
     __shared__ int32_t wcnt[kFastThreads / 64];
     __shared__ int scratch[16];
     const int wg = xcd_remap(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * gridDim.y);
@@ -523,7 +539,8 @@ __global__ __launch_bounds__(kFastThreads) void k_fast_cells(BatchArgs a, int ce
         return make_uint4(v[0], v[1], v[2], v[3]);
     };
     DevPolicy p{scratch};
-    CellScratch cs{T, M, list, wcnt};
+    fast_cell_tables<CP>(g, sh, lut, emask);  // synced with the ROI staging (fast_cell_run)
+    CellScratch cs{T, M, list, wcnt, lut, emask};
     const int n = fast_cell_run<CP>(p, src, G.pitch, sh, dword_ok, g, a.ini_th, a.min_th, cs, key_out, ld16);
     if (threadIdx.x == 0) *cnt_out = n;
 }
