@@ -22,54 +22,56 @@ __host__ __device__ inline int cv_round(float v) { return (int)__builtin_rintf(v
 // the domain the descriptor produces, 0 <= x < 2 pi (angles from fastAtan2 in [0, 360) degrees
 // times factorPI); checked bit-exact against the host libm on every float of [0, 6.2832), with
 // and without FMA contraction of the polynomial (tests/test_host_harness.py).
-struct SinCosTab {
-    double c0, c1, c2, c3, c4;  // cos polynomial, sign-adjusted per quadrant pair
-};
-__host__ __device__ inline float libm_poly(double x, double x2, double c0, double c1, double c2, double c3,
-                                           double c4, int odd_cos) {
-    if (!odd_cos) {  // sin: x + x^3 s1 + x^7 (s2 + x^2 s3)
-        const double s1 = -0x1.555545995a603p-3, s2 = 0x1.1107605230bc4p-7, s3 = -0x1.994eb3774cf24p-13;
-        const double x3 = x * x2;
-        const double t1 = s2 + x2 * s3;
-        const double x7 = x3 * x2;
-        const double s = x + x3 * s1;
-        return (float)(s + x7 * t1);
-    }
-    const double x4 = x2 * x2;  // cos: (c0 + x^2 c1) + x^4 c2 + x^6 (c3 + x^2 c4)
+// sin polynomial x + x^3 s1 + x^7 (s2 + x^2 s3) and cos polynomial
+// (c0 + x^2 c1) + x^4 c2 + x^6 (c3 + x^2 c4), each rounded to float as glibc's sincosf does
+__host__ __device__ inline float libm_sin_poly(double x, double x2) {
+    const double s1 = -0x1.555545995a603p-3, s2 = 0x1.1107605230bc4p-7, s3 = -0x1.994eb3774cf24p-13;
+    const double x3 = x * x2;
+    const double t1 = s2 + x2 * s3;
+    const double x7 = x3 * x2;
+    const double s = x + x3 * s1;
+    return (float)(s + x7 * t1);
+}
+__host__ __device__ inline float libm_cos_poly(double x2) {
+    const double c0 = 0x1p0, c1 = -0x1.ffffffd0c621cp-2, c2 = 0x1.55553e1068f19p-5, c3 = -0x1.6c087e89a359dp-10,
+                 c4 = 0x1.99343027bf8c3p-16;
+    const double x4 = x2 * x2;
     const double t2 = c3 + x2 * c4;
     const double t1 = c0 + x2 * c1;
     const double x6 = x4 * x2;
     const double c = t1 + x4 * c2;
     return (float)(c + x6 * t2);
 }
-// libm sinf(y) and cosf(y) for 0 <= y < 120.
+// libm sinf(y) and cosf(y) for 0 <= y < 120.  glibc evaluates, after the reduction to
+// x in [-pi/4, pi/4] with quadrant n, sinf = poly(x s, n) and cosf = poly(x s, n ^ 1), where an
+// odd selector takes the cos polynomial with coefficients negated for n & 2 (table 1) and
+// s = {1, -1, -1, 1}[n & 3].  Both results therefore come from ONE sin and ONE cos polynomial
+// of x s, swapped for odd n; the negated coefficients negate the cos polynomial exactly
+// (every operation is sign-symmetric under round-to-nearest), so the sign is applied to the
+// float result.
 __host__ __device__ inline void libm_sincosf(float y, float* sn, float* cs) {
-    const double C0 = 0x1p0, C1 = -0x1.ffffffd0c621cp-2, C2 = 0x1.55553e1068f19p-5, C3 = -0x1.6c087e89a359dp-10,
-                 C4 = 0x1.99343027bf8c3p-16;
     double x = y;
-    uint32_t u = __builtin_bit_cast(uint32_t, y);
+    const uint32_t u = __builtin_bit_cast(uint32_t, y);
     const uint32_t top = (u >> 20) & 0x7ff;
-    if (top < 0x3f4u) {  // |y| < pi/4 (abstop12(0x1.921FB6p-1f))
-        if (top < 0x398u) {  // |y| < 2^-12
-            *sn = y;
-            *cs = 1.0f;
-            return;
-        }
-        const double x2 = x * x;
-        *sn = libm_poly(x, x2, C0, C1, C2, C3, C4, 0);
-        *cs = libm_poly(x, x2, C0, C1, C2, C3, C4, 1);
+    if (top < 0x398u) {  // |y| < 2^-12
+        *sn = y;
+        *cs = 1.0f;
         return;
     }
-    // reduce_fast: n = round(x * 2/pi) in 8.24 fixed point, r = x - n * pi/2
-    const double r = x * 0x1.45F306DC9C883p+23;
-    const int n = ((int32_t)r + 0x800000) >> 24;
-    x = x - n * 0x1.921FB54442D18p0;
-    const double sgn = ((n + 1) & 2) ? -1.0 : 1.0;  // {1, -1, -1, 1}[n & 3]
-    const double f = (n & 2) ? -1.0 : 1.0;           // table 1: negated cos coefficients
-    const double xs = x * sgn, x2 = x * x;
-    // sinf: poly(x * s, n), cosf: poly(x * s, n ^ 1); an odd selector means the cos polynomial
-    *sn = libm_poly(xs, x2, f * C0, f * C1, f * C2, f * C3, f * C4, n & 1);
-    *cs = libm_poly(xs, x2, f * C0, f * C1, f * C2, f * C3, f * C4, (n ^ 1) & 1);
+    int n = 0;
+    if (top >= 0x3f4u) {  // |y| >= pi/4 (abstop12(0x1.921FB6p-1f)): reduce_fast
+        // n = round(x * 2/pi) in 8.24 fixed point, r = x - n * pi/2, times {1, -1, -1, 1}[n & 3]
+        const double r = x * 0x1.45F306DC9C883p+23;
+        n = ((int32_t)r + 0x800000) >> 24;
+        x = x - n * 0x1.921FB54442D18p0;
+        x = ((n + 1) & 2) ? -x : x;
+    }
+    const double x2 = x * x;
+    const float ps = libm_sin_poly(x, x2);
+    float pc = libm_cos_poly(x2);
+    pc = (n & 2) ? -pc : pc;
+    *sn = (n & 1) ? pc : ps;
+    *cs = (n & 1) ? ps : pc;
 }
 
 // atanf / atan2f / tanf of the host libm the oracle links (glibc 2.35, this image and the GPU
