@@ -163,7 +163,25 @@ __host__ __device__ void fast_cell_stage(Pol& p, const uint8_t* src, long long p
         const int nq = (sh + cols + 15) >> 4;
         uint4* T128 = reinterpret_cast<uint4*>(T);
         uint4* M128 = reinterpret_cast<uint4*>(M);
-        for (int i = tid; i < rows * RQ; i += NT) {
+        // the first kIt chunks per thread are all loaded before any is stored, so their round
+        // trips overlap (a rolled load -> wait -> store loop pays one round trip per chunk);
+        // kIt covers every chunk at 128 threads (the device's workgroup), the loop after it the rest
+        constexpr int kIt = (CP * RQ + 127) / 128;
+        uint4 v[kIt];
+#pragma unroll
+        for (int k = 0; k < kIt; ++k) {
+            const int i = tid + k * NT, r = i / RQ, q = i % RQ;
+            if (i < rows * RQ && q < nq) v[k] = ld16((long long)r * pitch + 16 * q);
+        }
+#pragma unroll
+        for (int k = 0; k < kIt; ++k) {
+            const int i = tid + k * NT, q = i % RQ;
+            if (i < rows * RQ && q < nq) {
+                T128[i] = v[k];
+                M128[i] = make_uint4(0, 0, 0, 0);
+            }
+        }
+        for (int i = tid + kIt * NT; i < rows * RQ; i += NT) {
             const int r = i / RQ, q = i % RQ;
             if (q < nq) {
                 T128[i] = ld16((long long)r * pitch + 16 * q);

@@ -184,7 +184,7 @@ __device__ inline BlurTile blur_tile(const BatchArgs& a, int t) {
     int k = t % a.total_tiles;
     int l = 0;
     while (l + 1 < a.nlevels && k >= a.lv[l + 1].tile_first) ++l;
-    const LevelGeom& G = a.lv[l];
+    const LevelGeom G = a.lv[l];
     k -= G.tile_first;
     bt.l = l;
     bt.ty0 = (k / G.tiles_x) * kBlurTH;
@@ -199,7 +199,7 @@ __device__ inline BlurTile blur_tile(const BatchArgs& a, int t) {
 // bytes outside the plane that the taps reach are reflected in LDS afterwards (blur_fix_cols).
 template <int kAux = 0>
 __device__ inline uint4 blur_chunk(const BatchArgs& a, const BlurTile& bt, int i, int IWQ) {
-    const LevelGeom& G = a.lv[bt.l];
+    const LevelGeom G = a.lv[bt.l];
     const int r = i / IWQ, cq = i - r * IWQ;
     // rows beyond the reflected range feed only zero weights or unwritten outputs: clamp
     const int y = min(max(refl101(bt.ty0 + r - 4, G.h), 0), G.h - 1);
@@ -323,7 +323,7 @@ __global__ __launch_bounds__(256) void k_blur(BatchArgs a, int tile0, int ntile)
     }
     for (; t < t_end; ++t) {
         const BlurTile cur = bt;
-        const LevelGeom& G = a.lv[cur.l];
+        const LevelGeom G = a.lv[cur.l];
         const int ty0 = cur.ty0, tx0 = cur.tx0;
         uint8_t* dst = cur.dst;
         __syncthreads();  // the previous tile's passes are done with tin4 / hp
@@ -374,8 +374,8 @@ template <int kAux>
 __device__ inline void br_tile(const BatchArgs& a, int l, bool resize, int img, int by, int bx, BrSmem& sm) {
     constexpr int IW = kBlurTW + 32, IH = kBlurTH + 8, IWQ = IW / 16;
     constexpr int NCH = (IH * IWQ + 255) / 256;
-    const LevelGeom& S = a.lv[l - 1];
-    const LevelGeom& G = a.lv[resize ? l : l - 1];
+    const LevelGeom S = a.lv[l - 1];
+    const LevelGeom G = a.lv[resize ? l : l - 1];
     BlurTile bt;
     bt.l = l - 1;
     bt.ty0 = by * kBlurTH;
@@ -470,7 +470,7 @@ __device__ inline int div_magic(int n, uint32_t magic) {
 
 __global__ __launch_bounds__(256) void k_blur_resize(BatchArgs a, int l, uint32_t per_magic, uint32_t tx_magic) {
     __shared__ BrSmem sm;
-    const LevelGeom& S = a.lv[l - 1];
+    const LevelGeom S = a.lv[l - 1];
     const int per = S.tiles_x * S.tiles_y;
     const int wg = xcd_remap(blockIdx.x, gridDim.x);  // an image's tiles on one XCD
     const int irel = div_magic(wg, per_magic);
@@ -481,7 +481,7 @@ __global__ __launch_bounds__(256) void k_blur_resize(BatchArgs a, int l, uint32_
 
 
 hipError_t launch_blur_resize(const BatchArgs& a, int l, hipStream_t s) {
-    const LevelGeom& S = a.lv[l - 1];
+    const LevelGeom S = a.lv[l - 1];
     auto magic = [](uint32_t d) { return d > 1 ? 0xFFFFFFFFu / d + 1u : 0u; };  // exact for n < 2^32 / d
     hipLaunchKernelGGL(k_blur_resize, dim3(S.tiles_x * S.tiles_y * a.nimages), dim3(256), 0, s, a, l,
                        magic((uint32_t)(S.tiles_x * S.tiles_y)), magic((uint32_t)S.tiles_x));
@@ -514,7 +514,7 @@ __global__ __launch_bounds__(kFastThreads) void k_fast_cells(BatchArgs a, int ce
     const int4 e0 = a.rtab[a.fast_tab_off + 2 * gcell];
     const int4 e1 = a.rtab[a.fast_tab_off + 2 * gcell + 1];
     const int l = e0.x;
-    const LevelGeom& G = a.lv[l];
+    const LevelGeom G = a.lv[l];
     int32_t* cnt_out = a.cellcnt + (long long)img * a.cellcnt_img_stride + e1.x;
     uint32_t* key_out = a.cellkeys + (long long)img * a.cellkeys_img_stride + e1.y;
     CellGeom g;
@@ -557,7 +557,7 @@ template <bool kLdsPath>
 __device__ __attribute__((always_inline)) inline void octree_level(const BatchArgs& a, int img, int l,
                                                                    uint8_t* nodemem_lds, int* scratch,
                                                                    OctShared& sh, const OctCfg q) {
-    const LevelGeom& G = a.lv[l];
+    const LevelGeom G = a.lv[l];
     DevPolicy p{scratch};
     const int32_t* cnt = a.cellcnt + (long long)img * a.cellcnt_img_stride + G.cellcnt_off;
     const uint32_t* ck = a.cellkeys + (long long)img * a.cellkeys_img_stride + G.cellkey_off;
@@ -748,7 +748,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kOdLanes ==
     const int irel = gridDim.x == 1 ? wg : (int)__umulhi((uint32_t)wg, nblk_magic);
     const int img = a.img0 + irel, bx = wg - irel * (int)gridDim.x;
     const int l = a.rtab[a.od_tab_off + bx].x;
-    const LevelGeom& G = a.lv[l];
+    const LevelGeom G = a.lv[l];
     const int sub = threadIdx.x % kOdLanes, grp = threadIdx.x / kOdLanes;
     const int count = a.lvlcnt[img * kMaxLevels + l];
     const long long kbase = (long long)img * a.lvlkp_img_stride + G.kp_off;
@@ -1324,7 +1324,7 @@ __global__ __launch_bounds__(kKnnThreads) void k_knn2_mfma_plain(const uint8_t* 
 
 // ---------------------------------------------------------------------------------------------
 hipError_t launch_blur_level(const BatchArgs& a, int l, hipStream_t s) {
-    const LevelGeom& G = a.lv[l];
+    const LevelGeom G = a.lv[l];
     const int n = G.tiles_x * G.tiles_y;
     hipLaunchKernelGGL(k_blur, dim3(std::min(n * a.nimages, 8192)), dim3(256), 0, s, a, G.tile_first, n);
     return hipGetLastError();
