@@ -6,8 +6,8 @@
   (lowest index wins, cv::BFMatcher k=2 / SURVEY §8 a10) is exercised.
 * The batch matcher (orbgpu_match_stereo_batch) with more than 4096 train rows per pair, and the
   C5 batch the bench's side line runs (1920x1080, 12 levels, 5000 features, 16 pairs).
-* The exact bench batch (bench.py: 128 pairs from 16 distinct seeded pairs, 4 chunk streams,
-  staggered first step, then the steady state), sampled against the oracle.
+* The exact bench batch (bench.py: 256 pairs tiled from the distinct seeded pairs, 3 chunk
+  streams, staggered first step, then the steady state), sampled against the oracle.
 * Consumers given an explicit stream right after a multi-stream batch (they must wait
   for the chunk streams), and the IDL one-call entry with a padded stride and a buffer that ends
   at the last pixel.
@@ -114,7 +114,7 @@ def test_split_knn2_one_pair_past_4096_rows(oracle, monkeypatch):
 
 def test_c5_batch_16_pairs(oracle):
     """The C5 side line's batch (bench.py other_configs: 1920x1080, 12 levels, 5000 features,
-    16 pairs tiled from 4 seeded pairs, 4 chunk streams): every pair's 5000 x 5000 kNN2 against
+    16 pairs tiled from 4 seeded pairs, on the context's chunk streams): every pair's 5000 x 5000 kNN2 against
     the oracle matcher, sampled images against the oracle extractor."""
     import orbslam3lib_amd as og
     cu = [synth.stereo_pair(1080, 1920, 500 + i) for i in range(4)]
@@ -192,7 +192,7 @@ def _hip():
 
 
 def test_explicit_stream_after_chunked_batch(oracle):
-    """A 256-image batch runs on the 4 chunk streams; kNN2, stereo matching and the grid are
+    """A 256-image batch runs on the context's chunk streams; kNN2, stereo matching and the grid are
     then launched on a caller stream without synchronising first: they must wait for the chunks
     (orbgpu_match_stereo_batch / stereo_matches_batch / undistort_grid_batch join the context's
     streams), and the next batch must wait for them."""

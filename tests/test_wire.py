@@ -101,9 +101,9 @@ def test_gpu_sbs_ingest_from_device_memory(oracle):
     lib = og.load_library()
     dptr = lib.orbgpu_device_sbs_input(be.ctx.handle)
     assert dptr
-    hip = C.CDLL("libamdhip64.so.7")  # the runtime liborbgpu.so already loaded
-    hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
-    assert hip.hipMemcpy(dptr, frames.ctypes.data, frames.nbytes, 1) == 0  # hipMemcpyHostToDevice
+    memcpy = og.hip_function("hipMemcpy")  # the runtime liborbgpu.so is bound to
+    memcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+    assert memcpy(dptr, frames.ctypes.data, frames.nbytes, 1) == 0  # hipMemcpyHostToDevice
     be.ingest_sbs(dptr, 2, 1280)
     be.run()
     be.synchronize()
