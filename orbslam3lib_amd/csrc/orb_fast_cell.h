@@ -344,6 +344,9 @@ __host__ __device__ int fast_cell_detect(Pol& p, int sh, const CellGeom& g, int 
             na += p.popc64(m);
         }
 #endif
+#if FAST_VAR == 3
+        return na;
+#endif
         // exact strength of every candidate (m > t <=> corner at t), corners kept in order; the
         // next batch's list entries are read one batch ahead (the in-place writes of a batch
         // land below its own start, never on entries not yet read)
@@ -353,7 +356,7 @@ __host__ __device__ int fast_cell_detect(Pol& p, int sh, const CellGeom& g, int 
             const int j = base + lane;
             const int o = o_next;
             if (base + L < na) o_next = list[base + L + lane < na ? base + L + lane : na - 1];
-#if FAST_VAR == 1  // measurement variant: every candidate a corner of strength t + 1
+#if FAST_VAR == 1  // measurement variants (tools/build_variants.sh): 1 = every candidate a corner of strength t + 1
             const int sm = t + 1;
 #else
             const int sm = fast_strength_packed<CP>(&T[o]);
@@ -390,6 +393,9 @@ __host__ __device__ int fast_cell_detect(Pol& p, int sh, const CellGeom& g, int 
         return make_int2(tot, before);
     };
     int nb = build(tini);
+#if FAST_VAR == 3 || FAST_VAR == 4  // measurement variants: pre-test (+ strength) at iniThFAST only
+    return nb;
+#endif
     p.sync();  // M complete: nonmax reads neighbours owned by other waves
     int2 cb = count_kept(nb, tini);
     int t = tini;
@@ -426,6 +432,9 @@ __host__ __device__ int fast_cell_run(Pol& p, const uint8_t* src, long long pitc
                                       const CellScratch& cs, uint32_t* keys_out, Ld16 ld16) {
     fast_cell_stage<CP>(p, src, pitch, sh, dword_ok, g, cs, ld16);
     p.sync();
+#if FAST_VAR == 2  // measurement variant: staging only
+    return cs.T[p.tid()] & 1;
+#endif
     return fast_cell_detect<CP>(p, sh, g, ini_th, min_th, cs, keys_out);
 }
 
