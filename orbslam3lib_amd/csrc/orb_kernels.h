@@ -207,8 +207,15 @@ __host__ __device__ inline OctLayout oct_layout(int n_cap, int C) {
 }
 
 // Kernel launchers (orb_kernels.hip).  Each returns hipGetLastError() of its launch.
+// k_blur / k_blur_resize tile: kBlurTW x kBlurTH outputs of the blur (kBlurTH a multiple of 16:
+// 8 row groups of kBlurTH / 8 rows, an even count, in the vertical pass)
+#ifndef BLUR_TH
+#define BLUR_TH 32
+#endif
+constexpr int kBlurTW = 128, kBlurTH = BLUR_TH;
+static_assert(kBlurTH % 16 == 0, "blur tile height");
 constexpr int kBrMaxQuads = 40;  // k_blur_resize: level-l column quads / rows one blur tile owns
-constexpr int kBrMaxRows = 34;
+constexpr int kBrMaxRows = kBlurTH + 2;
 // The blur of level l - 1 and the resize to level l in one launch (every level except the last
 // blur, which launch_blur_level does).
 hipError_t launch_blur_resize(const BatchArgs& a, int level, hipStream_t s);

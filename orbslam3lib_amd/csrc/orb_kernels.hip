@@ -170,7 +170,6 @@ __device__ inline int refl101(int p, int n) {
 // Vertical pass: each output row is 4 v_dot2_u32_u16 over row pairs with weight pairs
 // {0,18}{34,48}{56,48}{34,18} (even rows) or {18,34}{48,56}{48,34}{18,0} (odd rows), the
 // accumulator seeded with the 2^15 rounding term.
-constexpr int kBlurTW = 128, kBlurTH = 32;
 
 struct BlurTile {
     int l, ty0, tx0;
@@ -261,12 +260,14 @@ __device__ inline void blur_tile_compute(const LevelGeom& G, int tx0, int ty0, u
         hp[rp][cq] = make_uint4(h[0], h[1], h[2], h[3]);
     }
     __syncthreads();
-    // vertical: thread -> column quad cq, output rows 4rg .. 4rg+3 (row pairs 2rg .. 2rg+5)
+    // vertical: thread -> column quad cq, output rows R rg .. R rg + R - 1 (row pairs
+    // (R/2) rg .. (R/2) rg + R/2 + 3); output row r takes window rows r + 1 .. r + 7
+    constexpr int R = kBlurTH / 8;
     const int cq = threadIdx.x & 31, rg = threadIdx.x >> 5;
-    uint32_t V[6][4];
+    uint32_t V[R / 2 + 4][4];
 #pragma unroll
-    for (int k = 0; k < 6; ++k) {
-        const uint4 q = hp[2 * rg + k][cq];
+    for (int k = 0; k < R / 2 + 4; ++k) {
+        const uint4 q = hp[(R / 2) * rg + k][cq];
         V[k][0] = q.x;
         V[k][1] = q.y;
         V[k][2] = q.z;
@@ -278,9 +279,9 @@ __device__ inline void blur_tile_compute(const LevelGeom& G, int tx0, int ty0, u
                          as_u16x2(48u | (34u << 16)), as_u16x2(18u | (0u << 16))};
     const int x = tx0 + 4 * cq;
 #pragma unroll
-    for (int o = 0; o < 4; ++o) {
-        const int y = ty0 + 4 * rg + o;
-        const int k0 = (o + 1) >> 1;  // first row pair: o=0 -> 0, 1 -> 1, 2 -> 1, 3 -> 2
+    for (int o = 0; o < R; ++o) {
+        const int y = ty0 + R * rg + o;
+        const int k0 = (o + 1) >> 1;  // first row pair: o=0 -> 0, 1 -> 1, 2 -> 1, 3 -> 2, ...
         uint32_t sv[4];
 #pragma unroll
         for (int c = 0; c < 4; ++c) {

@@ -336,8 +336,8 @@ int set_geometry(orbgpu_ctx* c, int w, int h) {
         ows += oct_layout(G.cand_cap, G.oct_cap).total;
         G.scale = c->scale[l];
         G.patch = (int)(31 * c->scale[l]);
-        G.tiles_x = (G.w + 127) / 128;   // k_blur tile 128 x 32
-        G.tiles_y = (G.h + 31) / 32;
+        G.tiles_x = (G.w + kBlurTW - 1) / kBlurTW;  // k_blur tile kBlurTW x kBlurTH
+        G.tiles_y = (G.h + kBlurTH - 1) / kBlurTH;
         G.tile_first = tile_first;
         tile_first += G.tiles_x * G.tiles_y;
         G.od_blocks = std::max(1, (G.N + 16 + od_per_block - 1) / od_per_block);  // k_orient_desc blocks
@@ -365,11 +365,11 @@ int set_geometry(orbgpu_ctx* c, int w, int h) {
             std::vector<int> band(S.tiles_y + 1), tq(S.tiles_x + 1);
             const int nquads = (G.w + 3) / 4;
             for (int b = 0, dy = 0; b <= S.tiles_y; ++b) {
-                while (dy < G.h && (b == S.tiles_y || (G.area2 ? 2 * dy : yt[dy].x) < 32 * b)) ++dy;
+                while (dy < G.h && (b == S.tiles_y || (G.area2 ? 2 * dy : yt[dy].x) < kBlurTH * b)) ++dy;
                 band[b] = b == S.tiles_y ? G.h : dy;
             }
             for (int j = 0, q = 0; j <= S.tiles_x; ++j) {
-                while (q < nquads && (j == S.tiles_x || (G.area2 ? 8 * q : xt[4 * q].x) < 128 * j)) ++q;
+                while (q < nquads && (j == S.tiles_x || (G.area2 ? 8 * q : xt[4 * q].x) < kBlurTW * j)) ++q;
                 tq[j] = j == S.tiles_x ? nquads : q;
             }
             for (int b = 0; b < S.tiles_y; ++b)
