@@ -10,7 +10,11 @@ streams) and compared with the oracle bit-exact, keypoints, descriptors and per-
 * low-contrast noise (128 +- 6): no corner at iniThFAST anywhere (|difference| <= 12), so every
   cell reruns at minThFAST (ORBextractor_old.cc:845-861), and few find one there (0.035%);
 * a saturated half frame (left 255, right 0) with a noisy seam: empty cells beside dense ones,
-  levels where most cells keep nothing.
+  levels where most cells keep nothing;
+* a period-4 0/255 pattern (rows 0011 / 1100) on which EVERY level-0 pixel passes k_fast_cells'
+  antipodal-pair pre-test (each pair {0,8}, {2,10}, {4,12}, {6,14} holds an opposite value), so
+  the candidate lists fill completely and the compaction's unused slots past the last lane land
+  in the spare list entries (orb_fast_cell.h fast_list_slack).
 """
 import numpy as np
 import pytest
@@ -32,9 +36,45 @@ def _frames():
     return [noise, salt, low, half, salt[::-1].copy(), noise[:, ::-1].copy()]
 
 
+def _saturating_frames():
+    rng = np.random.default_rng(77)
+    tile = np.array([[0, 0, 1, 1], [1, 1, 0, 0]] * 2, np.uint8) * 255
+    pat = np.tile(tile, (H // 4, W // 4))
+    noisy = np.clip(pat.astype(np.int16) + rng.integers(-5, 6, (H, W)), 0, 255).astype(np.uint8)
+    shifted = np.roll(pat, (1, 3), axis=(0, 1))
+    return [pat, noisy, shifted, np.roll(noisy, (2, 1), axis=(0, 1))]
+
+
+def _pretest_pass_fraction(img, t=20):
+    """numpy restatement of fw_pretest4 on the detection area of the whole frame"""
+    im = img.astype(np.int32)
+    v = im[3:-3, 3:-3]
+
+    def at(dx, dy):
+        return im[3 + dy:im.shape[0] - 3 + dy, 3 + dx:im.shape[1] - 3 + dx]
+
+    pairs = [((0, 3), (0, -3)), ((2, 2), (-2, -2)), ((3, 0), (-3, 0)), ((2, -2), (-2, 2))]
+    dark = np.ones_like(v, bool)
+    bright = np.ones_like(v, bool)
+    for a, b in pairs:
+        dark &= (at(*a) < v - t) | (at(*b) < v - t)
+        bright &= (at(*a) > v + t) | (at(*b) > v + t)
+    return float((dark | bright).mean())
+
+
+def test_pretest_saturating_pattern(oracle):
+    imgs = _saturating_frames()
+    assert _pretest_pass_fraction(imgs[0]) == 1.0
+    _check_batch(oracle, imgs)
+
+
 def test_adversarial_textures_batch(oracle):
+    _check_batch(oracle, _frames(), dense=True)
+
+
+def _check_batch(oracle, frames, dense=False):
     import orbslam3lib_amd as og
-    imgs = np.stack(_frames())
+    imgs = np.stack(frames)
     n = len(imgs)
     be = og.BatchExtractor(2000, 1.2, 8, 20, 7, width=W, height=H, max_images=n)
     be.upload(imgs)
@@ -42,8 +82,9 @@ def test_adversarial_textures_batch(oracle):
     be.run(laps)
     be.match_stereo(False)
     be.synchronize()
-    cand = be.candidate_counts()
-    assert cand[0] > 16384, cand  # the iid-noise frame reaches the dense octree path
+    if dense:
+        cand = be.candidate_counts()
+        assert cand[0] > 16384, cand  # the iid-noise frame reaches the dense octree path
     for i in range(n):
         k, d, m = be.result(i)
         rk, rd, rm = oracle.extract(imgs[i], nfeatures=2000, lap=tuple(laps[i]))
