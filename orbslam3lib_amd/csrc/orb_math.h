@@ -260,7 +260,8 @@ __host__ __device__ inline int ring_dy(int k) {
 // and the 3x3 nonmax rule of FAST_t<16> becomes
 //   kept_t(p) <=> m(p) > t && m(p) >= 2 && for each 8-neighbour q in the same cell detection
 //                 region: m(q) <= t || m(p) > m(q).
-// When the 4-compass pre-test at t_min fails, S_max <= t_min and 0 is stored instead (exact
+// When a necessary-condition pre-test at t_min fails (the 4-point compass in fast_strength below,
+// the 8-point antipodal-pair test in k_fast_cells), S_max <= t_min and 0 is stored instead (exact
 // for every t >= t_min).  Reference call sites: cv::FAST at ORBextractor_old.cc:828,847.
 // Exact strength of a pixel already known to be a corner at some t >= 0 (no pre-test).
 __host__ __device__ inline int fast_strength_corner(const uint8_t* c, int stride) {
