@@ -764,14 +764,21 @@ def main():
             cb_.close() if hasattr(cb_, "close") else None
             del cb_
 
-    # C5's exchange step when several GPUs run: every rank contributes its camera
-    # (pair 0's left eye), one RCCL all_gather moves the descriptors, each rank matches its own
-    # against all others on its GPU.  Reported beside the headline, never part of it.
+    # C5's exchange step (BASELINE configs[4]) when several GPUs run: every rank
+    # contributes one C5 camera -- its own 1920x1080 frame, 12 levels, 5000 features, extracted on
+    # its GPU -- one RCCL all_gather moves the descriptors (5000 x 32 B per camera), and each rank
+    # matches its camera against every other camera on its GPU.  Reported beside the headline,
+    # never part of it.
     cross = None
     if world > 1:
         try:
             from orbslam3lib_amd.dist import cross_camera_match, cross_camera_match_device
-            kl0, dl0, _ = be.result(0)
+            C5W, C5H, C5L, C5N = 1920, 1080, 12, 5000
+            c5 = og.BatchExtractor(C5N, 1.2, C5L, 20, 7, device=local, width=C5W, height=C5H, max_images=2)
+            c5.upload(np.stack(synth.stereo_pair(C5H, C5W, 500 + base)))  # this rank's camera = image 0
+            c5.run()
+            c5.synchronize()
+            kl0, dl0, _ = c5.result(0)
             device_path = has_cuda
             res = None
             for _ in range(2):  # the first exchange sets up the communicator and buffers
@@ -780,10 +787,10 @@ def main():
                 if device_path:
                     # descriptors stay in HBM: export -> all_gather (RCCL over xGMI; under gloo
                     # staged through the host) -> device kNN2 on every other camera
-                    res = cross_camera_match_device(dist, be, 0)
+                    res = cross_camera_match_device(dist, c5, 0)
                     torch.cuda.synchronize()
                 else:  # no GPU (the stub test): the host exchange
-                    res = cross_camera_match(dist, dl0, be.knn_match)
+                    res = cross_camera_match(dist, dl0, c5.knn_match)
                 c1 = time.perf_counter()
             cel = max_over_ranks(dist, c1 - c0)
             nqm = sum_over_ranks(dist, len(dl0) * len(res))
@@ -791,16 +798,20 @@ def main():
             ok = 1.0
             if device_path:
                 from orbslam3lib_amd.dist import cross_camera_match as host_x
-                ref = host_x(dist, dl0, be.knn_match)
+                ref = host_x(dist, dl0, c5.knn_match)
                 for r_, got in res.items():
                     g = got.cpu().numpy()
                     ok = min(ok, float(all(np.array_equal(g[k], ref[r_][k]) for k in range(4))))
             ok = -max_over_ranks(dist, -ok)
-            cross = {"cameras": world, "queries_per_camera": len(dl0), "ms": round(cel * 1e3, 3),
+            cross = {"workload": "C5 camera per rank: %dx%d, %d levels, %d feat/frame (BASELINE configs[4])"
+                                 % (C5W, C5H, C5L, C5N),
+                     "cameras": world, "queries_per_camera": len(dl0), "ms": round(cel * 1e3, 3),
                      "mmatches_s": round(nqm / cel / 1e6, 3),
                      "device_matches_equal_host_matcher": bool(ok == 1.0) if device_path else None,
                      "exchange": "all_gather (%s%s)" % (dist.get_backend(), ", device-resident rows"
                                                         if device_path else ", host rows")}
+            c5.close()
+            del c5
         except Exception as e:  # reported, never fatal to the headline line
             cross = {"error": repr(e)[:200]}
 

@@ -42,7 +42,8 @@ enum {
     ORBGPU_ERR_INVALID = -3,      /* bad argument */
     ORBGPU_ERR_HIP = -4,          /* HIP runtime error (see orbgpu_last_error) */
     ORBGPU_ERR_OVERFLOW = -5,     /* device-side workspace overflow (keys / nodes) */
-    ORBGPU_ERR_NO_DEVICE = -6     /* no usable gfx950 device */
+    ORBGPU_ERR_NO_DEVICE = -6,    /* no usable gfx950 device */
+    ORBGPU_ERR_RUNTIME = -7       /* two HIP runtimes mapped into the process (import torch first) */
 };
 
 /* The 5 ORB parameters of the ORBextractor ctor / Settings.cc:443-451. */
@@ -321,6 +322,12 @@ int orbgpu_num_stages(void);
 const char* orbgpu_stage_name(int stage);
 int orbgpu_stage_times(orbgpu_ctx* ctx, double* ms, int64_t* launches, int max_stages);
 int orbgpu_reset_stage_times(orbgpu_ctx* ctx);
+
+/* Measurement knobs (ORBGPU_STREAMS, ORBGPU_OCT_SPLIT, ORBGPU_FAST_PITCH, ...) change launch
+ * shapes and kernel variants; the library reads them only when ORBGPU_DIAGNOSTICS=1 is also set.
+ * Writes the knobs in effect as "NAME=value;..." (NUL-terminated, truncated to cap) and returns
+ * their count: 0 in a deployment. */
+int orbgpu_diagnostic_knobs(char* buf, size_t cap);
 
 const char* orbgpu_last_error(void);
 int orbgpu_abi_version(void);

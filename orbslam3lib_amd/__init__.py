@@ -51,6 +51,7 @@ EXPORTED = [
     "orbgpu_set_profiling", "orbgpu_num_stages", "orbgpu_stage_name", "orbgpu_stage_times",
     "orbgpu_reset_stage_times", "orbgpu_last_error", "orbgpu_abi_version",
     "orbgpu_fisheye_stereo_batch", "orbgpu_download_fisheye", "orbgpu_run_batch_match",
+    "orbgpu_diagnostic_knobs",
 ]
 
 
@@ -107,6 +108,7 @@ def load_library(path: str = LIB_PATH):
     lib.orbgpu_device_sbs_input.argtypes = [C.c_void_p]
     lib.orbgpu_host_alloc.argtypes = [C.c_size_t, C.POINTER(C.c_void_p)]
     lib.orbgpu_host_free.argtypes = [C.c_void_p]
+    lib.orbgpu_diagnostic_knobs.argtypes = [C.c_char_p, C.c_size_t]
     lib.orbgpu_export_descriptors.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_int,
                                               C.POINTER(C.c_int), C.c_void_p]
     lib.orbgpu_match_knn2_device.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int] + \
@@ -124,6 +126,15 @@ def hip_function(name: str):
     then its dependencies in load order, i.e. the libamdhip64 it actually mapped (torch's bundled
     copy when torch was imported first) -- no soname is hard-coded.  Test / bench plumbing."""
     return getattr(load_library(), name)
+
+
+def diagnostic_knobs() -> dict:
+    """The measurement knobs liborbgpu.so honours right now (orbgpu_diagnostic_knobs): empty
+    unless ORBGPU_DIAGNOSTICS=1 is set beside them."""
+    buf = C.create_string_buffer(4096)
+    load_library().orbgpu_diagnostic_knobs(buf, len(buf))
+    txt = buf.value.decode()
+    return dict(kv.split("=", 1) for kv in txt.split(";")) if txt else {}
 
 
 def _check(code):

@@ -1357,17 +1357,21 @@ hipError_t launch_fast_cells(const BatchArgs& a, int tile, hipStream_t s) {
     return hipGetLastError();
 }
 hipError_t launch_octree(const BatchArgs& a, hipStream_t s) {
-    // the dynamic-LDS limit is raised once per size (not on every launch: the launch sequence may
-    // be captured into a hipGraph, orb_runtime.cpp run_batch)
-    static std::atomic<int> lds_set{65536};
-    if (a.oct_lds_bytes > lds_set.load()) {
+    // the dynamic-LDS limit is raised once per size and device (the attribute is per device; not
+    // on every launch: the launch sequence may be captured into a hipGraph, orb_runtime.cpp)
+    constexpr int kMaxDevices = 64;
+    static std::atomic<int> lds_set[kMaxDevices];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) dev = kMaxDevices - 1;
+    std::atomic<int>& set = lds_set[dev];
+    if (a.oct_lds_bytes > 65536 && a.oct_lds_bytes > set.load()) {
         for (const void* f : {reinterpret_cast<const void*>(k_octree<512>),
                               reinterpret_cast<const void*>(k_octree_retry)}) {
             hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, a.oct_lds_bytes);
             if (e != hipSuccess) return e;
         }
-        int cur = lds_set.load();
-        while (a.oct_lds_bytes > cur && !lds_set.compare_exchange_weak(cur, a.oct_lds_bytes)) {}
+        int cur = set.load();
+        while (a.oct_lds_bytes > cur && !set.compare_exchange_weak(cur, a.oct_lds_bytes)) {}
     }
     const int split = a.nimages < a.oct_split_min_images ? a.nlevels : std::min(a.oct_split, a.nlevels);
     if (split > 0)

@@ -5,6 +5,7 @@
 // tables on the host with the reference's own float/double formulas, and enqueues the kernels
 // of orb_kernels.hip.  There is no CPU compute path: every result comes from the device.
 #include <hip/hip_runtime.h>
+#include <link.h>
 
 #include <algorithm>
 #include <cfloat>
@@ -27,9 +28,61 @@ namespace {
 
 thread_local std::string g_err;
 
+constexpr size_t kGraphCacheSize = 4;  // captured batch sequences kept per context
+
 int fail(int code, const std::string& msg) {
     g_err = msg;
     return code;
+}
+
+// Measurement knobs (launch shapes, stream counts, kernel variants, phase clocks) are read only
+// when ORBGPU_DIAGNOSTICS=1 is set as well: a stray ORBGPU_* variable in a deployment never
+// changes the product's kernel path.  orbgpu_diagnostic_knobs reports the ones in effect.
+const char* const kDiagKnobs[] = {"ORBGPU_OD_ITERS",      "ORBGPU_OCT_SMALL_LDS", "ORBGPU_OCT_SMALL_THREADS",
+                                  "ORBGPU_OCT_SPLIT",     "ORBGPU_OCT_GENERIC",   "ORBGPU_OCT_PYR",
+                                  "ORBGPU_FAST_PITCH",    "ORBGPU_STREAMS",       "ORBGPU_ISOLATE",
+                                  "ORBGPU_STAGGER",       "ORBGPU_OCT_STAMPS",    "ORBGPU_GRAPH",
+                                  "ORBGPU_KNN_NOSPLIT"};
+
+bool diagnostics_on() {
+    const char* g = getenv("ORBGPU_DIAGNOSTICS");
+    return g && std::strcmp(g, "1") == 0;
+}
+
+const char* diag_env(const char* name) { return diagnostics_on() ? getenv(name) : nullptr; }
+
+// torch bundles its own libamdhip64 (loaded by path, so a copy of the same soname from /opt/rocm
+// that liborbgpu mapped first does not satisfy it): two HIP runtimes in one process then each own
+// the device, and torch's sees none.  Entry points that start device work refuse that state with
+// ORBGPU_ERR_RUNTIME instead of letting the other runtime fail silently later.  The object list
+// is only rescanned when the process has loaded something since the last check (dlpi_adds).
+int check_single_hip_runtime() {
+    struct Scan { unsigned long long adds; std::vector<std::string> paths; };
+    static unsigned long long checked_adds = ~0ull;
+    static int verdict = 0;
+    static std::string paths_msg;
+    Scan sc{0, {}};
+    dl_iterate_phdr([](dl_phdr_info* i, size_t, void* d) -> int {
+        static_cast<Scan*>(d)->adds = i->dlpi_adds;
+        return 1;  // the counter is the same in every entry: stop at the first
+    }, &sc);
+    if (sc.adds == checked_adds) return verdict;
+    dl_iterate_phdr([](dl_phdr_info* i, size_t, void* d) -> int {
+        const char* nm = i->dlpi_name;
+        if (!nm || !*nm) return 0;
+        const char* base = std::strrchr(nm, '/');
+        base = base ? base + 1 : nm;
+        if (std::strncmp(base, "libamdhip64.so", 14) == 0) static_cast<Scan*>(d)->paths.push_back(nm);
+        return 0;
+    }, &sc);
+    checked_adds = sc.adds;
+    verdict = sc.paths.size() > 1 ? ORBGPU_ERR_RUNTIME : 0;
+    paths_msg.clear();
+    for (const auto& q : sc.paths) paths_msg += (paths_msg.empty() ? "" : ", ") + q;
+    if (verdict)
+        g_err = "two HIP runtimes are mapped into this process (" + paths_msg +
+                "): import torch before loading liborbgpu.so, so that both bind to one runtime";
+    return verdict;
 }
 
 #define HIP_TRY(expr)                                                                  \
@@ -139,10 +192,13 @@ struct orbgpu_ctx {
     unsigned isolate_mask = 0;
     bool serialize = false;  // profiling: every stage isolated
     bool oct_stamps = false; // ORBGPU_OCT_STAMPS (read once at create): octree phase clocks
-    // the captured launch sequence of a one-stream batch (run_batch), keyed by {n, w, h, slot}
+    // the captured launch sequences of one-stream batches (run_batch / run_batch_match), keyed by
+    // {images, width, height, input slot, match pairs, stereo rows only}: one exec per key, so
+    // alternating input slots (async uploads) or match variants replay instead of recapturing
     bool use_graph = true;   // ORBGPU_GRAPH=0 launches every kernel directly (A/B)
-    hipGraphExec_t graph_exec = nullptr;
-    int graph_key[6] = {-1, -1, -1, -1, -1, -1};  // images, width, height, input slot, match pairs, rows
+    struct GraphRec { int key[6]; hipGraphExec_t exec; unsigned long long used; };
+    std::vector<GraphRec> graphs;
+    unsigned long long graph_tick = 0;
     bool knn_nosplit = false;  // ORBGPU_KNN_NOSPLIT (read once at create): no split kNN2 launches
     std::vector<int32_t> laps_host;  // lapping areas currently in `laps` (device), per image
     bool need_fork = true;           // the main stream holds work the sub streams must wait for
@@ -259,10 +315,13 @@ int alloc_all(orbgpu_ctx* c, int n_images) {
 
 int ctx_sync(orbgpu_ctx* c, bool with_copy = false);
 
+// Graph execs are launched on c->stream: the last launch of one may still run when it is
+// destroyed, so the stream drains first.
 void drop_graph(orbgpu_ctx* c) {
-    if (c->graph_exec) hipGraphExecDestroy(c->graph_exec);
-    c->graph_exec = nullptr;
-    c->graph_key[0] = -1;
+    if (c->graphs.empty()) return;
+    hipStreamSynchronize(c->stream);
+    for (auto& g : c->graphs) hipGraphExecDestroy(g.exec);
+    c->graphs.clear();
 }
 
 // Level geometry for a w x h image (input row stride = w in the batch buffer).
@@ -284,7 +343,7 @@ int set_geometry(orbgpu_ctx* c, int w, int h) {
     // keypoints per k_orient_desc workgroup: kOdKpBlock per pass, od_iters passes (the key of the
     // next pass is prefetched during the current one; the table setup is paid once).  2 passes:
     // 488-490 us per 512 images vs 504 at 4, 497-504 at 1, 540 at 8 (round 3, single stream)
-    const char* odi = getenv("ORBGPU_OD_ITERS");
+    const char* odi = diag_env("ORBGPU_OD_ITERS");
     const int od_per_block = kOdKpBlock * std::max(1, odi ? atoi(odi) : 2);
     for (int l = 0; l < L; ++l) {
         LevelGeom& G = A.lv[l];
@@ -405,9 +464,9 @@ int set_geometry(orbgpu_ctx* c, int w, int h) {
     // is what the node phases' serial latency needs.  oct_split = the first level from which on
     // the node state leaves room for >= 1024 labels (0 for 640x480-class pyramids: every level).
     {
-        const char* eb = getenv("ORBGPU_OCT_SMALL_LDS");
+        const char* eb = diag_env("ORBGPU_OCT_SMALL_LDS");
         const int budget = eb ? atoi(eb) : kOctSmallLds;
-        const char* et = getenv("ORBGPU_OCT_SMALL_THREADS");
+        const char* et = diag_env("ORBGPU_OCT_SMALL_THREADS");
         A.oct2_threads = et && atoi(et) == 128 ? 128 : kOctSmallThreads;
         auto layout = [&](int s0) {
             int n2 = 0, c2 = 0;
@@ -426,7 +485,7 @@ int set_geometry(orbgpu_ctx* c, int w, int h) {
         // launches back to back and measured slower (C5: 90 vs 98 Mfeatures/s).  Launches of
         // fewer than kOctSmallMinImages images stay in the 512-thread shape too (latency, not
         // occupancy, bounds them: C4 0.31 vs 0.26 ms per pair).  ORBGPU_OCT_SPLIT forces a split.
-        if (const char* e = getenv("ORBGPU_OCT_SPLIT")) {
+        if (const char* e = diag_env("ORBGPU_OCT_SPLIT")) {
             A.oct_split = std::max(0, std::min(L, atoi(e)));
             if (A.oct_split < L && !layout(A.oct_split)) A.oct_split = L;
             A.oct_split_min_images = 0;
@@ -443,10 +502,10 @@ int set_geometry(orbgpu_ctx* c, int w, int h) {
         if (G.oct_cap > lds_nodes || G.ncells > A.oct_nq_off / 4) A.oct_may_retry = 1;
         if (l >= A.oct_split && (G.oct_cap > A.oct2_lds_nodes || G.ncells > A.oct2_nq_off / 4)) A.oct_may_retry = 1;
     }
-    A.oct_force_retry = getenv("ORBGPU_OCT_GENERIC") ? 1 : 0;  // diagnostics / tests
+    A.oct_force_retry = diag_env("ORBGPU_OCT_GENERIC") ? 1 : 0;  // diagnostics / tests
     // ORBGPU_OCT_PYR=<d>: cap the count pyramid's depth (0: the label-pass formulation only)
     A.oct_pyr_max = kOctPyrMaxD;
-    if (const char* e = getenv("ORBGPU_OCT_PYR")) A.oct_pyr_max = std::max(0, std::min(kOctPyrMaxD, atoi(e)));
+    if (const char* e = diag_env("ORBGPU_OCT_PYR")) A.oct_pyr_max = std::max(0, std::min(kOctPyrMaxD, atoi(e)));
     if (A.oct_force_retry) A.oct_may_retry = 1;
     A.total_cells = cell_first;
     // FAST LDS tiles: each level takes the smallest tile its cell ROIs (+3 alignment bytes) fit:
@@ -456,7 +515,7 @@ int set_geometry(orbgpu_ctx* c, int w, int h) {
     auto fits = [&](int l, int P) { return A.lv[l].wCell + 9 <= P && A.lv[l].hCell + 6 <= P; };
     int tier[kMaxLevels];
     int min_tier = 0;
-    if (const char* fp = getenv("ORBGPU_FAST_PITCH")) {  // diagnostics: force the larger tiles
+    if (const char* fp = diag_env("ORBGPU_FAST_PITCH")) {  // diagnostics: force the larger tiles
         const int P = atoi(fp);
         min_tier = P == kCellMax ? 2 : P == kCellPitchSmall ? 1 : 0;
     }
@@ -653,6 +712,22 @@ int drop_pending_upload(orbgpu_ctx* c) {
 extern "C" {
 
 const char* orbgpu_last_error(void) { return g_err.c_str(); }
+
+int orbgpu_diagnostic_knobs(char* buf, size_t cap) {
+    std::string out;
+    int n = 0;
+    for (const char* k : kDiagKnobs)
+        if (const char* v = diag_env(k)) {
+            out += (out.empty() ? "" : ";") + std::string(k) + "=" + v;
+            ++n;
+        }
+    if (buf && cap) {
+        const size_t m = std::min(cap - 1, out.size());
+        std::memcpy(buf, out.data(), m);
+        buf[m] = 0;
+    }
+    return n;
+}
 int orbgpu_abi_version(void) { return ORBGPU_ABI_VERSION; }
 int orbgpu_num_stages(void) { return ST_COUNT; }
 const char* orbgpu_stage_name(int s) { return (s >= 0 && s < ST_COUNT) ? kStageNames[s] : ""; }
@@ -669,6 +744,7 @@ int orbgpu_create(const orbgpu_params* p, int device, int max_width, int max_hei
     // of a resize step stay inside that window only for scale steps up to 2
     if (p->scale_factor > 2.0f)
         return fail(ORBGPU_ERR_INVALID, "scale_factor above 2 is not supported");
+    if (int e = check_single_hip_runtime()) return e;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
         return fail(ORBGPU_ERR_NO_DEVICE, "no HIP device");
@@ -699,7 +775,7 @@ int orbgpu_create(const orbgpu_params* p, int device, int max_width, int max_hei
         // extractor) gets one stream: chunks are whole pairs, and every stream takes one of the
         // process's hardware queues, which a second context (the other eye's thread) needs for its
         // own work not to queue behind this one's.
-        const char* e = getenv("ORBGPU_STREAMS");
+        const char* e = diag_env("ORBGPU_STREAMS");
         const int ns = std::max(1, std::min({8, e ? atoi(e) : 3, max_images / 2}));
         for (int k = 1; k < ns; ++k) {
             hipStream_t st;
@@ -717,13 +793,13 @@ int orbgpu_create(const orbgpu_params* p, int device, int max_width, int max_hei
             orbgpu_destroy(c);
             return fail(ORBGPU_ERR_HIP, "hipEventCreate failed");
         }
-        const char* iso = getenv("ORBGPU_ISOLATE");  // stage bit mask (diagnostics)
+        const char* iso = diag_env("ORBGPU_ISOLATE");  // stage bit mask (diagnostics)
         if (iso) c->isolate_mask = (unsigned)strtoul(iso, nullptr, 0);
-        const char* sg = getenv("ORBGPU_STAGGER");
+        const char* sg = diag_env("ORBGPU_STAGGER");
         if (sg) c->stagger = atoi(sg) != 0;
-        c->oct_stamps = getenv("ORBGPU_OCT_STAMPS") != nullptr;
-        if (const char* g = getenv("ORBGPU_GRAPH")) c->use_graph = atoi(g) != 0;
-        c->knn_nosplit = getenv("ORBGPU_KNN_NOSPLIT") != nullptr;
+        c->oct_stamps = diag_env("ORBGPU_OCT_STAMPS") != nullptr;
+        if (const char* g = diag_env("ORBGPU_GRAPH")) c->use_graph = atoi(g) != 0;
+        c->knn_nosplit = diag_env("ORBGPU_KNN_NOSPLIT") != nullptr;
     }
     int r = ensure_input(c, 1, max_width, max_height);
     if (!r) r = set_geometry(c, max_width, max_height);
@@ -860,6 +936,7 @@ static int run_batch_impl(orbgpu_ctx* c, int n, int w, int h, const int32_t* lap
                           int match_pairs, int stereo_only, bool* matched) {
     if (matched) *matched = false;
     if (!c) return fail(ORBGPU_ERR_INVALID, "null ctx");
+    if (int e = check_single_hip_runtime()) return e;
     if (w <= 0 || h <= 0) return fail(ORBGPU_ERR_EMPTY_IMAGE, "empty image");
     int r = ensure_input(c, n, w, h);
     if (r) return r;
@@ -1044,8 +1121,18 @@ static int run_batch_impl(orbgpu_ctx* c, int n, int w, int h, const int32_t* lap
     };
     if (graphable) {
         const int key[6] = {n, w, h, c->in_slot, with_match ? match_pairs : 0, with_match ? stereo_only : 0};
-        if (!c->graph_exec || std::memcmp(key, c->graph_key, sizeof key) != 0) {
-            drop_graph(c);
+        orbgpu_ctx::GraphRec* rec = nullptr;
+        for (auto& g : c->graphs)
+            if (std::memcmp(key, g.key, sizeof key) == 0) rec = &g;
+        if (!rec) {
+            if (c->graphs.size() >= kGraphCacheSize) {  // evict the least recently launched exec
+                size_t lru = 0;
+                for (size_t k = 1; k < c->graphs.size(); ++k)
+                    if (c->graphs[k].used < c->graphs[lru].used) lru = k;
+                HIP_TRY(hipStreamSynchronize(c->stream));  // its last launch may still run
+                hipGraphExecDestroy(c->graphs[lru].exec);
+                c->graphs.erase(c->graphs.begin() + lru);
+            }
             HIP_TRY(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
             int rr = launch_all();
             if (!rr && with_match) rr = launch_match();
@@ -1055,15 +1142,19 @@ static int run_batch_impl(orbgpu_ctx* c, int n, int w, int h, const int32_t* lap
                 if (g) hipGraphDestroy(g);
                 return rr ? rr : fail(ORBGPU_ERR_HIP, std::string("hipStreamEndCapture: ") + hipGetErrorString(ec));
             }
-            const hipError_t ei = hipGraphInstantiate(&c->graph_exec, g, nullptr, nullptr, 0);
+            hipGraphExec_t ex = nullptr;
+            const hipError_t ei = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
             hipGraphDestroy(g);
-            if (ei != hipSuccess) {
-                c->graph_exec = nullptr;
+            if (ei != hipSuccess)
                 return fail(ORBGPU_ERR_HIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(ei));
-            }
-            std::memcpy(c->graph_key, key, sizeof key);
+            orbgpu_ctx::GraphRec nr{};
+            std::memcpy(nr.key, key, sizeof key);
+            nr.exec = ex;
+            c->graphs.push_back(nr);
+            rec = &c->graphs.back();
         }
-        HIP_TRY(hipGraphLaunch(c->graph_exec, s));
+        rec->used = ++c->graph_tick;
+        HIP_TRY(hipGraphLaunch(rec->exec, s));
     } else if ((r = launch_all())) {
         return r;
     }

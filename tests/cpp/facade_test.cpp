@@ -4,7 +4,9 @@
 #include <dlfcn.h>
 
 #include <cstdint>
+#include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -99,7 +101,8 @@ int main(int argc, char** argv) {
     auto ox = (oracle_extract_t)dlsym(h, "oracle_extract");
     auto oknn = (oracle_knn2_t)dlsym(h, "oracle_knn2");
     if (!ox || !oknn) { printf("oracle symbols\n"); return 2; }
-    const int W = 640, H = 480;
+    // the eye geometry: 640x480 by default; 640 400 is the headset's (LynxHardwareAccelerator.h:20-21)
+    const int W = argc > 3 ? atoi(argv[2]) : 640, H = argc > 3 ? atoi(argv[3]) : 480;
     std::vector<uint8_t> L = texture(W, H, 7), R = texture(W, H, 8);
     ORB_SLAM3::ORBextractor ex(2000, 1.2f, 8, 20, 7);
     if (ex.GetLevels() != 8 || ex.GetScaleFactors().size() != 8) { printf("getters\n"); return 1; }
@@ -112,7 +115,11 @@ int main(int argc, char** argv) {
     int rn = 0;
     int rmono = ox(2000, 1.2f, 8, 20, 7, L.data(), W, H, W, 0, 1000, rk.data(), rd.data(), 20000, &rn);
     int bad = compare("mono", kps, desc, mono, rk.data(), rd.data(), rn, rmono);
-    if (ex.mvImagePyramid.size() != 8 || ex.mvImagePyramid[1].cols != 533 || ex.mvImagePyramid[7].rows != 134) {
+    // level sizes cvRound(W * invScale) (ComputePyramid :1336): 533 and 134 at 640x480
+    const std::vector<float> inv = ex.GetInverseScaleFactors();
+    if (ex.mvImagePyramid.size() != 8 || ex.mvImagePyramid[1].cols != (int)lrintf((float)W * inv[1]) ||
+        ex.mvImagePyramid[7].rows != (int)lrintf((float)H * inv[7]) ||
+        (W == 640 && H == 480 && (ex.mvImagePyramid[1].cols != 533 || ex.mvImagePyramid[7].rows != 134))) {
         printf("pyramid export\n");
         bad = 1;
     }
@@ -200,6 +207,6 @@ int main(int argc, char** argv) {
     if (dd != ref) { printf("DescriptorDistance %d vs %d\n", dd, ref); bad = 1; }
     cv::Mat empty;
     if (ex(empty, cv::Mat(), kps, desc, lap) != -1) bad = 1;
-    printf(bad ? "FACADE FAIL\n" : "FACADE OK %zu keypoints\n", kps.size());
+    printf(bad ? "FACADE FAIL %dx%d\n" : "FACADE OK %dx%d %zu keypoints\n", W, H, kps.size());
     return bad;
 }

@@ -106,6 +106,7 @@ def test_split_knn2_one_pair_past_4096_rows(oracle, monkeypatch):
     assert len(dr) > 4096 and len(dl) > 4096, (len(dl), len(dr))
     split = be.matches(0)
     _same_knn(split, oracle.knn2(dl, dr), "split")
+    monkeypatch.setenv("ORBGPU_DIAGNOSTICS", "1")
     monkeypatch.setenv("ORBGPU_KNN_NOSPLIT", "1")
     be.match_stereo(False)
     be.synchronize()

@@ -42,6 +42,7 @@ def test_bench_gpus_n_spawns_ranks(n):
     cross = line["cross_camera"]
     assert cross and "error" not in cross, cross
     assert cross["cameras"] == n and cross["exchange"].startswith("all_gather (gloo")
+    assert "1920x1080, 12 levels, 5000" in cross["workload"]  # the C5 camera, not a C2 eye
     assert line["data"].startswith("stub")
 
 

@@ -223,14 +223,18 @@ def test_descriptor_distance_matches_reference(oracle):
         assert og.ORBmatcher.DescriptorDistance(a, b) == oracle.descriptor_distance(a, b)
 
 
-def test_cpp_facade():
-    """The C++ ORB_SLAM3::ORBextractor facade (what an ORB-SLAM3 build links) vs the oracle."""
+@pytest.mark.parametrize("w,h", [(640, 480), (640, 400)])
+def test_cpp_facade(w, h):
+    """The C++ ORB_SLAM3::ORBextractor facade (what an ORB-SLAM3 build links) vs the oracle: mono
+    operator(), the side-by-side / two-image / AHardwareBuffer stereo forms and BFMatchORB, at
+    640x480 and at the headset's 640x400 eyes (1280x400 side-by-side AHB,
+    LynxHardwareAccelerator.h:20-21, ORBextractor.cc:136-143)."""
     import os
     import subprocess
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     exe = os.path.join(root, "tests", "cpp", "build", "facade_test")
     assert os.path.exists(exe), "run make (builds tests/cpp/build/facade_test)"
-    r = subprocess.run([exe, os.path.join(root, "oracle", "build", "liborb_oracle.so")],
+    r = subprocess.run([exe, os.path.join(root, "oracle", "build", "liborb_oracle.so"), str(w), str(h)],
                        capture_output=True, text=True, timeout=300, cwd=root)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "FACADE OK" in r.stdout
@@ -273,6 +277,7 @@ def test_octree_launch_shapes(oracle, monkeypatch, env):
     both small workgroup sizes and a layout with all labels in LDS give the oracle's keypoints."""
     import orbslam3lib_amd as og
     for k, v in env.items():
+        monkeypatch.setenv("ORBGPU_DIAGNOSTICS", "1")
         monkeypatch.setenv(k, v)
     imgs = synth.stereo_batch(480, 640, 2, first=11)
     be = og.BatchExtractor(2000, 1.2, 8, 20, 7, width=640, height=480, max_images=4)
@@ -293,6 +298,7 @@ def test_forced_fast_tile(oracle, frame0, monkeypatch, pitch):
     a 640x480 pyramid, 64 for its top levels and 80 for cells wider than 55 px) on every level
     of the 640x480 frame, forced through ORBGPU_FAST_PITCH."""
     L, _ = frame0
+    monkeypatch.setenv("ORBGPU_DIAGNOSTICS", "1")
     monkeypatch.setenv("ORBGPU_FAST_PITCH", pitch)
     ex = _extractor()
     k, d, m = ex(L)
@@ -316,6 +322,7 @@ def test_octree_generic_instantiation(oracle, frame0, monkeypatch):
     """Every level through k_octree_retry (generic pointers, the path taken by levels with
     more candidates than the LDS label capacity), forced with ORBGPU_OCT_GENERIC."""
     L, _ = frame0
+    monkeypatch.setenv("ORBGPU_DIAGNOSTICS", "1")
     monkeypatch.setenv("ORBGPU_OCT_GENERIC", "1")
     ex = _extractor()
     k, d, m = ex(L)

@@ -1,5 +1,5 @@
 """C4 step time (one pair per step, extraction + kNN2): run_match vs run + match_stereo, 200 steps
-each after warmup.  ORBGPU_GRAPH=0 in the environment disables the graph capture."""
+each after warmup.  ORBGPU_DIAGNOSTICS=1 ORBGPU_GRAPH=0 in the environment disables the graph capture."""
 import os, sys, time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np

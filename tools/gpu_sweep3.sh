@@ -5,7 +5,7 @@ O=gpurun_out/sweep3
 mkdir -p $O
 B="--no-cpu-baseline --no-sbp --no-wire --no-stereo --no-grid --no-configs"
 for st in 3 4 2 3; do
-  ORBGPU_STREAMS=$st timeout -k 10 200 python bench.py $B > $O/s$st.json 2>/dev/null || exit 1
+  ORBGPU_DIAGNOSTICS=1 ORBGPU_STREAMS=$st timeout -k 10 200 python bench.py $B > $O/s$st.json 2>/dev/null || exit 1
   echo "streams $st $(python3 -c "import json;d=json.load(open('$O/s$st.json'));print(d['value'],d['ms_per_step'])")"
 done
 timeout -k 10 200 python bench.py $B --pairs 384 > $O/p384.json 2>/dev/null || exit 1

@@ -1,6 +1,7 @@
 """Diagnostic: run one 64-pair batch with ORBGPU_OCT_STAMPS=1 to print octree phase times."""
 import os, sys
 os.environ["ORBGPU_OCT_STAMPS"] = "1"
+os.environ["ORBGPU_DIAGNOSTICS"] = "1"
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np
 import orbslam3lib_amd as og

@@ -2,7 +2,7 @@
 # PMC passes over tools/profile_batch.py (one counter group per rocprofv3 run, kernel trace only).
 # One stream so each dispatch is one kernel over the whole batch.  Usage: tools/pmc.sh OUTDIR
 cd "$(dirname "$0")/.."
-export TMPDIR=/tmp ORBGPU_STREAMS=1
+export TMPDIR=/tmp ORBGPU_DIAGNOSTICS=1 ORBGPU_STREAMS=1
 OUT=${1:-gpurun_out/pmc}
 mkdir -p $OUT
 i=0

@@ -1,7 +1,7 @@
 #!/bin/bash
 # MFMA-pipe counters for the kNN kernel (tools/profile_batch.py, one stream); one pass per group.
 cd "$(dirname "$0")/.."
-export TMPDIR=/tmp ORBGPU_STREAMS=1
+export TMPDIR=/tmp ORBGPU_DIAGNOSTICS=1 ORBGPU_STREAMS=1
 OUT=${1:-gpurun_out/pmck}
 mkdir -p $OUT
 i=0

@@ -4,7 +4,7 @@
 # of bench.py's serialized pass.  Usage: tools/pmc_traffic.sh OUTDIR (PAIRS / STEPS as profile_batch)
 set -e
 cd "$(dirname "$0")/.."
-export TMPDIR=/tmp ORBGPU_STREAMS=1
+export TMPDIR=/tmp ORBGPU_DIAGNOSTICS=1 ORBGPU_STREAMS=1
 OUT=${1:-gpurun_out/pmct}
 mkdir -p $OUT
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/p0 -o pmc -- python3 tools/profile_batch.py > $OUT/p0.log 2>&1

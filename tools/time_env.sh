@@ -2,7 +2,7 @@
 # Single-stream kernel stats of tools/profile_batch.py under each environment setting given,
 # e.g. tools/time_env.sh k_octree "ORBGPU_OCT_SPLIT=8" "ORBGPU_OCT_SPLIT=3"
 cd "$(dirname "$0")/.."
-export TMPDIR=/tmp ORBGPU_STREAMS=1
+export TMPDIR=/tmp ORBGPU_DIAGNOSTICS=1 ORBGPU_STREAMS=1
 K=$1; shift
 i=0
 for setting in "$@"; do

@@ -2,7 +2,7 @@
 # Single-stream kernel stats of tools/profile_batch.py for each library under orbslam3lib_amd/variants
 # (plus the default build).  Usage: tools/time_variants.sh [KERNEL_SUBSTRING]
 cd "$(dirname "$0")/.."
-export TMPDIR=/tmp ORBGPU_STREAMS=1
+export TMPDIR=/tmp ORBGPU_DIAGNOSTICS=1 ORBGPU_STREAMS=1
 K=${1:-k_fast_cells}
 for lib in orbslam3lib_amd/liborbgpu.so orbslam3lib_amd/variants/*.so; do
   n=$(basename $lib .so)

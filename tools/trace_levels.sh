@@ -2,7 +2,7 @@
 # Kernel trace of a few single-stream batch steps (each dispatch = one stage over the whole batch):
 # per-dispatch durations in order, for per-level timing of the pyramid kernels.
 cd "$(dirname "$0")/.."
-export TMPDIR=/tmp ORBGPU_STREAMS=1
+export TMPDIR=/tmp ORBGPU_DIAGNOSTICS=1 ORBGPU_STREAMS=1
 O=${1:-gpurun_out/trace}
 mkdir -p $O
 timeout -k 10 120 rocprofv3 --kernel-trace --output-format csv -d $O -o run -- python3 tools/profile_batch.py > $O/log.txt 2>&1 || { tail $O/log.txt; exit 1; }

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Kernel trace of the bench batch on one stream (each launch alone): per-launch durations.
 cd "$(dirname "$0")/.."
-export TMPDIR=/tmp ORBGPU_STREAMS=1
+export TMPDIR=/tmp ORBGPU_DIAGNOSTICS=1 ORBGPU_STREAMS=1
 OUT=${1:-gpurun_out/trace1}
 mkdir -p $OUT
 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $OUT -o tr -- python3 tools/profile_batch.py > $OUT/log 2>&1 || exit 1

@@ -2,7 +2,7 @@
 # Kernel time (single stream) and FETCH_SIZE / WRITE_SIZE of one stage for the default build and
 # each library under orbslam3lib_amd/variants.  Usage: tools/variant_traffic.sh KERNEL_SUBSTRING
 cd "$(dirname "$0")/.."
-export TMPDIR=/tmp ORBGPU_STREAMS=1
+export TMPDIR=/tmp ORBGPU_DIAGNOSTICS=1 ORBGPU_STREAMS=1
 K=${1:-k_octree}
 for lib in orbslam3lib_amd/liborbgpu.so orbslam3lib_amd/variants/*.so; do
   n=$(basename $lib .so)
