@@ -58,21 +58,27 @@ def fast_tiers(w, h, sf=1.2, L=8):
     return out
 
 
-def algorithmic_bytes(w, h, L, nkp, sf=1.2, ncand=0.0):
+def algorithmic_bytes(w, h, L, nkp, sf=1.2, ncand=0.0, tail0=None):
     """Per-image bytes by stage: pyramid sum(A_{l-1}+A_l), FAST sum(A_l) (split
     between the 48-, 64- and 80-byte tile launches), blur 2*sum(A_l), 48 B per output keypoint
     (16 B keypoint + 32 B descriptor) for orientation + descriptor; the octree reads its 4-byte
     candidate keys and writes 4 bytes per kept keypoint; the assembly reads the level keypoint
-    (key, angle, descriptor: 40 B) and writes the cv::KeyPoint and the descriptor (60 B)."""
+    (key, angle, descriptor: 40 B) and writes the cv::KeyPoint and the descriptor (60 B).
+    tail0: first level k_pyr_tail makes (it reads level tail0 - 1 once and writes the blurs of
+    levels tail0 - 1 .. L-1 and levels tail0 .. L-1); None: k_blur_resize for every level and
+    k_blur for the last level's blur."""
     A = [a * b for a, b in level_sizes(w, h, sf, L)]
     tier = fast_tiers(w, h, sf, L)
+    t = tail0 if tail0 is not None else L + 1
+    last_br = t if t <= L else L
     return {
         # one pass over level l-1 per launch: read it, write its blur and level l
-        "k_blur_resize": sum(2 * A[l - 1] + A[l] for l in range(1, L)),
+        "k_blur_resize": sum(2 * A[l - 1] + A[l] for l in range(1, last_br)),
+        "k_pyr_tail": (A[t - 1] + sum(A[t - 1:]) + sum(A[t:])) if t <= L else 0,
         "k_fast_cells<48>": sum(a for a, t in zip(A, tier) if t == 48),
         "k_fast_cells<64>": sum(a for a, t in zip(A, tier) if t == 64),
         "k_fast_cells<80>": sum(a for a, t in zip(A, tier) if t == 80),
-        "k_blur": 2 * A[L - 1],  # the last level's blur (the others ride in k_blur_resize)
+        "k_blur": 2 * A[L - 1] if t > L else 0,  # the last level's blur (the others ride in k_blur_resize)
         "k_orient_desc": 48 * nkp,
         "k_octree": 4 * ncand + 4 * nkp,
         "k_finalize": 100 * nkp,
@@ -427,7 +433,11 @@ def main():
     # launch of the same whole-batch launch (profiles/traffic_r*.json, per image and step there)
     n_img = 2 * P
     nser = 3
-    per_img = algorithmic_bytes(W, H, args.nlevels, feats_per_step / n_img, ncand=cand_per_img)
+    # k_pyr_tail's first level from the serialized pass: k_blur_resize runs once per level below it
+    tail0 = None
+    if "k_pyr_tail" in stages_all and "k_blur_resize" in stages_all:
+        tail0 = int(round(stages_all["k_blur_resize"][1] / nser)) + 1
+    per_img = algorithmic_bytes(W, H, args.nlevels, feats_per_step / n_img, ncand=cand_per_img, tail0=tail0)
     traffic_tab, traffic_src = {}, None
     tps = sorted(glob.glob(os.path.join(ROOT, "profiles", "traffic_r*.json")))
     if tps:
@@ -500,7 +510,7 @@ def main():
     # the serialized pass.  The pyramid kernel also writes each level's blur (k_blur_resize reads
     # level l-1 once for both), so its time carries the blur: the bytes are SURVEY §8d's B_fp plus
     # the blur's 2 sum(A_l) (B_extract without the 48 B per keypoint)
-    fp_names = [k for k in stages_all if k in ("k_blur_resize", "k_blur") or k.startswith("k_fast_cells")]
+    fp_names = [k for k in stages_all if k in ("k_blur_resize", "k_blur", "k_pyr_tail") or k.startswith("k_fast_cells")]
     fp_ms = sum(stages_all[k][0] for k in fp_names) / 3.0  # 3 serialized steps
     roof_fp = None
     if fp_ms > 0:

@@ -58,52 +58,52 @@ typedef unsigned short fw_u16x2 __attribute__((ext_vector_type(2)));
 __device__ inline fw_u16x2 fw_as16(uint32_t x) { return __builtin_bit_cast(fw_u16x2, x); }
 __device__ inline uint32_t fw_as32(fw_u16x2 x) { return __builtin_bit_cast(uint32_t, x); }
 
-// Pre-test of the 4 pixels of LDS dword C, device only: bit k set when, for each of the four
-// antipodal pairs of ring points {0,8}, {2,10}, {4,12}, {6,14}, one point of the pair is darker
-// than v-t (or, for all four pairs, one point is brighter than v+t).  Any 9-arc of the 16-point
-// ring holds one point of every antipodal pair, so a FAST corner at t passes (a necessary
-// condition; the exact strength decides).  On the SURVEY 8d frames 26% of the detection pixels
-// pass at iniThFAST (the 4-point compass {0,8} x {4,12} of rounds 1-3 passed 43%; corners 14%).
+// Pre-test of the 4 pixels of LDS dword C, device only: byte k of the result is 0x80 when, for
+// each of the four antipodal pairs of ring points {0,8}, {2,10}, {4,12}, {6,14}, one point of the
+// pair is darker than v-t (or, for all four pairs, one point is brighter than v+t), 0 otherwise.
+// Any 9-arc of the 16-point ring holds one point of every antipodal pair, so a FAST corner at t
+// passes (a necessary condition; the exact strength decides).  On the SURVEY 8d frames 26% of
+// the detection pixels pass at iniThFAST (the 4-point compass {0,8} x {4,12} of rounds 1-3
+// passed 43%; corners 14%).
 // Inputs: row 0 (C and the dwords left / right of it: Cm, Cp), rows -3 / +3 (U3, D3: the same
-// column only), rows -2 / +2 with both neighbours (U2m, U2, U2p; D2m, D2, D2p).  The pixels go
-// through packed 16-bit arithmetic in pairs (0, 2) and (1, 3) built with v_perm; the high byte
-// of every half is 0x04, so each half is a normal f16 of one exponent and the gfx950 3-input
-// v_pk_maximum3_f16 / v_pk_minimum3_f16 order them as integers (orb_math.h pk_max3).
+// column only), rows -2 / +2 with both neighbours (U2m, U2, U2p; D2m, D2, D2p); kt = 255 - t and
+// tt = t in both u16 halves.
+// All four pixels are compared at once, one byte each (SWAR): v_lerp_u8 averages bytes, so with
+// nlo = ~lo, lo = sat(v - t):  (p + nlo + 1) >> 1 >= 128  <=>  p >= lo  (not darker), and with
+// nhi = ~hi, hi = sat(v + t):  (p + nhi) >> 1 >= 128  <=>  p > hi  (brighter): one instruction
+// per ring point and side, bit 7 of each byte.  lo / hi come from 16-bit halves (v_perm split,
+// clamped v_pk_sub_u16) -- 40 VALU per 4 pixels where the packed-16-bit form took ~62.
 __device__ inline uint32_t fw_pretest4(uint32_t C, uint32_t Cm, uint32_t Cp, uint32_t U3, uint32_t D3,
                                        uint32_t U2m, uint32_t U2, uint32_t U2p, uint32_t D2m, uint32_t D2,
-                                       uint32_t D2p, uint32_t tt) {
-    const uint32_t K = 0x04040404u;
+                                       uint32_t D2p, uint32_t tt, uint32_t kt) {
     const uint32_t L3 = __builtin_amdgcn_alignbyte(C, Cm, 1);    // (-3, 0): ring 12
     const uint32_t R3 = __builtin_amdgcn_alignbyte(Cp, C, 3);    // (+3, 0): ring 4
     const uint32_t UL = __builtin_amdgcn_alignbyte(U2, U2m, 2);  // (-2, -2): ring 10
     const uint32_t UR = __builtin_amdgcn_alignbyte(U2p, U2, 2);  // (+2, -2): ring 6
     const uint32_t DL = __builtin_amdgcn_alignbyte(D2, D2m, 2);  // (-2, +2): ring 14
     const uint32_t DR = __builtin_amdgcn_alignbyte(D2p, D2, 2);  // (+2, +2): ring 2
-    const fw_u16x2 T2 = fw_as16(tt);
-    auto test = [&](uint32_t sel) {
-        auto px = [&](uint32_t x) { return fw_as16(__builtin_amdgcn_perm(K, x, sel)); };
-        const fw_u16x2 v = px(C);
-        const fw_u16x2 p0 = px(D3), p8 = px(U3), p4 = px(R3), p12 = px(L3);
-        const fw_u16x2 p2 = px(DR), p10 = px(UL), p6 = px(UR), p14 = px(DL);
-        const fw_u16x2 lo = __builtin_elementwise_sub_sat(v, T2), hi = v + T2;
-        const fw_u16x2 dk = pk_max3(__builtin_elementwise_min(p0, p8), __builtin_elementwise_min(p4, p12),
-                                    __builtin_elementwise_max(__builtin_elementwise_min(p2, p10),
-                                                              __builtin_elementwise_min(p6, p14)));
-        const fw_u16x2 bk = pk_min3(__builtin_elementwise_max(p0, p8), __builtin_elementwise_max(p4, p12),
-                                    __builtin_elementwise_min(__builtin_elementwise_max(p2, p10),
-                                                              __builtin_elementwise_max(p6, p14)));
-        // dk < v - t  <=>  sat(lo - dk) > 0;   bk > v + t  <=>  sat(bk - hi) > 0
-        const fw_u16x2 r = __builtin_elementwise_sub_sat(lo, dk) | __builtin_elementwise_sub_sat(bk, hi);
-        // min(r, 1) per half as one v_pk_min_u16 (left to itself the compiler rewrites it as two
-        // compares, two selects and a v_perm); the constant in a register: an inline constant of
-        // a packed op reaches the high half only through op_sel_hi
-        uint32_t one;
-        asm("v_pk_min_u16 %0, %1, %2" : "=v"(one) : "v"(fw_as32(r)), "s"(0x00010001u));
-        return one;
-    };
-    const uint32_t e = test(0x04020400u), o = test(0x04030401u);  // pixels (0, 2) and (1, 3)
-    const uint32_t comb = e | (o << 1);                           // halves: p0 | p1 << 1, p2 | p3 << 1
-    return (comb & 3u) | ((comb >> 14) & 0xCu);
+    // bytes 0, 2 and 1, 3 of C as u16 halves
+    const fw_u16x2 E = fw_as16(__builtin_amdgcn_perm(0u, C, 0x0c020c00u));
+    const fw_u16x2 O = fw_as16(__builtin_amdgcn_perm(0u, C, 0x0c030c01u));
+    const fw_u16x2 T2 = fw_as16(tt), K2 = fw_as16(kt);
+    // lo = sat(v - t); nhi = ~sat(v + t) = sat(255 - t - v); both repacked to bytes
+    const uint32_t loE = fw_as32(__builtin_elementwise_sub_sat(E, T2)), loO = fw_as32(__builtin_elementwise_sub_sat(O, T2));
+    const uint32_t nhE = fw_as32(__builtin_elementwise_sub_sat(K2, E)), nhO = fw_as32(__builtin_elementwise_sub_sat(K2, O));
+    const uint32_t nlo = ~__builtin_amdgcn_perm(loO, loE, 0x06020400u);
+    const uint32_t nhi = __builtin_amdgcn_perm(nhO, nhE, 0x06020400u);
+    auto nd = [&](uint32_t p) { return __builtin_amdgcn_lerp(p, nlo, 0x01010101u); };  // bit 7: p >= lo
+    auto br = [&](uint32_t p) { return __builtin_amdgcn_lerp(p, nhi, 0u); };          // bit 7: p > hi
+    // dark: every pair has a point < lo  <=>  no pair has both points >= lo
+    uint32_t x = nd(R3) & nd(L3);
+    x = (nd(D3) & nd(U3)) | x;
+    x = (nd(DR) & nd(UL)) | x;
+    x = (nd(UR) & nd(DL)) | x;
+    // bright: every pair has a point > hi
+    uint32_t y = br(R3) | br(L3);
+    y = (br(D3) | br(U3)) & y;
+    y = (br(DR) | br(UL)) & y;
+    y = (br(UR) | br(DL)) & y;
+    return (~x | y) & 0x80808080u;
 }
 
 // Per-cell scratch (LDS on the GPU).
@@ -116,7 +116,7 @@ struct CellScratch {
     // device only (fast_cell_tables): per 4-bit pre-test mask, the positions of its set bits as
     // u16 pairs (p0 | p1 << 16, p2 | p3 << 16), and the detection-pixel mask of each dword group
     const uint2* lut = nullptr;  // [16]
-    const uint8_t* emask = nullptr;  // [ng <= 20]
+    const uint32_t* emask = nullptr;  // [ng <= 20]: 0x80 in the bytes of detection pixels
 };
 
 // List entries past cell_list_cap on the device: each wave's list is followed by 4 spare
@@ -127,7 +127,7 @@ __host__ __device__ constexpr int fast_list_slack(int waves) { return 4 * waves 
 // Builds CellScratch's lut / emask tables (threads < 16 and < ng); the caller syncs before
 // fast_cell_detect.
 template <int CP>
-__device__ inline void fast_cell_tables(const CellGeom& g, int sh, uint2* lut, uint8_t* emask) {
+__device__ inline void fast_cell_tables(const CellGeom& g, int sh, uint2* lut, uint32_t* emask) {
     const int tid = threadIdx.x;
     if (tid < 16) {
         int pos[4] = {0, 0, 0, 0}, n = 0;
@@ -142,7 +142,9 @@ __device__ inline void fast_cell_tables(const CellGeom& g, int sh, uint2* lut, u
     if (tid < ng) {
         const uint32_t first4 = 0xFu & ~((1u << (xs - 4 * g0)) - 1u);
         const uint32_t last4 = (1u << (xe - 4 * (g0 + ng - 1))) - 1u;
-        emask[tid] = (uint8_t)((tid == 0 ? first4 : 0xFu) & (tid == ng - 1 ? last4 : 0xFu));
+        const uint32_t m4 = (tid == 0 ? first4 : 0xFu) & (tid == ng - 1 ? last4 : 0xFu);
+        emask[tid] = (m4 & 1u ? 0x80u : 0u) | (m4 & 2u ? 0x8000u : 0u) | (m4 & 4u ? 0x800000u : 0u) |
+                     (m4 & 8u ? 0x80000000u : 0u);
     }
 }
 
@@ -268,7 +270,7 @@ __host__ __device__ int fast_cell_detect(Pol& p, int sh, const CellGeom& g, int 
         {
             constexpr int RW = CP / 4;
             const uint32_t* T32 = reinterpret_cast<const uint32_t*>(T);
-            const uint32_t tt = (uint32_t)t * 0x00010001u;
+            const uint32_t tt = (uint32_t)t * 0x00010001u, kt = (uint32_t)(255 - t) * 0x00010001u;
             auto rank = [](uint64_t b) {  // set lanes of b below this lane
                 return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32),
                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
@@ -287,14 +289,16 @@ __host__ __device__ int fast_cell_detect(Pol& p, int sh, const CellGeom& g, int 
             }
             for (int base = j0; base < j1; base += L) {
                 const int i = base + lane;
-                uint32_t m4 = 0;
+                uint32_t m8 = 0;  // 0x80 per passing pixel
                 if (i < j1) {
-                    m4 = fw_pretest4(T32[dw], T32[dw - 1], T32[dw + 1], T32[dw - 3 * RW], T32[dw + 3 * RW],
+                    m8 = fw_pretest4(T32[dw], T32[dw - 1], T32[dw + 1], T32[dw - 3 * RW], T32[dw + 3 * RW],
                                      T32[dw - 2 * RW - 1], T32[dw - 2 * RW], T32[dw - 2 * RW + 1],
-                                     T32[dw + 2 * RW - 1], T32[dw + 2 * RW], T32[dw + 2 * RW + 1], tt);
-                    m4 &= cs.emask[q];  // detection pixels of the row's first / last group
+                                     T32[dw + 2 * RW - 1], T32[dw + 2 * RW], T32[dw + 2 * RW + 1], tt, kt);
+                    m8 &= cs.emask[q];  // detection pixels of the row's first / last group
                 }
-                const int c = __builtin_popcount(m4);
+                // the 4-bit pass mask (bit k = byte k) by one v_dot4_u32_u8 of the 0x80 bytes
+                const uint32_t m4 = __builtin_amdgcn_udot4(m8, 0x08040201u, 0u, false) >> 7;
+                const int c = __builtin_popcount(m8);
                 const uint64_t b0 = p.ballot(c & 1), b1 = p.ballot(c & 2), b2 = p.ballot(c & 4);
                 const int pos = na + rank(b0) + 2 * rank(b1) + 4 * rank(b2);
                 // the lane's c entries 4 dw + (set bit positions), as u16 pairs from the table,

@@ -39,6 +39,7 @@ struct LevelGeom {
     // source column is >= 128 j (tiles_x(l-1) + 1 entries)
     int band_row_off, tile_quad_off;
     int od_blocks, od_first;   // orientation/descriptor blocks for this level
+    int tpitch;                // k_pyr_tail: LDS row pitch of this level (levels >= tail0 - 1)
 };
 
 struct BatchArgs {
@@ -86,6 +87,10 @@ struct BatchArgs {
     int oct_may_retry;               // some level can exceed the LDS instantiation of k_octree
     int oct_force_retry;             // diagnostics: every level through the generic instantiation
     int oct_pyr_max;                 // deepest count pyramid of k_octree (0: label passes only)
+    // k_pyr_tail: levels [tail0, nlevels) and the blurs of [tail0 - 1, nlevels) in one launch
+    // (tail0 = nlevels + 1: no tail, k_blur_resize for every level and k_blur for the last)
+    int tail0;
+    int tail_lds, tail_buf1, tail_tab, tail_maxq, tail_maxrows;  // its LDS layout (bytes / entries)
 };
 
 struct MatchArgs {
@@ -220,6 +225,9 @@ constexpr int kBrMaxRows = kBlurTH + 2;
 // blur, which launch_blur_level does).
 hipError_t launch_blur_resize(const BatchArgs& a, int level, hipStream_t s);
 hipError_t launch_blur_level(const BatchArgs& a, int level, hipStream_t s);
+constexpr int kTailPad = 16;          // k_pyr_tail: left pad of an LDS row (>= 3 reflected columns)
+constexpr int kTailLdsMax = 160 * 1024;  // the LDS one workgroup may hold on gfx950
+hipError_t launch_pyr_tail(const BatchArgs& a, hipStream_t s);
 // FAST cells of the levels that run the `tile`-byte LDS tile (48, 64 or kCellMax = 80):
 // fast_cell_range gives their flattened cell range, launch_fast_cells launches nothing if empty
 void fast_cell_range(const BatchArgs& a, int tile, int* c0, int* c1);

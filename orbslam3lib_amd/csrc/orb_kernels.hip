@@ -490,6 +490,213 @@ hipError_t launch_blur_resize(const BatchArgs& a, int l, hipStream_t s) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// k_pyr_tail: the small levels of the pyramid in ONE launch, one 1024-thread workgroup per image.
+// Level s0 = tail0 - 1 (made by the last k_blur_resize) is loaded into LDS once; then for
+// s = s0 .. L-1 the workgroup writes level s's blur (GaussianBlur 7x7, :1146-1147) and makes level
+// s + 1 (cv::resize INTER_LINEAR / exact-2x INTER_AREA, :1342-1344) from the LDS copy into the
+// other LDS buffer and to HBM.  Each of these levels took its own launch of a few thousand
+// 128 x 32 tiles before, and every such launch was latency-bound (level 7: 32 us per 512 images
+// for 24 K pixels per image).  Two buffers alternate (level s0 + 2k in buffer 0, s0 + 2k + 1 in
+// buffer 1; each level is smaller than the one two steps before).  Row pitch Pitch(l) holds kTailPad
+// bytes on the left (REFLECT_101 columns -3 .. -1) and >= 12 on the right (resize reads 12
+// bytes from a quad's first tap), so the blur and rs_quad read the same window layout as k_blur.
+constexpr int kTailThreads = 1024;
+
+__device__ inline void tail_fill_pads(uint8_t* buf, int P, int w, int h) {
+    for (int i = threadIdx.x; i < h * 6; i += kTailThreads) {
+        const int y = i / 6, k = i - 6 * y;
+        uint8_t* row = buf + __mul24(y, P) + kTailPad;
+        if (k < 3) row[-1 - k] = row[1 + k];          // columns -1, -2, -3 <- 1, 2, 3
+        else row[w + k - 3] = row[w - 2 - (k - 3)];    // columns w, w+1, w+2 <- w-2, w-3, w-4
+    }
+}
+
+// Horizontal 7-tap sums of the 4 columns 4cq .. 4cq+3 of two LDS rows as u16 pairs (row a, row b):
+// the same v_perm / v_pk_mad_u16 form as blur_tile_compute (window bytes 4cq+12 .. 4cq+23).
+__device__ inline void tail_hpair(const uint8_t* ra, const uint8_t* rb, int cq, uint32_t out[4]) {
+    const uint32_t* pa = reinterpret_cast<const uint32_t*>(ra) + cq + 3;
+    const uint32_t* pb = reinterpret_cast<const uint32_t*>(rb) + cq + 3;
+    uint32_t A[3], B[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+        A[d] = pa[d];
+        B[d] = pb[d];
+    }
+    u16x2 Pp[12];
+#pragma unroll
+    for (int j = 1; j < 11; ++j) {
+        const uint32_t b = j & 3;
+        Pp[j] = as_u16x2(__builtin_amdgcn_perm(B[j >> 2], A[j >> 2], b | 0x0c00u | ((4 + b) << 16) | 0x0c000000u));
+    }
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+        const u16x2* q = Pp + 1 + o;  // q[0] = column x-3 ... q[6] = column x+3
+        u16x2 acc = (u16x2)(56) * q[3];
+        acc = (u16x2)(48) * (q[2] + q[4]) + acc;
+        acc = (u16x2)(34) * (q[1] + q[5]) + acc;
+        acc = (u16x2)(18) * (q[0] + q[6]) + acc;
+        out[o] = as_u32(acc);
+    }
+}
+
+// Blur of one LDS-resident level.  Task = (column quad, segment of R rows), with the segment
+// count chosen so the workgroup's 1024 threads get one task each where the level allows; a task
+// slides down its rows with the last five row pairs in registers, so every row's horizontal sums
+// are formed once (plus four pairs of prologue).  Row pair j of a task covers rows
+// y0-4+2j, y0-3+2j (REFLECT_101 by index); output rows y0+2m / y0+2m+1 take pairs m .. m+3 with the
+// even weights / m+1 .. m+4 with the odd ones (blur_tile_compute's vertical pass).
+__device__ inline void tail_blur(const uint8_t* buf, int P, const LevelGeom& G, uint8_t* dst) {
+    const int nq = (G.w + 3) >> 2;
+    const int per = kTailThreads / nq > 0 ? kTailThreads / nq : 1;  // segments per column
+    int R = (G.h + per - 1) / per;
+    R = (R + 1) & ~1;
+    const int nseg = (G.h + R - 1) / R;
+    const u16x2 WE[4] = {as_u16x2(0u | (18u << 16)), as_u16x2(34u | (48u << 16)),
+                         as_u16x2(56u | (48u << 16)), as_u16x2(34u | (18u << 16))};
+    const u16x2 WO[4] = {as_u16x2(18u | (34u << 16)), as_u16x2(48u | (56u << 16)),
+                         as_u16x2(48u | (34u << 16)), as_u16x2(18u | (0u << 16))};
+    auto row = [&](int y) { return buf + __mul24(min(max(refl101(y, G.h), 0), G.h - 1), P); };
+    for (int t0 = 0; t0 < nq * nseg; t0 += kTailThreads) {
+        const int t = t0 + (int)threadIdx.x;
+        const int sg = t / nq, cq = t - sg * nq;  // one division per task
+        if (sg >= nseg) break;
+        const int y0 = sg * R, y1 = min(y0 + R, G.h);
+        uint32_t V[5][4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) tail_hpair(row(y0 - 4 + 2 * j), row(y0 - 3 + 2 * j), cq, V[j]);
+        const int x = 4 * cq;
+        uint8_t* d = dst + plane_off(y0, G.bpitch, x);
+        for (int y = y0; y < y1; y += 2) {
+            tail_hpair(row(y + 4), row(y + 5), cq, V[4]);  // pair m + 4
+#pragma unroll
+            for (int o = 0; o < 2; ++o) {
+                uint32_t sv[4];
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    uint32_t acc = 1u << 15;
+#pragma unroll
+                    for (int k = 0; k < 4; ++k)
+                        acc = __builtin_amdgcn_udot2(as_u16x2(V[o + k][c]), o ? WO[k] : WE[k], acc, false);
+                    sv[c] = acc;
+                }
+                const uint32_t lo = __builtin_amdgcn_perm(sv[1], sv[0], 0x0c0c0602u);
+                const uint32_t hi = __builtin_amdgcn_perm(sv[3], sv[2], 0x0c0c0602u);
+                if (y + o < y1) *reinterpret_cast<uint32_t*>(d + o * G.bpitch) = lo | (hi << 16);
+            }
+            d += 2 * G.bpitch;
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int c = 0; c < 4; ++c) V[j][c] = V[j + 1][c];
+        }
+    }
+}
+
+__global__ __launch_bounds__(kTailThreads) void k_pyr_tail(BatchArgs a) {
+    extern __shared__ uint4 tail_lds[];
+    uint8_t* lds = reinterpret_cast<uint8_t*>(tail_lds);
+    const int img = a.img0 + blockIdx.x;
+    const int s0 = a.tail0 - 1, L = a.nlevels;
+    // buffers as offsets from the LDS base (an array of pointers would decay to generic
+    // pointers: flat accesses, which fault on the 4-byte-aligned 12-byte row reads)
+    auto buf = [&](int k) { return lds + (k ? a.tail_buf1 : 0); };
+    int4* xsel = reinterpret_cast<int4*>(lds + a.tail_tab);
+    int4* xcw = xsel + a.tail_maxq;
+    int4* yts = xcw + a.tail_maxq;
+    int* xbase = reinterpret_cast<int*>(yts + a.tail_maxrows);
+    {   // level s0 from HBM (16-byte loads, 16-byte aligned LDS rows)
+        const LevelGeom S = a.lv[s0];
+        const uint8_t* src = a.lvl_base[s0] + (long long)img * S.img_stride;
+        const int nch = (S.w + 15) >> 4, P = S.tpitch;
+        for (int i = threadIdx.x; i < nch * S.h; i += kTailThreads) {
+            const int y = i / nch, c = i - y * nch;
+            *reinterpret_cast<uint4*>(buf(0) + __mul24(y, P) + kTailPad + 16 * c) =
+                *reinterpret_cast<const uint4*>(src + plane_off(y, S.pitch, 16 * c));
+        }
+        __syncthreads();
+        tail_fill_pads(buf(0), P, S.w, S.h);
+        __syncthreads();
+    }
+    for (int s = s0; s < L; ++s) {
+        const LevelGeom S = a.lv[s];
+        const uint8_t* cur = buf((s - s0) & 1);
+        const bool resize = s + 1 < L;
+        const LevelGeom G = a.lv[resize ? s + 1 : s];
+        const int nq = (G.w + 3) >> 2;
+        if (resize && !G.area2) {  // level s + 1's quad and row coefficients (as br_tile)
+            for (int q = threadIdx.x; q < nq; q += kTailThreads) {
+                int4 xx[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) xx[k] = a.rtab[G.xtab_off + min(4 * q + k, G.w - 1)];
+                const int base = xx[0].x;
+                int sl[4], cl[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    sl[k] = (xx[k].x - base) | 0x0c00 | ((xx[k].y - base) << 16) | 0x0c000000;
+                    cl[k] = (xx[k].z << 4) | (xx[k].w << 20);
+                }
+                xsel[q] = make_int4(sl[0], sl[1], sl[2], sl[3]);
+                xcw[q] = make_int4(cl[0], cl[1], cl[2], cl[3]);
+                xbase[q] = base;
+            }
+            for (int r = threadIdx.x; r < G.h; r += kTailThreads) {
+                const int4 y = a.rtab[G.ytab_off + r];
+                yts[r] = make_int4(y.x, y.y, y.z << 8, y.w << 8);
+            }
+        }
+        tail_blur(cur, S.tpitch, S, a.blur_base[s] + (long long)img * S.bimg_stride);
+        if (!resize) break;
+        __syncthreads();  // coefficient tables
+        uint8_t* nxt = buf((s + 1 - s0) & 1);
+        uint8_t* dst = a.lvl_base[s + 1] + (long long)img * G.img_stride;
+        const uint8_t* rowp = cur + kTailPad;
+        // thread -> (quad q, rows dy0, dy0 + step, ...): one division per level
+        const int step = max(kTailThreads / nq, 1);
+        const int q = (int)threadIdx.x % nq, dyt = (int)threadIdx.x / nq;
+        for (int dy = dyt; dy < G.h && dyt < step; dy += step) {
+            const int dx0 = 4 * q;
+            uint32_t packed = 0;
+            if (G.area2) {
+                const uint8_t* s0r = rowp + __mul24(2 * dy, S.tpitch);
+                const uint8_t* s1r = s0r + S.tpitch;
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk) {
+                    const int dx = min(dx0 + kk, G.w - 1);
+                    const int o = (s0r[2 * dx] + s0r[2 * dx + 1] + s1r[2 * dx] + s1r[2 * dx + 1] + 2) >> 2;
+                    packed |= (uint32_t)o << (8 * kk);
+                }
+            } else {
+                const int4 yt = yts[dy];
+                packed = rs_quad(rowp + __mul24(yt.x, S.tpitch), rowp + __mul24(yt.y, S.tpitch), xbase[q], xsel[q],
+                                 xcw[q], yt.z, yt.w, dx0, G.simd_end);
+            }
+            *reinterpret_cast<uint32_t*>(nxt + __mul24(dy, G.tpitch) + kTailPad + dx0) = packed;
+            *reinterpret_cast<uint32_t*>(dst + plane_off(dy, G.pitch, dx0)) = packed;
+        }
+        __syncthreads();  // level s + 1 complete in LDS; level s's buffer and the tables are free
+        tail_fill_pads(nxt, G.tpitch, G.w, G.h);
+        __syncthreads();
+    }
+}
+
+hipError_t launch_pyr_tail(const BatchArgs& a, hipStream_t s) {
+    // the dynamic-LDS limit is raised once per size and device (see launch_octree)
+    constexpr int kMaxDevices = 64;
+    static std::atomic<int> lds_set[kMaxDevices];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) dev = kMaxDevices - 1;
+    if (a.tail_lds > 65536 && a.tail_lds > lds_set[dev].load()) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k_pyr_tail),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, a.tail_lds);
+        if (e != hipSuccess) return e;
+        int cur = lds_set[dev].load();
+        while (a.tail_lds > cur && !lds_set[dev].compare_exchange_weak(cur, a.tail_lds)) {}
+    }
+    hipLaunchKernelGGL(k_pyr_tail, dim3(a.nimages), dim3(kTailThreads), a.tail_lds, s, a);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
 // k_fast_cells: one workgroup per (level, cell), image = blockIdx.y.  Restates the cell loop of
 // ComputeKeyPointsOctTree (ORBextractor_old.cc:807-871) with cv::FAST(cell, kps, th, true):
 // detection on [3,rows-3)x[3,cols-3) of the cell ROI, 3x3 nonmax inside the cell only, iniTh
@@ -503,7 +710,7 @@ __global__ __launch_bounds__(kFastThreads) void k_fast_cells(BatchArgs a, int ce
     __shared__ __attribute__((aligned(16))) uint8_t M[CP * CP];  // 16-byte rows when CP % 16 == 0
     __shared__ __attribute__((aligned(8))) uint16_t list[kList + fast_list_slack(kFastThreads / 64)];
     __shared__ uint2 lut[16];
-    __shared__ uint8_t emask[32];
+    __shared__ uint32_t emask[32];
     __shared__ int32_t wcnt[kFastThreads / 64];
     __shared__ int scratch[16];
     const int wg = xcd_remap(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * gridDim.y);

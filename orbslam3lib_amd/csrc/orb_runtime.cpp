@@ -42,7 +42,7 @@ const char* const kDiagKnobs[] = {"ORBGPU_OD_ITERS",      "ORBGPU_OCT_SMALL_LDS"
                                   "ORBGPU_OCT_SPLIT",     "ORBGPU_OCT_GENERIC",   "ORBGPU_OCT_PYR",
                                   "ORBGPU_FAST_PITCH",    "ORBGPU_STREAMS",       "ORBGPU_ISOLATE",
                                   "ORBGPU_STAGGER",       "ORBGPU_OCT_STAMPS",    "ORBGPU_GRAPH",
-                                  "ORBGPU_KNN_NOSPLIT"};
+                                  "ORBGPU_KNN_NOSPLIT",   "ORBGPU_NO_TAIL"};
 
 bool diagnostics_on() {
     const char* g = getenv("ORBGPU_DIAGNOSTICS");
@@ -93,13 +93,13 @@ int check_single_hip_runtime() {
     } while (0)
 
 enum Stage { ST_RESIZE, ST_BLUR, ST_FAST48, ST_FAST, ST_FAST_TOP, ST_OCTREE, ST_ORIENT, ST_FINAL, ST_KNN,
-             ST_STEREO, ST_GRID, ST_SBS, ST_SOA, ST_SBP, ST_FISHEYE, ST_COUNT };
+             ST_STEREO, ST_GRID, ST_SBS, ST_SOA, ST_SBP, ST_FISHEYE, ST_TAIL, ST_COUNT };
 // names as rocprofv3 shows the kernels (templates with their argument)
 const char* kStageNames[ST_COUNT] = {"k_blur_resize",    "k_blur",   "k_fast_cells<48>", "k_fast_cells<64>",
                                      "k_fast_cells<80>", "k_octree", "k_orient_desc",    "k_finalize",
                                      "k_knn2",           "k_stereo",  "k_undistort_grid",
                                      "k_sbs_split",      "k_pack_soa",       "k_sbp",
-                                     "k_fisheye_stereo"};
+                                     "k_fisheye_stereo", "k_pyr_tail"};
 
 struct DevBuf {
     void* p = nullptr;
@@ -440,6 +440,28 @@ int set_geometry(orbgpu_ctx* c, int w, int h) {
             G.tile_quad_off = push_ints(tq);
         }
     }
+    // k_pyr_tail: the smallest t >= 2 such that level t - 1 and level t (and level t's resize
+    // tables) fit one workgroup's LDS together; the tail then makes levels t .. L-1 and blurs
+    // t - 1 .. L-1 (ORBGPU_NO_TAIL under diagnostics: per-level launches only)
+    for (int l = 0; l < L; ++l) A.lv[l].tpitch = round_up(A.lv[l].w + 28, 16);
+    A.tail0 = L + 1;
+    if (!diag_env("ORBGPU_NO_TAIL"))
+        for (int t = 2; t <= L; ++t) {
+            const LevelGeom& S0 = A.lv[t - 1];
+            const long long b0 = round_up_ll((long long)S0.tpitch * S0.h, 16);
+            const long long b1 = t < L ? round_up_ll((long long)A.lv[t].tpitch * A.lv[t].h, 16) : 0;
+            const int maxq = t < L ? (A.lv[t].w + 3) / 4 : 0, maxrows = t < L ? A.lv[t].h : 0;
+            const long long tab = (long long)maxq * (16 + 16 + 4) + (long long)maxrows * 16;
+            if (b0 + b1 + tab + 16 <= kTailLdsMax && (S0.w + 3) / 4 <= 1024) {  // one resize quad per thread
+                A.tail0 = t;
+                A.tail_buf1 = (int)b0;
+                A.tail_tab = (int)(b0 + b1);
+                A.tail_maxq = maxq;
+                A.tail_maxrows = maxrows;
+                A.tail_lds = (int)round_up_ll(b0 + b1 + tab, 16);
+                break;
+            }
+        }
     c->pyr_img = round_up_ll(pyr, 256);
     c->blur_img = round_up_ll(blr, 256);
     c->cellkeys_img = ck;
@@ -1044,6 +1066,9 @@ static int run_batch_impl(orbgpu_ctx* c, int n, int w, int h, const int32_t* lap
     // the kernel sequence of this batch (every launch goes to the chunk streams)
     auto launch_all = [&]() -> int {
         int r = 0;
+        // k_blur_resize makes levels 1 .. last_br - 1; k_pyr_tail the rest (or k_blur the last blur)
+        const bool tail = A.tail0 <= A.nlevels;
+        const int last_br = tail ? A.tail0 : A.nlevels;
         if (stagger) {
             // chunk-major: chunk k's first kernel waits for chunk k-1's pyramid + blur
             for (size_t k = 0; k < chunks.size(); ++k) {
@@ -1052,20 +1077,28 @@ static int run_batch_impl(orbgpu_ctx* c, int n, int w, int h, const int32_t* lap
                 B.img0 = ch.img0;
                 B.nimages = ch.n;
                 if (k > 0) HIP_TRY(hipStreamWaitEvent(ch.st, c->stagger_ev[k - 1], 0));
-                for (int l = 1; l < A.nlevels; ++l)
+                for (int l = 1; l < last_br; ++l)
                     if ((r = timed(c, ST_RESIZE, ch.st, [&] { return launch_blur_resize(B, l, ch.st); }))) return r;
-                const int lt = A.nlevels - 1;
-                if ((r = timed(c, ST_BLUR, ch.st, [&] { return launch_blur_level(B, lt, ch.st); }))) return r;
+                if (tail) {
+                    if ((r = timed(c, ST_TAIL, ch.st, [&] { return launch_pyr_tail(B, ch.st); }))) return r;
+                } else {
+                    const int lt = A.nlevels - 1;
+                    if ((r = timed(c, ST_BLUR, ch.st, [&] { return launch_blur_level(B, lt, ch.st); }))) return r;
+                }
                 HIP_TRY(hipEventRecord(c->stagger_ev[k], ch.st));
             }
         } else {
             // level l - 1's blur and level l in one pass over level l - 1, then the last level's blur
-            for (int l = 1; l < A.nlevels; ++l) {
+            for (int l = 1; l < last_br; ++l) {
                 r = each(ST_RESIZE, [&](const BatchArgs& B, hipStream_t st) { return launch_blur_resize(B, l, st); });
                 if (r) return r;
             }
-            const int lt = A.nlevels - 1;
-            if ((r = each(ST_BLUR, [&](const BatchArgs& B, hipStream_t st) { return launch_blur_level(B, lt, st); }))) return r;
+            if (tail) {
+                if ((r = each(ST_TAIL, [](const BatchArgs& B, hipStream_t st) { return launch_pyr_tail(B, st); }))) return r;
+            } else {
+                const int lt = A.nlevels - 1;
+                if ((r = each(ST_BLUR, [&](const BatchArgs& B, hipStream_t st) { return launch_blur_level(B, lt, st); }))) return r;
+            }
         }
         {   // the FAST tiles as one group: one join / fork around all of them when isolated
             const int tiles[3] = {kCellPitchTiny, kCellPitchSmall, kCellMax};

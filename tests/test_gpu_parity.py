@@ -340,18 +340,28 @@ def _check_pyramid(ex, oracle, imgs, sf=1.2, L=8):
                                           err_msg="img %d blur level %d" % (i, l))
 
 
-def test_pyramid_per_level_path(oracle):
-    """The per-level k_blur_resize launches + the last level's k_blur: pyramid and blurred levels
-    of a stereo pair."""
+@pytest.mark.parametrize("tail", [True, False])
+def test_pyramid_per_level_path(oracle, monkeypatch, tail):
+    """The per-level k_blur_resize launches then k_pyr_tail (levels 5-7 and the blurs of 4-7 of
+    a 640x480 pyramid in one launch) -- or, with the tail off (ORBGPU_NO_TAIL), k_blur_resize for
+    every level and k_blur for the last: pyramid and blurred levels of a stereo pair."""
+    if not tail:
+        monkeypatch.setenv("ORBGPU_DIAGNOSTICS", "1")
+        monkeypatch.setenv("ORBGPU_NO_TAIL", "1")
     L, R = synth.stereo_pair(480, 640, 3)
     ex = _extractor()
     ex.extract_stereo(L, R)
     _check_pyramid(ex, oracle, [L, R])
 
 
-def test_pyramid_exact_2x_area_path(oracle):
+@pytest.mark.parametrize("tail", [True, False])
+def test_pyramid_exact_2x_area_path(oracle, monkeypatch, tail):
     """Scale factor 2 on a 640x480 frame: every level is an exact 2x downscale, which OpenCV
-    serves with INTER_AREA (2x2 mean) instead of INTER_LINEAR (k_blur_resize's area path)."""
+    serves with INTER_AREA (2x2 mean) instead of INTER_LINEAR (the area path of k_blur_resize
+    for level 1 and of k_pyr_tail for level 2; with the tail off, k_blur_resize's for both)."""
+    if not tail:
+        monkeypatch.setenv("ORBGPU_DIAGNOSTICS", "1")
+        monkeypatch.setenv("ORBGPU_NO_TAIL", "1")
     img = synth.frame(480, 640, 6)
     ex = _extractor(nf=500, L=3, sf=2.0)
     k, d, m = ex(img)
