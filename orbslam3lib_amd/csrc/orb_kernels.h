@@ -10,6 +10,15 @@ constexpr int kMaxLevels = 16;
 constexpr int kMinBorder = 16;   // EDGE_THRESHOLD - 3 (ORBextractor_old.cc:791)
 constexpr int kEdge = 19;        // EDGE_THRESHOLD (:75)
 
+// XCD-aware block order (cdna_hip_programming.md T1, bijective form): the dispatcher places
+// block b on XCD b % 8, so a grid walked in (b % 8, b / 8) order gives every XCD one
+// contiguous range of work -- neighbouring cells / tiles of one image then share that XCD's L2
+// instead of being fetched once per XCD.  Speed only: any placement stays correct.
+__device__ inline int xcd_remap(int orig, int nwg) {
+    const int xcd = orig % 8, q = nwg / 8, r = nwg % 8;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
+}
+
 // Per-level geometry, computed on the host (orb_runtime.cpp) from the reference formulas.
 struct LevelGeom {
     int w, h, pitch;           // plane size; pitch in bytes (level 0: the input's row stride)
@@ -91,6 +100,13 @@ struct BatchArgs {
     // (tail0 = nlevels + 1: no tail, k_blur_resize for every level and k_blur for the last)
     int tail0;
     int tail_lds, tail_buf1, tail_tab, tail_maxq, tail_maxrows;  // its LDS layout (bytes / entries)
+    // k_fast_bands (orb_fast.hip): records {level, cell row, first cell, end cell} at rtab index
+    // fast_band_off, grouped by workgroup width: [fast_band_grp[w-1], fast_band_grp[w]) run w waves
+    // with fast_band_lds[w-1] bytes of dynamic LDS
+    int fast_dense;                  // 1: k_fast_bands; 0: k_fast_cells (diagnostics)
+    int fast_band_off;
+    int fast_band_grp[5];
+    int fast_band_lds[4];
 };
 
 struct MatchArgs {
@@ -232,6 +248,8 @@ hipError_t launch_pyr_tail(const BatchArgs& a, hipStream_t s);
 // fast_cell_range gives their flattened cell range, launch_fast_cells launches nothing if empty
 void fast_cell_range(const BatchArgs& a, int tile, int* c0, int* c1);
 hipError_t launch_fast_cells(const BatchArgs& a, int tile, hipStream_t s);
+constexpr int kFastBandMaxWaves = 4;  // k_fast_bands: widest segment (62 owned quads per wave)
+hipError_t launch_fast_bands(const BatchArgs& a, hipStream_t s);  // orb_fast.hip
 hipError_t launch_octree(const BatchArgs& a, hipStream_t s);
 hipError_t launch_orient_desc(const BatchArgs& a, hipStream_t s);
 hipError_t launch_finalize(const BatchArgs& a, hipStream_t s);

@@ -31,15 +31,6 @@ namespace orbgpu {
 
 static_assert(sizeof(BatchArgs) <= 4096, "kernel argument block too large");
 
-// XCD-aware block order (cdna_hip_programming.md T1, bijective form): the dispatcher places
-// block b on XCD b % 8, so a grid walked in (b % 8, b / 8) order gives every XCD one
-// contiguous range of work -- neighbouring cells / tiles of one image then share that XCD's L2
-// instead of being fetched once per XCD.  Speed only: any placement stays correct.
-__device__ inline int xcd_remap(int orig, int nwg) {
-    const int xcd = orig % 8, q = nwg / 8, r = nwg % 8;
-    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
-}
-
 // rBRIEF pattern decoded at compile time from the hex data: 256 pairs (x0,y0,x1,y1) int8.
 struct PatternTable {
     int8_t v[1024];

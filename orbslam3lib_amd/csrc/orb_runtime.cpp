@@ -42,7 +42,8 @@ const char* const kDiagKnobs[] = {"ORBGPU_OD_ITERS",      "ORBGPU_OCT_SMALL_LDS"
                                   "ORBGPU_OCT_SPLIT",     "ORBGPU_OCT_GENERIC",   "ORBGPU_OCT_PYR",
                                   "ORBGPU_FAST_PITCH",    "ORBGPU_STREAMS",       "ORBGPU_ISOLATE",
                                   "ORBGPU_STAGGER",       "ORBGPU_OCT_STAMPS",    "ORBGPU_GRAPH",
-                                  "ORBGPU_KNN_NOSPLIT",   "ORBGPU_NO_TAIL"};
+                                  "ORBGPU_KNN_NOSPLIT",   "ORBGPU_NO_TAIL",
+                                  "ORBGPU_FAST_BANDS"};
 
 bool diagnostics_on() {
     const char* g = getenv("ORBGPU_DIAGNOSTICS");
@@ -93,13 +94,13 @@ int check_single_hip_runtime() {
     } while (0)
 
 enum Stage { ST_RESIZE, ST_BLUR, ST_FAST48, ST_FAST, ST_FAST_TOP, ST_OCTREE, ST_ORIENT, ST_FINAL, ST_KNN,
-             ST_STEREO, ST_GRID, ST_SBS, ST_SOA, ST_SBP, ST_FISHEYE, ST_TAIL, ST_COUNT };
+             ST_STEREO, ST_GRID, ST_SBS, ST_SOA, ST_SBP, ST_FISHEYE, ST_TAIL, ST_FASTB, ST_COUNT };
 // names as rocprofv3 shows the kernels (templates with their argument)
 const char* kStageNames[ST_COUNT] = {"k_blur_resize",    "k_blur",   "k_fast_cells<48>", "k_fast_cells<64>",
                                      "k_fast_cells<80>", "k_octree", "k_orient_desc",    "k_finalize",
                                      "k_knn2",           "k_stereo",  "k_undistort_grid",
                                      "k_sbs_split",      "k_pack_soa",       "k_sbp",
-                                     "k_fisheye_stereo", "k_pyr_tail"};
+                                     "k_fisheye_stereo", "k_pyr_tail", "k_fast_bands"};
 
 struct DevBuf {
     void* p = nullptr;
@@ -570,6 +571,54 @@ int set_geometry(orbgpu_ctx* c, int w, int h) {
     }
     A.fast_n48 = tier_end[0];
     A.fast_n64 = tier_end[1];
+    // k_fast_bands segments: each cell row of a level split into runs of whole cells at most
+    // kFastBandMaxWaves x 62 column quads wide (every cell's detection pixels in one workgroup)
+    // k_fast_bands (dense, threshold-independent; bit-exact) measured slower than the sparse
+    // per-cell kernel on gfx950: diagnostics only
+    A.fast_dense = diag_env("ORBGPU_FAST_BANDS") ? 1 : 0;
+    {
+        std::vector<int4> recs[kFastBandMaxWaves];
+        int lds[kFastBandMaxWaves] = {0, 0, 0, 0};
+        for (int l = 0; l < L; ++l) {
+            const LevelGeom& G = A.lv[l];
+            auto x0 = [&](int j) { return kMinBorder + j * G.wCell + 3; };
+            auto x1 = [&](int j) {
+                const int iniX = kMinBorder + j * G.wCell;
+                return iniX >= G.maxBX - 6 ? x0(j) : std::min(iniX + G.wCell + 6, G.maxBX) - 3;
+            };
+            for (int i = 0; i < G.nRows; ++i) {
+                const int iniY = kMinBorder + i * G.hCell;
+                const int nrows = iniY >= G.maxBY - 3 ? 0 : std::max(std::min(iniY + G.hCell + 6, G.maxBY) - 6 - iniY, 0);
+                int j0 = 0;
+                while (j0 < G.nCols) {
+                    auto quads = [&](int ja, int jb) {
+                        int xe = x0(ja);
+                        for (int j = ja; j < jb; ++j) xe = std::max(xe, x1(j));
+                        return xe > x0(ja) ? ((xe - 1) >> 2) - (x0(ja) >> 2) + 1 : 0;
+                    };
+                    int j1 = j0 + 1;
+                    while (j1 < G.nCols && quads(j0, j1 + 1) <= 62 * kFastBandMaxWaves) ++j1;
+                    const int nq = quads(j0, j1);
+                    const int nw = std::max(1, (nq + 61) / 62);
+                    if (nw > kFastBandMaxWaves) return fail(ORBGPU_ERR_INVALID, "FAST band segment too wide");
+                    recs[nw - 1].push_back(make_int4(l, i, j0, j1));
+                    const int bytes = 4 * (16 * ((j1 - j0 + 15) / 16) + nrows * nq);
+                    lds[nw - 1] = std::max(lds[nw - 1], bytes);
+                    j0 = j1;
+                }
+            }
+        }
+        A.fast_band_off = (int)c->rtab_host.size();
+        int n = 0;
+        A.fast_band_grp[0] = 0;
+        for (int w = 0; w < kFastBandMaxWaves; ++w) {
+            for (const int4& r4 : recs[w]) c->rtab_host.push_back(r4);
+            n += (int)recs[w].size();
+            A.fast_band_grp[w + 1] = n;
+            A.fast_band_lds[w] = (lds[w] + 15) & ~15;
+            if (A.fast_band_lds[w] > kTailLdsMax) return fail(ORBGPU_ERR_INVALID, "FAST band LDS");
+        }
+    }
     A.total_tiles = tile_first;
     A.total_od_blocks = od_first;
     A.od_tab_off = (int)c->rtab_host.size();
@@ -1100,7 +1149,9 @@ static int run_batch_impl(orbgpu_ctx* c, int n, int w, int h, const int32_t* lap
                 if ((r = each(ST_BLUR, [&](const BatchArgs& B, hipStream_t st) { return launch_blur_level(B, lt, st); }))) return r;
             }
         }
-        {   // the FAST tiles as one group: one join / fork around all of them when isolated
+        if (A.fast_dense) {
+            if ((r = each(ST_FASTB, [](const BatchArgs& B, hipStream_t st) { return launch_fast_bands(B, st); }))) return r;
+        } else {   // the FAST tiles as one group: one join / fork around all of them when isolated
             const int tiles[3] = {kCellPitchTiny, kCellPitchSmall, kCellMax};
             const int stages[3] = {ST_FAST48, ST_FAST, ST_FAST_TOP};
             bool any[3], iso = false;

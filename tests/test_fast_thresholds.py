@@ -23,8 +23,14 @@ def _frames():
 
 
 @pytest.mark.parametrize("ini,mn", THRESHOLDS)
-def test_fast_threshold_range(oracle, ini, mn):
+@pytest.mark.parametrize("bands", [False, True])
+def test_fast_threshold_range(oracle, monkeypatch, ini, mn, bands):
+    """k_fast_cells, and the dense k_fast_bands (ORBGPU_FAST_BANDS, orb_fast.hip: one strength
+    pass, the threshold applied at emission) over the same range."""
     import orbslam3lib_amd as og
+    if bands:
+        monkeypatch.setenv("ORBGPU_DIAGNOSTICS", "1")
+        monkeypatch.setenv("ORBGPU_FAST_BANDS", "1")
     imgs = _frames()
     be = og.BatchExtractor(2000, 1.2, 8, ini, mn, width=W, height=H, max_images=len(imgs))
     be.upload(imgs)
