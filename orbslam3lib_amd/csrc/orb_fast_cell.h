@@ -18,6 +18,9 @@
 #ifndef FAST_VAR
 #define FAST_VAR 0
 #endif
+#ifndef FAST_SINK
+#define FAST_SINK 0
+#endif
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -122,7 +125,7 @@ struct CellScratch {
 // List entries past cell_list_cap on the device: each wave's list is followed by 4 spare
 // entries (the compaction writes 4 slots per lane, the ones past the lane's candidates are
 // overwritten by later lanes or land in the spare entries), then 4 sink entries.
-__host__ __device__ constexpr int fast_list_slack(int waves) { return 4 * waves + 4; }
+__host__ __device__ constexpr int fast_list_slack(int waves) { return 4 * waves + (FAST_SINK == 2 ? 512 : 4); }
 
 // Builds CellScratch's lut / emask tables (threads < 16 and < ng); the caller syncs before
 // fast_cell_detect.
@@ -309,6 +312,28 @@ __host__ __device__ int fast_cell_detect(Pol& p, int sh, const CellGeom& g, int 
                 const uint2 lv = cs.lut[m4];
                 const uint32_t e01 = __umul24((uint32_t)(4 * dw), 0x10001u) + lv.x;  // v_mad_u32_u24
                 const uint32_t e23 = __umul24((uint32_t)(4 * dw), 0x10001u) + lv.y;
+#if FAST_SINK == 1  // measurement variant: lanes without candidates write nothing
+                if (c) {
+                    uint16_t* d = list + pos;
+                    d[3] = (uint16_t)(e23 >> 16);
+                    asm volatile("" ::: "memory");
+                    d[2] = (uint16_t)e23;
+                    asm volatile("" ::: "memory");
+                    d[1] = (uint16_t)(e01 >> 16);
+                    asm volatile("" ::: "memory");
+                    d[0] = (uint16_t)e01;
+                }
+#elif FAST_SINK == 2  // measurement variant: one sink column per lane (no shared address)
+                uint16_t* d = c ? list + pos : sink + 2 * lane;
+                const int st = c ? 1 : 128;
+                d[3 * st] = (uint16_t)(e23 >> 16);
+                asm volatile("" ::: "memory");
+                d[2 * st] = (uint16_t)e23;
+                asm volatile("" ::: "memory");
+                d[st] = (uint16_t)(e01 >> 16);
+                asm volatile("" ::: "memory");
+                d[0] = (uint16_t)e01;
+#else
                 uint16_t* d = c ? list + pos : sink;
                 d[3] = (uint16_t)(e23 >> 16);
                 asm volatile("" ::: "memory");  // keep the slot order (k = 3 .. 0)
@@ -317,6 +342,7 @@ __host__ __device__ int fast_cell_detect(Pol& p, int sh, const CellGeom& g, int 
                 d[1] = (uint16_t)(e01 >> 16);
                 asm volatile("" ::: "memory");
                 d[0] = (uint16_t)e01;
+#endif
                 na += p.popc64(b0) + 2 * p.popc64(b1) + 4 * p.popc64(b2);
                 q += dq;
                 dw += ddw;
