@@ -103,7 +103,8 @@ struct BatchArgs {
     // k_fast_bands (orb_fast.hip): records {level, cell row, first cell, end cell} at rtab index
     // fast_band_off, grouped by workgroup width: [fast_band_grp[w-1], fast_band_grp[w]) run w waves
     // with fast_band_lds[w-1] bytes of dynamic LDS
-    int fast_dense;                  // 1: k_fast_bands; 0: k_fast_cells (diagnostics)
+    int fast_dense;                  // 0: k_fast_cells, 1: k_fast_bands, 2: k_fast_sb
+    int fast_sb_off, fast_sb_n;      // k_fast_sb records {level, cell row, first cell, end cell}
     int fast_band_off;
     int fast_band_grp[5];
     int fast_band_lds[4];
@@ -250,6 +251,7 @@ void fast_cell_range(const BatchArgs& a, int tile, int* c0, int* c1);
 hipError_t launch_fast_cells(const BatchArgs& a, int tile, hipStream_t s);
 constexpr int kFastBandMaxWaves = 4;  // k_fast_bands: widest segment (62 owned quads per wave)
 hipError_t launch_fast_bands(const BatchArgs& a, hipStream_t s);  // orb_fast.hip
+hipError_t launch_fast_sb(const BatchArgs& a, hipStream_t s);     // orb_fast.hip
 hipError_t launch_octree(const BatchArgs& a, hipStream_t s);
 hipError_t launch_orient_desc(const BatchArgs& a, hipStream_t s);
 hipError_t launch_finalize(const BatchArgs& a, hipStream_t s);

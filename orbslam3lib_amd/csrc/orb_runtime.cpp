@@ -43,7 +43,7 @@ const char* const kDiagKnobs[] = {"ORBGPU_OD_ITERS",      "ORBGPU_OCT_SMALL_LDS"
                                   "ORBGPU_FAST_PITCH",    "ORBGPU_STREAMS",       "ORBGPU_ISOLATE",
                                   "ORBGPU_STAGGER",       "ORBGPU_OCT_STAMPS",    "ORBGPU_GRAPH",
                                   "ORBGPU_KNN_NOSPLIT",   "ORBGPU_NO_TAIL",
-                                  "ORBGPU_FAST_BANDS"};
+                                  "ORBGPU_FAST_BANDS",    "ORBGPU_FAST_SB"};
 
 bool diagnostics_on() {
     const char* g = getenv("ORBGPU_DIAGNOSTICS");
@@ -94,13 +94,13 @@ int check_single_hip_runtime() {
     } while (0)
 
 enum Stage { ST_RESIZE, ST_BLUR, ST_FAST48, ST_FAST, ST_FAST_TOP, ST_OCTREE, ST_ORIENT, ST_FINAL, ST_KNN,
-             ST_STEREO, ST_GRID, ST_SBS, ST_SOA, ST_SBP, ST_FISHEYE, ST_TAIL, ST_FASTB, ST_COUNT };
+             ST_STEREO, ST_GRID, ST_SBS, ST_SOA, ST_SBP, ST_FISHEYE, ST_TAIL, ST_FASTB, ST_FASTSB, ST_COUNT };
 // names as rocprofv3 shows the kernels (templates with their argument)
 const char* kStageNames[ST_COUNT] = {"k_blur_resize",    "k_blur",   "k_fast_cells<48>", "k_fast_cells<64>",
                                      "k_fast_cells<80>", "k_octree", "k_orient_desc",    "k_finalize",
                                      "k_knn2",           "k_stereo",  "k_undistort_grid",
                                      "k_sbs_split",      "k_pack_soa",       "k_sbp",
-                                     "k_fisheye_stereo", "k_pyr_tail", "k_fast_bands"};
+                                     "k_fisheye_stereo", "k_pyr_tail", "k_fast_bands", "k_fast_sb"};
 
 struct DevBuf {
     void* p = nullptr;
@@ -575,7 +575,7 @@ int set_geometry(orbgpu_ctx* c, int w, int h) {
     // kFastBandMaxWaves x 62 column quads wide (every cell's detection pixels in one workgroup)
     // k_fast_bands (dense, threshold-independent; bit-exact) measured slower than the sparse
     // per-cell kernel on gfx950: diagnostics only
-    A.fast_dense = diag_env("ORBGPU_FAST_BANDS") ? 1 : 0;
+    A.fast_dense = diag_env("ORBGPU_FAST_BANDS") ? 1 : diag_env("ORBGPU_FAST_SB") ? 2 : 0;
     {
         std::vector<int4> recs[kFastBandMaxWaves];
         int lds[kFastBandMaxWaves] = {0, 0, 0, 0};
@@ -608,6 +608,32 @@ int set_geometry(orbgpu_ctx* c, int w, int h) {
                 }
             }
         }
+        // k_fast_sb: one wave per run of whole cells spanning at most 62 column quads
+        std::vector<int4> sb;
+        for (int l = 0; l < L; ++l) {
+            const LevelGeom& G = A.lv[l];
+            auto x0 = [&](int j) { return kMinBorder + j * G.wCell + 3; };
+            auto x1 = [&](int j) {
+                const int iniX = kMinBorder + j * G.wCell;
+                return iniX >= G.maxBX - 6 ? x0(j) : std::min(iniX + G.wCell + 6, G.maxBX) - 3;
+            };
+            auto quads = [&](int ja, int jb) {
+                int xe = x0(ja);
+                for (int j = ja; j < jb; ++j) xe = std::max(xe, x1(j));
+                return xe > x0(ja) ? ((xe - 1) >> 2) - (x0(ja) >> 2) + 1 : 0;
+            };
+            for (int i = 0; i < G.nRows; ++i)
+                for (int ja = 0; ja < G.nCols;) {
+                    int jb = ja + 1;
+                    while (jb < G.nCols && jb - ja < 8 && quads(ja, jb + 1) <= 62) ++jb;
+                    if (quads(ja, jb) > 62) return fail(ORBGPU_ERR_INVALID, "FAST cell wider than a wave");
+                    sb.push_back(make_int4(l, i, ja, jb));
+                    ja = jb;
+                }
+        }
+        A.fast_sb_off = (int)c->rtab_host.size();
+        A.fast_sb_n = (int)sb.size();
+        c->rtab_host.insert(c->rtab_host.end(), sb.begin(), sb.end());
         A.fast_band_off = (int)c->rtab_host.size();
         int n = 0;
         A.fast_band_grp[0] = 0;
@@ -1149,7 +1175,9 @@ static int run_batch_impl(orbgpu_ctx* c, int n, int w, int h, const int32_t* lap
                 if ((r = each(ST_BLUR, [&](const BatchArgs& B, hipStream_t st) { return launch_blur_level(B, lt, st); }))) return r;
             }
         }
-        if (A.fast_dense) {
+        if (A.fast_dense == 2) {
+            if ((r = each(ST_FASTSB, [](const BatchArgs& B, hipStream_t st) { return launch_fast_sb(B, st); }))) return r;
+        } else if (A.fast_dense == 1) {
             if ((r = each(ST_FASTB, [](const BatchArgs& B, hipStream_t st) { return launch_fast_bands(B, st); }))) return r;
         } else {   // the FAST tiles as one group: one join / fork around all of them when isolated
             const int tiles[3] = {kCellPitchTiny, kCellPitchSmall, kCellMax};

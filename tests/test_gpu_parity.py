@@ -167,13 +167,13 @@ def test_euroc_size_and_other_frames(oracle):
         np.testing.assert_array_equal(g[1], r[1])
 
 
-@pytest.mark.parametrize("bands", [False, True])
-def test_c5_1080p_12_levels(oracle, monkeypatch, bands):
-    """C5's frame; with ORBGPU_FAST_BANDS its 1882-px level 0 splits each cell row into two
-    k_fast_bands segments (four waves each)."""
-    if bands:
+@pytest.mark.parametrize("kernel", ["cells", "sb", "bands"])
+def test_c5_1080p_12_levels(oracle, monkeypatch, kernel):
+    """C5's frame through each FAST kernel; its 1882-px level 0 splits every cell row into
+    eight k_fast_sb waves and two k_fast_bands segments (four waves each)."""
+    if kernel != "cells":
         monkeypatch.setenv("ORBGPU_DIAGNOSTICS", "1")
-        monkeypatch.setenv("ORBGPU_FAST_BANDS", "1")
+        monkeypatch.setenv("ORBGPU_FAST_SB" if kernel == "sb" else "ORBGPU_FAST_BANDS", "1")
     img = synth.frame(1080, 1920, 2)
     ex = _extractor(nf=5000, L=12, w=1920, h=1080)
     g = ex(img, None, (0, 0))
@@ -313,13 +313,14 @@ def test_forced_fast_tile(oracle, frame0, monkeypatch, pitch):
     np.testing.assert_array_equal(d, rd)
 
 
-@pytest.mark.parametrize("bands", [False, True])
-def test_general_fast_tile_small_frame(oracle, monkeypatch, bands):
-    """A small frame (cells wider than 55 px on its top levels): k_fast_cells picks its 80-byte
-    tile by itself there; the dense k_fast_bands (ORBGPU_FAST_BANDS) on the same frame."""
-    if bands:
+@pytest.mark.parametrize("kernel", ["cells", "sb", "bands"])
+def test_general_fast_tile_small_frame(oracle, monkeypatch, kernel):
+    """A small frame (cells wider than 55 px on its top levels) through each FAST kernel:
+    k_fast_cells (the product path; it picks its 80-byte tile by itself there), the sparse-band
+    k_fast_sb (ORBGPU_FAST_SB) and the dense k_fast_bands (ORBGPU_FAST_BANDS)."""
+    if kernel != "cells":
         monkeypatch.setenv("ORBGPU_DIAGNOSTICS", "1")
-        monkeypatch.setenv("ORBGPU_FAST_BANDS", "1")
+        monkeypatch.setenv("ORBGPU_FAST_SB" if kernel == "sb" else "ORBGPU_FAST_BANDS", "1")
     img = synth.frame(120, 160, 5)
     ex = _extractor(nf=300, L=4, w=160, h=120)
     k, d, m = ex(img)
