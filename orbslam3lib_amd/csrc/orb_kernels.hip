@@ -908,36 +908,39 @@ __global__ __launch_bounds__(512, 1) void k_octree_retry(BatchArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// k_orient_desc: IC_Angle on the raw level (ORBextractor_old.cc:78-105) then
-// computeOrbDescriptor on the blurred level (:108-148): a = (float)cos, b = (float)sin of
-// angle*pi/180 (float), sample center[cvRound(x*b + y*a)*step + cvRound(x*a - y*b)].
-// kOdLanes lanes per keypoint (independent groups inside a wave): lane `sub` owns disc rows
-// v = sub - 15 + h * kOdLanes (one row at 32 lanes) for the moments and 256 / kOdLanes of the
-// test pairs, sampled from the keypoint's blurred patch staged in LDS.  The kernel waits on
-// three dependent memory round trips per keypoint (key, moment rows + patch, samples); few
-// vector-memory instructions and registers per lane keep many of them in flight.
 constexpr int kOdLanes = OD_LANES;             // lanes per keypoint (orb_kernels.h)
-constexpr int kOdRows = 32 / kOdLanes;         // disc rows per lane
 constexpr int kOdPairs = 256 / kOdLanes;       // test pairs per lane
+static_assert(kOdLanes == 32, "k_orient_desc: one disc row and 8 test pairs per lane");
 static_assert(kOdKpBlock == 256 / kOdLanes, "orb_kernels.h kOdKpBlock");
 
 constexpr int kOdPatchR = 18;                    // |rotated pattern offset| <= 13*sqrt(2) < 19
 constexpr int kOdPatchRows = 2 * kOdPatchR + 1;  // 37
 constexpr int kOdPatchPitch = 48;                // 3 x 16 B: covers x-18..x+18 from the dword below
+constexpr int kOdPatchChunks = kOdPatchRows * 3; // 16-byte chunks per patch
+constexpr int kOdPatchIt = (kOdPatchChunks + kOdLanes - 1) / kOdLanes;
 
-// Sum of v over each kOdLanes-lane group of the wave, in every lane: DPP quad_perm xor 1 / xor 2,
-// row half-mirror (pairs the two quads of 8 lanes) and row mirror (the two halves of a 16-lane
-// row), then for 32-lane groups the other row of the 32 through ds_swizzle (xor mask 16).
+// Sum of v over each 32-lane group of the wave, in every lane: DPP quad_perm xor 1 / xor 2, row
+// half-mirror (pairs the two quads of 8 lanes) and row mirror (the two halves of a 16-lane row),
+// then the other row of the 32 through ds_swizzle (xor mask 16).
 __device__ inline int od_sum(int v) {
     v += __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
     v += __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
     v += __builtin_amdgcn_update_dpp(0, v, 0x141, 0xF, 0xF, false);  // row_half_mirror
     v += __builtin_amdgcn_update_dpp(0, v, 0x140, 0xF, 0xF, false);  // row_mirror
-    if constexpr (kOdLanes == 32) v += __builtin_amdgcn_ds_swizzle(v, 0x401F);  // lane ^ 16 within 32
-    return v;
+    return v + __builtin_amdgcn_ds_swizzle(v, 0x401F);               // lane ^ 16 within 32
 }
 
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kOdLanes == 32 ? 6 : 5))) void k_orient_desc(
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// k_orient_desc: IC_Angle on the raw level (ORBextractor_old.cc:78-105) then
+// computeOrbDescriptor on the blurred level (:108-148): a = (float)cos, b = (float)sin of
+// angle*pi/180 (float), sample center[cvRound(x*b + y*a)*step + cvRound(x*a - y*b)].
+// 32 lanes per keypoint (two independent groups per wave): lane `sub` owns disc row v = sub - 15
+// for the moments and test pairs [8 sub, 8 sub + 8), sampled from the keypoint's blurred patch
+// staged in LDS.  The kernel waits on dependent memory round trips per keypoint (key, moment
+// rows + patch); few vector-memory instructions and registers per lane keep many of them in
+// flight.
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k_orient_desc(
     BatchArgs a, uint32_t nblk_magic) {
     // per keypoint group: the blurred patch around the keypoint, staged with 16-byte loads
     __shared__ __attribute__((aligned(16))) uint8_t patch[kOdKpBlock][kOdPatchRows * kOdPatchPitch];
@@ -958,17 +961,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kOdLanes ==
     const __amdgpu_buffer_rsrc_t brs =
         __builtin_amdgcn_make_buffer_rsrc((void*)blr, (short)0, G.bpitch * G.h, 0x00020000);
     const int stride_k = G.od_blocks * kOdKpBlock;
-    // per disc row v = s - 15 (s = 0..31): byte masks of the 32-byte window u = -15..16 restricted
-    // to |u| <= umax[|v|] (rows past v = 15 are empty), and the packed test pairs (x0,y0,x1,y1
-    // int8): both in LDS tables shared by the workgroup instead of 16 VGPRs per lane
-    // Both tables are stored index-major ([i][sub], [b][sub]): the 32 lanes of a keypoint read 32
-    // consecutive entries per instruction, conflict-free (a [sub][i] layout puts every lane of a
-    // b128 read on the same 4 banks: 32-way conflicts, measured as half the kernel's LDS time)
-    static_assert((kOdLanes == 16 || kOdLanes == 32) && kOdLanes * kOdRows == 32 && kOdLanes * kOdPairs == 256,
-                  "LDS table shapes");
-    __shared__ __attribute__((aligned(16))) uint32_t s_msk[8][32];  // [dword][disc row index v + 15]
-    // test pair j = sub * kOdPairs + b as floats {x0, x1, y0, y1} at s_pat[b][sub]: the two samples
-    // of a pair rotate as one packed pair
+    // per disc row v = s - 15 (s = 0..31) and dword i of the 32-byte window u = -15..16, the byte
+    // weights restricted to |u| <= umax[|v|] (rows past v = 15 are empty): ones (sum of p) and
+    // u + 15 (sum of (u + 15) p), so each dword is one v_alignbyte and two v_dot4_u32_u8; and the
+    // test pairs (floats {x0, x1, y0, y1}: the x and y pairs are packed-f32 operands).  Both in
+    // LDS tables shared by the workgroup, index-major ([i][row], [b][sub]): the 32 lanes of a
+    // keypoint read 32 consecutive entries per instruction, conflict-free
+    __shared__ __attribute__((aligned(16))) uint2 s_w[8][32];  // {ones, u + 15} masked
     __shared__ __attribute__((aligned(16))) uint4 s_pat[kOdPairs][kOdLanes];
     {
         const int ts = threadIdx.x / 8, ti = threadIdx.x % 8;
@@ -980,142 +979,119 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kOdLanes ==
             const int u = 4 * ti + j - 15;
             m |= ((u < 0 ? -u : u) <= d ? 0xFFu : 0u) << (8 * j);
         }
-        s_msk[ti][ts] = m;
+        s_w[ti][ts] = make_uint2(m & 0x01010101u, m & ((uint32_t)(4 * ti) * 0x01010101u + 0x03020100u));
         const int8_t* pv = c_pattern.v + 4 * threadIdx.x;  // x0, y0, x1, y1 of pair threadIdx.x
         s_pat[threadIdx.x % kOdPairs][threadIdx.x / kOdPairs] = make_uint4(__float_as_uint((float)pv[0]), __float_as_uint((float)pv[2]),
                                         __float_as_uint((float)pv[1]), __float_as_uint((float)pv[3]));
     }
     __syncthreads();
-    int vrow[kOdRows];
-#pragma unroll
-    for (int h = 0; h < kOdRows; ++h) {
-        const int v = sub - 15 + h * kOdLanes;
-        vrow[h] = v > 15 ? 0 : v;
-    }
+    const int v = sub - 15;
+    const int vrow = v > 15 ? 0 : v;
+    uint8_t* pt = patch[grp];
     // uniform trip count per wave so the group shuffles see all lanes
-    const int wave_first = (bx - G.od_first) * kOdKpBlock + (threadIdx.x >> 6) * (64 / kOdLanes);
+    const int wave_first = (bx - G.od_first) * kOdKpBlock + (threadIdx.x >> 6) * 2;
     // each iteration's key is loaded one iteration ahead, so its round trip overlaps the
     // previous keypoint's work
     auto key_at = [&](int kb) {
-        const int kp = kb + (grp % (64 / kOdLanes));
+        const int kp = kb + (grp & 1);
         return kp < count ? a.lvlkey[kbase + kp] : a.lvlkey[kbase + kb];
     };
     uint32_t key_next = wave_first < count ? key_at(wave_first) : 0u;
     for (int kb = wave_first; kb < count; kb += stride_k) {
-        const int kp = kb + (grp % (64 / kOdLanes));
+        const int kp = kb + (grp & 1);
         const bool valid = kp < count;
         const uint32_t key = key_next;
         if (kb + stride_k < count) key_next = key_at(kb + stride_k);
         const int x = key_x(key) + kMinBorder, y = key_y(key) + kMinBorder;
-        // IC_Angle moments (ORBextractor_old.cc:78-105): the row window is byte-aligned with
-        // v_alignbyte, masked to the disc, then
-        //   s = sum of bytes (v_sad_u8), sum u*p = dot4(bytes, {4i..4i+3}) - 15 s
-        int m10 = 0, m01 = 0;
         const int x0 = x - 15;
         const int xa = raw_dw ? (x0 & ~3) : x0;
         const int shf = x0 - xa;
         // the moment row (round trip 1) and the 37 x 37 blurred patch (rows y-18..y+18 from the
         // dword at or below x-18, 16-byte buffer loads, out-of-range bytes read as 0 and never
         // sampled) are both requested before either is used, so the two round trips overlap
-        uint32_t w[kOdRows][9];
-#pragma unroll
-        for (int h = 0; h < kOdRows; ++h) {
-            const uint8_t* row = lvl + plane_off(y + vrow[h], G.pitch, 0);
-            if (raw_dw) {  // 2 x dwordx4 + 1 dword (global loads need only dword alignment)
-                const uint4 A = *reinterpret_cast<const uint4*>(row + xa);
-                const uint4 B = *reinterpret_cast<const uint4*>(row + xa + 16);
-                w[h][0] = A.x; w[h][1] = A.y; w[h][2] = A.z; w[h][3] = A.w;
-                w[h][4] = B.x; w[h][5] = B.y; w[h][6] = B.z; w[h][7] = B.w;
-                w[h][8] = *reinterpret_cast<const uint32_t*>(row + xa + 32);
+        uint32_t w[9];
+        {
+            const uint8_t* row = lvl + plane_off(y + vrow, G.pitch, 0) + xa;
+            if (raw_dw) {  // 2 x dwordx4 (+ 1 dword when the window starts past byte 1 of its
+                           // first dword: otherwise w[8] only meets the zero weight of u = 16)
+                const uint4 A = *reinterpret_cast<const uint4*>(row);
+                const uint4 B = *reinterpret_cast<const uint4*>(row + 16);
+                w[0] = A.x; w[1] = A.y; w[2] = A.z; w[3] = A.w;
+                w[4] = B.x; w[5] = B.y; w[6] = B.z; w[7] = B.w;
+                w[8] = shf > 1 ? *reinterpret_cast<const uint32_t*>(row + 32) : 0u;
             } else {
 #pragma unroll
                 for (int i = 0; i < 9; ++i) {
-                    const uint8_t* q = row + xa + 4 * i;
-                    w[h][i] = (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16) | ((uint32_t)q[3] << 24);
+                    const uint8_t* q = row + 4 * i;
+                    w[i] = (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16) | ((uint32_t)q[3] << 24);
                 }
             }
         }
-        const int pitch = G.bpitch;
         const int xb = (x - kOdPatchR) & ~3;
-        const int pofs = (y - kOdPatchR) * pitch + xb;
-        constexpr int kPatchChunks = kOdPatchRows * 3, kPatchIt = (kPatchChunks + kOdLanes - 1) / kOdLanes;
-        uint4 pv[kPatchIt];
+        const int pofs = (y - kOdPatchR) * G.bpitch + xb;
+        uint4 pv[kOdPatchIt];
 #pragma unroll
-        for (int it = 0; it < kPatchIt; ++it) {
+        for (int it = 0; it < kOdPatchIt; ++it) {
             const int c = sub + it * kOdLanes;
             const int r = c / 3, part = c - 3 * r;
-            if (c < kPatchChunks) {
-                const auto v = __builtin_amdgcn_raw_buffer_load_b128(brs, pofs + r * pitch + 16 * part, 0, 0);
-                pv[it] = make_uint4(v[0], v[1], v[2], v[3]);
+            if (c < kOdPatchChunks) {
+                const auto q = __builtin_amdgcn_raw_buffer_load_b128(brs, pofs + r * G.bpitch + 16 * part, 0, 0);
+                pv[it] = make_uint4(q[0], q[1], q[2], q[3]);
             }
         }
-        // IC_Angle moments (ORBextractor_old.cc:78-105): the row window is byte-aligned with
-        // v_alignbyte, masked to the disc, then
-        //   s = sum of bytes (v_sad_u8), sum u*p = dot4(bytes, {4i..4i+3}) - 15 s
+        // IC_Angle (:78-105): s = sum of p, t = sum of (u + 15) p over the row's disc span
+        uint32_t s = 0, t = 0;
 #pragma unroll
-        for (int h = 0; h < kOdRows; ++h) {
-            uint32_t sacc = 0, uacc = 0;
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                const uint32_t b = __builtin_amdgcn_alignbyte(w[h][i + 1], w[h][i], shf) & s_msk[i][sub + h * kOdLanes];
-                sacc = __builtin_amdgcn_sad_u8(b, 0u, sacc);
-                const uint32_t wu = (uint32_t)(4 * i) * 0x01010101u + 0x03020100u;
-                uacc = __builtin_amdgcn_udot4(b, wu, uacc, false);
-            }
-            m10 += (int)uacc - 15 * (int)sacc;
-            m01 += vrow[h] * (int)sacc;
+        for (int i = 0; i < 8; ++i) {
+            const uint2 wt = s_w[i][sub];
+            const uint32_t b = __builtin_amdgcn_alignbyte(w[i + 1], w[i], shf);
+            s = __builtin_amdgcn_udot4(b, wt.x, s, false);
+            t = __builtin_amdgcn_udot4(b, wt.y, t, false);
         }
-        // sums over the keypoint's lanes: xor 1, xor 2 (quad_perm), the 8- and 16-lane mirrors
-        // (DPP, no LDS round trip), then for 32 lanes lane ^ 16 (ds_swizzle)
-        m10 = od_sum(m10);
-        m01 = od_sum(m01);
+        // sums over the keypoint's lanes (DPP, no LDS round trip but the last step)
+        const int m10 = od_sum((int)t - 15 * (int)s), m01 = od_sum(vrow * (int)s);
         const float angle = fast_atan2_deg((float)m01, (float)m10);
-        // computeOrbDescriptor (:108-148): lane `sub` makes bits [sub * kOdPairs, + kOdPairs)
+        // computeOrbDescriptor (:108-148): lane `sub` makes bits [8 sub, 8 sub + 8)
         const float factorPI = (float)(3.14159265358979323846 / 180.0);
-        const float ang = angle * factorPI;
         float sn, ca;  // std::sin(float) / std::cos(float) (:114-115): libm sinf / cosf
-        libm_sincosf(ang, &sn, &ca);
+        libm_sincosf(angle * factorPI, &sn, &ca);
         // the patch to LDS: every sample is then an LDS byte read (4 vector-memory instructions
         // per lane instead of one scattered byte load per sample)
-        uint8_t* pt = patch[grp];
 #pragma unroll
-        for (int it = 0; it < kPatchIt; ++it) {
+        for (int it = 0; it < kOdPatchIt; ++it) {
             const int c = sub + it * kOdLanes;
             const int r = c / 3, part = c - 3 * r;
-            if (c < kPatchChunks) *reinterpret_cast<uint4*>(pt + r * kOdPatchPitch + 16 * part) = pv[it];
+            if (c < kOdPatchChunks) *reinterpret_cast<uint4*>(pt + r * kOdPatchPitch + 16 * part) = pv[it];
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the group's own lanes read it
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         const int pc = kOdPatchR * kOdPatchPitch + (x - xb);  // patch offset of the keypoint
-        // both samples of a test pair as a float pair (each element an IEEE single operation, no
+        // both samples of a test pair as packed f32 (each element an IEEE single operation, no
         // contraction): row = x*b + y*a, col = x*a - y*b as the reference's float expressions
         // (:116-121), then cvRound by adding 1.5 * 2^23 (round to nearest even, |value| < 19),
         // whose low 24 bits are 2^22 + the rounded value: the LDS offset is one v_mad_u32_u24 of
         // the two bit patterns and a per-keypoint constant (no v_rndne / v_cvt per sample)
         const float magic = 12582912.0f;
         const uint32_t kofs = (uint32_t)pc - 0x4B400000u - 0x400000u * (uint32_t)kOdPatchPitch;
+        const f32x2 snv = {sn, sn}, cav = {ca, ca}, mg = {magic, magic};
         uint32_t bits = 0;
 #pragma unroll
-        for (int b = 0; b < kOdPairs; ++b) {
+        for (int b = kOdPairs - 1; b >= 0; --b) {  // bits = 2 bits + test, last pair first
             uint4 pw = s_pat[b][sub];  // float bit patterns {x0, x1, y0, y1}
             asm volatile("" : "+v"(pw.x), "+v"(pw.y), "+v"(pw.z), "+v"(pw.w));  // not hoisted
-            const float x0 = __uint_as_float(pw.x), x1 = __uint_as_float(pw.y);
-            const float y0 = __uint_as_float(pw.z), y1 = __uint_as_float(pw.w);
-            const uint32_t r0 = __float_as_uint((x0 * sn + y0 * ca) + magic);
-            const uint32_t c0 = __float_as_uint((x0 * ca - y0 * sn) + magic);
-            const uint32_t r1 = __float_as_uint((x1 * sn + y1 * ca) + magic);
-            const uint32_t c1 = __float_as_uint((x1 * ca - y1 * sn) + magic);
+            const f32x2 X = {__uint_as_float(pw.x), __uint_as_float(pw.y)};
+            const f32x2 Y = {__uint_as_float(pw.z), __uint_as_float(pw.w)};
+            const f32x2 R = (X * snv + Y * cav) + mg;
+            const f32x2 C = (X * cav - Y * snv) + mg;
             // the unsigned sums wrap to the small patch offsets; index with them as int
-            const int o0 = (int)(__umul24(r0, (uint32_t)kOdPatchPitch) + c0 + kofs);
-            const int o1 = (int)(__umul24(r1, (uint32_t)kOdPatchPitch) + c1 + kofs);
-            bits |= (uint32_t)(pt[o0] < pt[o1]) << b;
+            const int o0 = (int)(__umul24(__float_as_uint(R.x), (uint32_t)kOdPatchPitch) + __float_as_uint(C.x) + kofs);
+            const int o1 = (int)(__umul24(__float_as_uint(R.y), (uint32_t)kOdPatchPitch) + __float_as_uint(C.y) + kofs);
+            bits = bits + bits + (pt[o0] < pt[o1] ? 1u : 0u);
         }
         if (valid) {
             if (sub == 0) a.lvlangle[kbase + kp] = angle;
-            uint8_t* dd = a.lvldesc + (kbase + kp) * 32;
-            if (kOdPairs == 8) dd[sub] = (uint8_t)bits;
-            else reinterpret_cast<uint16_t*>(dd)[sub] = (uint16_t)bits;
+            a.lvldesc[(kbase + kp) * 32 + sub] = (uint8_t)bits;
         }
     }
 }

@@ -38,6 +38,34 @@ OP_KERNEL(k_bitop3_b32, "v_bitop3_b32 %0, %0, %1, %0 bitop3:0xc8")
 OP_KERNEL(k_dot4_u32_u8, "v_dot4_u32_u8 %0, %0, %1, %0")
 OP_KERNEL(k_pk_mad_u16, "v_pk_mad_u16 %0, %0, %1, %0")
 OP_KERNEL(k_mov_dpp, "v_mov_b32_dpp %0, %1 wave_shr:1 row_mask:0xf bank_mask:0xf")
+OP_KERNEL(k_mul_f32, "v_mul_f32 %0, %0, %1")
+OP_KERNEL(k_mad_u32_u24, "v_mad_u32_u24 %0, %0, %1, %0")
+OP_KERNEL(k_add3_u32, "v_add3_u32 %0, %0, %1, %0")
+OP_KERNEL(k_sad_u8, "v_sad_u8 %0, %0, %1, %0")
+
+// 64-bit operands (register pairs): packed f32 and f64
+#define OP_KERNEL64(NAME, ASM)                                                            \
+    __global__ __launch_bounds__(256) void NAME(uint32_t* out, int iters, uint32_t s) {   \
+        uint64_t v0 = threadIdx.x, v1 = v0 * 3, v2 = v0 * 5, v3 = v0 * 7, v4 = v0 ^ s,   \
+                 v5 = v0 + s, v6 = v0 * 11, v7 = v0 * 13;                                 \
+        const uint64_t k = s * 0x0101010101010101ull;                                     \
+        for (int i = 0; i < iters; ++i) {                                                 \
+            _Pragma("unroll") for (int r = 0; r < 4; ++r) {                                \
+                asm volatile(ASM : "+v"(v0) : "v"(k));                                    \
+                asm volatile(ASM : "+v"(v1) : "v"(k));                                    \
+                asm volatile(ASM : "+v"(v2) : "v"(k));                                    \
+                asm volatile(ASM : "+v"(v3) : "v"(k));                                    \
+                asm volatile(ASM : "+v"(v4) : "v"(k));                                    \
+                asm volatile(ASM : "+v"(v5) : "v"(k));                                    \
+                asm volatile(ASM : "+v"(v6) : "v"(k));                                    \
+                asm volatile(ASM : "+v"(v7) : "v"(k));                                    \
+            }                                                                             \
+        }                                                                                 \
+        out[blockIdx.x * 256 + threadIdx.x] = (uint32_t)(v0 + v1 + v2 + v3 + v4 + v5 + v6 + v7); \
+    }
+OP_KERNEL64(k_pk_mul_f32, "v_pk_mul_f32 %0, %0, %1")
+OP_KERNEL64(k_pk_add_f32, "v_pk_add_f32 %0, %0, %1")
+OP_KERNEL64(k_mul_f64, "v_mul_f64 %0, %0, %1")
 
 typedef void (*kfn)(uint32_t*, int, uint32_t);
 
@@ -47,7 +75,10 @@ int main() {
         {"v_pk_max_u16", k_pk_max_u16}, {"v_pk_sub_u16 clamp", k_pk_sub_u16},
         {"v_pk_maximum3_f16", k_pk_maximum3_f16}, {"v_perm_b32", k_perm_b32},
         {"v_alignbyte_b32", k_alignbyte_b32}, {"v_lerp_u8", k_lerp_u8}, {"v_bitop3_b32", k_bitop3_b32},
-        {"v_dot4_u32_u8", k_dot4_u32_u8}, {"v_pk_mad_u16", k_pk_mad_u16}, {"v_mov_b32_dpp wave_shr", k_mov_dpp}};
+        {"v_dot4_u32_u8", k_dot4_u32_u8}, {"v_pk_mad_u16", k_pk_mad_u16}, {"v_mov_b32_dpp wave_shr", k_mov_dpp},
+        {"v_mul_f32", k_mul_f32}, {"v_mad_u32_u24", k_mad_u32_u24}, {"v_add3_u32", k_add3_u32},
+        {"v_sad_u8", k_sad_u8}, {"v_pk_mul_f32", k_pk_mul_f32}, {"v_pk_add_f32", k_pk_add_f32},
+        {"v_mul_f64", k_mul_f64}};
     hipDeviceProp_t prop;
     hipGetDeviceProperties(&prop, 0);
     const int cus = prop.multiProcessorCount;
