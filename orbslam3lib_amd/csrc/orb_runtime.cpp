@@ -204,6 +204,7 @@ struct orbgpu_ctx {
     std::vector<int32_t> laps_host;  // lapping areas currently in `laps` (device), per image
     bool need_fork = true;           // the main stream holds work the sub streams must wait for
     bool stagger = true;             // ORBGPU_STAGGER=0: the chunks start every layout in lockstep
+    bool restagger = false;          // the next batch re-staggers the chunks (after serialized runs)
     std::vector<hipEvent_t> stagger_ev;
     struct ChunkRec { int img0, n; hipStream_t st; };
     std::vector<ChunkRec> last_chunks;
@@ -864,16 +865,19 @@ int orbgpu_create(const orbgpu_params* p, int device, int max_width, int max_hei
     }
     c->sub.push_back(c->stream);
     {
-        // 3 chunk streams: with the copy stream of orbgpu_upload_images_async that is 4, the
-        // hardware queues a process gets (GPU_MAX_HW_QUEUES = 4); a 5th stream shares a queue
-        // and the ingest copy then serialises with the kernels (measured: 3.16 vs 1.75 ms per
-        // 128-pair step with the upload beside it; 3 and 4 chunk streams compute equally fast)
+        // 2 chunk streams (with the copy stream of orbgpu_upload_images_async, 3 of the 4
+        // hardware queues a process gets, GPU_MAX_HW_QUEUES = 4; a 5th stream shares a queue and
+        // the ingest copy then serialises with the kernels: 3.16 vs 1.75 ms per 128-pair step).
+        // Round 4, C2 at 256 pairs: 2 streams 503-508 Mfeatures/s, 3 streams 485-492, 4 streams
+        // 467-500, 1 stream 469 (tools/stagger_ab.sh); a token ring that lets one chunk at a time
+        // run its pyramid + FAST while the others run octree / orientation / matching: 498 at 2
+        // streams, 477-486 at 3 (the stages do not overlap better than side by side)
         // A context that can never hold more than one stereo pair (the single-pair / one-eye
         // extractor) gets one stream: chunks are whole pairs, and every stream takes one of the
         // process's hardware queues, which a second context (the other eye's thread) needs for its
         // own work not to queue behind this one's.
         const char* e = diag_env("ORBGPU_STREAMS");
-        const int ns = std::max(1, std::min({8, e ? atoi(e) : 3, max_images / 2}));
+        const int ns = std::max(1, std::min({8, e ? atoi(e) : 2, max_images / 2}));
         for (int k = 1; k < ns; ++k) {
             hipStream_t st;
             if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) break;
@@ -1110,7 +1114,10 @@ static int run_batch_impl(orbgpu_ctx* c, int n, int w, int h, const int32_t* lap
         for (const Chunk& ch : chunks) HIP_TRY(hipStreamWaitEvent(ch.st, c->slot_ready, 0));
     // first step of a layout: chunk k starts after chunk k-1 finished its pyramid + blur, so the
     // chunks run different stages (memory-, VALU- and latency-bound ones) at the same time
-    const bool stagger = relayout && c->stagger && chunks.size() > 1 && !c->serialize;
+    // (also after serialized profiling runs, which leave every chunk stream joined: without a new
+    // stagger the chunks would run each stage side by side from then on)
+    const bool stagger = (relayout || c->restagger) && c->stagger && chunks.size() > 1 && !c->serialize;
+    if (stagger) c->restagger = false;
     while (stagger && c->stagger_ev.size() < chunks.size()) {
         hipEvent_t ev;
         HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
@@ -2142,7 +2149,9 @@ int orbgpu_set_profiling(orbgpu_ctx* c, int enable) {
     // selected stages; bit 30 also runs every stage as one whole-batch launch (serial timing)
     const unsigned e = (unsigned)enable;
     c->prof_mask = e == 0 ? 0u : e == 1 ? 0xFFFFFFFFu : (e & 0x3FFFFFFFu);
+    const bool was_serial = c->serialize;
     c->serialize = e != 0 && e != 1 && (e & (1u << 30));
+    if (was_serial && !c->serialize) c->restagger = true;
     return ORBGPU_OK;
 }
 

@@ -1,6 +1,6 @@
 """GPU parity on adversarial textures (VERDICT r1 "test data is narrow"): frames chosen for the
-code paths they force, run through the production batch path (3 stereo pairs -> 3 chunk
-streams) and compared with the oracle bit-exact, keypoints, descriptors and per-pair kNN2.
+code paths they force, run through the production batch path (3 stereo pairs -> 2 chunk
+streams of 1 and 2 pairs) and compared with the oracle bit-exact, keypoints, descriptors and per-pair kNN2.
 
 * iid uniform noise: the densest corner map (25.5% of level-0 pixels are FAST corners at
   iniThFAST, 35% at minThFAST), so more than 16384 keys enter DistributeOctTree (labels in the

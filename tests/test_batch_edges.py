@@ -6,8 +6,9 @@
   (lowest index wins, cv::BFMatcher k=2 / SURVEY §8 a10) is exercised.
 * The batch matcher (orbgpu_match_stereo_batch) with more than 4096 train rows per pair, and the
   C5 batch the bench's side line runs (1920x1080, 12 levels, 5000 features, 16 pairs).
-* The exact bench batch (bench.py: 256 pairs tiled from the distinct seeded pairs, 3 chunk
-  streams, staggered first step, then the steady state), sampled against the oracle.
+* The exact bench batch (bench.py: 256 pairs tiled from the distinct seeded pairs, 2 chunk
+  streams (the default; 3 forced too), staggered first step, then the steady state), sampled
+  against the oracle.
 * Consumers given an explicit stream right after a multi-stream batch (they must wait
   for the chunk streams), and the IDL one-call entry with a padded stride and a buffer that ends
   at the last pixel.
@@ -139,10 +140,14 @@ def test_c5_batch_16_pairs(oracle):
         _same_knn(be.matches(p), oracle.knn2(res[2 * p][1], res[2 * p + 1][1]), "pair %d" % p)
 
 
-@pytest.mark.parametrize("P", [128, 256])
-def test_bench_batch_pairs(oracle, P):
+@pytest.mark.parametrize("P,streams", [(128, None), (256, None), (256, 3)])
+def test_bench_batch_pairs(oracle, monkeypatch, P, streams):
     """bench.py's headline batch exactly (256 pairs since round 2; 128 in round 1): 16 distinct
-    seeded pairs tiled, 3 chunk streams, the staggered first step and the steady state after it."""
+    seeded pairs tiled, 2 chunk streams (the default since round 4; 3 before, forced through
+    ORBGPU_STREAMS), the staggered first step and the steady state after it."""
+    if streams:
+        monkeypatch.setenv("ORBGPU_DIAGNOSTICS", "1")
+        monkeypatch.setenv("ORBGPU_STREAMS", str(streams))
     import orbslam3lib_amd as og
     from orbslam3lib_amd.dist import pair_seed_base
     U, W, H = 16, 640, 480

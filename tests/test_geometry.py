@@ -73,7 +73,7 @@ def test_headset_sbs_1280x400(oracle):
 @pytest.mark.parametrize("w,h", [(641, 401), (643, 479), (753, 481), (637, 403)])
 def test_odd_level0_sizes(oracle, w, h):
     """Odd / non-multiple-of-4 level-0 sizes through the single-image path and the chunked batch
-    path (3 chunk streams), with lapping areas ending inside the frame."""
+    path (chunk streams), with lapping areas ending inside the frame."""
     import orbslam3lib_amd as og
     ex = og.ORBextractor(2000, 1.2, 8, 20, 7, max_width=w, max_height=h)
     img = synth.frame(h, w, 40 + w)
