@@ -865,7 +865,7 @@ int orbgpu_create(const orbgpu_params* p, int device, int max_width, int max_hei
     }
     c->sub.push_back(c->stream);
     {
-        // 2 chunk streams (with the copy stream of orbgpu_upload_images_async, 3 of the 4
+        // 2 or 3 chunk streams (with the copy stream of orbgpu_upload_images_async, 3 or 4 of the 4
         // hardware queues a process gets, GPU_MAX_HW_QUEUES = 4; a 5th stream shares a queue and
         // the ingest copy then serialises with the kernels: 3.16 vs 1.75 ms per 128-pair step).
         // Round 4, C2 at 256 pairs: 2 streams 503-508 Mfeatures/s, 3 streams 485-492, 4 streams
@@ -877,7 +877,10 @@ int orbgpu_create(const orbgpu_params* p, int device, int max_width, int max_hei
         // process's hardware queues, which a second context (the other eye's thread) needs for its
         // own work not to queue behind this one's.
         const char* e = diag_env("ORBGPU_STREAMS");
-        const int ns = std::max(1, std::min({8, e ? atoi(e) : 2, max_images / 2}));
+        // batches of >= 128 pairs: 2 chunk streams (each chunk fills the GPU); smaller batches
+        // (C5's 16 1080p pairs: 161 vs 154 Mfeatures/s) keep 3
+        const int ns_default = max_images >= 256 ? 2 : 3;
+        const int ns = std::max(1, std::min({8, e ? atoi(e) : ns_default, max_images / 2}));
         for (int k = 1; k < ns; ++k) {
             hipStream_t st;
             if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) break;
