@@ -429,28 +429,38 @@ __device__ inline void br_tile(const BatchArgs& a, int l, bool resize, int img, 
     const uint8_t* wb = reinterpret_cast<const uint8_t*>(&sm.tin4[0][0]);
     const int wy0 = bt.ty0 - 4, wx0 = bt.tx0 - 16;
     uint8_t* dst = a.lvl_base[l] + (long long)img * G.img_stride;
-    const float inv_nq = nq > 0 ? 1.f / (float)nq : 0.f;
-    for (int it = threadIdx.x; it < nr * nq; it += 256) {
-        const int rr = (int)(((float)it + 0.5f) * inv_nq);  // exact: it < 34 * 40
-        const int q = it - __mul24(rr, nq);
-        const int dy = r0 + rr, dx0 = 4 * (q0 + q);
-        uint32_t packed = 0;
-        if (G.area2) {
+    // thread -> (quad q, rows rr0, rr0 + step, ...): the quad's selectors and coefficients are
+    // read once per tile, one division per tile instead of one per output quad
+    if (nq <= 0) return;
+    const int step = max(256 / nq, 1);
+    const int q = (int)threadIdx.x % nq, rr0 = (int)threadIdx.x / nq;
+    if (rr0 >= step) return;
+    const int dx0 = 4 * (q0 + q);
+    if (G.area2) {
+        for (int rr = rr0; rr < nr; rr += step) {
+            const int dy = r0 + rr;
             const uint8_t* s0 = wb + __mul24(2 * dy - wy0, IW) - wx0;
             const uint8_t* s1 = s0 + IW;
+            uint32_t packed = 0;
 #pragma unroll
             for (int kk = 0; kk < 4; ++kk) {
                 const int dx = min(dx0 + kk, G.w - 1);
                 const int o = (s0[2 * dx] + s0[2 * dx + 1] + s1[2 * dx] + s1[2 * dx + 1] + 2) >> 2;
                 packed |= (uint32_t)o << (8 * kk);
             }
-        } else {
+            *reinterpret_cast<uint32_t*>(dst + plane_off(dy, G.pitch, dx0)) = packed;
+        }
+    } else {
+        const int4 xsel = sm.xsel[q], xcw = sm.xcw[q];
+        const int xbase = sm.xbase[q];
+        for (int rr = rr0; rr < nr; rr += step) {
+            const int dy = r0 + rr;
             const int4 yt = sm.yts[rr];
             const uint8_t* row0 = wb + __mul24(yt.x - wy0, IW) - wx0;
             const uint8_t* row1 = wb + __mul24(yt.y - wy0, IW) - wx0;
-            packed = rs_quad(row0, row1, sm.xbase[q], sm.xsel[q], sm.xcw[q], yt.z, yt.w, dx0, G.simd_end);
+            const uint32_t packed = rs_quad(row0, row1, xbase, xsel, xcw, yt.z, yt.w, dx0, G.simd_end);
+            *reinterpret_cast<uint32_t*>(dst + plane_off(dy, G.pitch, dx0)) = packed;
         }
-        *reinterpret_cast<uint32_t*>(dst + plane_off(dy, G.pitch, dx0)) = packed;
     }
 }
 
