@@ -127,17 +127,32 @@ struct CellScratch {
 // overwritten by later lanes or land in the spare entries), then 4 sink entries.
 __host__ __device__ constexpr int fast_list_slack(int waves) { return 4 * waves + (FAST_SINK == 2 ? 512 : 4); }
 
+// The positions of the set bits of every 4-bit pre-test mask as u16 pairs (p0 | p1 << 16,
+// p2 | p3 << 16): a constant table, copied to LDS per workgroup (one load per lane, not the ~45
+// VALU per wave of building it).
+struct FastLutTable {
+    uint32_t v[32];
+};
+constexpr FastLutTable make_fast_lut() {
+    FastLutTable t{};
+    for (int m = 0; m < 16; ++m) {
+        uint32_t pos[4] = {0, 0, 0, 0};
+        int n = 0;
+        for (int k = 0; k < 4; ++k)
+            if ((m >> k) & 1) pos[n++] = (uint32_t)k;
+        t.v[2 * m] = pos[0] | (pos[1] << 16);
+        t.v[2 * m + 1] = pos[2] | (pos[3] << 16);
+    }
+    return t;
+}
+__constant__ FastLutTable c_fast_lut = make_fast_lut();
+
 // Builds CellScratch's lut / emask tables (threads < 16 and < ng); the caller syncs before
 // fast_cell_detect.
 template <int CP>
 __device__ inline void fast_cell_tables(const CellGeom& g, int sh, uint2* lut, uint32_t* emask) {
     const int tid = threadIdx.x;
-    if (tid < 16) {
-        int pos[4] = {0, 0, 0, 0}, n = 0;
-        for (int k = 0; k < 4; ++k)
-            if ((tid >> k) & 1) pos[n++] = k;
-        lut[tid] = make_uint2((uint32_t)pos[0] | ((uint32_t)pos[1] << 16), (uint32_t)pos[2] | ((uint32_t)pos[3] << 16));
-    }
+    if (tid < 16) lut[tid] = make_uint2(c_fast_lut.v[2 * tid], c_fast_lut.v[2 * tid + 1]);
     const int dc = g.cols - 6 > 0 ? g.cols - 6 : 0;
     const int xs = 3 + sh, xe = 3 + sh + dc;
     const int g0 = xs >> 2;
@@ -241,7 +256,9 @@ __host__ __device__ int fast_cell_detect(Pol& p, int sh, const CellGeom& g, int 
     const int ng = dc > 0 ? ((xe - 1) >> 2) - g0 + 1 : 0;
     const int items = dr * ng;
     const int j0 = w * items / W, j1 = (w + 1) * items / W;
-    const float inv_ng = ng > 0 ? 1.f / (float)ng : 0.f;
+    // v_rcp_f32 (1 ulp): every quotient below is (k + 0.5) / ng with k < 1500, at least 0.5 / ng
+    // (>= 0.025) from an integer, far beyond the error -- the floors are exact
+    const float inv_ng = ng > 0 ? __builtin_amdgcn_rcpf((float)ng) : 0.f;
     auto pix_before = [&](int j) {  // detection pixels of the items before item j
         if (ng == 0) return 0;
         const int r = (int)(((float)j + 0.5f) * inv_ng), q = j - r * ng;

@@ -154,10 +154,34 @@ __device__ inline int refl101(int p, int n) {
     return p >= n ? 2 * n - p - 2 : p;
 }
 
+// Horizontal 7-tap sums of 4 columns of two rows as u16 pairs (row a low, row b high), from the
+// 12 window bytes of each row that start 1 byte before the first output's first tap (A[0] byte 1 =
+// column x-3 of output 0): per row and output, the taps x-3 .. x as one byte window (v_alignbyte)
+// times {18, 34, 48, 56} and x+1 .. x+3 times {48, 34, 18, 0}, two v_dot4_u32_u8 (sums <= 65280).
+// 32 VALU per two rows of 4 columns (the u16-pair form with v_perm / v_pk_mad_u16 took 38).
+__device__ inline void hsum_pair(const uint32_t A[3], const uint32_t B[3], uint32_t out[4]) {
+    constexpr uint32_t W03 = 18u | (34u << 8) | (48u << 16) | (56u << 24);
+    constexpr uint32_t W46 = 48u | (34u << 8) | (18u << 16);
+    auto row = [&](const uint32_t* X, uint32_t h[4]) {
+        const uint32_t lo[4] = {__builtin_amdgcn_alignbyte(X[1], X[0], 1), __builtin_amdgcn_alignbyte(X[1], X[0], 2),
+                                __builtin_amdgcn_alignbyte(X[1], X[0], 3), X[1]};
+        const uint32_t hi[4] = {__builtin_amdgcn_alignbyte(X[2], X[1], 1), __builtin_amdgcn_alignbyte(X[2], X[1], 2),
+                                __builtin_amdgcn_alignbyte(X[2], X[1], 3), X[2]};
+#pragma unroll
+        for (int o = 0; o < 4; ++o)
+            h[o] = __builtin_amdgcn_udot4(hi[o], W46, __builtin_amdgcn_udot4(lo[o], W03, 0u, false), false);
+    };
+    uint32_t ha[4], hb[4];
+    row(A, ha);
+    row(B, hb);
+#pragma unroll
+    for (int o = 0; o < 4; ++o) out[o] = ha[o] | (hb[o] << 16);
+}
+
 // Tile 128 x 32 outputs; the input window is rows ty0-4 .. ty0+35 (one spare row each side so
 // rows pair up) x cols tx0-16 .. tx0+143, staged in LDS with 16-byte loads.
 // Horizontal pass in "row-pair" u16x2 lanes: lane lo = row 2rp, lane hi = row 2rp+1 of the
-// same column (v_perm builds them from two row dwords), 7 taps by v_pk_add/v_pk_mad_u16.
+// same column, 7 taps as two v_dot4_u32_u8 per row and column (hsum_pair).
 // Vertical pass: each output row is 4 v_dot2_u32_u16 over row pairs with weight pairs
 // {0,18}{34,48}{56,48}{34,18} (even rows) or {18,34}{48,56}{48,34}{18,0} (odd rows), the
 // accumulator seeded with the 2^15 rounding term.
@@ -232,22 +256,8 @@ __device__ inline void blur_tile_compute(const LevelGeom& G, int tx0, int ty0, u
             A[d] = tin[2 * rp][cq + 3 + d];
             B[d] = tin[2 * rp + 1][cq + 3 + d];
         }
-        u16x2 P[12];
-#pragma unroll
-        for (int j = 1; j < 11; ++j) {
-            const uint32_t b = j & 3;
-            P[j] = as_u16x2(__builtin_amdgcn_perm(B[j >> 2], A[j >> 2], b | 0x0c00u | ((4 + b) << 16) | 0x0c000000u));
-        }
         uint32_t h[4];
-#pragma unroll
-        for (int o = 0; o < 4; ++o) {
-            const u16x2* q = P + 1 + o;  // q[0] = column x-3 ... q[6] = column x+3
-            u16x2 acc = (u16x2)(56) * q[3];
-            acc = (u16x2)(48) * (q[2] + q[4]) + acc;
-            acc = (u16x2)(34) * (q[1] + q[5]) + acc;
-            acc = (u16x2)(18) * (q[0] + q[6]) + acc;
-            h[o] = as_u32(acc);
-        }
+        hsum_pair(A, B, h);
         hp[rp][cq] = make_uint4(h[0], h[1], h[2], h[3]);
     }
     __syncthreads();
@@ -513,7 +523,7 @@ __device__ inline void tail_fill_pads(uint8_t* buf, int P, int w, int h) {
 }
 
 // Horizontal 7-tap sums of the 4 columns 4cq .. 4cq+3 of two LDS rows as u16 pairs (row a, row b):
-// the same v_perm / v_pk_mad_u16 form as blur_tile_compute (window bytes 4cq+12 .. 4cq+23).
+// hsum_pair, as blur_tile_compute (window bytes 4cq+12 .. 4cq+23).
 __device__ inline void tail_hpair(const uint8_t* ra, const uint8_t* rb, int cq, uint32_t out[4]) {
     const uint32_t* pa = reinterpret_cast<const uint32_t*>(ra) + cq + 3;
     const uint32_t* pb = reinterpret_cast<const uint32_t*>(rb) + cq + 3;
@@ -523,21 +533,7 @@ __device__ inline void tail_hpair(const uint8_t* ra, const uint8_t* rb, int cq, 
         A[d] = pa[d];
         B[d] = pb[d];
     }
-    u16x2 Pp[12];
-#pragma unroll
-    for (int j = 1; j < 11; ++j) {
-        const uint32_t b = j & 3;
-        Pp[j] = as_u16x2(__builtin_amdgcn_perm(B[j >> 2], A[j >> 2], b | 0x0c00u | ((4 + b) << 16) | 0x0c000000u));
-    }
-#pragma unroll
-    for (int o = 0; o < 4; ++o) {
-        const u16x2* q = Pp + 1 + o;  // q[0] = column x-3 ... q[6] = column x+3
-        u16x2 acc = (u16x2)(56) * q[3];
-        acc = (u16x2)(48) * (q[2] + q[4]) + acc;
-        acc = (u16x2)(34) * (q[1] + q[5]) + acc;
-        acc = (u16x2)(18) * (q[0] + q[6]) + acc;
-        out[o] = as_u32(acc);
-    }
+    hsum_pair(A, B, out);
 }
 
 // Blur of one LDS-resident level.  Task = (column quad, segment of R rows), with the segment
