@@ -12,7 +12,10 @@ import json
 import sys
 
 bench = json.load(open(sys.argv[1]))
-chunks = int(sys.argv[3]) if len(sys.argv) > 3 else 3  # ORBGPU_STREAMS default
+# chunk streams of the bench context: the runtime's default (orb_runtime.cpp orbgpu_create): 2 for
+# contexts of >= 128 pairs, else 3, never more than the pairs
+_imgs = bench.get("config", {}).get("images_per_gpu_per_step", 512)
+chunks = int(sys.argv[3]) if len(sys.argv) > 3 else min(2 if _imgs >= 256 else 3, max(1, _imgs // 2))
 roof = bench["roofline"]
 name = roof["kernel"]
 steps, warmup = bench["steps"], bench.get("warmup", 3)
