@@ -157,12 +157,14 @@ __device__ inline void fast_cell_tables(const CellGeom& g, int sh, uint2* lut, u
     const int xs = 3 + sh, xe = 3 + sh + dc;
     const int g0 = xs >> 2;
     const int ng = dc > 0 ? ((xe - 1) >> 2) - g0 + 1 : 0;
-    if (tid < ng) {
-        const uint32_t first4 = 0xFu & ~((1u << (xs - 4 * g0)) - 1u);
-        const uint32_t last4 = (1u << (xe - 4 * (g0 + ng - 1))) - 1u;
-        const uint32_t m4 = (tid == 0 ? first4 : 0xFu) & (tid == ng - 1 ? last4 : 0xFu);
-        emask[tid] = (m4 & 1u ? 0x80u : 0u) | (m4 & 2u ? 0x8000u : 0u) | (m4 & 4u ? 0x800000u : 0u) |
-                     (m4 & 8u ? 0x80000000u : 0u);
+    if (tid < ng) {  // the first and last groups' masks are workgroup-uniform (scalar)
+        auto bytes = [](uint32_t m4) {
+            return (m4 & 1u ? 0x80u : 0u) | (m4 & 2u ? 0x8000u : 0u) | (m4 & 4u ? 0x800000u : 0u) |
+                   (m4 & 8u ? 0x80000000u : 0u);
+        };
+        const uint32_t first = bytes(0xFu & ~((1u << (xs - 4 * g0)) - 1u));
+        const uint32_t last = bytes((1u << (xe - 4 * (g0 + ng - 1))) - 1u);
+        emask[tid] = (tid == 0 ? first : 0x80808080u) & (tid == ng - 1 ? last : 0x80808080u);
     }
 }
 

@@ -279,9 +279,14 @@ __device__ inline void blur_tile_compute(const LevelGeom& G, int tx0, int ty0, u
     const u16x2 WO[4] = {as_u16x2(18u | (34u << 16)), as_u16x2(48u | (56u << 16)),
                          as_u16x2(48u | (34u << 16)), as_u16x2(18u | (0u << 16))};
     const int x = tx0 + 4 * cq;
+    // this thread's rows ybase .. ybase + R - 1: the ones inside [rlo, rhi) and the plane, at one
+    // compare per row; the row address from a per-thread base plus a uniform row offset
+    const int ybase = ty0 + R * rg;
+    const int ylo = max(rlo, ybase), yhi = x < G.w ? min(min(rhi, G.h), ybase + R) : ybase;
+    const int olo = ylo - ybase, ohi = yhi - ybase;
+    uint8_t* dbase = dst + plane_off(ybase, G.bpitch, x);
 #pragma unroll
     for (int o = 0; o < R; ++o) {
-        const int y = ty0 + R * rg + o;
         const int k0 = (o + 1) >> 1;  // first row pair: o=0 -> 0, 1 -> 1, 2 -> 1, 3 -> 2, ...
         uint32_t sv[4];
 #pragma unroll
@@ -296,7 +301,7 @@ __device__ inline void blur_tile_compute(const LevelGeom& G, int tx0, int ty0, u
         const uint32_t lo = __builtin_amdgcn_perm(sv[1], sv[0], 0x0c0c0602u);
         const uint32_t hi = __builtin_amdgcn_perm(sv[3], sv[2], 0x0c0c0602u);
         const uint32_t packed = lo | (hi << 16);
-        if (y >= rlo && y < rhi && y < G.h && x < G.w) *reinterpret_cast<uint32_t*>(dst + plane_off(y, G.bpitch, x)) = packed;
+        if (o >= olo && o < ohi) *reinterpret_cast<uint32_t*>(dbase + o * G.bpitch) = packed;
     }
 }
 
