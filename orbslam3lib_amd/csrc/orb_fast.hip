@@ -511,7 +511,6 @@ __global__ __launch_bounds__(64) void k_fast_sb(BatchArgs a, uint32_t nseg_magic
         }
     };
     const int tini = min(max(a.ini_th, 0), 255), tmin = min(max(a.min_th, 0), 255);
-    const uint64_t lt = (1ull << lane) - 1ull;
     auto rank = [](uint64_t b) {
         return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
     };
