@@ -12,7 +12,7 @@ all: $(LIB) oracle facade_test idl_test
 
 # one object per translation unit (each launcher sits beside its kernels: no relocatable device
 # code needed), so `make -j` compiles them in parallel
-LIBSRC := orb_kernels.hip orb_fast.hip orb_stereo.hip orb_frame.hip orb_io.hip orb_sbp.hip orb_fisheye.hip orb_runtime.cpp
+LIBSRC := orb_kernels.hip orb_stereo.hip orb_frame.hip orb_io.hip orb_sbp.hip orb_fisheye.hip orb_runtime.cpp
 OBJDIR := $(CSRC)/build
 LIBOBJ := $(patsubst %,$(OBJDIR)/%.o,$(LIBSRC))
 

@@ -78,8 +78,6 @@ def algorithmic_bytes(w, h, L, nkp, sf=1.2, ncand=0.0, tail0=None):
         "k_fast_cells<48>": sum(a for a, t in zip(A, tier) if t == 48),
         "k_fast_cells<64>": sum(a for a, t in zip(A, tier) if t == 64),
         "k_fast_cells<80>": sum(a for a, t in zip(A, tier) if t == 80),
-        "k_fast_bands": sum(A),  # every level read once (orb_fast.hip)
-        "k_fast_sb": sum(A),
         "k_blur": 2 * A[L - 1] if t > L else 0,  # the last level's blur (the others ride in k_blur_resize)
         "k_orient_desc": 48 * nkp,
         "k_octree": 4 * ncand + 4 * nkp,
@@ -512,7 +510,7 @@ def main():
     # the serialized pass.  The pyramid kernel also writes each level's blur (k_blur_resize reads
     # level l-1 once for both), so its time carries the blur: the bytes are SURVEY §8d's B_fp plus
     # the blur's 2 sum(A_l) (B_extract without the 48 B per keypoint)
-    fp_names = [k for k in stages_all if k in ("k_blur_resize", "k_blur", "k_pyr_tail", "k_fast_bands", "k_fast_sb")
+    fp_names = [k for k in stages_all if k in ("k_blur_resize", "k_blur", "k_pyr_tail")
                 or k.startswith("k_fast_cells")]
     fp_ms = sum(stages_all[k][0] for k in fp_names) / 3.0  # 3 serialized steps
     roof_fp = None

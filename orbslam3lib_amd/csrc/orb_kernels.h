@@ -100,14 +100,7 @@ struct BatchArgs {
     // (tail0 = nlevels + 1: no tail, k_blur_resize for every level and k_blur for the last)
     int tail0;
     int tail_lds, tail_buf1, tail_tab, tail_maxq, tail_maxrows;  // its LDS layout (bytes / entries)
-    // k_fast_bands (orb_fast.hip): records {level, cell row, first cell, end cell} at rtab index
-    // fast_band_off, grouped by workgroup width: [fast_band_grp[w-1], fast_band_grp[w]) run w waves
-    // with fast_band_lds[w-1] bytes of dynamic LDS
-    int fast_dense;                  // 0: k_fast_cells, 1: k_fast_bands, 2: k_fast_sb
-    int fast_sb_off, fast_sb_n;      // k_fast_sb records {level, cell row, first cell, end cell}
-    int fast_band_off;
-    int fast_band_grp[5];
-    int fast_band_lds[4];
+    int tail_min;              // launches of fewer images take the per-level path (host only)
 };
 
 struct MatchArgs {
@@ -244,14 +237,12 @@ hipError_t launch_blur_resize(const BatchArgs& a, int level, hipStream_t s);
 hipError_t launch_blur_level(const BatchArgs& a, int level, hipStream_t s);
 constexpr int kTailPad = 16;          // k_pyr_tail: left pad of an LDS row (>= 3 reflected columns)
 constexpr int kTailLdsMax = 160 * 1024;  // the LDS one workgroup may hold on gfx950
+constexpr int kTailMinImages = 128;     // k_pyr_tail only for launches of >= this many images
 hipError_t launch_pyr_tail(const BatchArgs& a, hipStream_t s);
 // FAST cells of the levels that run the `tile`-byte LDS tile (48, 64 or kCellMax = 80):
 // fast_cell_range gives their flattened cell range, launch_fast_cells launches nothing if empty
 void fast_cell_range(const BatchArgs& a, int tile, int* c0, int* c1);
 hipError_t launch_fast_cells(const BatchArgs& a, int tile, hipStream_t s);
-constexpr int kFastBandMaxWaves = 4;  // k_fast_bands: widest segment (62 owned quads per wave)
-hipError_t launch_fast_bands(const BatchArgs& a, hipStream_t s);  // orb_fast.hip
-hipError_t launch_fast_sb(const BatchArgs& a, hipStream_t s);     // orb_fast.hip
 hipError_t launch_octree(const BatchArgs& a, hipStream_t s);
 hipError_t launch_orient_desc(const BatchArgs& a, hipStream_t s);
 hipError_t launch_finalize(const BatchArgs& a, hipStream_t s);

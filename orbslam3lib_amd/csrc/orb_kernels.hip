@@ -972,32 +972,52 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
     const __amdgpu_buffer_rsrc_t brs =
         __builtin_amdgcn_make_buffer_rsrc((void*)blr, (short)0, G.bpitch * G.h, 0x00020000);
     const int stride_k = G.od_blocks * kOdKpBlock;
-    // per disc row v = s - 15 (s = 0..31) and dword i of the 32-byte window u = -15..16, the byte
-    // weights restricted to |u| <= umax[|v|] (rows past v = 15 are empty): ones (sum of p) and
-    // u + 15 (sum of (u + 15) p), so each dword is one v_alignbyte and two v_dot4_u32_u8; and the
-    // test pairs (floats {x0, x1, y0, y1}: the x and y pairs are packed-f32 operands).  Both in
-    // LDS tables shared by the workgroup, index-major ([i][row], [b][sub]): the 32 lanes of a
-    // keypoint read 32 consecutive entries per instruction, conflict-free
-    __shared__ __attribute__((aligned(16))) uint2 s_w[8][32];  // {ones, u + 15} masked
+    // Moments from coalesced row chunks: the 31 disc rows of a keypoint are read as 16-byte
+    // aligned chunks of the 48-byte window that starts at xa16 = (x - 15) & ~15 (it holds
+    // x - 15 .. x + 15 for every x).  Chunk slot i = sub + 32 it (it < 3) is disc row r = i / 3
+    // (v = r - 15; r = 31 lies past the disc) and part i % 3, so the three lanes of a row read 48
+    // contiguous bytes -- one or two cache lines per row instead of three 16-byte / dword loads
+    // per row lane (round 4: ~105 of the ~160 L1 accesses per keypoint were those).  Each chunk
+    // adds its masked byte sums: s = sum of p, c = sum of (column - xa16) p over the disc span
+    // |u| <= umax[|v|], i.e. chunk bytes [m, n) with m, n from the alignment a = (x - 15) & 15 and
+    // two per-lane constants; the byte masks of every [m, n) are an LDS table, so a chunk is one
+    // b128 LDS read, 4 ANDs and 8 v_dot4_u32_u8.  Then m_10 = sum c - (15 + a) sum s and
+    // m_01 = sum v s.
+    __shared__ __attribute__((aligned(16))) uint4 s_rng[17][17];  // bytes [m, n) of 16 (none if n <= m)
     __shared__ __attribute__((aligned(16))) uint4 s_pat[kOdPairs][kOdLanes];
-    {
-        const int ts = threadIdx.x / 8, ti = threadIdx.x % 8;
-        const int v = ts - 15;
-        const int d = v > 15 ? -1 : c_umax[v < 0 ? -v : v];
-        uint32_t m = 0;
+    for (int e = threadIdx.x; e < 17 * 17; e += 256) {
+        const int m = e / 17, n = e - 17 * m;
+        uint32_t w4[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int u = 4 * ti + j - 15;
-            m |= ((u < 0 ? -u : u) <= d ? 0xFFu : 0u) << (8 * j);
+        for (int k = 0; k < 4; ++k) {
+            w4[k] = 0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) w4[k] |= (4 * k + j >= m && 4 * k + j < n ? 0xFFu : 0u) << (8 * j);
         }
-        s_w[ti][ts] = make_uint2(m & 0x01010101u, m & ((uint32_t)(4 * ti) * 0x01010101u + 0x03020100u));
+        s_rng[m][n] = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+    }
+    {
         const int8_t* pv = c_pattern.v + 4 * threadIdx.x;  // x0, y0, x1, y1 of pair threadIdx.x
         s_pat[threadIdx.x % kOdPairs][threadIdx.x / kOdPairs] = make_uint4(__float_as_uint((float)pv[0]), __float_as_uint((float)pv[2]),
                                         __float_as_uint((float)pv[1]), __float_as_uint((float)pv[3]));
     }
     __syncthreads();
-    const int v = sub - 15;
-    const int vrow = v > 15 ? 0 : v;
+    // this lane's three chunk slots: row v, chunk bytes [lo + a, hi + a) clamped to [0, 16) are
+    // the disc span (lo = 15 - d - 16 part, hi = 16 + d - 16 part, d = umax[|v|], -1 past the
+    // disc), the part's column offset and the byte offset from the window
+    int mv[3], mlo[3], mhi[3], mofs[3], mp16[3];
+#pragma unroll
+    for (int it = 0; it < 3; ++it) {
+        const int i = sub + 32 * it, r = i / 3, part = i - 3 * r;
+        mv[it] = r - 15;
+        const int d = r < 31 ? c_umax[mv[it] < 0 ? -mv[it] : mv[it]] : -1;
+        mlo[it] = 15 - d - 16 * part;
+        mhi[it] = 16 + d - 16 * part;
+        mofs[it] = (r < 31 ? mv[it] : 15) * G.pitch + 16 * part;
+        mp16[it] = 16 * part;
+    }
+    const __amdgpu_buffer_rsrc_t lrs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)lvl, (short)0, (int)min((long long)G.pitch * G.h, 0x7fffffffLL), 0x00020000);
     uint8_t* pt = patch[grp];
     // uniform trip count per wave so the group shuffles see all lanes
     const int wave_first = (bx - G.od_first) * kOdKpBlock + (threadIdx.x >> 6) * 2;
@@ -1014,28 +1034,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
         const uint32_t key = key_next;
         if (kb + stride_k < count) key_next = key_at(kb + stride_k);
         const int x = key_x(key) + kMinBorder, y = key_y(key) + kMinBorder;
-        const int x0 = x - 15;
-        const int xa = raw_dw ? (x0 & ~3) : x0;
-        const int shf = x0 - xa;
-        // the moment row (round trip 1) and the 37 x 37 blurred patch (rows y-18..y+18 from the
-        // dword at or below x-18, 16-byte buffer loads, out-of-range bytes read as 0 and never
-        // sampled) are both requested before either is used, so the two round trips overlap
-        uint32_t w[9];
-        {
-            const uint8_t* row = lvl + plane_off(y + vrow, G.pitch, 0) + xa;
-            if (raw_dw) {  // 2 x dwordx4 (+ 1 dword when the window starts past byte 1 of its
-                           // first dword: otherwise w[8] only meets the zero weight of u = 16)
-                const uint4 A = *reinterpret_cast<const uint4*>(row);
-                const uint4 B = *reinterpret_cast<const uint4*>(row + 16);
-                w[0] = A.x; w[1] = A.y; w[2] = A.z; w[3] = A.w;
-                w[4] = B.x; w[5] = B.y; w[6] = B.z; w[7] = B.w;
-                w[8] = shf > 1 ? *reinterpret_cast<const uint32_t*>(row + 32) : 0u;
-            } else {
+        const int al = (x - 15) & 15;
+        const int wofs = y * G.pitch + (x - 15 - al);  // the 48-byte window of disc row 0
+        // the three moment chunks (round trip 1) and the 37 x 37 blurred patch (rows y-18..y+18
+        // from the dword at or below x-18, 16-byte buffer loads, out-of-range bytes read as 0
+        // and never sampled) are both requested before either is used, so the two round trips
+        // overlap; window bytes past x + 15 (or past the plane: 0) only meet zero masks
+        uint4 mc[3];
 #pragma unroll
-                for (int i = 0; i < 9; ++i) {
-                    const uint8_t* q = row + 4 * i;
-                    w[i] = (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16) | ((uint32_t)q[3] << 24);
-                }
+        for (int it = 0; it < 3; ++it) {
+            if (raw_dw) {
+                const auto q = __builtin_amdgcn_raw_buffer_load_b128(lrs, wofs + mofs[it], 0, 0);
+                mc[it] = make_uint4(q[0], q[1], q[2], q[3]);
+            } else {  // level-0 rows not 4-byte aligned: bytes
+                const uint8_t* q = lvl + wofs + mofs[it];
+                uint32_t d4[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    d4[k] = (uint32_t)q[4 * k] | ((uint32_t)q[4 * k + 1] << 8) | ((uint32_t)q[4 * k + 2] << 16) |
+                            ((uint32_t)q[4 * k + 3] << 24);
+                mc[it] = make_uint4(d4[0], d4[1], d4[2], d4[3]);
             }
         }
         const int xb = (x - kOdPatchR) & ~3;
@@ -1050,17 +1068,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
                 pv[it] = make_uint4(q[0], q[1], q[2], q[3]);
             }
         }
-        // IC_Angle (:78-105): s = sum of p, t = sum of (u + 15) p over the row's disc span
-        uint32_t s = 0, t = 0;
+        // IC_Angle (:78-105) over this lane's three chunks
+        int s_all = 0, c_all = 0, m01p = 0;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const uint2 wt = s_w[i][sub];
-            const uint32_t b = __builtin_amdgcn_alignbyte(w[i + 1], w[i], shf);
-            s = __builtin_amdgcn_udot4(b, wt.x, s, false);
-            t = __builtin_amdgcn_udot4(b, wt.y, t, false);
+        for (int it = 0; it < 3; ++it) {
+            const int m = min(max(mlo[it] + al, 0), 16), n = min(max(mhi[it] + al, 0), 16);
+            const uint4 mk = s_rng[m][n];
+            const uint32_t p0 = mc[it].x & mk.x, p1 = mc[it].y & mk.y, p2 = mc[it].z & mk.z, p3 = mc[it].w & mk.w;
+            uint32_t sc = __builtin_amdgcn_udot4(p0, 0x01010101u, 0u, false);
+            sc = __builtin_amdgcn_udot4(p1, 0x01010101u, sc, false);
+            sc = __builtin_amdgcn_udot4(p2, 0x01010101u, sc, false);
+            sc = __builtin_amdgcn_udot4(p3, 0x01010101u, sc, false);
+            uint32_t cc = __builtin_amdgcn_udot4(p0, 0x03020100u, 0u, false);  // column within the chunk
+            cc = __builtin_amdgcn_udot4(p1, 0x07060504u, cc, false);
+            cc = __builtin_amdgcn_udot4(p2, 0x0B0A0908u, cc, false);
+            cc = __builtin_amdgcn_udot4(p3, 0x0F0E0D0Cu, cc, false);
+            s_all += (int)sc;
+            c_all += (int)cc + mp16[it] * (int)sc;
+            m01p += mv[it] * (int)sc;
         }
         // sums over the keypoint's lanes (DPP, no LDS round trip but the last step)
-        const int m10 = od_sum((int)t - 15 * (int)s), m01 = od_sum(vrow * (int)s);
+        const int m10 = od_sum(c_all - (15 + al) * s_all), m01 = od_sum(m01p);
         const float angle = fast_atan2_deg((float)m01, (float)m10);
         // computeOrbDescriptor (:108-148): lane `sub` makes bits [8 sub, 8 sub + 8)
         const float factorPI = (float)(3.14159265358979323846 / 180.0);
@@ -1277,6 +1305,13 @@ constexpr int kKnnWaves = KNN_WAVES;     // waves per workgroup, 32 queries each
 constexpr int kKnnThreads = 64 * kKnnWaves;
 constexpr int kKnnQ = 32 * kKnnWaves;    // queries per workgroup
 constexpr int kKnnPitch = 272;           // bytes per expanded train row in LDS (256 + 16: no bank conflicts)
+// 32-row tiles per LDS stage (one barrier per stage).  Round 5 (single stream, 512 images):
+// 1 tile 243-246 us, 2 tiles 251-253 us -- the barrier per tile is not what the waves wait on
+#ifndef KNN_STAGE
+#define KNN_STAGE 1
+#endif
+constexpr int kKnnStage = KNN_STAGE;
+static_assert(kKnnStage == 1 || kKnnStage == 2 || kKnnStage == 4, "stage size");
 constexpr int kKnnSeg = 4096;            // train rows per key segment
 static_assert(kKnnWaves == 4 || kKnnWaves == 8, "expansion roles");
 
@@ -1341,25 +1376,35 @@ __device__ __attribute__((always_inline)) inline void knn2_mfma_block(
         else
             return (uint32_t)*reinterpret_cast<const uint16_t*>(t + (long long)row * 32 + 2 * ed);
     };
-    auto store_expanded = [&](int buf, uint32_t w) __attribute__((always_inline)) {
+    // tile u's rows live in LDS stage buffer ((u - ts) / kKnnStage) & 1, slot (u - ts) % kKnnStage
+    auto tile_lds = [&](int u) __attribute__((always_inline)) {
+        const int v = u - ts;
+        return lds + (((v / kKnnStage) & 1) * kKnnStage + v % kKnnStage) * (32 * kKnnPitch);
+    };
+    auto store_expanded = [&](int u, uint32_t w) __attribute__((always_inline)) {
         if constexpr (kKnnWaves == 4) {
-            uint8_t* dst = lds + buf * (32 * kKnnPitch) + er * kKnnPitch + 32 * ed;
+            uint8_t* dst = tile_lds(u) + er * kKnnPitch + 32 * ed;
             const bool kswap = ed >= 4;
             const uint32_t ws = kswap ? __builtin_amdgcn_alignbit(w, w, 16) : w;  // halves swapped
             const knn_v4i first = knn_expand16(ws & 0xFFFFu), second = knn_expand16(ws >> 16);
             *reinterpret_cast<knn_v4i*>(dst + (kswap ? 16 : 0)) = first;
             *reinterpret_cast<knn_v4i*>(dst + (kswap ? 0 : 16)) = second;
         } else {
-            uint8_t* dst = lds + buf * (32 * kKnnPitch) + er * kKnnPitch + 16 * ed;
+            uint8_t* dst = tile_lds(u) + er * kKnnPitch + 16 * ed;
             *reinterpret_cast<knn_v4i*>(dst) = knn_expand16(w);
         }
     };
-    // packed train words run two tiles ahead of the MFMAs (one in LDS, one in flight): the word
-    // of tile u lives in pk[u & 1]; loads are unconditional (clamped rows) so waits stay counted
+    // Stages of kKnnStage tiles, double-buffered: the waves meet at one barrier per stage (the
+    // stage's tiles expanded, the other buffer free), and each tile's body expands the tile one
+    // stage ahead (u + kKnnStage) into the other buffer, so the expansion work per tile is the
+    // same as with one barrier per tile.  Packed train words run one tile ahead of their
+    // expansion: the word of tile u is loaded in body(u - kKnnStage - 1) and lives in
+    // pk[u & 1]; loads are unconditional (clamped rows) so waits stay counted
     uint32_t pk0 = 0, pk1 = 0;
     if (te > ts) {
-        store_expanded(0, load_packed(ts));
-        pk1 = load_packed(ts + 1);
+        for (int u = ts; u < ts + kKnnStage && u < te; ++u) store_expanded(u, load_packed(u));
+        if ((ts + kKnnStage) & 1) pk1 = load_packed(ts + kKnnStage);
+        else pk0 = load_packed(ts + kKnnStage);
     }
     // accumulator preload, the same for every tile: row(g) = (g & 3) + 8 (g >> 2) + 4 h, so
     // C0[g] = 4095 - 4 h - rowc(g) is 4095 - (tile-local row) and tile k of a segment yields
@@ -1395,13 +1440,17 @@ __device__ __attribute__((always_inline)) inline void knn2_mfma_block(
                 kb1 = knn_max3_i32(kb1, x1, y1);
             }
         };
-        // one tile: PAR = ti & 1 picks the LDS buffer, the accumulator and the packed word
-        auto body = [&](int ti, auto par, knn_v16i& acc, const knn_v16i& prev, uint32_t& pk_use,
-                        uint32_t& pk_load) __attribute__((always_inline)) {
-            constexpr int PAR = decltype(par)::value;
-            __syncthreads();  // tile ti expanded; the other buffer is free
-            pk_load = load_packed(ti + 2);  // word of tile ti + 2 (pk[ti & 1] is free)
-            const uint8_t* ab = lds + PAR * (32 * kKnnPitch) + r * kKnnPitch + 16 * h;
+        // one tile: PAR = ti & 1 picks the accumulator and the packed words
+        auto body = [&](int ti, auto par, knn_v16i& acc, const knn_v16i& prev) __attribute__((always_inline)) {
+            constexpr int PAR = decltype(par)::value;  // ti & 1 (ts is even)
+            // pk[u & 1] holds the word of tile u: this body expands tile ti + kKnnStage and loads
+            // the word of tile ti + kKnnStage + 1
+            uint32_t& pk_use = ((PAR + kKnnStage) & 1) ? pk1 : pk0;
+            uint32_t& pk_load = ((PAR + kKnnStage) & 1) ? pk0 : pk1;
+            if (kKnnStage == 1 || (PAR == 0 && (kKnnStage == 2 || (ti - ts) % kKnnStage == 0)))
+                __syncthreads();  // this stage expanded; the other buffer is free
+            pk_load = load_packed(ti + kKnnStage + 1);
+            const uint8_t* ab = tile_lds(ti) + r * kKnnPitch + 16 * h;
             {
                 const knn_v4i a = *reinterpret_cast<const knn_v4i*>(ab);
                 acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, qf[0], C0, 0, 0, 0);
@@ -1412,7 +1461,7 @@ __device__ __attribute__((always_inline)) inline void knn2_mfma_block(
                 acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, qf[s], acc, 0, 0, 0);
             }
             if (ti > tile0) select(prev, ti - 1 > tile0);
-            if (ti + 1 < te) store_expanded(PAR ^ 1, pk_use);  // word of tile ti + 1
+            if (ti + kKnnStage < te) store_expanded(ti + kKnnStage, pk_use);
             if (ti * 32 + 32 > nt) {  // partial last tile: padding rows never win
 #pragma unroll
                 for (int g = 0; g < 16; ++g)
@@ -1424,11 +1473,11 @@ __device__ __attribute__((always_inline)) inline void knn2_mfma_block(
         knn_v16i acc0, acc1;
         int ti = tile0;
         for (; ti + 1 < tile1; ti += 2) {
-            body(ti, P0{}, acc0, acc1, pk1, pk0);
-            body(ti + 1, P1{}, acc1, acc0, pk0, pk1);
+            body(ti, P0{}, acc0, acc1);
+            body(ti + 1, P1{}, acc1, acc0);
         }
         if (ti < tile1) {
-            body(ti, P0{}, acc0, acc1, pk1, pk0);
+            body(ti, P0{}, acc0, acc1);
             select(acc0, ti > tile0);
         } else if (tile1 > tile0) {
             select(acc1, tile1 - 1 > tile0);
@@ -1461,7 +1510,7 @@ __device__ __attribute__((always_inline)) inline void knn2_mfma_block(
 }
 
 __global__ __launch_bounds__(kKnnThreads) void k_knn2_mfma_pairs(MatchArgs m) {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * 32 * kKnnPitch];
+    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * kKnnStage * 32 * kKnnPitch];
     const int pair = m.pair0 + blockIdx.y;
     const int qimg = 2 * pair, timg = 2 * pair + 1;
     const int qn = m.out_n[qimg], tn = m.out_n[timg];
@@ -1504,7 +1553,7 @@ __global__ __launch_bounds__(256) void k_knn2_merge(MatchArgs m, int nsplit) {
 
 __global__ __launch_bounds__(kKnnThreads) void k_knn2_mfma_plain(const uint8_t* q, int nq, const uint8_t* t, int nt,
                                                          int32_t* i1, int32_t* d1, int32_t* i2, int32_t* d2) {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * 32 * kKnnPitch];
+    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * kKnnStage * 32 * kKnnPitch];
     knn2_mfma_block(q, nq, t, nt, blockIdx.x, 0, (nt + 31) >> 5, i1, d1, i2, d2, nullptr, lds);
 }
 

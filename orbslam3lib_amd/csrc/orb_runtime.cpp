@@ -14,6 +14,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -30,6 +31,9 @@ thread_local std::string g_err;
 
 constexpr size_t kGraphCacheSize = 4;  // captured batch sequences kept per context
 
+// chunk streams a batch of n images is split over (whole stereo pairs per chunk)
+inline int kChunksFor(int n) { return n >= 256 ? 2 : 3; }
+
 int fail(int code, const std::string& msg) {
     g_err = msg;
     return code;
@@ -42,8 +46,7 @@ const char* const kDiagKnobs[] = {"ORBGPU_OD_ITERS",      "ORBGPU_OCT_SMALL_LDS"
                                   "ORBGPU_OCT_SPLIT",     "ORBGPU_OCT_GENERIC",   "ORBGPU_OCT_PYR",
                                   "ORBGPU_FAST_PITCH",    "ORBGPU_STREAMS",       "ORBGPU_ISOLATE",
                                   "ORBGPU_STAGGER",       "ORBGPU_OCT_STAMPS",    "ORBGPU_GRAPH",
-                                  "ORBGPU_KNN_NOSPLIT",   "ORBGPU_NO_TAIL",
-                                  "ORBGPU_FAST_BANDS",    "ORBGPU_FAST_SB"};
+                                  "ORBGPU_KNN_NOSPLIT",   "ORBGPU_NO_TAIL",       "ORBGPU_TAIL_MIN"};
 
 bool diagnostics_on() {
     const char* g = getenv("ORBGPU_DIAGNOSTICS");
@@ -59,30 +62,35 @@ const char* diag_env(const char* name) { return diagnostics_on() ? getenv(name) 
 // is only rescanned when the process has loaded something since the last check (dlpi_adds).
 int check_single_hip_runtime() {
     struct Scan { unsigned long long adds; std::vector<std::string> paths; };
+    // shared by every context and thread (one per eye in the headset): the cached verdict and
+    // its message are read and rescanned under one lock
+    static std::mutex mu;
     static unsigned long long checked_adds = ~0ull;
     static int verdict = 0;
-    static std::string paths_msg;
+    static std::string msg;
     Scan sc{0, {}};
     dl_iterate_phdr([](dl_phdr_info* i, size_t, void* d) -> int {
         static_cast<Scan*>(d)->adds = i->dlpi_adds;
         return 1;  // the counter is the same in every entry: stop at the first
     }, &sc);
-    if (sc.adds == checked_adds) return verdict;
-    dl_iterate_phdr([](dl_phdr_info* i, size_t, void* d) -> int {
-        const char* nm = i->dlpi_name;
-        if (!nm || !*nm) return 0;
-        const char* base = std::strrchr(nm, '/');
-        base = base ? base + 1 : nm;
-        if (std::strncmp(base, "libamdhip64.so", 14) == 0) static_cast<Scan*>(d)->paths.push_back(nm);
-        return 0;
-    }, &sc);
-    checked_adds = sc.adds;
-    verdict = sc.paths.size() > 1 ? ORBGPU_ERR_RUNTIME : 0;
-    paths_msg.clear();
-    for (const auto& q : sc.paths) paths_msg += (paths_msg.empty() ? "" : ", ") + q;
-    if (verdict)
-        g_err = "two HIP runtimes are mapped into this process (" + paths_msg +
-                "): import torch before loading liborbgpu.so, so that both bind to one runtime";
+    std::lock_guard<std::mutex> lk(mu);
+    if (sc.adds != checked_adds) {
+        dl_iterate_phdr([](dl_phdr_info* i, size_t, void* d) -> int {
+            const char* nm = i->dlpi_name;
+            if (!nm || !*nm) return 0;
+            const char* base = std::strrchr(nm, '/');
+            base = base ? base + 1 : nm;
+            if (std::strncmp(base, "libamdhip64.so", 14) == 0) static_cast<Scan*>(d)->paths.push_back(nm);
+            return 0;
+        }, &sc);
+        checked_adds = sc.adds;
+        verdict = sc.paths.size() > 1 ? ORBGPU_ERR_RUNTIME : 0;
+        std::string paths;
+        for (const auto& q : sc.paths) paths += (paths.empty() ? "" : ", ") + q;
+        msg = "two HIP runtimes are mapped into this process (" + paths +
+              "): import torch before loading liborbgpu.so, so that both bind to one runtime";
+    }
+    if (verdict) g_err = msg;  // every refusal, cached or fresh, on every thread
     return verdict;
 }
 
@@ -94,13 +102,13 @@ int check_single_hip_runtime() {
     } while (0)
 
 enum Stage { ST_RESIZE, ST_BLUR, ST_FAST48, ST_FAST, ST_FAST_TOP, ST_OCTREE, ST_ORIENT, ST_FINAL, ST_KNN,
-             ST_STEREO, ST_GRID, ST_SBS, ST_SOA, ST_SBP, ST_FISHEYE, ST_TAIL, ST_FASTB, ST_FASTSB, ST_COUNT };
+             ST_STEREO, ST_GRID, ST_SBS, ST_SOA, ST_SBP, ST_FISHEYE, ST_TAIL, ST_COUNT };
 // names as rocprofv3 shows the kernels (templates with their argument)
 const char* kStageNames[ST_COUNT] = {"k_blur_resize",    "k_blur",   "k_fast_cells<48>", "k_fast_cells<64>",
                                      "k_fast_cells<80>", "k_octree", "k_orient_desc",    "k_finalize",
                                      "k_knn2",           "k_stereo",  "k_undistort_grid",
                                      "k_sbs_split",      "k_pack_soa",       "k_sbp",
-                                     "k_fisheye_stereo", "k_pyr_tail", "k_fast_bands", "k_fast_sb"};
+                                     "k_fisheye_stereo", "k_pyr_tail"};
 
 struct DevBuf {
     void* p = nullptr;
@@ -196,6 +204,7 @@ struct orbgpu_ctx {
     // the captured launch sequences of one-stream batches (run_batch / run_batch_match), keyed by
     // {images, width, height, input slot, match pairs, stereo rows only}: one exec per key, so
     // alternating input slots (async uploads) or match variants replay instead of recapturing
+    bool streams_forced = false;  // ORBGPU_STREAMS (diagnostics): every sub stream is a chunk
     bool use_graph = true;   // ORBGPU_GRAPH=0 launches every kernel directly (A/B)
     struct GraphRec { int key[6]; hipGraphExec_t exec; unsigned long long used; };
     std::vector<GraphRec> graphs;
@@ -444,7 +453,9 @@ int set_geometry(orbgpu_ctx* c, int w, int h) {
     }
     // k_pyr_tail: the smallest t >= 2 such that level t - 1 and level t (and level t's resize
     // tables) fit one workgroup's LDS together; the tail then makes levels t .. L-1 and blurs
-    // t - 1 .. L-1 (ORBGPU_NO_TAIL under diagnostics: per-level launches only)
+    // t - 1 .. L-1 (ORBGPU_NO_TAIL under diagnostics: per-level launches only).  Its pad columns
+    // and row reflection take one REFLECT_101 step, exact for levels of >= 4 px: every level
+    // passed the 2 * kEdge + 4 check above.
     for (int l = 0; l < L; ++l) A.lv[l].tpitch = round_up(A.lv[l].w + 28, 16);
     A.tail0 = L + 1;
     if (!diag_env("ORBGPU_NO_TAIL"))
@@ -464,6 +475,11 @@ int set_geometry(orbgpu_ctx* c, int w, int h) {
                 break;
             }
         }
+    // the tail runs for launches of at least tail_min images (one 1024-thread workgroup per image
+    // makes levels tail0 .. L-1 serially: 46 us for one pair, where the per-level launches take
+    // ~20 us; with hundreds of images the tail's single pass wins)
+    A.tail_min = kTailMinImages;
+    if (const char* e = diag_env("ORBGPU_TAIL_MIN")) A.tail_min = std::max(0, atoi(e));
     c->pyr_img = round_up_ll(pyr, 256);
     c->blur_img = round_up_ll(blr, 256);
     c->cellkeys_img = ck;
@@ -572,80 +588,6 @@ int set_geometry(orbgpu_ctx* c, int w, int h) {
     }
     A.fast_n48 = tier_end[0];
     A.fast_n64 = tier_end[1];
-    // k_fast_bands segments: each cell row of a level split into runs of whole cells at most
-    // kFastBandMaxWaves x 62 column quads wide (every cell's detection pixels in one workgroup)
-    // k_fast_bands (dense, threshold-independent; bit-exact) measured slower than the sparse
-    // per-cell kernel on gfx950: diagnostics only
-    A.fast_dense = diag_env("ORBGPU_FAST_BANDS") ? 1 : diag_env("ORBGPU_FAST_SB") ? 2 : 0;
-    {
-        std::vector<int4> recs[kFastBandMaxWaves];
-        int lds[kFastBandMaxWaves] = {0, 0, 0, 0};
-        for (int l = 0; l < L; ++l) {
-            const LevelGeom& G = A.lv[l];
-            auto x0 = [&](int j) { return kMinBorder + j * G.wCell + 3; };
-            auto x1 = [&](int j) {
-                const int iniX = kMinBorder + j * G.wCell;
-                return iniX >= G.maxBX - 6 ? x0(j) : std::min(iniX + G.wCell + 6, G.maxBX) - 3;
-            };
-            for (int i = 0; i < G.nRows; ++i) {
-                const int iniY = kMinBorder + i * G.hCell;
-                const int nrows = iniY >= G.maxBY - 3 ? 0 : std::max(std::min(iniY + G.hCell + 6, G.maxBY) - 6 - iniY, 0);
-                int j0 = 0;
-                while (j0 < G.nCols) {
-                    auto quads = [&](int ja, int jb) {
-                        int xe = x0(ja);
-                        for (int j = ja; j < jb; ++j) xe = std::max(xe, x1(j));
-                        return xe > x0(ja) ? ((xe - 1) >> 2) - (x0(ja) >> 2) + 1 : 0;
-                    };
-                    int j1 = j0 + 1;
-                    while (j1 < G.nCols && quads(j0, j1 + 1) <= 62 * kFastBandMaxWaves) ++j1;
-                    const int nq = quads(j0, j1);
-                    const int nw = std::max(1, (nq + 61) / 62);
-                    if (nw > kFastBandMaxWaves) return fail(ORBGPU_ERR_INVALID, "FAST band segment too wide");
-                    recs[nw - 1].push_back(make_int4(l, i, j0, j1));
-                    const int bytes = 4 * (16 * ((j1 - j0 + 15) / 16) + nrows * nq);
-                    lds[nw - 1] = std::max(lds[nw - 1], bytes);
-                    j0 = j1;
-                }
-            }
-        }
-        // k_fast_sb: one wave per run of whole cells spanning at most 62 column quads
-        std::vector<int4> sb;
-        for (int l = 0; l < L; ++l) {
-            const LevelGeom& G = A.lv[l];
-            auto x0 = [&](int j) { return kMinBorder + j * G.wCell + 3; };
-            auto x1 = [&](int j) {
-                const int iniX = kMinBorder + j * G.wCell;
-                return iniX >= G.maxBX - 6 ? x0(j) : std::min(iniX + G.wCell + 6, G.maxBX) - 3;
-            };
-            auto quads = [&](int ja, int jb) {
-                int xe = x0(ja);
-                for (int j = ja; j < jb; ++j) xe = std::max(xe, x1(j));
-                return xe > x0(ja) ? ((xe - 1) >> 2) - (x0(ja) >> 2) + 1 : 0;
-            };
-            for (int i = 0; i < G.nRows; ++i)
-                for (int ja = 0; ja < G.nCols;) {
-                    int jb = ja + 1;
-                    while (jb < G.nCols && jb - ja < 8 && quads(ja, jb + 1) <= 62) ++jb;
-                    if (quads(ja, jb) > 62) return fail(ORBGPU_ERR_INVALID, "FAST cell wider than a wave");
-                    sb.push_back(make_int4(l, i, ja, jb));
-                    ja = jb;
-                }
-        }
-        A.fast_sb_off = (int)c->rtab_host.size();
-        A.fast_sb_n = (int)sb.size();
-        c->rtab_host.insert(c->rtab_host.end(), sb.begin(), sb.end());
-        A.fast_band_off = (int)c->rtab_host.size();
-        int n = 0;
-        A.fast_band_grp[0] = 0;
-        for (int w = 0; w < kFastBandMaxWaves; ++w) {
-            for (const int4& r4 : recs[w]) c->rtab_host.push_back(r4);
-            n += (int)recs[w].size();
-            A.fast_band_grp[w + 1] = n;
-            A.fast_band_lds[w] = (lds[w] + 15) & ~15;
-            if (A.fast_band_lds[w] > kTailLdsMax) return fail(ORBGPU_ERR_INVALID, "FAST band LDS");
-        }
-    }
     A.total_tiles = tile_first;
     A.total_od_blocks = od_first;
     A.od_tab_off = (int)c->rtab_host.size();
@@ -877,10 +819,9 @@ int orbgpu_create(const orbgpu_params* p, int device, int max_width, int max_hei
         // process's hardware queues, which a second context (the other eye's thread) needs for its
         // own work not to queue behind this one's.
         const char* e = diag_env("ORBGPU_STREAMS");
-        // batches of >= 128 pairs: 2 chunk streams (each chunk fills the GPU); smaller batches
-        // (C5's 16 1080p pairs: 161 vs 154 Mfeatures/s) keep 3
-        const int ns_default = max_images >= 256 ? 2 : 3;
-        const int ns = std::max(1, std::min({8, e ? atoi(e) : ns_default, max_images / 2}));
+        // up to 3 chunk streams; run_batch_impl picks the chunk count per batch (kChunksFor)
+        c->streams_forced = e != nullptr;
+        const int ns = std::max(1, std::min({8, e ? atoi(e) : 3, max_images / 2}));
         for (int k = 1; k < ns; ++k) {
             hipStream_t st;
             if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) break;
@@ -1090,7 +1031,10 @@ static int run_batch_impl(orbgpu_ctx* c, int n, int w, int h, const int32_t* lap
     // bottlenecks (octree latency, FAST VALU, blur/resize HBM), so their phases overlap.
     struct Chunk { int img0, n; hipStream_t st; };
     std::vector<Chunk> chunks;
-    const int K = (!stream && (n % 2) == 0) ? std::min((int)c->sub.size(), n / 2) : 1;
+    // chunks per batch: batches of >= 128 pairs take 2 (each chunk fills the GPU); smaller ones
+    // 3 (C5's 16 1080p pairs: 161 vs 154 Mfeatures/s); ORBGPU_STREAMS forces the stream count
+    const int kmax = c->streams_forced ? (int)c->sub.size() : kChunksFor(n);
+    const int K = (!stream && (n % 2) == 0) ? std::min({(int)c->sub.size(), kmax, n / 2}) : 1;
     // a different sub-batch layout than last time may put an image on another stream: drain first
     if (!c->last_chunks.empty() && ((int)c->last_chunks.size() != K || c->last_images != n))
         if (int e_ = ctx_sync(c)) return e_;
@@ -1152,7 +1096,10 @@ static int run_batch_impl(orbgpu_ctx* c, int n, int w, int h, const int32_t* lap
     auto launch_all = [&]() -> int {
         int r = 0;
         // k_blur_resize makes levels 1 .. last_br - 1; k_pyr_tail the rest (or k_blur the last blur)
-        const bool tail = A.tail0 <= A.nlevels;
+        int chunk_images = 0;
+        for (const Chunk& ch : chunks) chunk_images = std::max(chunk_images, ch.n);
+        if (c->serialize || chunks.size() == 1) chunk_images = n;
+        const bool tail = A.tail0 <= A.nlevels && chunk_images >= A.tail_min;
         const int last_br = tail ? A.tail0 : A.nlevels;
         if (stagger) {
             // chunk-major: chunk k's first kernel waits for chunk k-1's pyramid + blur
@@ -1185,11 +1132,7 @@ static int run_batch_impl(orbgpu_ctx* c, int n, int w, int h, const int32_t* lap
                 if ((r = each(ST_BLUR, [&](const BatchArgs& B, hipStream_t st) { return launch_blur_level(B, lt, st); }))) return r;
             }
         }
-        if (A.fast_dense == 2) {
-            if ((r = each(ST_FASTSB, [](const BatchArgs& B, hipStream_t st) { return launch_fast_sb(B, st); }))) return r;
-        } else if (A.fast_dense == 1) {
-            if ((r = each(ST_FASTB, [](const BatchArgs& B, hipStream_t st) { return launch_fast_bands(B, st); }))) return r;
-        } else {   // the FAST tiles as one group: one join / fork around all of them when isolated
+        {   // the FAST tiles as one group: one join / fork around all of them when isolated
             const int tiles[3] = {kCellPitchTiny, kCellPitchSmall, kCellMax};
             const int stages[3] = {ST_FAST48, ST_FAST, ST_FAST_TOP};
             bool any[3], iso = false;

@@ -72,17 +72,6 @@ def test_adversarial_textures_batch(oracle):
     _check_batch(oracle, _frames(), dense=True)
 
 
-@pytest.mark.parametrize("kernel", ["sb", "bands"])
-def test_adversarial_textures_other_fast_kernels(oracle, monkeypatch, kernel):
-    """The same frames (and the saturating pattern) through the sparse-band k_fast_sb (ORBGPU_FAST_SB) and
-    the dense k_fast_bands (ORBGPU_FAST_BANDS): every cell of the low-contrast frame falls back
-    to minThFAST, the salt-and-pepper frame has many equal strengths beside each other."""
-    monkeypatch.setenv("ORBGPU_DIAGNOSTICS", "1")
-    monkeypatch.setenv("ORBGPU_FAST_SB" if kernel == "sb" else "ORBGPU_FAST_BANDS", "1")
-    _check_batch(oracle, _frames(), dense=True)
-    _check_batch(oracle, _saturating_frames())
-
-
 def _check_batch(oracle, frames, dense=False):
     import orbslam3lib_amd as og
     imgs = np.stack(frames)

@@ -1,5 +1,5 @@
-"""CPU: the dense, threshold-independent formulation k_fast_bands (orbslam3lib_amd/csrc/orb_fast.hip)
-is built on, restated in numpy and checked against the oracle's cell loop
+"""CPU: the dense, threshold-independent FAST formulation (round 4's k_fast_bands, measured slower
+than k_fast_cells and removed from the library in round 5), restated in numpy and checked against the oracle's cell loop
 (ComputeKeyPointsOctTree, ORBextractor_old.cc:807-871, with cv::FAST per cell ROI):
 
   m(p)   = max(v - min over 9-arcs of the arc maximum, max over 9-arcs of the arc minimum - v, 0)

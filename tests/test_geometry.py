@@ -39,11 +39,21 @@ def _check_knn(oracle, be, p, q, t):
         np.testing.assert_array_equal(a, b, err_msg="pair %d %s" % (p, name))
 
 
-def test_headset_sbs_1280x400(oracle):
+def _force_tail(monkeypatch, tail):
+    """tail="forced": k_pyr_tail even for these few-image launches (the product takes it from 128
+    images per launch on), so both pyramid paths see the geometry."""
+    if tail == "forced":
+        monkeypatch.setenv("ORBGPU_DIAGNOSTICS", "1")
+        monkeypatch.setenv("ORBGPU_TAIL_MIN", "0")
+
+
+@pytest.mark.parametrize("tail", ["default", "forced"])
+def test_headset_sbs_1280x400(oracle, monkeypatch, tail):
     """Three 1280x400 side-by-side frames -> split on the device -> extraction of every eye and
     the stereo-row kNN2 (BFMatchORB, Frame.cc:1164) of every pair; pyramid and blurred levels of
     one eye as well."""
     import orbslam3lib_amd as og
+    _force_tail(monkeypatch, tail)
     W, H = 640, 400
     pairs = [synth.stereo_pair(H, W, 300 + s) for s in range(3)]
     frames = np.ascontiguousarray(np.stack([np.concatenate([L, R], 1) for L, R in pairs]))
@@ -70,11 +80,13 @@ def test_headset_sbs_1280x400(oracle):
                                       err_msg="blurred level %d" % l)
 
 
+@pytest.mark.parametrize("tail", ["default", "forced"])
 @pytest.mark.parametrize("w,h", [(641, 401), (643, 479), (753, 481), (637, 403)])
-def test_odd_level0_sizes(oracle, w, h):
+def test_odd_level0_sizes(oracle, monkeypatch, w, h, tail):
     """Odd / non-multiple-of-4 level-0 sizes through the single-image path and the chunked batch
     path (chunk streams), with lapping areas ending inside the frame."""
     import orbslam3lib_amd as og
+    _force_tail(monkeypatch, tail)
     ex = og.ORBextractor(2000, 1.2, 8, 20, 7, max_width=w, max_height=h)
     img = synth.frame(h, w, 40 + w)
     for lap in ((0, 0), (101, w - 37)):

@@ -167,13 +167,8 @@ def test_euroc_size_and_other_frames(oracle):
         np.testing.assert_array_equal(g[1], r[1])
 
 
-@pytest.mark.parametrize("kernel", ["cells", "sb", "bands"])
-def test_c5_1080p_12_levels(oracle, monkeypatch, kernel):
-    """C5's frame through each FAST kernel; its 1882-px level 0 splits every cell row into
-    eight k_fast_sb waves and two k_fast_bands segments (four waves each)."""
-    if kernel != "cells":
-        monkeypatch.setenv("ORBGPU_DIAGNOSTICS", "1")
-        monkeypatch.setenv("ORBGPU_FAST_SB" if kernel == "sb" else "ORBGPU_FAST_BANDS", "1")
+def test_c5_1080p_12_levels(oracle):
+    """C5's frame: 1920x1080, 12 levels, 5000 features."""
     img = synth.frame(1080, 1920, 2)
     ex = _extractor(nf=5000, L=12, w=1920, h=1080)
     g = ex(img, None, (0, 0))
@@ -313,14 +308,9 @@ def test_forced_fast_tile(oracle, frame0, monkeypatch, pitch):
     np.testing.assert_array_equal(d, rd)
 
 
-@pytest.mark.parametrize("kernel", ["cells", "sb", "bands"])
-def test_general_fast_tile_small_frame(oracle, monkeypatch, kernel):
-    """A small frame (cells wider than 55 px on its top levels) through each FAST kernel:
-    k_fast_cells (the product path; it picks its 80-byte tile by itself there), the sparse-band
-    k_fast_sb (ORBGPU_FAST_SB) and the dense k_fast_bands (ORBGPU_FAST_BANDS)."""
-    if kernel != "cells":
-        monkeypatch.setenv("ORBGPU_DIAGNOSTICS", "1")
-        monkeypatch.setenv("ORBGPU_FAST_SB" if kernel == "sb" else "ORBGPU_FAST_BANDS", "1")
+def test_general_fast_tile_small_frame(oracle):
+    """A small frame (cells wider than 55 px on its top levels): k_fast_cells picks its 80-byte
+    tile by itself there."""
     img = synth.frame(120, 160, 5)
     ex = _extractor(nf=300, L=4, w=160, h=120)
     k, d, m = ex(img)
@@ -354,11 +344,12 @@ def _check_pyramid(ex, oracle, imgs, sf=1.2, L=8):
 @pytest.mark.parametrize("tail", [True, False])
 def test_pyramid_per_level_path(oracle, monkeypatch, tail):
     """The per-level k_blur_resize launches then k_pyr_tail (levels 5-7 and the blurs of 4-7 of
-    a 640x480 pyramid in one launch) -- or, with the tail off (ORBGPU_NO_TAIL), k_blur_resize for
-    every level and k_blur for the last: pyramid and blurred levels of a stereo pair."""
-    if not tail:
-        monkeypatch.setenv("ORBGPU_DIAGNOSTICS", "1")
-        monkeypatch.setenv("ORBGPU_NO_TAIL", "1")
+    a 640x480 pyramid in one launch; forced with ORBGPU_TAIL_MIN=0, since the product takes the
+    tail only for launches of >= 128 images) -- or, with the tail off (ORBGPU_NO_TAIL, the path a
+    pair takes by default), k_blur_resize for every level and k_blur for the last: pyramid and
+    blurred levels of a stereo pair."""
+    monkeypatch.setenv("ORBGPU_DIAGNOSTICS", "1")
+    monkeypatch.setenv("ORBGPU_TAIL_MIN" if tail else "ORBGPU_NO_TAIL", "0" if tail else "1")
     L, R = synth.stereo_pair(480, 640, 3)
     ex = _extractor()
     ex.extract_stereo(L, R)
@@ -369,10 +360,10 @@ def test_pyramid_per_level_path(oracle, monkeypatch, tail):
 def test_pyramid_exact_2x_area_path(oracle, monkeypatch, tail):
     """Scale factor 2 on a 640x480 frame: every level is an exact 2x downscale, which OpenCV
     serves with INTER_AREA (2x2 mean) instead of INTER_LINEAR (the area path of k_blur_resize
-    for level 1 and of k_pyr_tail for level 2; with the tail off, k_blur_resize's for both)."""
-    if not tail:
-        monkeypatch.setenv("ORBGPU_DIAGNOSTICS", "1")
-        monkeypatch.setenv("ORBGPU_NO_TAIL", "1")
+    for level 1 and of k_pyr_tail for level 2, forced with ORBGPU_TAIL_MIN=0; with the tail off,
+    k_blur_resize's for both)."""
+    monkeypatch.setenv("ORBGPU_DIAGNOSTICS", "1")
+    monkeypatch.setenv("ORBGPU_TAIL_MIN" if tail else "ORBGPU_NO_TAIL", "0" if tail else "1")
     img = synth.frame(480, 640, 6)
     ex = _extractor(nf=500, L=3, sf=2.0)
     k, d, m = ex(img)

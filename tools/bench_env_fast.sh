@@ -1,6 +1,8 @@
 #!/bin/bash
 # Headline only (every side leg off) under each environment setting: value and ms_per_step.
 cd "$(dirname "$0")/.."
+# the library honours ORBGPU_* knobs only with the diagnostics gate on
+export ORBGPU_DIAGNOSTICS=1
 mkdir -p gpurun_out/benchenvf
 i=0
 for setting in "$@"; do
