@@ -21,6 +21,17 @@
 #ifndef FAST_SINK
 #define FAST_SINK 0
 #endif
+#ifndef FAST_PRETEST8
+#define FAST_PRETEST8 0  // pre-test: 8 pixels per lane, ds_read_b64 + DPP neighbours (0: 4 per lane)
+#endif
+#ifndef FAST_2X1
+#define FAST_2X1 0  // strength phase: two single-side candidates per lane (0: one two-sided)
+#endif
+#ifndef FAST_THREADS
+// k_fast_cells workgroup: one wave per cell.  Round 5 (single stream, 512 images, k_fast_cells<48>):
+// 2 waves per cell 678-684 us, 1 wave 648-664 us, 1 wave with the fixed-size policy 652-654 us
+#define FAST_THREADS 64
+#endif
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -76,9 +87,10 @@ __device__ inline uint32_t fw_as32(fw_u16x2 x) { return __builtin_bit_cast(uint3
 // nhi = ~hi, hi = sat(v + t):  (p + nhi) >> 1 >= 128  <=>  p > hi  (brighter): one instruction
 // per ring point and side, bit 7 of each byte.  lo / hi come from 16-bit halves (v_perm split,
 // clamped v_pk_sub_u16) -- 40 VALU per 4 pixels where the packed-16-bit form took ~62.
-__device__ inline uint32_t fw_pretest4(uint32_t C, uint32_t Cm, uint32_t Cp, uint32_t U3, uint32_t D3,
-                                       uint32_t U2m, uint32_t U2, uint32_t U2p, uint32_t D2m, uint32_t D2,
-                                       uint32_t D2p, uint32_t tt, uint32_t kt) {
+// Returns {dark, bright}: 0x80 in the bytes whose pixel passed on that side.
+__device__ inline uint2 fw_pretest4(uint32_t C, uint32_t Cm, uint32_t Cp, uint32_t U3, uint32_t D3,
+                                    uint32_t U2m, uint32_t U2, uint32_t U2p, uint32_t D2m, uint32_t D2,
+                                    uint32_t D2p, uint32_t tt, uint32_t kt) {
     const uint32_t L3 = __builtin_amdgcn_alignbyte(C, Cm, 1);    // (-3, 0): ring 12
     const uint32_t R3 = __builtin_amdgcn_alignbyte(Cp, C, 3);    // (+3, 0): ring 4
     const uint32_t UL = __builtin_amdgcn_alignbyte(U2, U2m, 2);  // (-2, -2): ring 10
@@ -106,7 +118,7 @@ __device__ inline uint32_t fw_pretest4(uint32_t C, uint32_t Cm, uint32_t Cp, uin
     y = (br(D3) | br(U3)) & y;
     y = (br(DR) | br(UL)) & y;
     y = (br(UR) | br(DL)) & y;
-    return (~x | y) & 0x80808080u;
+    return make_uint2(~x & 0x80808080u, y & 0x80808080u);
 }
 
 // Per-cell scratch (LDS on the GPU).
@@ -187,8 +199,8 @@ __host__ __device__ void fast_cell_stage(Pol& p, const uint8_t* src, long long p
         uint4* M128 = reinterpret_cast<uint4*>(M);
         // the first kIt chunks per thread are all loaded before any is stored, so their round
         // trips overlap (a rolled load -> wait -> store loop pays one round trip per chunk);
-        // kIt covers every chunk at 128 threads (the device's workgroup), the loop after it the rest
-        constexpr int kIt = (CP * RQ + 127) / 128;
+        // kIt covers every chunk at FAST_THREADS threads (the device's workgroup), the loop after it the rest
+        constexpr int kIt = (CP * RQ + FAST_THREADS - 1) / FAST_THREADS;
         uint4 v[kIt];
 #pragma unroll
         for (int k = 0; k < kIt; ++k) {
@@ -249,7 +261,14 @@ __host__ __device__ int fast_cell_detect(Pol& p, int sh, const CellGeom& g, int 
     const int tmin = min_th < 0 ? 0 : (min_th > 255 ? 255 : min_th);
     const int W = p.nwaves(), w = p.wave(), L = p.wave_width(), lane = p.lane();
     const uint64_t lt = p.lanemask_lt();
-#if defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__) && FAST_PRETEST8
+    // device: the pre-test takes the 8 pixels of one 8-byte LDS pair per lane (two fw_pretest4);
+    // a wave owns a contiguous range of detection rows, and its list starts after the detection
+    // pixels of the rows before it
+    const int r0 = w * dr / W, r1 = (w + 1) * dr / W;
+    const int i0 = r0 * dc;
+    (void)lane;
+#elif defined(__HIP_DEVICE_COMPILE__)
     // device: the pre-test takes 4 pixels per lane (fw_pretest4); a wave owns a contiguous
     // row-major range of (row, dword group) items, and its list starts after the detection
     // pixels of the items before it
@@ -289,6 +308,98 @@ __host__ __device__ int fast_cell_detect(Pol& p, int sh, const CellGeom& g, int 
     auto build = [&](int t) {
         int na = 0;
 #if defined(__HIP_DEVICE_COMPILE__)
+#if FAST_PRETEST8
+        {
+            // lane = (row rr of the iteration, 8-byte pair q of the LDS row): RP pairs per row
+            // cover the whole pitch, RPL rows per iteration (CP = 48: 10 rows x 6 pairs = 60
+            // lanes), so each row is read with 5 conflict-free ds_read_b64 (rows -3, -2, 0, 2, 3:
+            // 32 lanes read 32 consecutive pairs) and the dwords left / right of a pair come from
+            // the neighbouring lanes by DPP (wave_shr / wave_shl 1).  A row's first and last
+            // pairs get a neighbour of another row there, which only the halo pixels use.
+            constexpr int RP = CP / 8, RPL = 64 / RP, LN = RP * RPL;
+            const int rr = min(lane / RP, RPL - 1), q = lane - (lane / RP) * RP;
+            const uint32_t tt = (uint32_t)t * 0x00010001u, kt = (uint32_t)(255 - t) * 0x00010001u;
+            auto rank = [](uint64_t b) {  // set lanes of b below this lane
+                return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32),
+                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
+            };
+            // 0x80 in the bytes of detection columns [3 + sh, 3 + sh + dc) of this lane's pair
+            auto det_mask = [&](int b0) {
+                uint32_t m = 0;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) m |= (b0 + j >= 3 + sh && b0 + j < 3 + sh + dc) ? (0x80u << (8 * j)) : 0u;
+                return m;
+            };
+            const uint32_t em0 = lane < LN ? det_mask(8 * q) : 0u, em1 = lane < LN ? det_mask(8 * q + 4) : 0u;
+            // each pair read on its own address register: the compiler would fuse two of them
+            // into a ds_read2_b64, which takes 8 LDS cycles where two ds_read_b64 take 4
+            auto ld64 = [&](int off) {
+                asm volatile("" : "+v"(off));
+                return *reinterpret_cast<const uint2*>(T + off);
+            };
+            auto shr1 = [](uint32_t v) { return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x138, 0xF, 0xF, true); };
+            auto shl1 = [](uint32_t v) { return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x130, 0xF, 0xF, true); };
+            for (int rb = r0; rb < r1; rb += RPL) {
+                const int r = rb + rr;
+                const bool in = lane < LN && r < r1;
+                const int pr = (int)__umul24((uint32_t)(min(r, r1 - 1) + 3), (uint32_t)CP) + 8 * q;  // pair in tile row r + 3
+                const uint2 C = ld64(pr), U3 = ld64(pr - 3 * CP), D3 = ld64(pr + 3 * CP);
+                const uint2 U2 = ld64(pr - 2 * CP), D2 = ld64(pr + 2 * CP);
+                const uint32_t Cl = shr1(C.y), Cr = shl1(C.x);
+                const uint32_t U2l = shr1(U2.y), U2r = shl1(U2.x), D2l = shr1(D2.y), D2r = shl1(D2.x);
+                const uint2 s0 = fw_pretest4(C.x, Cl, C.y, U3.x, D3.x, U2l, U2.x, U2.y, D2l, D2.x, D2.y, tt, kt);
+                const uint2 s1 = fw_pretest4(C.y, C.x, Cr, U3.y, D3.y, U2.x, U2.y, U2r, D2.x, D2.y, D2r, tt, kt);
+                const uint32_t m0 = in ? (s0.x | s0.y) & em0 : 0u, m1 = in ? (s1.x | s1.y) & em1 : 0u;
+                // the sides that passed, per pixel, into the strength plane (0x80 bright, 0x40 dark;
+                // 0 for every other pixel of the row): the strength phase evaluates a candidate's
+                // passing side only, and overwrites the byte with m (corner) or 0
+                if (FAST_2X1 && in)
+                    *reinterpret_cast<uint2*>(M + pr) = make_uint2((s0.y & m0) | ((s0.x & m0) >> 1),
+                                                                   (s1.y & m1) | ((s1.x & m1) >> 1));
+                // 4-bit pass masks of the two dwords (bit k = byte k) by v_dot4_u32_u8 of the 0x80 bytes
+                const uint32_t n0 = __builtin_amdgcn_udot4(m0, 0x08040201u, 0u, false) >> 7;
+                const uint32_t n1 = __builtin_amdgcn_udot4(m1, 0x08040201u, 0u, false) >> 7;
+                const int c0 = __builtin_popcount(m0), c1 = __builtin_popcount(m1), c = c0 + c1;
+                const uint64_t b0 = p.ballot(c & 1), b1 = p.ballot(c & 2), b2 = p.ballot(c & 4), b3 = p.ballot(c & 8);
+                int pos = na + rank(b0) + 2 * rank(b1) + 4 * rank(b2);
+                if (b3) pos += 8 * rank(b3);
+                // the two dwords as two list runs in row-major order: run 0 = the c0 entries of
+                // dword 0 at pos, run 1 = the c1 entries of dword 1 at pos + c0.  Each run writes 4
+                // slots in the order k = 3, 2, 1, 0, runs interleaved (run 0 then run 1 per k):
+                // the slots of a run past its entries hold garbage that a later write overwrites
+                // (its own run 1, or a later lane's run at a smaller k), or that lands in the
+                // wave's spare entries; empty runs write the sink.  Slot 3 is written only when
+                // some run of the wave has 4 entries.
+                const uint2 lv0 = cs.lut[n0], lv1 = cs.lut[n1];
+                const uint32_t base = __umul24((uint32_t)pr, 0x10001u);  // inactive lanes: c = 0
+                const uint32_t e01a = base + lv0.x, e23a = base + lv0.y;
+                const uint32_t e01b = base + 0x40004u + lv1.x, e23b = base + 0x40004u + lv1.y;
+                uint16_t* da = c0 ? list + pos : sink;
+                uint16_t* db = c1 ? list + pos + c0 : sink;
+                if (p.ballot((n0 == 15u) | (n1 == 15u))) {
+                    da[3] = (uint16_t)(e23a >> 16);
+                    asm volatile("" ::: "memory");
+                    db[3] = (uint16_t)(e23b >> 16);
+                    asm volatile("" ::: "memory");
+                }
+                da[2] = (uint16_t)e23a;
+                asm volatile("" ::: "memory");  // keep the slot order
+                db[2] = (uint16_t)e23b;
+                asm volatile("" ::: "memory");
+                da[1] = (uint16_t)(e01a >> 16);
+                asm volatile("" ::: "memory");
+                db[1] = (uint16_t)(e01b >> 16);
+                asm volatile("" ::: "memory");
+                da[0] = (uint16_t)e01a;
+                asm volatile("" ::: "memory");
+                db[0] = (uint16_t)e01b;
+                na += p.popc64(b0) + 2 * p.popc64(b1) + 4 * p.popc64(b2) + 8 * p.popc64(b3);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the list is read by other lanes
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+#else
         {
             constexpr int RW = CP / 4;
             const uint32_t* T32 = reinterpret_cast<const uint32_t*>(T);
@@ -313,10 +424,12 @@ __host__ __device__ int fast_cell_detect(Pol& p, int sh, const CellGeom& g, int 
                 const int i = base + lane;
                 uint32_t m8 = 0;  // 0x80 per passing pixel
                 if (i < j1) {
-                    m8 = fw_pretest4(T32[dw], T32[dw - 1], T32[dw + 1], T32[dw - 3 * RW], T32[dw + 3 * RW],
-                                     T32[dw - 2 * RW - 1], T32[dw - 2 * RW], T32[dw - 2 * RW + 1],
-                                     T32[dw + 2 * RW - 1], T32[dw + 2 * RW], T32[dw + 2 * RW + 1], tt, kt);
-                    m8 &= cs.emask[q];  // detection pixels of the row's first / last group
+                    const uint2 sd = fw_pretest4(T32[dw], T32[dw - 1], T32[dw + 1], T32[dw - 3 * RW], T32[dw + 3 * RW],
+                                                 T32[dw - 2 * RW - 1], T32[dw - 2 * RW], T32[dw - 2 * RW + 1],
+                                                 T32[dw + 2 * RW - 1], T32[dw + 2 * RW], T32[dw + 2 * RW + 1], tt, kt);
+                    m8 = (sd.x | sd.y) & cs.emask[q];  // detection pixels of the row's first / last group
+                    if (FAST_2X1)  // the passing sides into the strength plane (0x80 bright, 0x40 dark)
+                        reinterpret_cast<uint32_t*>(M)[dw] = (sd.y & m8) | ((sd.x & m8) >> 1);
                 }
                 // the 4-bit pass mask (bit k = byte k) by one v_dot4_u32_u8 of the 0x80 bytes
                 const uint32_t m4 = __builtin_amdgcn_udot4(m8, 0x08040201u, 0u, false) >> 7;
@@ -374,6 +487,7 @@ __host__ __device__ int fast_cell_detect(Pol& p, int sh, const CellGeom& g, int 
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
+#endif
 #else
         for (int base = i0; base < i1; base += L) {
             const bool in = base + lane < i1;
@@ -396,6 +510,50 @@ __host__ __device__ int fast_cell_detect(Pol& p, int sh, const CellGeom& g, int 
 #if FAST_VAR == 3
         return na;
 #endif
+#if defined(__HIP_DEVICE_COMPILE__) && FAST_2X1
+        // exact strength of every candidate (m > t <=> corner at t), corners kept in order.  A
+        // batch is 128 candidates: lane j takes candidates base + j (half 0) and base + 64 + j
+        // (half 1) and evaluates only the side each passed (fast_strength_2x1, one packed
+        // evaluation for two candidates); a batch holding a candidate that passed both sides
+        // (0.1% of candidates on the SURVEY frames) evaluates both sides of each candidate
+        // instead (fast_strength_packed).  The next batch's entries are read one batch ahead (the
+        // in-place writes of a batch land below its own end, never on entries not yet read).
+        int nb = 0;
+        auto ent = [&](int j) { return (int)list[j < na ? j : na - 1]; };
+        int oa_n = na > 0 ? ent(lane) : 0, ob_n = na > 0 ? ent(64 + lane) : 0;
+        for (int base = 0; base < na; base += 128) {
+            const int ja = base + lane, jb = base + 64 + lane;
+            const int oa = oa_n, ob = ob_n;
+            if (base + 128 < na) {
+                oa_n = ent(base + 128 + lane);
+                ob_n = ent(base + 192 + lane);
+            }
+            const int fa = M[oa], fb = M[ob];  // pass flags: 0x80 bright, 0x40 dark
+            int sa, sb;
+#if FAST_VAR == 1  // measurement variant: every candidate a corner of strength t + 1
+            sa = sb = t + 1;
+#else
+            if (p.ballot((ja < na && fa == 0xC0) || (jb < na && fb == 0xC0))) {
+                sa = fast_strength_packed<CP>(&T[oa]);
+                sb = fast_strength_packed<CP>(&T[ob]);
+            } else {
+                // the pairs are packed with a v_perm per ring point: on gfx950 a
+                // ds_read_u8_d16_hi zeroes the low half of its register instead of keeping it
+                // (tools/d16_probe.hip), so the two bytes cannot be loaded into one register
+                fast_strength_2x1<CP>(&T[oa], &T[ob], (fa & 0x80) != 0, (fb & 0x80) != 0, &sa, &sb);
+            }
+#endif
+            const bool ca = ja < na && sa > t, cb = jb < na && sb > t;
+            const uint64_t ba = p.ballot(ca), bb = p.ballot(cb);
+            // the strength plane: m for corners, 0 for the other candidates (flags cleared)
+            if (ja < na) M[oa] = (uint8_t)(ca ? sa : 0);
+            if (jb < na) M[ob] = (uint8_t)(cb ? sb : 0);
+            if (ca) list[nb + p.popc64(ba & lt)] = (uint16_t)oa;  // in place: never passes the reads
+            if (cb) list[nb + p.popc64(ba) + p.popc64(bb & lt)] = (uint16_t)ob;
+            nb += p.popc64(ba) + p.popc64(bb);
+        }
+        return nb;
+#else
         // exact strength of every candidate (m > t <=> corner at t), corners kept in order; the
         // next batch's list entries are read one batch ahead (the in-place writes of a batch
         // land below its own start, never on entries not yet read)
@@ -419,6 +577,7 @@ __host__ __device__ int fast_cell_detect(Pol& p, int sh, const CellGeom& g, int 
             nb += p.popc64(m);
         }
         return nb;
+#endif
     };
     // nonmax at t for every corner of the list; the verdict is kept in bit 15 of the entry
     // (LDS offsets < 6400 use 13 bits) for the ordered write

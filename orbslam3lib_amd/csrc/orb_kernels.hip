@@ -703,7 +703,10 @@ hipError_t launch_pyr_tail(const BatchArgs& a, hipStream_t s) {
 // ComputeKeyPointsOctTree (ORBextractor_old.cc:807-871) with cv::FAST(cell, kps, th, true):
 // detection on [3,rows-3)x[3,cols-3) of the cell ROI, 3x3 nonmax inside the cell only, iniTh
 // then minTh if the cell yields nothing, keys emitted in row-major order.
-constexpr int kFastThreads = 128;  // one workgroup (2 waves) per cell
+constexpr int kFastThreads = FAST_THREADS;  // one workgroup per cell
+#ifndef FAST_FIXED_POLICY
+#define FAST_FIXED_POLICY 1  // compile-time workgroup size in the cell code (0: blockDim, A/B only)
+#endif
 
 template <int CP>
 __global__ __launch_bounds__(kFastThreads) void k_fast_cells(BatchArgs a, int cell0, uint32_t ncell_magic) {
@@ -748,7 +751,11 @@ __global__ __launch_bounds__(kFastThreads) void k_fast_cells(BatchArgs a, int ce
         const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(roi + off), 0, 0);
         return make_uint4(v[0], v[1], v[2], v[3]);
     };
+#if FAST_FIXED_POLICY
+    FixedDevPolicy<kFastThreads> p{{scratch}};
+#else
     DevPolicy p{scratch};
+#endif
     fast_cell_tables<CP>(g, sh, lut, emask);  // synced with the ROI staging (fast_cell_run)
     CellScratch cs{T, M, list, wcnt, lut, emask};
     const int n = fast_cell_run<CP>(p, src, G.pitch, sh, dword_ok, g, a.ini_th, a.min_th, cs, key_out, ld16);

@@ -336,6 +336,23 @@ __host__ __device__ inline orb_u16x2 pk_max3(orb_u16x2 a, orb_u16x2 b, orb_u16x2
 #endif
 }
 
+// max over the 16 9-arcs of the arc minimum, per u16 half.  The 16 arcs pair up: arcs [2j, 2j+8]
+// and [2j+1, 2j+9] share the 8 points [2j+1, 2j+8], so max(min(arc 2j), min(arc 2j+1)) =
+// min(a8[2j+1], max(x[2j], x[2j+9])), and a8[2j+1] = min(a4[j], a4[j+2]) with a4[j] = min over
+// [2j+1, 2j+4]: 8 + 8 two-input mins, 8 max + 8 min3 for the pairs, 4 max3/max over the pairs =
+// 36 packed ops (47 with two-input ops only, 79 for the 16 arcs taken one by one).
+__host__ __device__ inline orb_u16x2 fast_arc_maxmin(const orb_u16x2 x[16]) {
+    orb_u16x2 a2[8], a4[8], pr[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a2[j] = __builtin_elementwise_min(x[2 * j + 1], x[(2 * j + 2) & 15]);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a4[j] = __builtin_elementwise_min(a2[j], a2[(j + 1) & 7]);   // [2j+1, 2j+4]
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+        pr[j] = pk_min3(a4[j], a4[(j + 2) & 7], __builtin_elementwise_max(x[2 * j], x[(2 * j + 9) & 15]));
+    return __builtin_elementwise_max(pk_max3(pr[0], pr[1], pr[2]), pk_max3(pr[3], pr[4], pk_max3(pr[5], pr[6], pr[7])));
+}
+
 template <int STRIDE>
 __host__ __device__ inline int fast_strength_packed(const uint8_t* c) {
     const int v = c[0];
@@ -346,24 +363,36 @@ __host__ __device__ inline int fast_strength_packed(const uint8_t* c) {
         const uint32_t p = c[ring_dx(k) + ring_dy(k) * STRIDE];
         x[k] = __builtin_bit_cast(orb_u16x2, p * 65535u + cv);
     }
-    // The 16 arcs pair up: arcs [2j, 2j+8] and [2j+1, 2j+9] share the 8 points [2j+1, 2j+8],
-    // so max(min(arc 2j), min(arc 2j+1)) = min(a8[2j+1], max(x[2j], x[2j+9])), and
-    // a8[2j+1] = min(a4[j], a4[j+2]) with a4[j] = min over [2j+1, 2j+4]: 8 + 8 two-input mins,
-    // 8 max + 8 min3 for the pairs, 4 max3/max over the pairs = 36 packed ops (47 with
-    // two-input ops only, 79 for the 16 arcs taken one by one).
-    orb_u16x2 a2[8], a4[8], pr[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) a2[j] = __builtin_elementwise_min(x[2 * j + 1], x[(2 * j + 2) & 15]);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) a4[j] = __builtin_elementwise_min(a2[j], a2[(j + 1) & 7]);   // [2j+1, 2j+4]
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-        pr[j] = pk_min3(a4[j], a4[(j + 2) & 7], __builtin_elementwise_max(x[2 * j], x[(2 * j + 9) & 15]));
-    const orb_u16x2 best = __builtin_elementwise_max(pk_max3(pr[0], pr[1], pr[2]),
-                                                     pk_max3(pr[3], pr[4], pk_max3(pr[5], pr[6], pr[7])));
+    const orb_u16x2 best = fast_arc_maxmin(x);
     int s = (int)(best.x > best.y ? best.x : best.y) - kFastBias;
     s = s < 0 ? 0 : s;
     return s > 255 ? 255 : s;
+}
+
+// Two candidates in one packed evaluation, ONE polarity each (the side the pre-test passed): half
+// 0 for the pixel at ca, half 1 for cb, each half holding kFastBias + s (v - p) (s = +1 for a dark
+// candidate, -1 for a bright one) before fast_arc_maxmin.  Returns the side strengths (max over
+// arcs of the arc minimum of s (v - p); <= 0 when no arc is all on that side) in *sa / *sb.  A
+// candidate that passed only one side of the pre-test at t has strength <= t on the other side,
+// so "m > t" and m itself follow from its side alone.
+template <int STRIDE>
+__host__ __device__ inline void fast_strength_2x1(const uint8_t* ca, const uint8_t* cb, bool bright_a,
+                                                  bool bright_b, int* sa, int* sb) {
+    const int va = ca[0], vb = cb[0];
+    // x = S * P + C per half (mod 2^16): dark S = -1, C = bias + v; bright S = +1, C = bias - v
+    const orb_u16x2 S = {(unsigned short)(bright_a ? 1 : 0xFFFF), (unsigned short)(bright_b ? 1 : 0xFFFF)};
+    const orb_u16x2 C = {(unsigned short)(bright_a ? kFastBias - va : kFastBias + va),
+                         (unsigned short)(bright_b ? kFastBias - vb : kFastBias + vb)};
+    orb_u16x2 x[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const int o = ring_dx(k) + ring_dy(k) * STRIDE;
+        const orb_u16x2 P = {(unsigned short)ca[o], (unsigned short)cb[o]};
+        x[k] = S * P + C;
+    }
+    const orb_u16x2 best = fast_arc_maxmin(x);
+    *sa = (int)best.x - kFastBias;
+    *sb = (int)best.y - kFastBias;
 }
 
 __host__ __device__ inline int fast_strength(const uint8_t* c, int stride, int t_min) {

@@ -190,6 +190,20 @@ struct DevPolicy {
     }
 };
 
+// A DevPolicy whose workgroup size is a compile-time constant (k_fast_cells: FAST_THREADS), so the
+// per-wave loops of the policy-templated code have constant trip counts; a one-wave workgroup
+// orders its LDS accesses with a wave barrier instead of s_barrier.
+template <int NT>
+struct FixedDevPolicy : DevPolicy {
+    __device__ int nthreads() const { return NT; }
+    __device__ int nwaves() const { return NT / 64; }
+    __device__ int wave() const { return NT == 64 ? 0 : DevPolicy::wave(); }
+    __device__ void sync() {
+        if constexpr (NT == 64) wave_sync();
+        else __syncthreads();
+    }
+};
+
 // One wave on its own (64 lanes), e.g. one FAST cell per wave: "sync" is a wave-level memory
 // ordering point (LDS ops of one wave complete in order; the fences stop compiler reordering).
 struct WavePolicy {

@@ -4,6 +4,8 @@
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp ORBGPU_DIAGNOSTICS=1 ORBGPU_STREAMS=1
 K=${1:-k_fast_cells}
+# the first process on a fresh box runs slow (clocks, code-object load): one untimed warm-up run
+timeout -k 10 120 python3 tools/profile_batch.py > /dev/null 2>&1
 for lib in orbslam3lib_amd/liborbgpu.so orbslam3lib_amd/variants/*.so; do
   n=$(basename $lib .so)
   O=gpurun_out/variants/$n
