@@ -205,7 +205,11 @@ __host__ __device__ void fast_cell_stage(Pol& p, const uint8_t* src, long long p
 #pragma unroll
         for (int k = 0; k < kIt; ++k) {
             const int i = tid + k * NT, r = i / RQ, q = i % RQ;
+#if defined(__HIP_DEVICE_COMPILE__)  // rows < 2^8, pitch < 2^24: one full-rate 24-bit multiply
+            if (i < rows * RQ && q < nq) v[k] = ld16((int)__umul24((uint32_t)r, (uint32_t)pitch) + 16 * q);
+#else
             if (i < rows * RQ && q < nq) v[k] = ld16((long long)r * pitch + 16 * q);
+#endif
         }
 #pragma unroll
         for (int k = 0; k < kIt; ++k) {
@@ -282,9 +286,9 @@ __host__ __device__ int fast_cell_detect(Pol& p, int sh, const CellGeom& g, int 
     const float inv_ng = ng > 0 ? __builtin_amdgcn_rcpf((float)ng) : 0.f;
     auto pix_before = [&](int j) {  // detection pixels of the items before item j
         if (ng == 0) return 0;
-        const int r = (int)(((float)j + 0.5f) * inv_ng), q = j - r * ng;
+        const int r = (int)(((float)j + 0.5f) * inv_ng), q = j - __mul24(r, ng);
         const int c = 4 * (g0 + q) - xs;
-        return r * dc + (c < 0 ? 0 : (c > dc ? dc : c));
+        return __mul24(r, dc) + (c < 0 ? 0 : (c > dc ? dc : c));
     };
     const int i0 = pix_before(j0);
     (void)lane;
@@ -414,11 +418,11 @@ __host__ __device__ int fast_cell_detect(Pol& p, int sh, const CellGeom& g, int 
             if (ng > 0) {
                 const int i = j0 + lane;
                 const int r = (int)(((float)i + 0.5f) * inv_ng);  // exact: i < 69 * 19 + 64
-                q = i - r * ng;
-                dw = (r + 3) * RW + g0 + q;
+                q = i - __mul24(r, ng);                           // (24-bit products: full rate)
+                dw = __mul24(r + 3, RW) + g0 + q;
                 const int dr = (int)(((float)L + 0.5f) * inv_ng);
-                dq = L - dr * ng;
-                ddw = dr * RW + dq;
+                dq = L - __mul24(dr, ng);
+                ddw = __mul24(dr, RW) + dq;
             }
             for (int base = j0; base < j1; base += L) {
                 const int i = base + lane;

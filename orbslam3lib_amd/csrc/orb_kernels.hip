@@ -447,8 +447,12 @@ __device__ inline void br_tile(const BatchArgs& a, int l, bool resize, int img, 
     // thread -> (quad q, rows rr0, rr0 + step, ...): the quad's selectors and coefficients are
     // read once per tile, one division per tile instead of one per output quad
     if (nq <= 0) return;
-    const int step = max(256 / nq, 1);
-    const int q = (int)threadIdx.x % nq, rr0 = (int)threadIdx.x / nq;
+    // t / nq and 256 / nq by v_rcp_f32 (1 ulp): (t + 0.5) / nq for t <= 256, nq <= kBrMaxQuads
+    // lies >= 0.5 / nq from an integer, far beyond the error, so the floors are exact (a full
+    // integer division here cost ~20 VALU per thread and tile)
+    const float rnq = __builtin_amdgcn_rcpf((float)nq);
+    const int step = max((int)(256.5f * rnq), 1);
+    const int rr0 = (int)(((float)threadIdx.x + 0.5f) * rnq), q = (int)threadIdx.x - rr0 * nq;
     if (rr0 >= step) return;
     const int dx0 = 4 * (q0 + q);
     if (G.area2) {
@@ -747,8 +751,9 @@ __global__ __launch_bounds__(kFastThreads) void k_fast_cells(BatchArgs a, int ce
     const uint8_t* src = base + roi;
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
         (void*)base, (short)0, (int)min(G.img_stride, 0x7fffffffLL), 0x00020000);
+    const int roi32 = (int)roi;  // planes are < 2 GB (buffer offsets are 32-bit)
     auto ld16 = [&](long long off) {
-        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(roi + off), 0, 0);
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, roi32 + (int)off, 0, 0);
         return make_uint4(v[0], v[1], v[2], v[3]);
     };
 #if FAST_FIXED_POLICY
@@ -958,6 +963,10 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 // staged in LDS.  The kernel waits on dependent memory round trips per keypoint (key, moment
 // rows + patch); few vector-memory instructions and registers per lane keep many of them in
 // flight.
+#ifndef OD_CHUNKS
+#define OD_CHUNKS 1  // moments from coalesced 16-byte row chunks (0: a disc row per lane, round 4)
+#endif
+#if OD_CHUNKS
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k_orient_desc(
     BatchArgs a, uint32_t nblk_magic) {
     // per keypoint group: the blurred patch around the keypoint, staged with 16-byte loads
@@ -1141,6 +1150,163 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
         }
     }
 }
+#else
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k_orient_desc(
+    BatchArgs a, uint32_t nblk_magic) {
+    // per keypoint group: the blurred patch around the keypoint, staged with 16-byte loads
+    __shared__ __attribute__((aligned(16))) uint8_t patch[kOdKpBlock][kOdPatchRows * kOdPatchPitch];
+    const int wg = xcd_remap(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * gridDim.y);
+    // wg / gridDim.x by the host's magic multiplier; the block's level from a host record (no
+    // level search with dependent kernarg loads)
+    const int irel = gridDim.x == 1 ? wg : (int)__umulhi((uint32_t)wg, nblk_magic);
+    const int img = a.img0 + irel, bx = wg - irel * (int)gridDim.x;
+    const int l = a.rtab[a.od_tab_off + bx].x;
+    const LevelGeom G = a.lv[l];
+    const int sub = threadIdx.x % kOdLanes, grp = threadIdx.x / kOdLanes;
+    const int count = a.lvlcnt[img * kMaxLevels + l];
+    const long long kbase = (long long)img * a.lvlkp_img_stride + G.kp_off;
+    const uint8_t* lvl = a.lvl_base[l] + (long long)img * G.img_stride;
+    const uint8_t* blr = a.blur_base[l] + (long long)img * G.bimg_stride;
+    const bool raw_dw = ((G.pitch | G.img_stride) & 3) == 0;
+    // raw buffer over this image's blurred level (dword 3 = gfx9 raw-buffer format word)
+    const __amdgpu_buffer_rsrc_t brs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)blr, (short)0, G.bpitch * G.h, 0x00020000);
+    const int stride_k = G.od_blocks * kOdKpBlock;
+    // per disc row v = s - 15 (s = 0..31) and dword i of the 32-byte window u = -15..16, the byte
+    // weights restricted to |u| <= umax[|v|] (rows past v = 15 are empty): ones (sum of p) and
+    // u + 15 (sum of (u + 15) p), so each dword is one v_alignbyte and two v_dot4_u32_u8; and the
+    // test pairs (floats {x0, x1, y0, y1}: the x and y pairs are packed-f32 operands).  Both in
+    // LDS tables shared by the workgroup, index-major ([i][row], [b][sub]): the 32 lanes of a
+    // keypoint read 32 consecutive entries per instruction, conflict-free
+    __shared__ __attribute__((aligned(16))) uint2 s_w[8][32];  // {ones, u + 15} masked
+    __shared__ __attribute__((aligned(16))) uint4 s_pat[kOdPairs][kOdLanes];
+    {
+        const int ts = threadIdx.x / 8, ti = threadIdx.x % 8;
+        const int v = ts - 15;
+        const int d = v > 15 ? -1 : c_umax[v < 0 ? -v : v];
+        uint32_t m = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int u = 4 * ti + j - 15;
+            m |= ((u < 0 ? -u : u) <= d ? 0xFFu : 0u) << (8 * j);
+        }
+        s_w[ti][ts] = make_uint2(m & 0x01010101u, m & ((uint32_t)(4 * ti) * 0x01010101u + 0x03020100u));
+        const int8_t* pv = c_pattern.v + 4 * threadIdx.x;  // x0, y0, x1, y1 of pair threadIdx.x
+        s_pat[threadIdx.x % kOdPairs][threadIdx.x / kOdPairs] = make_uint4(__float_as_uint((float)pv[0]), __float_as_uint((float)pv[2]),
+                                        __float_as_uint((float)pv[1]), __float_as_uint((float)pv[3]));
+    }
+    __syncthreads();
+    const int v = sub - 15;
+    const int vrow = v > 15 ? 0 : v;
+    uint8_t* pt = patch[grp];
+    // uniform trip count per wave so the group shuffles see all lanes
+    const int wave_first = (bx - G.od_first) * kOdKpBlock + (threadIdx.x >> 6) * 2;
+    // each iteration's key is loaded one iteration ahead, so its round trip overlaps the
+    // previous keypoint's work
+    auto key_at = [&](int kb) {
+        const int kp = kb + (grp & 1);
+        return kp < count ? a.lvlkey[kbase + kp] : a.lvlkey[kbase + kb];
+    };
+    uint32_t key_next = wave_first < count ? key_at(wave_first) : 0u;
+    for (int kb = wave_first; kb < count; kb += stride_k) {
+        const int kp = kb + (grp & 1);
+        const bool valid = kp < count;
+        const uint32_t key = key_next;
+        if (kb + stride_k < count) key_next = key_at(kb + stride_k);
+        const int x = key_x(key) + kMinBorder, y = key_y(key) + kMinBorder;
+        const int x0 = x - 15;
+        const int xa = raw_dw ? (x0 & ~3) : x0;
+        const int shf = x0 - xa;
+        // the moment row (round trip 1) and the 37 x 37 blurred patch (rows y-18..y+18 from the
+        // dword at or below x-18, 16-byte buffer loads, out-of-range bytes read as 0 and never
+        // sampled) are both requested before either is used, so the two round trips overlap
+        uint32_t w[9];
+        {
+            const uint8_t* row = lvl + plane_off(y + vrow, G.pitch, 0) + xa;
+            if (raw_dw) {  // 2 x dwordx4 (+ 1 dword when the window starts past byte 1 of its
+                           // first dword: otherwise w[8] only meets the zero weight of u = 16)
+                const uint4 A = *reinterpret_cast<const uint4*>(row);
+                const uint4 B = *reinterpret_cast<const uint4*>(row + 16);
+                w[0] = A.x; w[1] = A.y; w[2] = A.z; w[3] = A.w;
+                w[4] = B.x; w[5] = B.y; w[6] = B.z; w[7] = B.w;
+                w[8] = shf > 1 ? *reinterpret_cast<const uint32_t*>(row + 32) : 0u;
+            } else {
+#pragma unroll
+                for (int i = 0; i < 9; ++i) {
+                    const uint8_t* q = row + 4 * i;
+                    w[i] = (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16) | ((uint32_t)q[3] << 24);
+                }
+            }
+        }
+        const int xb = (x - kOdPatchR) & ~3;
+        const int pofs = (y - kOdPatchR) * G.bpitch + xb;
+        uint4 pv[kOdPatchIt];
+#pragma unroll
+        for (int it = 0; it < kOdPatchIt; ++it) {
+            const int c = sub + it * kOdLanes;
+            const int r = c / 3, part = c - 3 * r;
+            if (c < kOdPatchChunks) {
+                const auto q = __builtin_amdgcn_raw_buffer_load_b128(brs, pofs + r * G.bpitch + 16 * part, 0, 0);
+                pv[it] = make_uint4(q[0], q[1], q[2], q[3]);
+            }
+        }
+        // IC_Angle (:78-105): s = sum of p, t = sum of (u + 15) p over the row's disc span
+        uint32_t s = 0, t = 0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const uint2 wt = s_w[i][sub];
+            const uint32_t b = __builtin_amdgcn_alignbyte(w[i + 1], w[i], shf);
+            s = __builtin_amdgcn_udot4(b, wt.x, s, false);
+            t = __builtin_amdgcn_udot4(b, wt.y, t, false);
+        }
+        // sums over the keypoint's lanes (DPP, no LDS round trip but the last step)
+        const int m10 = od_sum((int)t - 15 * (int)s), m01 = od_sum(vrow * (int)s);
+        const float angle = fast_atan2_deg((float)m01, (float)m10);
+        // computeOrbDescriptor (:108-148): lane `sub` makes bits [8 sub, 8 sub + 8)
+        const float factorPI = (float)(3.14159265358979323846 / 180.0);
+        float sn, ca;  // std::sin(float) / std::cos(float) (:114-115): libm sinf / cosf
+        libm_sincosf(angle * factorPI, &sn, &ca);
+        // the patch to LDS: every sample is then an LDS byte read (4 vector-memory instructions
+        // per lane instead of one scattered byte load per sample)
+#pragma unroll
+        for (int it = 0; it < kOdPatchIt; ++it) {
+            const int c = sub + it * kOdLanes;
+            const int r = c / 3, part = c - 3 * r;
+            if (c < kOdPatchChunks) *reinterpret_cast<uint4*>(pt + r * kOdPatchPitch + 16 * part) = pv[it];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the group's own lanes read it
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const int pc = kOdPatchR * kOdPatchPitch + (x - xb);  // patch offset of the keypoint
+        // both samples of a test pair as packed f32 (each element an IEEE single operation, no
+        // contraction): row = x*b + y*a, col = x*a - y*b as the reference's float expressions
+        // (:116-121), then cvRound by adding 1.5 * 2^23 (round to nearest even, |value| < 19),
+        // whose low 24 bits are 2^22 + the rounded value: the LDS offset is one v_mad_u32_u24 of
+        // the two bit patterns and a per-keypoint constant (no v_rndne / v_cvt per sample)
+        const float magic = 12582912.0f;
+        const uint32_t kofs = (uint32_t)pc - 0x4B400000u - 0x400000u * (uint32_t)kOdPatchPitch;
+        const f32x2 snv = {sn, sn}, cav = {ca, ca}, mg = {magic, magic};
+        uint32_t bits = 0;
+#pragma unroll
+        for (int b = kOdPairs - 1; b >= 0; --b) {  // bits = 2 bits + test, last pair first
+            uint4 pw = s_pat[b][sub];  // float bit patterns {x0, x1, y0, y1}
+            asm volatile("" : "+v"(pw.x), "+v"(pw.y), "+v"(pw.z), "+v"(pw.w));  // not hoisted
+            const f32x2 X = {__uint_as_float(pw.x), __uint_as_float(pw.y)};
+            const f32x2 Y = {__uint_as_float(pw.z), __uint_as_float(pw.w)};
+            const f32x2 R = (X * snv + Y * cav) + mg;
+            const f32x2 C = (X * cav - Y * snv) + mg;
+            // the unsigned sums wrap to the small patch offsets; index with them as int
+            const int o0 = (int)(__umul24(__float_as_uint(R.x), (uint32_t)kOdPatchPitch) + __float_as_uint(C.x) + kofs);
+            const int o1 = (int)(__umul24(__float_as_uint(R.y), (uint32_t)kOdPatchPitch) + __float_as_uint(C.y) + kofs);
+            bits = bits + bits + (pt[o0] < pt[o1] ? 1u : 0u);
+        }
+        if (valid) {
+            if (sub == 0) a.lvlangle[kbase + kp] = angle;
+            a.lvldesc[(kbase + kp) * 32 + sub] = (uint8_t)bits;
+        }
+    }
+}
+#endif
 
 // ---------------------------------------------------------------------------------------------
 // k_finalize: ORBextractor::operator() assembly (ORBextractor_old.cc:1130-1190): levels in

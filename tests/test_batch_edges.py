@@ -467,3 +467,36 @@ def test_two_contexts_do_not_wait_for_each_other():
     t_a = time.perf_counter() - t0
     np.testing.assert_array_equal(dl, d0)
     assert t_b < 0.3 * t_a, (t_b, t_a, nb, t_one)
+
+
+def test_two_threads_two_contexts_concurrently(oracle):
+    """One context per eye, driven from two threads at the same time (the headset's per-eye
+    threads, Frame.cc:142-145): every call enters the library's per-call runtime check and the
+    launch sequence concurrently (ctypes releases the GIL), and each thread's results stay equal
+    to the oracle on its own frames."""
+    import threading
+
+    import orbslam3lib_amd as og
+    W, H = 640, 480
+    frames = [synth.frame(H, W, 900 + k) for k in range(2)]
+    refs = [oracle.extract(f, nfeatures=2000) for f in frames]
+    errors = []
+
+    def worker(k):
+        try:
+            ex = og.ORBextractor(2000, 1.2, 8, 20, 7, max_width=W, max_height=H, max_images=2)
+            for _ in range(12):
+                kp, d, m = ex(frames[k])
+                rk, rd, rm = refs[k]
+                assert m == rm and len(kp) == len(rk)
+                np.testing.assert_array_equal(d, rd.reshape(-1, 32))
+        except Exception as e:  # noqa: BLE001 -- reported by the main thread
+            errors.append((k, repr(e)))
+
+    ts = [threading.Thread(target=worker, args=(k,)) for k in range(2)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=120)
+    assert not any(t.is_alive() for t in ts)
+    assert not errors, errors
