@@ -826,6 +826,48 @@ def main():
         except Exception as e:  # reported, never fatal to the headline line
             cross = {"error": repr(e)[:200]}
 
+    # The C4 ingest-rank path (BASELINE configs[3]) when several GPUs run: rank 0 holds
+    # one 640x480 stereo pair per rank, one scatter hands each rank its pair, each rank extracts
+    # and matches it on its GPU, one gather brings every rank's results (counts, keypoints,
+    # descriptors, kNN2; orbgpu_export_batch) back to rank 0.  Reported beside the headline,
+    # never part of it.
+    ingest = None
+    if world > 1:
+        try:
+            from orbslam3lib_amd.dist import ingest_scatter_gather
+            ib = og.BatchExtractor(args.nfeatures, 1.2, args.nlevels, 20, 7, device=local, width=W, height=H,
+                                   max_images=2)
+            frames = (np.stack([x for r_ in range(world) for x in synth.stereo_pair(H, W, 700 + r_)])
+                      if rank == 0 else None)
+            got = None
+            for _ in range(4):  # the first exchanges set up the communicators and buffers
+                barrier(dist)
+                i0 = time.perf_counter()
+                got = ingest_scatter_gather(dist, ib, frames, pairs_per_rank=1, src=0)
+                if has_cuda:
+                    torch.cuda.synchronize()
+                i1 = time.perf_counter()
+            iel = max_over_ranks(dist, i1 - i0)
+            ok = 1.0
+            nfe = 0.0
+            if rank == 0:
+                for r_images, _ in got:
+                    nfe += sum(len(k) for k, _, _ in r_images)
+                for i, (k, d, m) in enumerate(got[0][0]):  # rank 0's own pair: equal to its local results
+                    lk, ld, lm = ib.result(i)
+                    ok = min(ok, float(m == lm and np.array_equal(d, ld)))
+            ingest = {"workload": "C4: one 640x480 stereo pair per rank per step, frames on rank 0 "
+                                  "(BASELINE configs[3]); extraction + kNN2 on every rank's GPU",
+                      "ranks": world, "ms_per_step": round(iel * 1e3, 3),
+                      "mfeatures_s": round(nfe / iel / 1e6, 3) if rank == 0 else None,
+                      "exchange": "scatter of frames + gather of results (%s%s)"
+                                  % (dist.get_backend(), ", device-resident" if has_cuda else ", host"),
+                      "rank0_results_equal_local": bool(ok == 1.0) if rank == 0 else None}
+            ib.close()
+            del ib
+        except Exception as e:  # reported, never fatal to the headline line
+            ingest = {"error": repr(e)[:200]}
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cb = cpu_baseline(W, H, args.nfeatures, args.cpu_seconds, args.map_points)
@@ -900,6 +942,7 @@ def main():
             "other_configs": configs,
             "wire": wire,
             "cross_camera": cross,
+            "ingest_c4": ingest,
         }
         print(json.dumps(out))
     if dist is not None:

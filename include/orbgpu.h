@@ -148,6 +148,24 @@ int orbgpu_match_knn2(orbgpu_ctx* ctx, const uint8_t* query, int nq, const uint8
  *     ordered after the batch that produced them;
  *   orbgpu_match_knn2_device: orbgpu_match_knn2 with query / train / outputs in device memory
  *     (idx1, dist1, idx2, dist2: int32 [nq] each), on `stream`. */
+/* The C4 ingest-rank path (frames ingested on one GPU, every result handed back to
+ * one caller, as LynxHardwareAccelerator.cpp:146-204 returns each frame's keypoints, descriptors
+ * and matches to its caller), device memory throughout so a collective can move both ends:
+ *   orbgpu_ingest_images: n images already in device memory (e.g. a scatter's receive buffer;
+ *     rows of `stride` bytes) -> the context's input buffer, device to device on `stream`; the
+ *     next orbgpu_run_batch / run_batch_match reads them;
+ *   orbgpu_export_batch: the last batch's results of images [0, n_images) and stereo pairs
+ *     [0, n_pairs) -> one device buffer (e.g. a gather's send buffer), device to device on
+ *     `stream`, ordered after the batch.  Layout (out_cap = *out_cap rows per image / pair):
+ *       int32 count[n_images], int32 mono[n_images], int32 n_queries[n_pairs],
+ *       orbgpu_keypoint kps[n_images][out_cap], uint8 desc[n_images][out_cap][32],
+ *       int32 idx1[n_pairs][out_cap], dist1[..], idx2[..], dist2[..]  (the last match call's);
+ *     orbgpu_export_batch_bytes gives its size. */
+int orbgpu_ingest_images(orbgpu_ctx* ctx, const uint8_t* device_images, int n_images, int width,
+                         int height, int stride, void* stream);
+size_t orbgpu_export_batch_bytes(const orbgpu_ctx* ctx, int n_images, int n_pairs);
+int orbgpu_export_batch(orbgpu_ctx* ctx, int n_images, int n_pairs, void* device_dst, size_t dst_bytes,
+                        int* out_cap, void* stream);
 int orbgpu_export_descriptors(orbgpu_ctx* ctx, int image, int row0, uint8_t* device_dst, int cap_rows,
                               int* n_rows, void* stream);
 int orbgpu_match_knn2_device(orbgpu_ctx* ctx, const uint8_t* d_query, int nq, const uint8_t* d_train, int nt,

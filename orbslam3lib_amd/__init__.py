@@ -51,7 +51,7 @@ EXPORTED = [
     "orbgpu_set_profiling", "orbgpu_num_stages", "orbgpu_stage_name", "orbgpu_stage_times",
     "orbgpu_reset_stage_times", "orbgpu_last_error", "orbgpu_abi_version",
     "orbgpu_fisheye_stereo_batch", "orbgpu_download_fisheye", "orbgpu_run_batch_match",
-    "orbgpu_diagnostic_knobs",
+    "orbgpu_diagnostic_knobs", "orbgpu_ingest_images", "orbgpu_export_batch_bytes", "orbgpu_export_batch",
 ]
 
 
@@ -113,6 +113,11 @@ def load_library(path: str = LIB_PATH):
                                               C.POINTER(C.c_int), C.c_void_p]
     lib.orbgpu_match_knn2_device.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int] + \
         [C.c_void_p] * 5
+    lib.orbgpu_ingest_images.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p]
+    lib.orbgpu_export_batch_bytes.restype = C.c_size_t
+    lib.orbgpu_export_batch_bytes.argtypes = [C.c_void_p, C.c_int, C.c_int]
+    lib.orbgpu_export_batch.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_size_t,
+                                        C.POINTER(C.c_int), C.c_void_p]
     for name in ("orbgpu_destroy", "orbgpu_synchronize", "orbgpu_set_profiling",
                  "orbgpu_reset_stage_times"):
         getattr(lib, name).argtypes = [C.c_void_p] + ([C.c_int] if name == "orbgpu_set_profiling" else [])
@@ -372,6 +377,44 @@ class BatchExtractor:
                                              int(nt), C.c_void_p(d_out), C.c_void_p(d_out + 4 * nq),
                                              C.c_void_p(d_out + 8 * nq), C.c_void_p(d_out + 12 * nq),
                                              C.c_void_p(stream) if stream else None))
+
+    def ingest_images(self, device_ptr, n, stride=None, stream=None):
+        """n images of this context's size already in device memory (rows of `stride` bytes,
+        e.g. a collective's receive buffer) -> the input buffer, device to device
+        (orbgpu_ingest_images); the next run() / run_match() reads them."""
+        _check(_lib.orbgpu_ingest_images(self.ctx.handle, C.c_void_p(device_ptr), int(n), self.width, self.height,
+                                         int(stride or self.width), C.c_void_p(stream) if stream else None))
+        self.n = int(n)
+        self._staged = None
+
+    def export_batch_bytes(self, n_images, n_pairs):
+        return int(_lib.orbgpu_export_batch_bytes(self.ctx.handle, int(n_images), int(n_pairs)))
+
+    def export_batch(self, device_ptr, n_images, n_pairs, nbytes, stream=None):
+        """The last batch's results of images [0, n_images) and pairs [0, n_pairs) into one device
+        buffer (orbgpu_export_batch, device to device); returns out_cap for decode_export."""
+        cap = C.c_int(0)
+        _check(_lib.orbgpu_export_batch(self.ctx.handle, int(n_images), int(n_pairs), C.c_void_p(device_ptr),
+                                        int(nbytes), C.byref(cap), C.c_void_p(stream) if stream else None))
+        return cap.value
+
+    @staticmethod
+    def decode_export(buf, n_images, n_pairs, out_cap):
+        """Host view of an orbgpu_export_batch buffer (uint8 array): per image (keypoints in the
+        cv::KeyPoint layout, descriptors [n, 32], mono index) and per pair (idx1, dist1, idx2,
+        dist2) over the pair's query rows -- what result() / matches() return."""
+        b = np.ascontiguousarray(buf, dtype=np.uint8).reshape(-1)
+        o = 0
+        counts = b[o:o + 4 * n_images].view(np.int32); o += 4 * n_images
+        mono = b[o:o + 4 * n_images].view(np.int32); o += 4 * n_images
+        nq = b[o:o + 4 * n_pairs].view(np.int32); o += 4 * n_pairs
+        kps = b[o:o + 28 * out_cap * n_images].view(KEYPOINT_DTYPE).reshape(n_images, out_cap)
+        o += 28 * out_cap * n_images
+        desc = b[o:o + 32 * out_cap * n_images].reshape(n_images, out_cap, 32); o += 32 * out_cap * n_images
+        m = b[o:o + 16 * out_cap * n_pairs].view(np.int32).reshape(4, n_pairs, out_cap) if n_pairs else None
+        images = [(kps[i, :counts[i]].copy(), desc[i, :counts[i]].copy(), int(mono[i])) for i in range(n_images)]
+        pairs = [tuple(m[k, p, :nq[p]].copy() for k in range(4)) for p in range(n_pairs)]
+        return images, pairs
 
     def upload_async(self, images):
         """Stage the NEXT batch (orbgpu_upload_images_async): the copy runs beside the current

@@ -1473,6 +1473,62 @@ int orbgpu_export_descriptors(orbgpu_ctx* c, int img, int row0, uint8_t* dst, in
     return rejoin(c, s);
 }
 
+int orbgpu_ingest_images(orbgpu_ctx* c, const uint8_t* device_images, int n, int w, int h, int stride,
+                         void* stream) {
+    if (!c || !device_images) return fail(ORBGPU_ERR_INVALID, "null argument");
+    if (w <= 0 || h <= 0) return fail(ORBGPU_ERR_EMPTY_IMAGE, "empty image");
+    if (stride < w) return fail(ORBGPU_ERR_INVALID, "stride < width");
+    int r = ensure_input(c, n, w, h);
+    if (r) return r;
+    HIP_TRY(hipSetDevice(c->device));
+    if (!device_ptr(device_images)) return fail(ORBGPU_ERR_INVALID, "device_images is not device memory");
+    if ((r = drop_pending_upload(c))) return r;
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    if ((r = join_all(c, s))) return r;  // the chunk streams may still read the previous images
+    HIP_TRY(hipMemcpy2DAsync(cur_input(c), w, device_images, stride, w, (size_t)h * n, hipMemcpyDeviceToDevice, s));
+    c->need_fork = true;
+    return rejoin(c, s);
+}
+
+size_t orbgpu_export_batch_bytes(const orbgpu_ctx* c, int n_images, int n_pairs) {
+    if (!c || n_images < 0 || n_pairs < 0) return 0;
+    const size_t cap = (size_t)c->out_cap;
+    return 8 * (size_t)n_images + 4 * (size_t)n_pairs + cap * (sizeof(orbgpu_keypoint) + 32) * (size_t)n_images +
+           16 * cap * (size_t)n_pairs;
+}
+
+int orbgpu_export_batch(orbgpu_ctx* c, int n_images, int n_pairs, void* device_dst, size_t dst_bytes,
+                        int* out_cap, void* stream) {
+    if (!c || n_images < 0 || n_images > c->last_images || n_pairs < 0 || n_pairs > c->last_pairs ||
+        2 * n_pairs > n_images)
+        return fail(ORBGPU_ERR_INVALID, "bad image / pair count");
+    if (out_cap) *out_cap = c->out_cap;
+    const size_t need = orbgpu_export_batch_bytes(c, n_images, n_pairs);
+    if (need == 0) return ORBGPU_OK;
+    if (!device_dst) return fail(ORBGPU_ERR_INVALID, "null argument");
+    if (dst_bytes < need) return fail(ORBGPU_ERR_CAPACITY, "export buffer too small");
+    HIP_TRY(hipSetDevice(c->device));
+    if (!device_ptr(device_dst)) return fail(ORBGPU_ERR_INVALID, "device_dst is not device memory");
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    int r = join_all(c, s);  // the outputs come from the chunk streams
+    if (r) return r;
+    const size_t cap = (size_t)c->out_cap;
+    uint8_t* d = static_cast<uint8_t*>(device_dst);
+    auto put = [&](const void* src, size_t bytes) -> int {
+        if (bytes) HIP_TRY(hipMemcpyAsync(d, src, bytes, hipMemcpyDeviceToDevice, s));
+        d += bytes;
+        return 0;
+    };
+    if ((r = put(c->outn.p, 4 * (size_t)n_images)) || (r = put(c->outmono.p, 4 * (size_t)n_images)) ||
+        (r = put(c->mnq.p, 4 * (size_t)n_pairs)) ||
+        (r = put(c->outkps.p, sizeof(orbgpu_keypoint) * cap * n_images)) ||
+        (r = put(c->outdesc.p, 32 * cap * n_images)))
+        return r;
+    for (DevBuf* b : {&c->midx1, &c->mdist1, &c->midx2, &c->mdist2})
+        if ((r = put(b->p, 4 * cap * n_pairs))) return r;
+    return rejoin(c, s);
+}
+
 int orbgpu_match_knn2_device(orbgpu_ctx* c, const uint8_t* q, int nq, const uint8_t* t, int nt, int32_t* i1,
                              int32_t* d1, int32_t* i2, int32_t* d2, void* stream) {
     if (!c || nq < 0 || nt < 0 || (nq && (!q || !i1 || !d1 || !i2 || !d2)) || (nt && !t))

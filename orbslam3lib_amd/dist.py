@@ -1,8 +1,9 @@
 """Multi-GPU plumbing for the batch path: one process per GPU (torch.distributed, RCCL on the
 GPU box, gloo on CPU).  Stereo pairs are independent, so the hot path shards them with no
 data-path collective; only the timing barrier and the max/sum reductions of bench.py cross
-ranks ("replicas only").  The one real exchange step of §8e, the cross-camera
-BFMatch of C5 (one camera per GPU), is cross_camera_match."""
+ranks ("replicas only").  The exchange steps of §8e: the cross-camera BFMatch of C5
+(one camera per GPU, cross_camera_match / cross_camera_match_device) and, for frames ingested
+on one GPU, the C4 scatter of frames and gather of results (ingest_scatter_gather)."""
 from __future__ import annotations
 
 
@@ -90,6 +91,49 @@ def cross_camera_match_device(dist, be, image=0, row0=0):
         be.match_knn2_device(buf.data_ptr(), n_local, rows[r].data_ptr(), counts[r], res.data_ptr(), stream)
         out[r] = res[:, :n_local]
     return out
+
+
+def ingest_scatter_gather(dist, be, frames=None, pairs_per_rank=1, src=0, stereo_rows_only=False):
+    """The C4 ingest-rank path ("if frames are ingested on one GPU"): rank `src` holds
+    the frames of every rank's stereo pairs, uint8 [world * 2P, H, W] (pair p = images 2p, 2p + 1;
+    rank r owns pairs [rP, (r + 1)P)).  One scatter hands each rank its 2P images, each rank runs
+    extraction + stereo kNN2 on its own GPU (BatchExtractor `be`: ingest_images -> run_match), and
+    one gather brings every rank's export_batch buffer back to `src` -- the reference hands each
+    frame's keypoints, descriptors and matches back to its one caller
+    (cpp/src/LynxHardwareAcceleration/LynxHardwareAccelerator.cpp:146-204).  Under RCCL the
+    frames and results move device to device over xGMI; under gloo the collectives are staged
+    through host tensors (the extractor still ingests from / exports to device memory when it is
+    device-resident).  Returns, on `src`, one (images, pairs) per rank as
+    BatchExtractor.decode_export gives them; None on the other ranks."""
+    import torch
+    world, rank = dist.get_world_size(), dist.get_rank()
+    nccl = dist.get_backend() == "nccl"
+    on_device = nccl or (bool(getattr(be, "device_resident", False)) and torch.cuda.is_available())
+    dev = torch.device("cuda", torch.cuda.current_device()) if on_device else torch.device("cpu")
+    comm = dev if nccl else torch.device("cpu")
+    stream = torch.cuda.current_stream().cuda_stream if on_device else None
+    n_img, h, w = 2 * pairs_per_rank, be.height, be.width
+    recv = torch.empty((n_img, h, w), dtype=torch.uint8, device=comm)
+    parts = None
+    if rank == src:
+        ft = torch.as_tensor(frames).reshape(world * n_img, h, w).to(comm)
+        parts = list(ft.chunk(world))
+    dist.scatter(recv, parts, src=src)
+    img = recv if recv.device == dev else recv.to(dev)
+    be.ingest_images(img.data_ptr(), n_img, w, stream)
+    be.run_match(stereo_rows_only=stereo_rows_only)
+    nbytes = be.export_batch_bytes(n_img, pairs_per_rank)
+    out = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    cap = be.export_batch(out.data_ptr(), n_img, pairs_per_rank, nbytes, stream)
+    if out.device != comm:
+        if out.device.type == "cuda":
+            torch.cuda.current_stream().synchronize()
+        out = out.to(comm)
+    bufs = [torch.empty_like(out) for _ in range(world)] if rank == src else None
+    dist.gather(out, bufs, dst=src)
+    if rank != src:
+        return None
+    return [be.decode_export(b.cpu().numpy(), n_img, pairs_per_rank, cap) for b in bufs]
 
 
 def reduce_scalar(dist, x: float, op: str = "max") -> float:

@@ -78,6 +78,42 @@ class BatchExtractor:
         d2 = d[r, i2] if t.shape[0] > 1 else np.full(len(q), 0x7FFFFFFF)
         return (i1.astype(np.int32), d1.astype(np.int32), np.asarray(i2, np.int32), np.asarray(d2, np.int32))
 
+    def ingest_images(self, ptr, n, stride=None, stream=None):
+        import ctypes
+        stride = stride or self.width
+        a = np.ctypeslib.as_array((ctypes.c_uint8 * (n * self.height * stride)).from_address(ptr))
+        self.upload(a.reshape(n, self.height, stride)[:, :, :self.width].copy())
+
+    _CAP = 64
+
+    def export_batch_bytes(self, n_img, n_pairs):
+        return 8 * n_img + 4 * n_pairs + self._CAP * 60 * n_img + 16 * self._CAP * n_pairs
+
+    def export_batch(self, ptr, n_img, n_pairs, nbytes, stream=None):
+        """The orbgpu_export_batch layout over the stub's results (zero keypoints)."""
+        import ctypes
+        cap = self._CAP
+        counts = np.array([self._count(i) for i in range(n_img)], np.int32)
+        parts = [counts, counts.copy(), counts[0::2][:n_pairs].copy(),  # mono = n, as result()
+                 np.zeros(28 * cap * n_img, np.uint8)]
+        desc = np.zeros((n_img, cap, 32), np.uint8)
+        for i in range(n_img):
+            desc[i, :counts[i]] = self.result(i)[1]
+        mm = np.zeros((4, n_pairs, cap), np.int32)
+        for p in range(n_pairs):
+            res = self.knn_match(self.result(2 * p)[1], self.result(2 * p + 1)[1])
+            for k in range(4):
+                mm[k, p, :len(res[k])] = res[k]
+        buf = np.concatenate([x.view(np.uint8).reshape(-1) for x in parts + [desc, mm]])
+        assert buf.nbytes == nbytes
+        ctypes.memmove(ptr, buf.ctypes.data, nbytes)
+        return cap
+
+    @staticmethod
+    def decode_export(buf, n_images, n_pairs, out_cap):
+        from orbslam3lib_amd import BatchExtractor as _B
+        return _B.decode_export(buf, n_images, n_pairs, out_cap)
+
     def set_profiling(self, on=True, stages=None, serialize=False):
         self._prof, self._serial = bool(on), bool(serialize)
 

@@ -500,3 +500,61 @@ def test_two_threads_two_contexts_concurrently(oracle):
         t.join(timeout=120)
     assert not any(t.is_alive() for t in ts)
     assert not errors, errors
+
+
+@pytest.mark.parametrize("stereo_rows_only", [False, True])
+def test_device_ingest_and_batch_export(oracle, stereo_rows_only):
+    """The C4 ingest-rank path's two entry points (dist.ingest_scatter_gather): frames already
+    in device memory (a padded stride, as a collective's receive buffer may have) go in through
+    orbgpu_ingest_images, and orbgpu_export_batch writes the batch's counts, keypoints,
+    descriptors and kNN2 results into one device buffer; decoded, it equals result() /
+    matches() and the oracle, bit for bit."""
+    import orbslam3lib_amd as og
+    hip = _hip()
+    hip.hipMalloc.argtypes = [C.POINTER(C.c_void_p), C.c_size_t]
+    hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+    hip.hipFree.argtypes = [C.c_void_p]
+    hip.hipDeviceSynchronize.argtypes = []
+    P, W, H, S = 2, 640, 480, 704
+    imgs = np.stack([x for i in range(P) for x in synth.stereo_pair(H, W, 140 + i)])
+    padded = np.zeros((2 * P, H, S), np.uint8)
+    padded[:, :, :W] = imgs
+    padded[:, :, W:] = 255  # bytes past the width must not leak into the images
+    laps = np.array([[0, 0], [60, 590]] * P, np.int32)
+    be = og.BatchExtractor(2000, 1.2, 8, 20, 7, width=W, height=H, max_images=2 * P)
+    bufs = []
+    try:
+        src, dst = C.c_void_p(), C.c_void_p()
+        assert hip.hipMalloc(C.byref(src), padded.nbytes) == 0
+        bufs.append(src)
+        assert hip.hipMemcpy(src.value, padded.ctypes.data, padded.nbytes, 1) == 0
+        be.ingest_images(src.value, 2 * P, stride=S)
+        be.run_match(laps=laps, stereo_rows_only=stereo_rows_only)
+        nbytes = be.export_batch_bytes(2 * P, P)
+        assert hip.hipMalloc(C.byref(dst), nbytes) == 0
+        bufs.append(dst)
+        cap = be.export_batch(dst.value, 2 * P, P, nbytes)
+        be.synchronize()
+        host = np.zeros(nbytes, np.uint8)
+        assert hip.hipMemcpy(host.ctypes.data, dst.value, nbytes, 2) == 0
+        images, pairs = og.BatchExtractor.decode_export(host, 2 * P, P, cap)
+        for i in range(2 * P):
+            k, d, m = be.result(i)
+            ek, ed, em = images[i]
+            assert em == m
+            np.testing.assert_array_equal(ek.view(np.uint8), k.view(np.uint8))
+            np.testing.assert_array_equal(ed, d)
+            rk, rd, rm = oracle.extract(imgs[i], nfeatures=2000, lap=tuple(laps[i]))
+            assert rm == m
+            np.testing.assert_array_equal(ed, rd.reshape(-1, 32))
+        for p in range(P):
+            for a, b in zip(pairs[p], be.matches(p)):
+                np.testing.assert_array_equal(a, b)
+        with pytest.raises(og.OrbGpuError):
+            be.export_batch(dst.value, 2 * P, P, nbytes - 1)  # buffer too small
+        with pytest.raises(og.OrbGpuError):
+            be.ingest_images(padded.ctypes.data, 2 * P, stride=S)  # host pointer refused
+    finally:
+        be.synchronize()
+        for p in bufs:
+            hip.hipFree(p)

@@ -43,6 +43,10 @@ def test_bench_gpus_n_spawns_ranks(n):
     assert cross and "error" not in cross, cross
     assert cross["cameras"] == n and cross["exchange"].startswith("all_gather (gloo")
     assert "1920x1080, 12 levels, 5000" in cross["workload"]  # the C5 camera, not a C2 eye
+    ing = line["ingest_c4"]
+    assert ing and "error" not in ing, ing
+    assert ing["ranks"] == n and ing["exchange"].startswith("scatter of frames + gather of results (gloo")
+    assert ing["rank0_results_equal_local"] is True and ing["mfeatures_s"] > 0
     assert line["data"].startswith("stub")
 
 

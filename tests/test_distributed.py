@@ -163,3 +163,117 @@ def test_gloo_cross_camera_match_device_path_world2():
         p.join(timeout=60)
         assert p.exitcode == 0
     assert all(ok for _, ok in res)
+
+
+class _HostBatch:
+    """Stands in for BatchExtractor on the CPU for ingest_scatter_gather: ingest_images /
+    run_match / export_batch over host addresses (the oracle as the extractor and matcher),
+    writing the orbgpu_export_batch layout that BatchExtractor.decode_export reads."""
+
+    device_resident = False
+
+    def __init__(self, h, w, nfeatures=300, nlevels=4):
+        self.height, self.width, self.nf, self.nl = h, w, nfeatures, nlevels
+        self.out_cap = 512
+
+    def ingest_images(self, ptr, n, stride=None, stream=None):
+        import ctypes
+
+        import numpy as np
+        stride = stride or self.width
+        a = np.ctypeslib.as_array((ctypes.c_uint8 * (n * self.height * stride)).from_address(ptr))
+        self.imgs = a.reshape(n, self.height, stride)[:, :, :self.width].copy()
+
+    def run_match(self, stereo_rows_only=False):
+        from oracle import oracle_py as O
+        self.res = [O.extract(im, nfeatures=self.nf, nlevels=self.nl) for im in self.imgs]
+        self.m = [O.knn2(self.res[2 * p][1], self.res[2 * p + 1][1]) for p in range(len(self.imgs) // 2)]
+
+    def export_batch_bytes(self, n_img, n_pairs):
+        return 8 * n_img + 4 * n_pairs + self.out_cap * 60 * n_img + 16 * self.out_cap * n_pairs
+
+    def export_batch(self, ptr, n_img, n_pairs, nbytes, stream=None):
+        import ctypes
+
+        import numpy as np
+
+        from orbslam3lib_amd import KEYPOINT_DTYPE
+        cap = self.out_cap
+        buf = np.zeros(nbytes, np.uint8)
+        o = 0
+        counts = np.array([len(r[0]) for r in self.res], np.int32)
+        buf[o:o + 4 * n_img] = counts.view(np.uint8); o += 4 * n_img
+        buf[o:o + 4 * n_img] = np.array([r[2] for r in self.res], np.int32).view(np.uint8); o += 4 * n_img
+        buf[o:o + 4 * n_pairs] = counts[0::2].view(np.uint8); o += 4 * n_pairs
+        kp = np.zeros((n_img, cap), KEYPOINT_DTYPE)
+        desc = np.zeros((n_img, cap, 32), np.uint8)
+        for i, (k, d, _) in enumerate(self.res):
+            kp[i, :len(k)] = k
+            desc[i, :len(k)] = d.reshape(-1, 32)
+        buf[o:o + kp.nbytes] = kp.view(np.uint8).reshape(-1); o += kp.nbytes
+        buf[o:o + desc.nbytes] = desc.reshape(-1); o += desc.nbytes
+        mm = np.zeros((4, n_pairs, cap), np.int32)
+        for p, res in enumerate(self.m):
+            for k in range(4):
+                mm[k, p, :len(res[k])] = res[k]
+        buf[o:o + mm.nbytes] = mm.view(np.uint8).reshape(-1)
+        ctypes.memmove(ptr, buf.ctypes.data, nbytes)
+        return cap
+
+    @staticmethod
+    def decode_export(buf, n_images, n_pairs, out_cap):
+        from orbslam3lib_amd import BatchExtractor
+        return BatchExtractor.decode_export(buf, n_images, n_pairs, out_cap)
+
+
+def _frames_for(world, pairs, h, w):
+    from orbslam3lib_amd import synth
+    import numpy as np
+    return np.stack([synth.frame(h, w, 300 + i) for i in range(world * 2 * pairs)])
+
+
+def _ingest_worker(rank, world, port, q):
+    import numpy as np
+    import torch.distributed as dist
+
+    from oracle import oracle_py as O
+    from orbslam3lib_amd import dist as od
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    h, w, P = 120, 160, 1
+    frames = _frames_for(world, P, h, w) if rank == 0 else None
+    got = od.ingest_scatter_gather(dist, _HostBatch(h, w), frames, pairs_per_rank=P, src=0)
+    ok = True
+    if rank == 0:
+        ok = len(got) == world
+        for r, (images, pairs) in enumerate(got):
+            for i, (k, d, m) in enumerate(images):
+                rk, rd, rm = O.extract(frames[r * 2 * P + i], nfeatures=300, nlevels=4)
+                ok &= m == rm and np.array_equal(k, rk) and np.array_equal(d, rd.reshape(-1, 32))
+            for p, res in enumerate(pairs):
+                ref = O.knn2(images[2 * p][1], images[2 * p + 1][1])
+                ok &= all(np.array_equal(a, b) for a, b in zip(res, ref))
+    else:
+        ok = got is None
+    dist.barrier()
+    q.put((rank, bool(ok)))
+    dist.destroy_process_group()
+
+
+def test_gloo_ingest_scatter_gather_world2():
+    """The C4 ingest-rank path (dist.ingest_scatter_gather): rank 0's frames scattered one stereo
+    pair per rank, each rank's extraction + kNN2 results gathered back to rank 0 in the
+    orbgpu_export_batch layout, decoded and equal to the oracle on the frames that rank got."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ingest_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=180) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(ok for _, ok in res)
