@@ -148,6 +148,11 @@ int orbgpu_match_knn2(orbgpu_ctx* ctx, const uint8_t* query, int nq, const uint8
  *     ordered after the batch that produced them;
  *   orbgpu_match_knn2_device: orbgpu_match_knn2 with query / train / outputs in device memory
  *     (idx1, dist1, idx2, dist2: int32 [nq] each), on `stream`. */
+int orbgpu_export_descriptors(orbgpu_ctx* ctx, int image, int row0, uint8_t* device_dst, int cap_rows,
+                              int* n_rows, void* stream);
+int orbgpu_match_knn2_device(orbgpu_ctx* ctx, const uint8_t* d_query, int nq, const uint8_t* d_train, int nt,
+                             int32_t* d_idx1, int32_t* d_dist1, int32_t* d_idx2, int32_t* d_dist2, void* stream);
+
 /* The C4 ingest-rank path (frames ingested on one GPU, every result handed back to
  * one caller, as LynxHardwareAccelerator.cpp:146-204 returns each frame's keypoints, descriptors
  * and matches to its caller), device memory throughout so a collective can move both ends:
@@ -166,10 +171,6 @@ int orbgpu_ingest_images(orbgpu_ctx* ctx, const uint8_t* device_images, int n_im
 size_t orbgpu_export_batch_bytes(const orbgpu_ctx* ctx, int n_images, int n_pairs);
 int orbgpu_export_batch(orbgpu_ctx* ctx, int n_images, int n_pairs, void* device_dst, size_t dst_bytes,
                         int* out_cap, void* stream);
-int orbgpu_export_descriptors(orbgpu_ctx* ctx, int image, int row0, uint8_t* device_dst, int cap_rows,
-                              int* n_rows, void* stream);
-int orbgpu_match_knn2_device(orbgpu_ctx* ctx, const uint8_t* d_query, int nq, const uint8_t* d_train, int nt,
-                             int32_t* d_idx1, int32_t* d_dist1, int32_t* d_idx2, int32_t* d_dist2, void* stream);
 
 /* Batch stereo matching on device-resident results of the last orbgpu_run_batch: pair p
  * matches image 2p (query) against image 2p+1 (train), rows [mono..n) of each when
