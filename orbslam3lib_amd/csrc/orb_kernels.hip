@@ -1488,19 +1488,24 @@ static_assert(kKnnStage == 1 || kKnnStage == 2 || kKnnStage == 4, "stage size");
 constexpr int kKnnSeg = 4096;            // train rows per key segment
 static_assert(kKnnWaves == 4 || kKnnWaves == 8, "expansion roles");
 
-// 4 descriptor bits -> 4 int8 (+64 for a set bit, -64 otherwise), bit k -> byte k
-__device__ inline uint32_t knn_expand4(uint32_t n) {
-    uint32_t x;  // n * 0x204081 (n < 16) on the full-rate 24-bit multiplier
-    asm("v_mul_u32_u24 %0, 0x204081, %1" : "=v"(x) : "v"(n));
-    x &= 0x01010101u;
-    return (x << 7) ^ 0xC0C0C0C0u;
+// Descriptor dword w -> 32 int8 (-64 for a set bit, +64 otherwise; the sign is the same on both
+// operands, so the dot is still 4096 (256 - 2H)): K element 4 m + j of the dword's MFMA step is
+// bit m + 8 j, i.e. expanded dword m = ((w << (7 - m)) & 0x80808080) | 0x40404040 -- one shift and
+// one v_and_or_b32 per 4 bytes (round 4: bit k -> byte k through a 24-bit multiply, ~5 VALU).
+// Any bit -> K assignment is exact as long as queries and train rows share it.
+__device__ inline uint32_t knn_bytes_of(uint32_t ws) {
+    uint32_t r;  // one v_and_or_b32 (the compiler splits it into v_and + v_or)
+    asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(ws), "v"(0x80808080u), "v"(0x40404040u));
+    return r;
 }
-__device__ inline knn_v4i knn_expand16(uint32_t b) {  // 16 bits -> 16 int8
+// half hh (K elements 16 hh .. 16 hh + 15) of dword w: expanded dwords m = 4 hh .. 4 hh + 3
+__device__ inline knn_v4i knn_expand_half(uint32_t w, int hh) {
+    const uint32_t ws = w << (4 - 4 * hh);  // now every m of this half needs shift 3 - (m - 4 hh)
     knn_v4i v;
-    v[0] = (int)knn_expand4(b & 15u);
-    v[1] = (int)knn_expand4((b >> 4) & 15u);
-    v[2] = (int)knn_expand4((b >> 8) & 15u);
-    v[3] = (int)knn_expand4((b >> 12) & 15u);
+    v[0] = (int)knn_bytes_of(ws << 3);
+    v[1] = (int)knn_bytes_of(ws << 2);
+    v[2] = (int)knn_bytes_of(ws << 1);
+    v[3] = (int)knn_bytes_of(ws);
     return v;
 }
 
@@ -1533,13 +1538,13 @@ __device__ __attribute__((always_inline)) inline void knn2_mfma_block(
         const uint4 qa = qp[0], qc = qp[1];
         const uint32_t dw[8] = {qa.x, qa.y, qa.z, qa.w, qc.x, qc.y, qc.z, qc.w};
 #pragma unroll
-        for (int s = 0; s < 8; ++s) qf[s] = knn_expand16(dw[s] >> (16 * h));
+        for (int s = 0; s < 8; ++s) qf[s] = knn_expand_half(dw[s], h);
     }
     uint32_t g1 = 0xFFFFFFFFu, g2 = 0xFFFFFFFFu;  // (H << 16 | t), lexicographic min
     // expansion role.  4 waves: thread -> (row tid >> 3, dword tid & 7) of a tile, two 16-byte
     // stores (threads ed >= 4 store their upper half first, so each store instruction's 8 chunks
-    // start on 8 distinct 4-bank boundaries).  8 waves: thread -> (row tid >> 4, 16-bit piece
-    // tid & 15), one 16-byte store (8 lanes write 128 contiguous bytes: conflict-free).
+    // start on 8 distinct 4-bank boundaries).  8 waves: thread -> (row tid >> 4, half ed & 1 of
+    // dword ed >> 1), one 16-byte store (8 lanes write 128 contiguous bytes: conflict-free).
     constexpr int kPieces = kKnnThreads / 32;  // pieces per train row
     const int er = tid / kPieces, ed = tid % kPieces;
     auto load_packed = [&](int tile) __attribute__((always_inline)) {
@@ -1547,7 +1552,7 @@ __device__ __attribute__((always_inline)) inline void knn2_mfma_block(
         if constexpr (kKnnWaves == 4)
             return *reinterpret_cast<const uint32_t*>(t + (long long)row * 32 + 4 * ed);
         else
-            return (uint32_t)*reinterpret_cast<const uint16_t*>(t + (long long)row * 32 + 2 * ed);
+            return *reinterpret_cast<const uint32_t*>(t + (long long)row * 32 + 4 * (ed >> 1));
     };
     // tile u's rows live in LDS stage buffer ((u - ts) / kKnnStage) & 1, slot (u - ts) % kKnnStage
     auto tile_lds = [&](int u) __attribute__((always_inline)) {
@@ -1558,13 +1563,12 @@ __device__ __attribute__((always_inline)) inline void knn2_mfma_block(
         if constexpr (kKnnWaves == 4) {
             uint8_t* dst = tile_lds(u) + er * kKnnPitch + 32 * ed;
             const bool kswap = ed >= 4;
-            const uint32_t ws = kswap ? __builtin_amdgcn_alignbit(w, w, 16) : w;  // halves swapped
-            const knn_v4i first = knn_expand16(ws & 0xFFFFu), second = knn_expand16(ws >> 16);
+            const knn_v4i first = knn_expand_half(w, kswap ? 1 : 0), second = knn_expand_half(w, kswap ? 0 : 1);
             *reinterpret_cast<knn_v4i*>(dst + (kswap ? 16 : 0)) = first;
             *reinterpret_cast<knn_v4i*>(dst + (kswap ? 0 : 16)) = second;
         } else {
             uint8_t* dst = tile_lds(u) + er * kKnnPitch + 16 * ed;
-            *reinterpret_cast<knn_v4i*>(dst) = knn_expand16(w);
+            *reinterpret_cast<knn_v4i*>(dst) = knn_expand_half(w, ed & 1);
         }
     };
     // Stages of kKnnStage tiles, double-buffered: the waves meet at one barrier per stage (the
