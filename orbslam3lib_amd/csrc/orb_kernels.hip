@@ -305,6 +305,143 @@ __device__ inline void blur_tile_compute(const LevelGeom& G, int tx0, int ty0, u
     }
 }
 
+// The same 128 x 32 blur tile as two int8 GEMMs on the matrix cores (v_mfma_i32_32x32x32_i8; the
+// 7-tap kernel is banded, the zeros cost MFMA cycles that are otherwise idle, and the VALU keeps
+// only the operand and result packing).  Wave w owns output columns 32w .. 32w+31 of the tile.
+//   pass 1 (horizontal): D1[y][x] = sum_j (p[y][j] - 128) g[j - x - 13] over window columns
+//     32w .. 32w+63 (two K-steps), rows 0..31 and 32..63 of the window (two M-blocks; rows past
+//     the window's 40 read row 39 and only meet zero weights).  A = pixel rows straight from LDS
+//     (16 bytes per lane, ^0x80 makes them int8), B = the constant band.
+//   the pass-1 results (lane: column x, rows (g&3) + 8(g>>2) + 4h of the M-block) are split into
+//     two int8 planes, hi = byte 1 and lo = byte 0 ^ 0x80 of D1, so D1 + 128 = 256 hi + lo + 256;
+//     they are pass 2's A operand as they stand (lane = column x, its 16 rows = the K slots; the
+//     constant B is laid out for exactly that row order).
+//   pass 2 (vertical, transposed): D2[x][y'] = sum_y A2[x][y] g[y - y' - 1] -- lane = output
+//     row y', its 16 registers = columns (g&3) + 8(g>>2) + 4h, i.e. four runs of 4 consecutive
+//     bytes.  With S = the integer blur sum (sum of g = 256): 256 D2hi + D2lo = S - 2^23 - 2^15, so
+//     the rounded output byte (S + 2^15) >> 16 is byte 2 of 256 D2hi + D2lo + 2^16 (which stays
+//     in [-2^23, 2^23)) with bit 7 flipped.  The + 2^16 rides in K slot 4 of M-block 1 (a row >= 40
+//     that no output reads) in both lane halves: A2hi = -1 there, B = -128, 2 x 128 into D2hi.
+// Exact integer arithmetic throughout (no intermediate rounding), so bit-exact with the VALU path.
+#ifndef BLUR_MFMA
+#define BLUR_MFMA 0
+#endif
+typedef int blur_v4i __attribute__((ext_vector_type(4)));
+typedef int blur_v16i __attribute__((ext_vector_type(16)));
+struct BlurMfmaTab {
+    uint32_t b1[2][64][4];  // pass-1 B: [K-step s][lane (x = l & 31, h)], byte j: window column 32s + 16h + j
+    uint32_t b2[2][64][4];  // pass-2 B: [M-block mb][lane (y' = l & 31, h)], byte g: window row of slot g
+};
+constexpr BlurMfmaTab make_blur_mfma_tab() {
+    BlurMfmaTab t{};
+    const int g7[7] = {18, 34, 48, 56, 48, 34, 18};
+    for (int k = 0; k < 2; ++k)
+        for (int l = 0; l < 64; ++l) {
+            const int n = l & 31, h = l >> 5;
+            for (int j = 0; j < 16; ++j) {
+                const int d1 = 32 * k + 16 * h + j - (n + 13);                            // column tap
+                const int rho = 32 * k + (j & 3) + 8 * (j >> 2) + 4 * h, d2 = rho - (n + 1);  // row tap
+                const uint32_t w1 = d1 >= 0 && d1 < 7 ? (uint32_t)g7[d1] : 0u;
+                uint32_t w2 = d2 >= 0 && d2 < 7 ? (uint32_t)g7[d2] : 0u;
+                if (k == 1 && j == 4) w2 = 0x80u;  // -128: the + 2^16 slot (both halves h: 2 x 128)
+                t.b1[k][l][j >> 2] |= w1 << (8 * (j & 3));
+                t.b2[k][l][j >> 2] |= w2 << (8 * (j & 3));
+            }
+        }
+    return t;
+}
+__constant__ BlurMfmaTab c_blur_mfma = make_blur_mfma_tab();
+
+__device__ inline void blur_tile_compute_mfma(const LevelGeom& G, int tx0, int ty0, uint8_t* dst,
+                                              uint4 (*tin4)[(kBlurTW + 32) / 16],
+                                              uint4 (*hp)[kBlurTW / 4], int rlo, int rhi) {
+    constexpr int IW = kBlurTW + 32, IH = kBlurTH + 8;
+    static_assert(kBlurTW == 128 && kBlurTH == 32, "one 32-column strip per wave, one output block");
+    constexpr int OP = kBlurTW + 4;  // output staging pitch: 33 dwords, conflict-free column writes
+    if (tx0 == 0 || tx0 + kBlurTW + 3 > G.w) {  // REFLECT_101 of the 3 columns past each edge
+        uint8_t* wb = reinterpret_cast<uint8_t*>(&tin4[0][0]);
+        for (int i = threadIdx.x; i < IH * 6; i += 256) {
+            const int r = i / 6, k = i - 6 * r;
+            const int xx = k < 3 ? -1 - k : G.w + (k - 3);
+            const int wx = xx - (tx0 - 16);
+            if (wx >= 0 && wx < IW && (k < 3 ? tx0 == 0 : true)) {
+                const int sx = refl101(xx, G.w) - (tx0 - 16);
+                wb[r * IW + wx] = wb[r * IW + sx];
+            }
+        }
+        __syncthreads();
+    }
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int n = lane & 31, h = lane >> 5;
+    const uint8_t* wb = reinterpret_cast<const uint8_t*>(&tin4[0][0]);
+    auto ldc = [&](const uint32_t* p) {
+        const uint4 v = *reinterpret_cast<const uint4*>(p);
+        return blur_v4i{(int)v.x, (int)v.y, (int)v.z, (int)v.w};
+    };
+    const blur_v4i B1[2] = {ldc(c_blur_mfma.b1[0][lane]), ldc(c_blur_mfma.b1[1][lane])};
+    const blur_v4i B2[2] = {ldc(c_blur_mfma.b2[0][lane]), ldc(c_blur_mfma.b2[1][lane])};
+    blur_v4i hi[2], lo[2];
+    const blur_v16i zero = {};
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb) {
+        const int row = min(32 * mb + n, IH - 1);
+        const uint8_t* src = wb + row * IW + 32 * w + 16 * h;
+        blur_v16i acc = zero;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const uint4 v = *reinterpret_cast<const uint4*>(src + 32 * k);
+            const blur_v4i a = {(int)(v.x ^ 0x80808080u), (int)(v.y ^ 0x80808080u), (int)(v.z ^ 0x80808080u),
+                                (int)(v.w ^ 0x80808080u)};
+            acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, B1[k], acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            if (mb == 1 && q > 0) {  // rows >= 40: no output row reads them; slot 4 carries the + 2^16
+                hi[mb][q] = q == 1 ? 0x000000FF : 0;
+                lo[mb][q] = 0;
+                continue;
+            }
+            const uint32_t u0 = acc[4 * q], u1 = acc[4 * q + 1], u2 = acc[4 * q + 2], u3 = acc[4 * q + 3];
+            hi[mb][q] = (int)(__builtin_amdgcn_perm(u1, u0, 0x0c0c0501u) | (__builtin_amdgcn_perm(u3, u2, 0x0c0c0501u) << 16));
+            lo[mb][q] = (int)((__builtin_amdgcn_perm(u1, u0, 0x0c0c0400u) | (__builtin_amdgcn_perm(u3, u2, 0x0c0c0400u) << 16)) ^ 0x80808080u);
+        }
+    }
+    blur_v16i ah = zero, al = zero;
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb) {
+        ah = __builtin_amdgcn_mfma_i32_32x32x32_i8(hi[mb], B2[mb], ah, 0, 0, 0);
+        al = __builtin_amdgcn_mfma_i32_32x32x32_i8(lo[mb], B2[mb], al, 0, 0, 0);
+    }
+    // output row n: columns 32w + 8q + 4h .. +3 from registers 4q .. 4q+3, staged row-major in LDS
+    uint32_t* ob = reinterpret_cast<uint32_t*>(&hp[0][0]);  // hp is free: callers sync before reusing it
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        uint32_t t4[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) t4[k] = ((uint32_t)ah[4 * q + k] << 8) + (uint32_t)al[4 * q + k];
+        const uint32_t packed = (__builtin_amdgcn_perm(t4[1], t4[0], 0x0c0c0602u) |
+                                 (__builtin_amdgcn_perm(t4[3], t4[2], 0x0c0c0602u) << 16)) ^ 0x80808080u;
+        ob[n * (OP / 4) + 8 * w + 2 * q + h] = packed;
+    }
+    __syncthreads();
+    // stores as the VALU path: thread -> column quad cq, rows R rg .. R rg + R - 1
+    constexpr int R = kBlurTH / 8;
+    const int cq = threadIdx.x & 31, rg = threadIdx.x >> 5;
+    const int x = tx0 + 4 * cq;
+    const int ybase = ty0 + R * rg;
+    const int ylo = max(rlo, ybase), yhi = x < G.w ? min(min(rhi, G.h), ybase + R) : ybase;
+    const int olo = ylo - ybase, ohi = yhi - ybase;
+    uint8_t* dbase = dst + plane_off(ybase, G.bpitch, x);
+#pragma unroll
+    for (int o = 0; o < R; ++o)
+        if (o >= olo && o < ohi) *reinterpret_cast<uint32_t*>(dbase + o * G.bpitch) = ob[(R * rg + o) * (OP / 4) + cq];
+}
+#if BLUR_MFMA
+#define BLUR_TILE_COMPUTE blur_tile_compute_mfma
+#else
+#define BLUR_TILE_COMPUTE blur_tile_compute
+#endif
+
 // Persistent over the tiles of the launch (images x levels x tiles): the next tile's window
 // is loaded into registers while the current one is filtered, so the global-memory round
 // trip is hidden behind the arithmetic of the previous tile.
@@ -349,7 +486,7 @@ __global__ __launch_bounds__(256) void k_blur(BatchArgs a, int tile0, int ntile)
             }
         }
         __syncthreads();
-        blur_tile_compute(G, tx0, ty0, dst, tin4, hp, 0, G.h);
+        BLUR_TILE_COMPUTE(G, tx0, ty0, dst, tin4, hp, 0, G.h);
     }
 }
 
@@ -434,7 +571,7 @@ __device__ inline void br_tile(const BatchArgs& a, int l, bool resize, int img, 
     }
     __syncthreads();
 #if BR_VAR != 2 && BR_VAR != 3  // measurement variants (tools/build_variants.sh): 2, 3 skip the blur
-    blur_tile_compute(S, bt.tx0, bt.ty0, bt.dst, sm.tin4, sm.hp, 0, S.h);  // fixes only off-plane columns
+    BLUR_TILE_COMPUTE(S, bt.tx0, bt.ty0, bt.dst, sm.tin4, sm.hp, 0, S.h);  // fixes only off-plane columns
 #endif
 #if BR_VAR == 1 || BR_VAR == 3  // 1, 3 skip the resize
     return;
@@ -1483,6 +1620,9 @@ constexpr int kKnnPitch = 272;           // bytes per expanded train row in LDS 
 #ifndef KNN_STAGE
 #define KNN_STAGE 1
 #endif
+#ifndef KNN_MFMA16
+#define KNN_MFMA16 0  // 1: v_mfma_i32_16x16x64_i8 tiles (knn2_mfma16_block)
+#endif
 constexpr int kKnnStage = KNN_STAGE;
 static_assert(kKnnStage == 1 || kKnnStage == 2 || kKnnStage == 4, "stage size");
 constexpr int kKnnSeg = 4096;            // train rows per key segment
@@ -1686,6 +1826,175 @@ __device__ __attribute__((always_inline)) inline void knn2_mfma_block(
     }
 }
 
+#if KNN_MFMA16
+// knn2_mfma_block on v_mfma_i32_16x16x64_i8 (same cycles per MAC as the 32x32x32 form; the
+// smaller tile draws less power, so the chip holds a higher clock under load -- MI355X_MICROARCH
+// "bare bf16 MFMA loops").  A wave still owns 32 queries and walks 32-row train tiles: per tile
+// 2 (train blocks mb) x 2 (query blocks nb) outputs of 16 x 16, each 4 MFMAs over K = 256.
+// B fragments: lane (c = lane & 15, kg = lane >> 4) of K-step s holds expanded dwords
+// 16 s + 4 kg .. + 3 of query 16 nb + c; A: train row 16 mb + c, the same 16 bytes of its expanded
+// row.  C/D (cdna_hip_programming.md §3): lane holds column c (its query) and rows 4 kg + reg.
+typedef int knn_v4 __attribute__((ext_vector_type(4)));
+__device__ __attribute__((always_inline)) inline void knn2_mfma16_block(
+    const uint8_t* q, int nq, const uint8_t* t, int nt, int qb, int ts, int te, int32_t* i1, int32_t* d1,
+    int32_t* i2, int32_t* d2, uint2* part, uint8_t* lds) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int c = lane & 15, kg = lane >> 4;
+    const int qw = qb * kKnnQ + wave * 32;  // the wave's first query
+    knn_v4i qf[2][4];
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) {
+        const int qi = qw + 16 * nb + c;
+        const uint4* qp = reinterpret_cast<const uint4*>(q + (long long)min(qi, max(nq - 1, 0)) * 32);
+        const uint4 qa = qp[0], qc = qp[1];
+        const uint32_t dw[8] = {qa.x, qa.y, qa.z, qa.w, qc.x, qc.y, qc.z, qc.w};
+#pragma unroll
+        for (int s = 0; s < 4; ++s) qf[nb][s] = knn_expand_half(dw[2 * s + (kg >> 1)], kg & 1);
+    }
+    uint32_t g1[2] = {0xFFFFFFFFu, 0xFFFFFFFFu}, g2[2] = {0xFFFFFFFFu, 0xFFFFFFFFu};
+    constexpr int kPieces = kKnnThreads / 32;  // pieces per train row
+    const int er = tid / kPieces, ed = tid % kPieces;
+    auto load_packed = [&](int tile) __attribute__((always_inline)) {
+        const int row = min(tile * 32 + er, nt - 1);
+        if constexpr (kKnnWaves == 4)
+            return *reinterpret_cast<const uint32_t*>(t + (long long)row * 32 + 4 * ed);
+        else
+            return *reinterpret_cast<const uint32_t*>(t + (long long)row * 32 + 4 * (ed >> 1));
+    };
+    auto tile_lds = [&](int u) __attribute__((always_inline)) {
+        const int v = u - ts;
+        return lds + (((v / kKnnStage) & 1) * kKnnStage + v % kKnnStage) * (32 * kKnnPitch);
+    };
+    auto store_expanded = [&](int u, uint32_t w) __attribute__((always_inline)) {
+        if constexpr (kKnnWaves == 4) {
+            uint8_t* dst = tile_lds(u) + er * kKnnPitch + 32 * ed;
+            const bool kswap = ed >= 4;
+            const knn_v4i first = knn_expand_half(w, kswap ? 1 : 0), second = knn_expand_half(w, kswap ? 0 : 1);
+            *reinterpret_cast<knn_v4i*>(dst + (kswap ? 16 : 0)) = first;
+            *reinterpret_cast<knn_v4i*>(dst + (kswap ? 0 : 16)) = second;
+        } else {
+            uint8_t* dst = tile_lds(u) + er * kKnnPitch + 16 * ed;
+            *reinterpret_cast<knn_v4i*>(dst) = knn_expand_half(w, ed & 1);
+        }
+    };
+    uint32_t pk0 = 0, pk1 = 0;
+    if (te > ts) {
+        for (int u = ts; u < ts + kKnnStage && u < te; ++u) store_expanded(u, load_packed(u));
+        if ((ts + kKnnStage) & 1) pk1 = load_packed(ts + kKnnStage);
+        else pk0 = load_packed(ts + kKnnStage);
+    }
+    // preload: 4095 - (tile-local train row 16 mb + 4 kg + reg), as the 32x32 form
+    knn_v4 C0[2];
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) C0[mb][g] = 4095 - 16 * mb - 4 * kg - g;
+    constexpr int kNone = -(1 << 30);
+    struct Acc {
+        knn_v4 v[2][2];  // [mb][nb]
+    };
+    for (int seg0 = (ts * 32 / kKnnSeg) * kKnnSeg; seg0 < te * 32; seg0 += kKnnSeg) {
+        const int tile0 = max(seg0 >> 5, ts), tile1 = min(te, (seg0 + kKnnSeg) >> 5);
+        int k1[2] = {kNone, kNone}, k2[2] = {kNone, kNone};  // per query block
+        auto select = [&](const Acc& v, bool shift) __attribute__((always_inline)) {
+            if (shift) {
+#pragma unroll
+                for (int nb = 0; nb < 2; ++nb) {
+                    k1[nb] += 32;
+                    k2[nb] += 32;
+                }
+            }
+#pragma unroll
+            for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+                for (int g = 0; g < 4; g += 2)
+#pragma unroll
+                    for (int nb = 0; nb < 2; ++nb) {
+                        const int x = v.v[mb][nb][g], y = v.v[mb][nb][g + 1];
+                        k2[nb] = max(k2[nb], knn_med3_i32(k1[nb], x, y));
+                        k1[nb] = knn_max3_i32(k1[nb], x, y);
+                    }
+        };
+        auto body = [&](int ti, auto par, Acc& acc, const Acc& prev) __attribute__((always_inline)) {
+            constexpr int PAR = decltype(par)::value;
+            uint32_t& pk_use = ((PAR + kKnnStage) & 1) ? pk1 : pk0;
+            uint32_t& pk_load = ((PAR + kKnnStage) & 1) ? pk0 : pk1;
+            if (kKnnStage == 1 || (PAR == 0 && (kKnnStage == 2 || (ti - ts) % kKnnStage == 0)))
+                __syncthreads();
+            pk_load = load_packed(ti + kKnnStage + 1);
+            const uint8_t* ab = tile_lds(ti) + c * kKnnPitch + 16 * kg;
+#pragma unroll
+            for (int s = 0; s < 4; ++s)
+#pragma unroll
+                for (int mb = 0; mb < 2; ++mb) {
+                    const knn_v4i a = *reinterpret_cast<const knn_v4i*>(ab + 16 * mb * kKnnPitch + 64 * s);
+#pragma unroll
+                    for (int nb = 0; nb < 2; ++nb)
+                        acc.v[mb][nb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, qf[nb][s], s ? acc.v[mb][nb] : C0[mb], 0, 0, 0);
+                }
+            if (ti > tile0) select(prev, ti - 1 > tile0);
+            if (ti + kKnnStage < te) store_expanded(ti + kKnnStage, pk_use);
+            if (ti * 32 + 32 > nt) {  // partial last tile: padding rows never win
+#pragma unroll
+                for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+                    for (int g = 0; g < 4; ++g)
+                        if (ti * 32 + 16 * mb + 4 * kg + g >= nt) acc.v[mb][0][g] = acc.v[mb][1][g] = kNone;
+            }
+        };
+        using P0 = std::integral_constant<int, 0>;
+        using P1 = std::integral_constant<int, 1>;
+        Acc acc0, acc1;
+        int ti = tile0;
+        for (; ti + 1 < tile1; ti += 2) {
+            body(ti, P0{}, acc0, acc1);
+            body(ti + 1, P1{}, acc1, acc0);
+        }
+        if (ti < tile1) {
+            body(ti, P0{}, acc0, acc1);
+            select(acc0, ti > tile0);
+        } else if (tile1 > tile0) {
+            select(acc1, tile1 - 1 > tile0);
+        }
+        const int unbias = 32 * (tile1 - 1 - tile0);
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb) {
+            auto fold = [&](int k) __attribute__((always_inline)) {
+                if (k < -(1 << 24)) return;  // padding rows only
+                const int tl = 4095 - (k & 4095), dotp = k >> 12;
+                const uint32_t key = ((uint32_t)((256 - dotp) >> 1) << 16) | (uint32_t)(32 * tile0 + tl);
+                g2[nb] = med3_u32(g1[nb], g2[nb], key);
+                g1[nb] = min(g1[nb], key);
+            };
+            fold(k1[nb] - unbias);
+            fold(k2[nb] - unbias);
+        }
+    }
+    // the four lanes c + 16 kg saw disjoint train rows of the same queries
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+        for (int x = 16; x <= 32; x *= 2) {
+            const uint32_t o1 = __shfl_xor(g1[nb], x), o2 = __shfl_xor(g2[nb], x);
+            g2[nb] = med3_u32(g1[nb], g2[nb], o1);
+            g1[nb] = min(g1[nb], o1);
+            g2[nb] = med3_u32(g1[nb], g2[nb], o2);
+            g1[nb] = min(g1[nb], o2);
+        }
+    if (kg < 2) {  // lanes kg = 0 / 1 write query block 0 / 1
+        const int nb = kg, qi = qw + 16 * nb + c;
+        const uint32_t k1 = nb ? g1[1] : g1[0], k2 = nb ? g2[1] : g2[0];
+        if (qi < nq) {
+            if (part) part[qi] = make_uint2(k1, k2);
+            else knn2_store(k1, k2, qi, i1, d1, i2, d2);
+        }
+    }
+}
+#define KNN_BLOCK knn2_mfma16_block
+#else
+#define KNN_BLOCK knn2_mfma_block
+#endif
+
 __global__ __launch_bounds__(kKnnThreads) void k_knn2_mfma_pairs(MatchArgs m) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[2 * kKnnStage * 32 * kKnnPitch];
     const int pair = m.pair0 + blockIdx.y;
@@ -1703,7 +2012,7 @@ __global__ __launch_bounds__(kKnnThreads) void k_knn2_mfma_pairs(MatchArgs m) {
     const int npt = (((nt + 31) >> 5) + 1) >> 1, S = gridDim.z, sp = blockIdx.z;  // tile pairs
     const int ts = 2 * (npt * sp / S), te = min((nt + 31) >> 5, 2 * (npt * (sp + 1) / S));
     uint2* part = m.part ? m.part + ((long long)(blockIdx.y * S + sp)) * m.out_cap : nullptr;
-    knn2_mfma_block(q, nq, t, nt, blockIdx.x, ts, te, m.idx1 + o, m.dist1 + o, m.idx2 + o, m.dist2 + o, part, lds);
+    KNN_BLOCK(q, nq, t, nt, blockIdx.x, ts, te, m.idx1 + o, m.dist1 + o, m.idx2 + o, m.dist2 + o, part, lds);
 }
 
 // The split launch's partial top-2 lists of one query, merged (keys are distinct train rows).
@@ -1731,7 +2040,7 @@ __global__ __launch_bounds__(256) void k_knn2_merge(MatchArgs m, int nsplit) {
 __global__ __launch_bounds__(kKnnThreads) void k_knn2_mfma_plain(const uint8_t* q, int nq, const uint8_t* t, int nt,
                                                          int32_t* i1, int32_t* d1, int32_t* i2, int32_t* d2) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[2 * kKnnStage * 32 * kKnnPitch];
-    knn2_mfma_block(q, nq, t, nt, blockIdx.x, 0, (nt + 31) >> 5, i1, d1, i2, d2, nullptr, lds);
+    KNN_BLOCK(q, nq, t, nt, blockIdx.x, 0, (nt + 31) >> 5, i1, d1, i2, d2, nullptr, lds);
 }
 
 // ---------------------------------------------------------------------------------------------
