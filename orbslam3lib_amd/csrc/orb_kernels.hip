@@ -324,7 +324,7 @@ __device__ inline void blur_tile_compute(const LevelGeom& G, int tx0, int ty0, u
 //     that no output reads) in both lane halves: A2hi = -1 there, B = -128, 2 x 128 into D2hi.
 // Exact integer arithmetic throughout (no intermediate rounding), so bit-exact with the VALU path.
 #ifndef BLUR_MFMA
-#define BLUR_MFMA 0
+#define BLUR_MFMA 1
 #endif
 typedef int blur_v4i __attribute__((ext_vector_type(4)));
 typedef int blur_v16i __attribute__((ext_vector_type(16)));
