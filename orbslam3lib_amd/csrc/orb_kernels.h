@@ -187,6 +187,17 @@ constexpr int kOctLdsNodes = 1024;
 #define OD_LANES 32
 #endif
 constexpr int kOdKpBlock = 256 / OD_LANES;  // keypoints per k_orient_desc pass (256 threads / lanes per keypoint)
+#ifndef OD_BATCH
+#define OD_BATCH 0  // k_orient_desc: moments, then one angle pass per batch, then descriptors (0: per pair)
+#endif
+#ifndef OD_WB
+#define OD_WB 16
+#endif
+constexpr int kOdWaveBatch = OD_WB;  // OD_BATCH: keypoints per wave batch
+// keypoints per k_orient_desc workgroup by default: 4 waves x one batch (OD_BATCH), or 2 passes of
+// kOdKpBlock (the per-pair kernel; round 3 single stream: 488-490 us per 512 images vs 504 at 4
+// passes, 497-504 at 1, 540 at 8)
+constexpr int kOdBlockKps = OD_BATCH ? 4 * kOdWaveBatch : 2 * kOdKpBlock;
 
 constexpr int kOctLdsKeys = 16384;  // per-key node labels (u16) kept in LDS up to this many keys
 constexpr int kFastMergeMaxImages = 4;  // launches this small run the 48/64 FAST cells as one launch

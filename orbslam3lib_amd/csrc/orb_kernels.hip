@@ -1103,7 +1103,204 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 #ifndef OD_CHUNKS
 #define OD_CHUNKS 1  // moments from coalesced 16-byte row chunks (0: a disc row per lane, round 4)
 #endif
-#if OD_CHUNKS
+#ifndef OD_PIPE
+#define OD_PIPE 1  // issue the next pair's loads before the current pair's arithmetic
+#endif
+#ifndef OD_WPE
+#define OD_WPE 4  // 106 VGPRs without spills (6: 40 spilled, 5: 6 spilled)
+#endif
+#if OD_BATCH
+// Batched per wave (orb_kernels.h kOdWaveBatch keypoints): the moments of every pair of the
+// batch first (32 lanes per keypoint, coalesced row chunks as below), their sums to LDS; then
+// ONE pass with a lane per keypoint for fastAtan2 and sin / cos (the float division and the
+// double-precision libm arithmetic, ~90 VALU, were computed by all 32 lanes of a keypoint); then
+// the descriptors of every pair from the blurred patches.  Keys are read once per batch into LDS;
+// each phase issues the next pair's loads before the current pair's arithmetic.
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OD_WPE))) void k_orient_desc(
+    BatchArgs a, uint32_t nblk_magic) {
+    __shared__ __attribute__((aligned(16))) uint8_t patch[kOdKpBlock][kOdPatchRows * kOdPatchPitch];
+    __shared__ __attribute__((aligned(16))) uint4 s_rng[17][17];  // bytes [m, n) of 16 (none if n <= m)
+    __shared__ __attribute__((aligned(16))) uint4 s_pat[kOdPairs][kOdLanes];
+    __shared__ uint32_t s_key[4][kOdWaveBatch];
+    __shared__ int2 s_mom[4][kOdWaveBatch];
+    __shared__ __attribute__((aligned(16))) float4 s_ang[4][kOdWaveBatch];  // angle, sin, cos
+    const int wg = xcd_remap(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * gridDim.y);
+    const int irel = gridDim.x == 1 ? wg : (int)__umulhi((uint32_t)wg, nblk_magic);
+    const int img = a.img0 + irel, bx = wg - irel * (int)gridDim.x;
+    const int l = a.rtab[a.od_tab_off + bx].x;
+    const LevelGeom G = a.lv[l];
+    const int sub = threadIdx.x % kOdLanes, grp = threadIdx.x / kOdLanes;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, half = grp & 1;
+    const int count = a.lvlcnt[img * kMaxLevels + l];
+    const long long kbase = (long long)img * a.lvlkp_img_stride + G.kp_off;
+    const uint8_t* lvl = a.lvl_base[l] + (long long)img * G.img_stride;
+    const uint8_t* blr = a.blur_base[l] + (long long)img * G.bimg_stride;
+    const bool raw_dw = ((G.pitch | G.img_stride) & 3) == 0;
+    const __amdgpu_buffer_rsrc_t brs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)blr, (short)0, G.bpitch * G.h, 0x00020000);
+    const __amdgpu_buffer_rsrc_t lrs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)lvl, (short)0, (int)min((long long)G.pitch * G.h, 0x7fffffffLL), 0x00020000);
+    for (int e = threadIdx.x; e < 17 * 17; e += 256) {
+        const int m = e / 17, n = e - 17 * m;
+        uint32_t w4[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            w4[k] = 0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) w4[k] |= (4 * k + j >= m && 4 * k + j < n ? 0xFFu : 0u) << (8 * j);
+        }
+        s_rng[m][n] = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+    }
+    {
+        const int8_t* pv = c_pattern.v + 4 * threadIdx.x;  // x0, y0, x1, y1 of pair threadIdx.x
+        s_pat[threadIdx.x % kOdPairs][threadIdx.x / kOdPairs] = make_uint4(__float_as_uint((float)pv[0]), __float_as_uint((float)pv[2]),
+                                        __float_as_uint((float)pv[1]), __float_as_uint((float)pv[3]));
+    }
+    __syncthreads();
+    // this lane's three moment chunk slots (as the OD_CHUNKS kernel below)
+    int mv[3], mlo[3], mhi[3], mofs[3], mp16[3];
+#pragma unroll
+    for (int it = 0; it < 3; ++it) {
+        const int i = sub + 32 * it, r = i / 3, part = i - 3 * r;
+        mv[it] = r - 15;
+        const int d = r < 31 ? c_umax[mv[it] < 0 ? -mv[it] : mv[it]] : -1;
+        mlo[it] = 15 - d - 16 * part;
+        mhi[it] = 16 + d - 16 * part;
+        mofs[it] = (r < 31 ? mv[it] : 15) * G.pitch + 16 * part;
+        mp16[it] = 16 * part;
+    }
+    uint8_t* pt = patch[grp];
+    auto wave_sync = [] {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+    auto moment_loads = [&](uint32_t key, uint4 mc[3]) __attribute__((always_inline)) {
+        const int x = key_x(key) + kMinBorder, y = key_y(key) + kMinBorder;
+        const int wofs = y * G.pitch + (x - 15 - ((x - 15) & 15));
+#pragma unroll
+        for (int it = 0; it < 3; ++it) {
+            if (raw_dw) {
+                const auto q = __builtin_amdgcn_raw_buffer_load_b128(lrs, wofs + mofs[it], 0, 0);
+                mc[it] = make_uint4(q[0], q[1], q[2], q[3]);
+            } else {  // level-0 rows not 4-byte aligned: bytes
+                const uint8_t* q = lvl + wofs + mofs[it];
+                uint32_t d4[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    d4[k] = (uint32_t)q[4 * k] | ((uint32_t)q[4 * k + 1] << 8) | ((uint32_t)q[4 * k + 2] << 16) |
+                            ((uint32_t)q[4 * k + 3] << 24);
+                mc[it] = make_uint4(d4[0], d4[1], d4[2], d4[3]);
+            }
+        }
+    };
+    auto patch_loads = [&](uint32_t key, uint4 pv[kOdPatchIt]) __attribute__((always_inline)) {
+        const int x = key_x(key) + kMinBorder, y = key_y(key) + kMinBorder;
+        const int pofs = (y - kOdPatchR) * G.bpitch + ((x - kOdPatchR) & ~3);
+#pragma unroll
+        for (int it = 0; it < kOdPatchIt; ++it) {
+            const int c = sub + it * kOdLanes;
+            const int r = c / 3, part = c - 3 * r;
+            if (c < kOdPatchChunks) {
+                const auto q = __builtin_amdgcn_raw_buffer_load_b128(brs, pofs + r * G.bpitch + 16 * part, 0, 0);
+                pv[it] = make_uint4(q[0], q[1], q[2], q[3]);
+            }
+        }
+    };
+    const int wave_stride = G.od_blocks * 4 * kOdWaveBatch;
+    for (int base = ((bx - G.od_first) * 4 + w) * kOdWaveBatch; base < count; base += wave_stride) {
+        const int nkb = min(kOdWaveBatch, count - base);  // wave-uniform
+        if (lane < nkb) s_key[w][lane] = a.lvlkey[kbase + base + lane];
+        wave_sync();
+        // keypoint j + half of pair j / 2 (the odd group of a last odd pair repeats keypoint j)
+        auto key_of = [&](int j) { return s_key[w][j + half < nkb ? j + half : j]; };
+        // ---- IC_Angle moments (:78-105) of every pair
+        uint4 mc[3], mcn[3];
+        if (OD_PIPE) moment_loads(key_of(0), mc);
+        for (int j = 0; j < nkb; j += 2) {
+            const uint32_t key = key_of(j);
+            if (!OD_PIPE) moment_loads(key, mc);
+            else if (j + 2 < nkb) moment_loads(key_of(j + 2), mcn);
+            const int al = (key_x(key) + kMinBorder - 15) & 15;
+            int s_all = 0, c_all = 0, m01p = 0;
+#pragma unroll
+            for (int it = 0; it < 3; ++it) {
+                const int m = min(max(mlo[it] + al, 0), 16), n = min(max(mhi[it] + al, 0), 16);
+                const uint4 mk = s_rng[m][n];
+                const uint32_t p0 = mc[it].x & mk.x, p1 = mc[it].y & mk.y, p2 = mc[it].z & mk.z, p3 = mc[it].w & mk.w;
+                uint32_t sc = __builtin_amdgcn_udot4(p0, 0x01010101u, 0u, false);
+                sc = __builtin_amdgcn_udot4(p1, 0x01010101u, sc, false);
+                sc = __builtin_amdgcn_udot4(p2, 0x01010101u, sc, false);
+                sc = __builtin_amdgcn_udot4(p3, 0x01010101u, sc, false);
+                uint32_t cc = __builtin_amdgcn_udot4(p0, 0x03020100u, 0u, false);
+                cc = __builtin_amdgcn_udot4(p1, 0x07060504u, cc, false);
+                cc = __builtin_amdgcn_udot4(p2, 0x0B0A0908u, cc, false);
+                cc = __builtin_amdgcn_udot4(p3, 0x0F0E0D0Cu, cc, false);
+                s_all += (int)sc;
+                c_all += (int)cc + mp16[it] * (int)sc;
+                m01p += mv[it] * (int)sc;
+            }
+            const int m10 = od_sum(c_all - (15 + al) * s_all), m01 = od_sum(m01p);
+            if (sub == 0 && j + half < nkb) s_mom[w][j + half] = make_int2(m10, m01);
+            if (OD_PIPE)
+#pragma unroll
+                for (int it = 0; it < 3; ++it) mc[it] = mcn[it];
+        }
+        wave_sync();
+        // ---- angle (fastAtan2) and std::sin / std::cos (:114-115), one lane per keypoint
+        if (lane < nkb) {
+            const int2 mm = s_mom[w][lane];
+            const float angle = fast_atan2_deg((float)mm.y, (float)mm.x);
+            const float factorPI = (float)(3.14159265358979323846 / 180.0);
+            float sn, ca;
+            libm_sincosf(angle * factorPI, &sn, &ca);
+            s_ang[w][lane] = make_float4(angle, sn, ca, 0.f);
+            a.lvlangle[kbase + base + lane] = angle;
+        }
+        wave_sync();
+        // ---- computeOrbDescriptor (:108-148) of every pair: lane `sub` makes bits [8 sub, 8 sub + 8)
+        uint4 pv[kOdPatchIt], pvn[kOdPatchIt];
+        if (OD_PIPE) patch_loads(key_of(0), pv);
+        for (int j = 0; j < nkb; j += 2) {
+            const uint32_t key = key_of(j);
+            const int x = key_x(key) + kMinBorder;
+            if (!OD_PIPE) patch_loads(key, pv);
+#pragma unroll
+            for (int it = 0; it < kOdPatchIt; ++it) {
+                const int c = sub + it * kOdLanes;
+                const int r = c / 3, part = c - 3 * r;
+                if (c < kOdPatchChunks) *reinterpret_cast<uint4*>(pt + r * kOdPatchPitch + 16 * part) = pv[it];
+            }
+            if (OD_PIPE && j + 2 < nkb) patch_loads(key_of(j + 2), pvn);
+            wave_sync();
+            const float4 ag = s_ang[w][j + half < nkb ? j + half : j];
+            const float sn = ag.y, ca = ag.z;
+            const int pc = kOdPatchR * kOdPatchPitch + (x - ((x - kOdPatchR) & ~3));
+            const float magic = 12582912.0f;
+            const uint32_t kofs = (uint32_t)pc - 0x4B400000u - 0x400000u * (uint32_t)kOdPatchPitch;
+            const f32x2 snv = {sn, sn}, cav = {ca, ca}, mg = {magic, magic};
+            uint32_t bits = 0;
+#pragma unroll
+            for (int b = kOdPairs - 1; b >= 0; --b) {
+                uint4 pw = s_pat[b][sub];
+                asm volatile("" : "+v"(pw.x), "+v"(pw.y), "+v"(pw.z), "+v"(pw.w));
+                const f32x2 X = {__uint_as_float(pw.x), __uint_as_float(pw.y)};
+                const f32x2 Y = {__uint_as_float(pw.z), __uint_as_float(pw.w)};
+                const f32x2 R = (X * snv + Y * cav) + mg;
+                const f32x2 C = (X * cav - Y * snv) + mg;
+                const int o0 = (int)(__umul24(__float_as_uint(R.x), (uint32_t)kOdPatchPitch) + __float_as_uint(C.x) + kofs);
+                const int o1 = (int)(__umul24(__float_as_uint(R.y), (uint32_t)kOdPatchPitch) + __float_as_uint(C.y) + kofs);
+                bits = bits + bits + (pt[o0] < pt[o1] ? 1u : 0u);
+            }
+            if (j + half < nkb) a.lvldesc[(kbase + base + j + half) * 32 + sub] = (uint8_t)bits;
+            if (OD_PIPE)
+#pragma unroll
+                for (int it = 0; it < kOdPatchIt; ++it) pv[it] = pvn[it];
+            wave_sync();  // the group's reads of the patch are done before the next pair's stores
+        }
+    }
+}
+#elif OD_CHUNKS
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k_orient_desc(
     BatchArgs a, uint32_t nblk_magic) {
     // per keypoint group: the blurred patch around the keypoint, staged with 16-byte loads

@@ -351,11 +351,10 @@ int set_geometry(orbgpu_ctx* c, int w, int h) {
     long long pyr_off[kMaxLevels] = {}, blur_off[kMaxLevels] = {};
     long long pyr = 0, blr = 0, ck = 0, ows = 0;
     int cc = 0, kpo = 0, cell_first = 0, tile_first = 0, od_first = 0;
-    // keypoints per k_orient_desc workgroup: kOdKpBlock per pass, od_iters passes (the key of the
-    // next pass is prefetched during the current one; the table setup is paid once).  2 passes:
-    // 488-490 us per 512 images vs 504 at 4, 497-504 at 1, 540 at 8 (round 3, single stream)
+    // keypoints per k_orient_desc workgroup (orb_kernels.h kOdBlockKps; ORBGPU_OD_ITERS: passes of
+    // kOdKpBlock instead, for A/B)
     const char* odi = diag_env("ORBGPU_OD_ITERS");
-    const int od_per_block = kOdKpBlock * std::max(1, odi ? atoi(odi) : 2);
+    const int od_per_block = odi ? kOdKpBlock * std::max(1, atoi(odi)) : kOdBlockKps;
     for (int l = 0; l < L; ++l) {
         LevelGeom& G = A.lv[l];
         G.w = cv_round_f((float)w * c->inv_scale[l]);   // ComputePyramid :1336
