@@ -116,6 +116,8 @@ struct MatchArgs {
     int32_t* nq;              // [pair]
     int pair0;                // first pair of this launch
     uint2* part;              // [kKnnSplitSlots][out_cap] partial top-2 keys of split launches, or null
+    uint32_t* cnt;            // split launches: per (pair, query block) arrival counters (zero between
+                              // launches), so the last split workgroup merges; null: k_knn2_merge does
 };
 constexpr int kKnnMaxSplit = 8;     // train-row splits of a launch with few pairs
 constexpr int kKnnSplitSlots = 8;   // pairs x splits the partial buffer holds (1 pair: 8 splits)

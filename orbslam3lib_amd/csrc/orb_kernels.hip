@@ -2210,6 +2210,45 @@ __global__ __launch_bounds__(kKnnThreads) void k_knn2_mfma_pairs(MatchArgs m) {
     const int ts = 2 * (npt * sp / S), te = min((nt + 31) >> 5, 2 * (npt * (sp + 1) / S));
     uint2* part = m.part ? m.part + ((long long)(blockIdx.y * S + sp)) * m.out_cap : nullptr;
     KNN_BLOCK(q, nq, t, nt, blockIdx.x, ts, te, m.idx1 + o, m.dist1 + o, m.idx2 + o, m.dist2 + o, part, lds);
+    if (!part || !m.cnt || S == 1) return;
+    // fused merge: the last of the S split workgroups of this query block merges their partial
+    // top-2 lists (k_knn2_merge's work, without its launch).  The hand-off follows
+    // cdna_hip_programming.md Guideline 16 (counter form): every wave drains its partial stores,
+    // one lane releases at agent scope (other XCDs' L2s), waits, and takes a ticket; the last
+    // arriver resets the counter (zeroed when allocated) and acquires before any wave reads the
+    // other splits' partials.  The "last" verdict goes through the kernel's one LDS array (a second
+    // __shared__ object can add vmcnt waits to the tile loop).
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int* s_last = reinterpret_cast<int*>(lds);  // every wave is past its last tile read
+    if (threadIdx.x == 0) {
+        uint32_t* c = m.cnt + blockIdx.y * gridDim.x + blockIdx.x;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const bool last = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)(S - 1);
+        if (last) {
+            __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // ready for the next launch
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        *s_last = last ? 1 : 0;
+    }
+    __syncthreads();
+    if (!*s_last) return;
+    const long long pb = (long long)blockIdx.y * S * m.out_cap;
+    for (int i = threadIdx.x; i < kKnnQ; i += kKnnThreads) {
+        const int qi = blockIdx.x * kKnnQ + i;
+        if (qi >= nq) break;
+        uint32_t g1 = 0xFFFFFFFFu, g2 = 0xFFFFFFFFu;
+        for (int k = 0; k < S; ++k) {
+            const uint2 kk = m.part[pb + (long long)k * m.out_cap + qi];
+            g2 = med3_u32(g1, g2, kk.x);
+            g1 = min(g1, kk.x);
+            g2 = med3_u32(g1, g2, kk.y);
+            g1 = min(g1, kk.y);
+        }
+        knn2_store(g1, g2, qi, m.idx1 + o, m.dist1 + o, m.idx2 + o, m.dist2 + o);
+    }
 }
 
 // The split launch's partial top-2 lists of one query, merged (keys are distinct train rows).
@@ -2316,8 +2355,10 @@ hipError_t launch_orient_desc(const BatchArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 hipError_t launch_finalize(const BatchArgs& a, hipStream_t s) {
-    // few images (the latency shape): 512 threads per image; full batches: 256
-    if (a.nimages <= kFinWideMaxImages) hipLaunchKernelGGL(k_finalize<512>, dim3(a.nimages), dim3(512), 0, s, a);
+    // few images (the latency shape): 1024 / 512 threads per image (one load round trip covers
+    // 2048 / 1024 keypoints); full batches: 256
+    if (a.nimages <= 2) hipLaunchKernelGGL(k_finalize<1024>, dim3(a.nimages), dim3(1024), 0, s, a);
+    else if (a.nimages <= kFinWideMaxImages) hipLaunchKernelGGL(k_finalize<512>, dim3(a.nimages), dim3(512), 0, s, a);
     else hipLaunchKernelGGL(k_finalize<256>, dim3(a.nimages), dim3(256), 0, s, a);
     return hipGetLastError();
 }
@@ -2327,7 +2368,7 @@ hipError_t launch_knn2_pairs(const MatchArgs& m, int npairs, hipStream_t s) {
     const int S = m.part ? std::max(1, std::min(kKnnMaxSplit, kKnnSplitSlots / std::max(npairs, 1))) : 1;
     if (S > 1) {
         hipLaunchKernelGGL(k_knn2_mfma_pairs, dim3((m.out_cap + kKnnQ - 1) / kKnnQ, npairs, S), dim3(kKnnThreads), 0, s, m);
-        hipLaunchKernelGGL(k_knn2_merge, dim3((m.out_cap + 255) / 256, npairs), dim3(256), 0, s, m, S);
+        if (!m.cnt) hipLaunchKernelGGL(k_knn2_merge, dim3((m.out_cap + 255) / 256, npairs), dim3(256), 0, s, m, S);
         return hipGetLastError();
     }
     MatchArgs m1 = m;
