@@ -91,6 +91,41 @@ def fast_pyramid_bytes(w, h, L, sf=1.2):
     return sum(A[l - 1] + A[l] for l in range(1, L)) + sum(A)
 
 
+def pmc_valu_table(root):
+    """Per-kernel VALU issue from the latest committed PMC summary (profiles/r*/pmc_summary.txt,
+    written by tools/refresh_profiles.sh from separate rocprofv3 --pmc passes of the same
+    whole-batch launches): instructions per launch and the fraction of SIMD cycles the VALU was
+    issuing, SQ_ACTIVE_INST_VALU quad-cycles x 4 / (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs).
+    Keys are the bench's stage names (k_fast_cells<48>, k_knn2, k_octree, ...)."""
+    import re
+    paths = sorted(glob.glob(os.path.join(root, "profiles", "r*", "pmc_summary.txt")))
+    if not paths:
+        return {}, None
+    out = {}
+    try:
+        txt = open(paths[-1]).read()
+    except OSError:
+        return {}, None
+    for block in re.split(r"\n(?=\S)", txt):
+        lines = block.strip().split("\n")
+        name = lines[0].replace("void ", "").replace("orbgpu::", "").strip()
+        c = {}
+        for ln in lines[1:]:
+            m = re.match(r"\s+(\w+)\s+([-\d.e+]+)$", ln)
+            if m:
+                c[m.group(1)] = float(m.group(2))
+        if "SQ_ACTIVE_INST_VALU" not in c or not c.get("GRBM_GUI_ACTIVE"):
+            continue
+        stage = name
+        for pre, st in (("k_knn2", "k_knn2"), ("k_octree", "k_octree"), ("k_finalize", "k_finalize")):
+            if name.startswith(pre):
+                stage = st
+        cyc = c["GRBM_GUI_ACTIVE"] / 8.0
+        out[stage] = {"valu_busy": round(c["SQ_ACTIVE_INST_VALU"] * 4.0 / 1024.0 / cyc, 3),
+                      "valu_instr_per_launch": c.get("SQ_INSTS_VALU")}
+    return out, os.path.relpath(paths[-1], root)
+
+
 def spawn_ranks(n):
     """`bench.py --gpus N` with no launcher: start N ranks of this script (rank r on GPU r,
     RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT in each child's environment, the
@@ -523,6 +558,23 @@ def main():
                    "includes": "pyramid + blur (fused) + FAST; bytes = B_fp + 2 sum(A_l)",
                    "us_per_step": round(fp_ms * 1e3, 1)}
 
+    # the bound that applies to the dominant kernel: VALU issue.  The busy
+    # fraction comes from the committed PMC passes; the instruction rate uses this run's time
+    roof_valu = None
+    try:
+        vt, vsrc = pmc_valu_table(ROOT)
+    except Exception:
+        vt, vsrc = {}, None
+    if dom is not None and dom in vt:
+        v = vt[dom]
+        roof_valu = {"kernel": dom, "bound": "valu", "busy": v["valu_busy"],
+                     "valu_instr_per_launch": v["valu_instr_per_launch"],
+                     "achieved_wave_instr_per_us": (round(v["valu_instr_per_launch"] / stage_rows[dom]["avg_us"], 1)
+                                                    if v["valu_instr_per_launch"] else None),
+                     "source": vsrc, "busy_by_kernel": {k: x["valu_busy"] for k, x in sorted(vt.items())},
+                     "definition": "SQ_ACTIVE_INST_VALU x 4 / (1024 SIMDs x GRBM_GUI_ACTIVE / 8), "
+                                   "whole-batch launches, kernel alone"}
+
     # the matcher's own roofline (north_star: "Hamming BFMatch"): it runs on the int8 matrix cores
     kr = stage_rows.get("k_knn2")
     roof_knn = None
@@ -933,6 +985,7 @@ def main():
             "roofline": roof,
             "roofline_fast_pyramid": roof_fp,
             "roofline_knn2": roof_knn,
+            "roofline_valu": roof_valu,
             "stages": stage_rows,
             "cpu_baseline": cpu,
             "stereo_matches": stereo,
