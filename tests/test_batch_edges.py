@@ -93,9 +93,10 @@ def test_batch_knn2_past_4096_train_rows(oracle):
 
 def test_split_knn2_one_pair_past_4096_rows(oracle, monkeypatch):
     """A one-pair batch (the C4 shape) matches with the train rows split over 8 workgroups per
-    query block plus k_knn2_merge (orb_kernels.hip launch_knn2_pairs); at 1920x1080 with 8200
-    features the splits straddle the 4096-row key segments.  Equal to the oracle, and to the
-    unsplit launch (ORBGPU_KNN_NOSPLIT)."""
+    query block, the last of which merges the partial lists (orb_kernels.hip k_knn2_mfma_pairs'
+    counter hand-off); at 1920x1080 with 8200 features the splits straddle the 4096-row key
+    segments.  Equal to the oracle on three launches in a row (the arrival counters reset
+    themselves), and to the unsplit launch (ORBGPU_KNN_NOSPLIT)."""
     import orbslam3lib_amd as og
     imgs = np.stack(synth.stereo_pair(1080, 1920, 61))
     be = _batch(og, 1920, 1080, 12, 8200, imgs)
@@ -107,11 +108,39 @@ def test_split_knn2_one_pair_past_4096_rows(oracle, monkeypatch):
     assert len(dr) > 4096 and len(dl) > 4096, (len(dl), len(dr))
     split = be.matches(0)
     _same_knn(split, oracle.knn2(dl, dr), "split")
+    for rep in range(2):
+        be.match_stereo(False)
+        be.synchronize()
+        _same_knn(be.matches(0), split, "split, launch %d" % (rep + 2))
     monkeypatch.setenv("ORBGPU_DIAGNOSTICS", "1")
     monkeypatch.setenv("ORBGPU_KNN_NOSPLIT", "1")
     be.match_stereo(False)
     be.synchronize()
     _same_knn(be.matches(0), split, "unsplit vs split")
+
+
+def test_small_batch_on_large_context(oracle):
+    """A context sized for the bench batch (512 images) running 2 pairs: the chunk count follows
+    the batch (orb_runtime.cpp kChunksFor), the one-pair split matcher and the 1024-thread
+    finalize take the small launches; keypoints, descriptors and matches equal the oracle."""
+    import orbslam3lib_amd as og
+    pairs = [synth.stereo_pair(480, 640, 70 + i) for i in range(2)]
+    imgs = np.stack([pairs[i // 2][i % 2] for i in range(4)])
+    be = og.BatchExtractor(2000, 1.2, 8, 20, 7, width=640, height=480, max_images=512)
+    be.upload(imgs)
+    for n in (4, 2):  # two pairs, then one pair on the same large context
+        be.n = n  # the first n uploaded images (orbgpu_run_batch reads images [0, n))
+        be.run()
+        be.match_stereo(False)
+        be.synchronize()
+        res = [be.result(i) for i in range(n)]
+        for i in range(n):
+            rk, rd, rm = oracle.extract(imgs[i], nfeatures=2000)
+            assert res[i][2] == rm
+            _same_kps(res[i][0], rk)
+            np.testing.assert_array_equal(res[i][1], rd)
+        for p in range(n // 2):
+            _same_knn(be.matches(p), oracle.knn2(res[2 * p][1], res[2 * p + 1][1]), "n %d pair %d" % (n, p))
 
 
 def test_c5_batch_16_pairs(oracle):
