@@ -66,8 +66,10 @@ typedef struct orbgpu_ctx orbgpu_ctx;
 /* Build a context for images up to max_width x max_height and batches of up to max_images
  * images.  Allocates all device memory once (nothing is allocated per call).  device = HIP
  * ordinal.  Replaces the ORBextractor ctor + LynxHardwareAccelerator ctor (orbslam3_open).
- * ORBGPU_ERR_INVALID for nlevels outside [1, 16], scale_factor not in (1, 2], negative
- * nfeatures or sizes outside (0, 4112); ORBGPU_ERR_NO_DEVICE without a HIP device. */
+ * ORBGPU_ERR_INVALID for nlevels outside [1, 16], scale_factor not above 1 (any value above 1,
+ * as ORBextractor; steps above 2 build the pyramid level by level from HBM), negative nfeatures
+ * or sizes outside (0, 4112), or a pyramid level under 42 px (at the first batch of that size);
+ * ORBGPU_ERR_NO_DEVICE without a HIP device. */
 int orbgpu_create(const orbgpu_params* params, int device, int max_width, int max_height,
                   int max_images, orbgpu_ctx** out_ctx);
 int orbgpu_destroy(orbgpu_ctx* ctx); /* orbslam3_close */

@@ -248,6 +248,7 @@ constexpr int kBrMaxRows = kBlurTH + 2;
 // blur, which launch_blur_level does).
 hipError_t launch_blur_resize(const BatchArgs& a, int level, hipStream_t s);
 hipError_t launch_blur_level(const BatchArgs& a, int level, hipStream_t s);
+hipError_t launch_level_linear(const BatchArgs& a, int level, hipStream_t s);  // scale steps > 2
 constexpr int kTailPad = 16;          // k_pyr_tail: left pad of an LDS row (>= 3 reflected columns)
 constexpr int kTailLdsMax = 160 * 1024;  // the LDS one workgroup may hold on gfx950
 constexpr int kTailMinImages = 128;     // k_pyr_tail only for launches of >= this many images

@@ -638,6 +638,52 @@ __global__ __launch_bounds__(256) void k_blur_resize(BatchArgs a, int l, uint32_
 }
 
 
+// k_level_linear: level l from level l - 1 in HBM for any scale step (ComputePyramid's cv::resize
+// INTER_LINEAR, ORBextractor_old.cc:1342-1344; the generic 2-tap path of OpenCV 4.2's resize, as
+// oracle/orb_oracle.cpp resize_linear restates it).  k_blur_resize stages one blur tile of level
+// l - 1 and makes the outputs whose taps it holds, which needs scale steps <= 2 (rs_quad reads the
+// 8 source bytes from a quad's first tap); scale factors above 2 (accepted by ORBextractor, not
+// used by ORB-SLAM3's configurations) take this kernel and then k_blur per level.  Thread = one
+// output quad of one row; every tap is a byte load from the previous level.
+__global__ __launch_bounds__(256) void k_level_linear(BatchArgs a, int l) {
+    const LevelGeom G = a.lv[l], S = a.lv[l - 1];
+    const int nq = (G.w + 3) >> 2;
+    const int item = blockIdx.x * 256 + threadIdx.x;
+    if (item >= nq * G.h) return;
+    const int img = a.img0 + blockIdx.y;
+    const int dy = item / nq, q = item - dy * nq;
+    const uint8_t* src = a.lvl_base[l - 1] + (long long)img * S.img_stride;
+    uint8_t* dst = a.lvl_base[l] + (long long)img * G.img_stride;
+    const int4 yt = a.rtab[G.ytab_off + dy];  // (sy0, sy1, b0, b1), rows clamped
+    const uint8_t* r0 = src + plane_off(yt.x, S.pitch, 0);
+    const uint8_t* r1 = src + plane_off(yt.y, S.pitch, 0);
+    uint32_t packed = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int dx = min(4 * q + k, G.w - 1);
+        const int4 xt = a.rtab[G.xtab_off + dx];  // (sx0, sx1, a0, a1), a1 = 0 past the last pair
+        const int d0 = r0[xt.x] * xt.z + r0[xt.y] * xt.w;
+        const int d1 = r1[xt.x] * xt.z + r1[xt.y] * xt.w;
+        int o;
+        if (dx < G.simd_end) {  // VResizeLinearVec_32s8u: v_mul_hi of the packed (D >> 4), v_rshr_pack_u<2>
+            const int t0 = min(d0 >> 4, 32767), t1 = min(d1 >> 4, 32767);
+            const int sum = min(max(((t0 * yt.z) >> 16) + ((t1 * yt.w) >> 16), -32768), 32767);
+            o = (sum + 2) >> 2;
+        } else {  // FixedPtCast<int, uchar, 22>
+            o = (d0 * yt.z + d1 * yt.w + (1 << 21)) >> 22;
+        }
+        packed |= (uint32_t)min(max(o, 0), 255) << (8 * k);
+    }
+    *reinterpret_cast<uint32_t*>(dst + plane_off(dy, G.pitch, 4 * q)) = packed;
+}
+
+hipError_t launch_level_linear(const BatchArgs& a, int l, hipStream_t s) {
+    const LevelGeom G = a.lv[l];
+    const int items = ((G.w + 3) >> 2) * G.h;
+    hipLaunchKernelGGL(k_level_linear, dim3((items + 255) / 256, a.nimages), dim3(256), 0, s, a, l);
+    return hipGetLastError();
+}
+
 hipError_t launch_blur_resize(const BatchArgs& a, int l, hipStream_t s) {
     const LevelGeom S = a.lv[l - 1];
     auto magic = [](uint32_t d) { return d > 1 ? 0xFFFFFFFFu / d + 1u : 0u; };  // exact for n < 2^32 / d

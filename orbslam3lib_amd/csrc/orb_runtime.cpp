@@ -201,6 +201,9 @@ struct orbgpu_ctx {
     unsigned isolate_mask = 0;
     bool serialize = false;  // profiling: every stage isolated
     bool oct_stamps = false; // ORBGPU_OCT_STAMPS (read once at create): octree phase clocks
+    // scale factors above 2: k_blur_resize's staged window does not hold a resize step's taps, so
+    // the pyramid is k_level_linear per level, then k_blur per level (no k_pyr_tail)
+    bool generic_pyr = false;
     // the captured launch sequences of one-stream batches (run_batch / run_batch_match), keyed by
     // {images, width, height, input slot, match pairs, stereo rows only}: one exec per key, so
     // alternating input slots (async uploads) or match variants replay instead of recapturing
@@ -463,7 +466,8 @@ int set_geometry(orbgpu_ctx* c, int w, int h) {
     // passed the 2 * kEdge + 4 check above.
     for (int l = 0; l < L; ++l) A.lv[l].tpitch = round_up(A.lv[l].w + 28, 16);
     A.tail0 = L + 1;
-    if (!diag_env("ORBGPU_NO_TAIL"))
+    c->generic_pyr = c->prm.scale_factor > 2.0f;
+    if (!diag_env("ORBGPU_NO_TAIL") && !c->generic_pyr)
         for (int t = 2; t <= L; ++t) {
             const LevelGeom& S0 = A.lv[t - 1];
             const long long b0 = round_up_ll((long long)S0.tpitch * S0.h, 16);
@@ -785,10 +789,6 @@ int orbgpu_create(const orbgpu_params* p, int device, int max_width, int max_hei
         max_width <= 0 || max_height <= 0 || max_images <= 0 || max_width >= 4096 + 16 ||
         max_height >= 4096 + 16)
         return fail(ORBGPU_ERR_INVALID, "invalid ORB parameters or sizes");
-    // k_blur_resize makes level l from the window of level l - 1 its tile has staged; the taps
-    // of a resize step stay inside that window only for scale steps up to 2
-    if (p->scale_factor > 2.0f)
-        return fail(ORBGPU_ERR_INVALID, "scale_factor above 2 is not supported");
     if (int e = check_single_hip_runtime()) return e;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
@@ -1107,7 +1107,16 @@ static int run_batch_impl(orbgpu_ctx* c, int n, int w, int h, const int32_t* lap
         if (c->serialize || chunks.size() == 1) chunk_images = n;
         const bool tail = A.tail0 <= A.nlevels && chunk_images >= A.tail_min;
         const int last_br = tail ? A.tail0 : A.nlevels;
-        if (stagger) {
+        if (c->generic_pyr) {  // scale steps above 2: every level from HBM, then every blur
+            for (int l = 1; l < A.nlevels; ++l) {
+                r = each(ST_RESIZE, [&](const BatchArgs& B, hipStream_t st) { return launch_level_linear(B, l, st); });
+                if (r) return r;
+            }
+            for (int l = 0; l < A.nlevels; ++l) {
+                r = each(ST_BLUR, [&](const BatchArgs& B, hipStream_t st) { return launch_blur_level(B, l, st); });
+                if (r) return r;
+            }
+        } else if (stagger) {
             // chunk-major: chunk k's first kernel waits for chunk k-1's pyramid + blur
             for (size_t k = 0; k < chunks.size(); ++k) {
                 const Chunk& ch = chunks[k];

@@ -29,7 +29,7 @@ def test_library_has_gfx950_code_object():
     data = open(os.path.join(ROOT, "orbslam3lib_amd", "liborbgpu.so"), "rb").read()
     assert b"gfx950" in data
     for k in (b"k_fast_cells", b"k_octree", b"k_orient_desc", b"k_knn2_mfma_pairs", b"k_blur_resize", b"k_blur",
-              b"k_pyr_tail"):
+              b"k_pyr_tail", b"k_level_linear"):
         assert k in data, k
     # the measured-slower alternates of rounds 1-4 are not in the product library
     for k in (b"k_fast_wave", b"k_pyramid", b"k_knn2_pairs", b"k_resize", b"k_fast_bands", b"k_fast_sb"):
@@ -52,11 +52,11 @@ def test_host_entry_points():
     assert lib.orbgpu_destroy(None) == 0
 
 
-@pytest.mark.parametrize("scale", [1.0, 2.5])
+@pytest.mark.parametrize("scale", [1.0, 0.8])
 def test_create_rejects_unsupported_scale_factor(scale):
-    """orbgpu_create validates the parameters before it looks for a device: a scale step of 1 or
-    above 2 (k_blur_resize makes level l from the staged window of level l - 1, which holds the
-    taps only for steps up to 2) is ORBGPU_ERR_INVALID, with or without a GPU."""
+    """orbgpu_create validates the parameters before it looks for a device: a scale factor that
+    is not above 1 (ORBextractor's only requirement) is ORBGPU_ERR_INVALID, with or without a
+    GPU.  Steps above 2 are accepted since round 5 (k_level_linear)."""
     import orbslam3lib_amd as og
     with pytest.raises(og.OrbGpuError) as e:
         og.ORBextractor(1000, scale, 8, 20, 7, max_width=640, max_height=480)

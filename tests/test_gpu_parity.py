@@ -178,6 +178,36 @@ def test_c5_1080p_12_levels(oracle):
     np.testing.assert_array_equal(g[1], r[1])
 
 
+@pytest.mark.parametrize("sf,L", [(2.5, 4), (3.0, 3)])
+def test_scale_factor_above_2(oracle, sf, L):
+    """Scale factors above 2 (ORBextractor accepts any value above 1; ORB-SLAM3's settings use
+    1.2): the pyramid takes k_level_linear per level from HBM and k_blur per level, since
+    k_blur_resize's staged window holds a resize step's taps only up to 2.  1920x1080, the
+    levels kept above the 42-px minimum: pyramid, blur, keypoints and descriptors equal the
+    oracle, through the single-image and the batch entry points."""
+    import orbslam3lib_amd as og
+    img = synth.frame(1080, 1920, 9)
+    ex = _extractor(nf=3000, L=L, w=1920, h=1080, sf=sf)
+    g = ex(img, None, (0, 0))
+    r = oracle.extract(img, nfeatures=3000, scale_factor=sf, nlevels=L, lap=(0, 0))
+    assert g[2] == r[2]
+    _same_kps(g[0], r[0])
+    np.testing.assert_array_equal(g[1], r[1])
+    ref = oracle.pyramid(img, scale_factor=sf, nlevels=L)
+    for l in range(L):
+        np.testing.assert_array_equal(ex.pyramid_level(0, l), ref[l], err_msg="level %d" % l)
+        np.testing.assert_array_equal(ex.pyramid_level(0, l, blurred=True), oracle.blur(ref[l]),
+                                      err_msg="blur level %d" % l)
+    be = og.BatchExtractor(3000, sf, L, 20, 7, width=1920, height=1080, max_images=2)
+    be.upload(np.stack([img, img[::-1].copy()]))
+    be.run()
+    be.synchronize()
+    k, d, m = be.result(0)
+    assert m == r[2]
+    _same_kps(k, r[0])
+    np.testing.assert_array_equal(d, r[1])
+
+
 def test_flat_and_empty_images(oracle):
     ex = _extractor()
     flat = np.full((480, 640), 128, np.uint8)
