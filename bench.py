@@ -837,11 +837,17 @@ def main():
         try:
             from orbslam3lib_amd.dist import cross_camera_match, cross_camera_match_device
             C5W, C5H, C5L, C5N = 1920, 1080, 12, 5000
-            c5 = og.BatchExtractor(C5N, 1.2, C5L, 20, 7, device=local, width=C5W, height=C5H, max_images=2)
-            c5.upload(np.stack(synth.stereo_pair(C5H, C5W, 500 + base)))  # this rank's camera = image 0
-            c5.run()
-            c5.synchronize()
-            kl0, dl0, _ = c5.result(0)
+            c5, setup_err = None, None
+            try:  # local setup first; every rank agrees on it before any collective of the leg
+                c5 = og.BatchExtractor(C5N, 1.2, C5L, 20, 7, device=local, width=C5W, height=C5H, max_images=2)
+                c5.upload(np.stack(synth.stereo_pair(C5H, C5W, 500 + base)))  # this rank's camera = image 0
+                c5.run()
+                c5.synchronize()
+                kl0, dl0, _ = c5.result(0)
+            except Exception as e:
+                setup_err = e
+            if -max_over_ranks(dist, -(0.0 if setup_err else 1.0)) < 1.0:
+                raise RuntimeError("cross-camera setup failed on a rank: %r" % (setup_err,))
             device_path = has_cuda
             res = None
             for _ in range(2):  # the first exchange sets up the communicator and buffers
@@ -887,10 +893,16 @@ def main():
     if world > 1:
         try:
             from orbslam3lib_amd.dist import ingest_scatter_gather
-            ib = og.BatchExtractor(args.nfeatures, 1.2, args.nlevels, 20, 7, device=local, width=W, height=H,
-                                   max_images=2)
-            frames = (np.stack([x for r_ in range(world) for x in synth.stereo_pair(H, W, 700 + r_)])
-                      if rank == 0 else None)
+            ib, frames, setup_err = None, None, None
+            try:  # local setup first; every rank agrees on it before any collective of the leg
+                ib = og.BatchExtractor(args.nfeatures, 1.2, args.nlevels, 20, 7, device=local, width=W, height=H,
+                                       max_images=2)
+                frames = (np.stack([x for r_ in range(world) for x in synth.stereo_pair(H, W, 700 + r_)])
+                          if rank == 0 else None)
+            except Exception as e:
+                setup_err = e
+            if -max_over_ranks(dist, -(0.0 if setup_err else 1.0)) < 1.0:
+                raise RuntimeError("ingest setup failed on a rank: %r" % (setup_err,))
             got = None
             for _ in range(4):  # the first exchanges set up the communicators and buffers
                 barrier(dist)
