@@ -27,6 +27,9 @@
 #ifndef FAST_2X1
 #define FAST_2X1 0  // strength phase: two single-side candidates per lane (0: one two-sided)
 #endif
+#ifndef FAST_DPP_SCAN
+#define FAST_DPP_SCAN 1  // candidate list positions by a DPP wave scan (0: bit-sliced ballots)
+#endif
 #ifndef FAST_THREADS
 // k_fast_cells workgroup: one wave per cell.  Round 5 (single stream, 512 images, k_fast_cells<48>):
 // 2 waves per cell 678-684 us, 1 wave 648-664 us, 1 wave with the fixed-size policy 652-654 us
@@ -408,10 +411,12 @@ __host__ __device__ int fast_cell_detect(Pol& p, int sh, const CellGeom& g, int 
             constexpr int RW = CP / 4;
             const uint32_t* T32 = reinterpret_cast<const uint32_t*>(T);
             const uint32_t tt = (uint32_t)t * 0x00010001u, kt = (uint32_t)(255 - t) * 0x00010001u;
+#if !FAST_DPP_SCAN
             auto rank = [](uint64_t b) {  // set lanes of b below this lane
                 return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32),
                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
             };
+#endif
             // this lane's item (row r, dword group q) as (q, LDS dword dw), advanced by L items
             // per iteration without a division: L = dr rows + dq groups (plus one row on wrap)
             int q = 0, dw = 0, dq = 0, ddw = 0;
@@ -435,17 +440,34 @@ __host__ __device__ int fast_cell_detect(Pol& p, int sh, const CellGeom& g, int 
                     if (FAST_2X1)  // the passing sides into the strength plane (0x80 bright, 0x40 dark)
                         reinterpret_cast<uint32_t*>(M)[dw] = (sd.y & m8) | ((sd.x & m8) >> 1);
                 }
-                // the 4-bit pass mask (bit k = byte k) by one v_dot4_u32_u8 of the 0x80 bytes
-                const uint32_t m4 = __builtin_amdgcn_udot4(m8, 0x08040201u, 0u, false) >> 7;
+                // the 4-bit pass mask (bit k = byte k) by one v_dot4_u32_u8 of the 0x80 bytes:
+                // 128 m4, so m4's 8-byte LUT entry sits at byte offset 128 m4 >> 4 (one shift)
+                const uint32_t m4x128 = __builtin_amdgcn_udot4(m8, 0x08040201u, 0u, false);
                 const int c = __builtin_popcount(m8);
+#if FAST_DPP_SCAN
+                // this lane's list position: an inclusive scan of c over the wave by DPP (rows of
+                // 16 by row_shr 1 / 2 / 4 / 8, then row_bcast 15 / 31 across rows; 6 v_add_u32_dpp),
+                // instead of bit-sliced ballots + 6 v_mbcnt (16 VALU)
+                int incl = c;
+                incl += __builtin_amdgcn_update_dpp(0, incl, 0x111, 0xF, 0xF, true);  // row_shr:1
+                incl += __builtin_amdgcn_update_dpp(0, incl, 0x112, 0xF, 0xF, true);  // row_shr:2
+                incl += __builtin_amdgcn_update_dpp(0, incl, 0x114, 0xF, 0xF, true);  // row_shr:4
+                incl += __builtin_amdgcn_update_dpp(0, incl, 0x118, 0xF, 0xF, true);  // row_shr:8
+                incl += __builtin_amdgcn_update_dpp(0, incl, 0x142, 0xA, 0xF, false); // row_bcast:15 -> rows 1, 3
+                incl += __builtin_amdgcn_update_dpp(0, incl, 0x143, 0xC, 0xF, false); // row_bcast:31 -> rows 2, 3
+                const int pos = na + incl - c;
+                const int wave_total = __builtin_amdgcn_readlane(incl, 63);
+#else
                 const uint64_t b0 = p.ballot(c & 1), b1 = p.ballot(c & 2), b2 = p.ballot(c & 4);
                 const int pos = na + rank(b0) + 2 * rank(b1) + 4 * rank(b2);
+                const int wave_total = p.popc64(b0) + 2 * p.popc64(b1) + 4 * p.popc64(b2);
+#endif
                 // the lane's c entries 4 dw + (set bit positions), as u16 pairs from the table,
                 // written to 4 consecutive slots from pos; slots past c hold garbage that a later
                 // lane's entry overwrites (its slot index k is smaller, and the slots are written
                 // in the order k = 3, 2, 1, 0) or that lands in the wave's spare entries; lanes
                 // without candidates write the sink
-                const uint2 lv = cs.lut[m4];
+                const uint2 lv = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint8_t*>(cs.lut) + (m4x128 >> 4));
                 const uint32_t e01 = __umul24((uint32_t)(4 * dw), 0x10001u) + lv.x;  // v_mad_u32_u24
                 const uint32_t e23 = __umul24((uint32_t)(4 * dw), 0x10001u) + lv.y;
 #if FAST_SINK == 1  // measurement variant: lanes without candidates write nothing
@@ -479,7 +501,7 @@ __host__ __device__ int fast_cell_detect(Pol& p, int sh, const CellGeom& g, int 
                 asm volatile("" ::: "memory");
                 d[0] = (uint16_t)e01;
 #endif
-                na += p.popc64(b0) + 2 * p.popc64(b1) + 4 * p.popc64(b2);
+                na += wave_total;
                 q += dq;
                 dw += ddw;
                 if (q >= ng) {
