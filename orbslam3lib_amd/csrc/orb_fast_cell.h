@@ -267,7 +267,6 @@ __host__ __device__ int fast_cell_detect(Pol& p, int sh, const CellGeom& g, int 
     const int tini = ini_th < 0 ? 0 : (ini_th > 255 ? 255 : ini_th);
     const int tmin = min_th < 0 ? 0 : (min_th > 255 ? 255 : min_th);
     const int W = p.nwaves(), w = p.wave(), L = p.wave_width(), lane = p.lane();
-    const uint64_t lt = p.lanemask_lt();
 #if defined(__HIP_DEVICE_COMPILE__) && FAST_PRETEST8
     // device: the pre-test takes the 8 pixels of one 8-byte LDS pair per lane (two fw_pretest4);
     // a wave owns a contiguous range of detection rows, and its list starts after the detection
@@ -529,7 +528,7 @@ __host__ __device__ int fast_cell_detect(Pol& p, int sh, const CellGeom& g, int 
             const int bk = imin(imin(imax(p0, p8), imax(p4, p12)), imin(imax(p2, p10), imax(p6, p14)));
             const bool cand = in & ((dk < lo) | (bk > hi));
             const uint64_t m = p.ballot(cand);
-            if (cand) list[na + p.popc64(m & lt)] = (uint16_t)o;
+            if (cand) list[na + p.rank(m)] = (uint16_t)o;
             na += p.popc64(m);
         }
 #endif
@@ -574,8 +573,8 @@ __host__ __device__ int fast_cell_detect(Pol& p, int sh, const CellGeom& g, int 
             // the strength plane: m for corners, 0 for the other candidates (flags cleared)
             if (ja < na) M[oa] = (uint8_t)(ca ? sa : 0);
             if (jb < na) M[ob] = (uint8_t)(cb ? sb : 0);
-            if (ca) list[nb + p.popc64(ba & lt)] = (uint16_t)oa;  // in place: never passes the reads
-            if (cb) list[nb + p.popc64(ba) + p.popc64(bb & lt)] = (uint16_t)ob;
+            if (ca) list[nb + p.rank(ba)] = (uint16_t)oa;  // in place: never passes the reads
+            if (cb) list[nb + p.popc64(ba) + p.rank(bb)] = (uint16_t)ob;
             nb += p.popc64(ba) + p.popc64(bb);
         }
         return nb;
@@ -595,9 +594,9 @@ __host__ __device__ int fast_cell_detect(Pol& p, int sh, const CellGeom& g, int 
             const int sm = fast_strength_packed<CP>(&T[o]);
 #endif
             const bool f = j < na && sm > t;
-            const uint64_t m = p.ballot(f);
+            const uint64_t m = p.ballot(j < na) & p.ballot(sm > t);  // two compares' masks, ANDed on the SALU
             if (f) {
-                list[nb + p.popc64(m & lt)] = (uint16_t)o;  // in place: never passes the reads
+                list[nb + p.rank(m)] = (uint16_t)o;  // in place: never passes the reads
                 M[o] = (uint8_t)sm;
             }
             nb += p.popc64(m);
@@ -652,7 +651,7 @@ __host__ __device__ int fast_cell_detect(Pol& p, int sh, const CellGeom& g, int 
             const int o = e & 0x1FFF;
             const int r = o / CP, c = o % CP - sh;
             const int resp = M[o] - 1;  // cornerScore<16> = m - 1
-            keys_out[cb.y + run + p.popc64(m & lt)] =
+            keys_out[cb.y + run + p.rank(m)] =
                 make_key(g.iniX + c - g.minBorder, g.iniY + r - g.minBorder, resp);
         }
         run += p.popc64(m);

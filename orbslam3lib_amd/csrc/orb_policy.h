@@ -116,6 +116,11 @@ struct DevPolicy {
     __device__ int wave_width() const { return 64; }
     __device__ uint64_t ballot(bool f) const { return __ballot(f); }
     __device__ uint64_t lanemask_lt() const { return (1ull << (threadIdx.x & 63)) - 1ull; }
+    // set bits of m below this lane: v_mbcnt_lo + v_mbcnt_hi (popc(m & lanemask_lt) costs 2 ANDs
+    // and 2 v_bcnt)
+    __device__ int rank(uint64_t m) const {
+        return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    }
     // OR of x over the 64 lanes of the calling wave (all lanes must participate)
     __device__ uint64_t wave_or(uint64_t x) const {
 #pragma unroll
@@ -278,6 +283,7 @@ struct SerialPolicy {
     __host__ __device__ int wave_width() const { return 1; }
     __host__ __device__ uint64_t ballot(bool f) const { return f ? 1ull : 0ull; }
     __host__ __device__ uint64_t lanemask_lt() const { return 0ull; }
+    __host__ __device__ int rank(uint64_t) const { return 0; }
 };
 
 }  // namespace orbgpu

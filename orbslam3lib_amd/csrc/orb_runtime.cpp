@@ -110,11 +110,21 @@ const char* kStageNames[ST_COUNT] = {"k_blur_resize",    "k_blur",   "k_fast_cel
                                      "k_sbs_split",      "k_pack_soa",       "k_sbp",
                                      "k_fisheye_stereo", "k_pyr_tail"};
 
+// hipMalloc / hipFree on one thread while another thread captures a stream into a graph fails
+// the allocation and invalidates the capture on this HIP (measured: two contexts run from two
+// threads, test_two_threads_two_contexts_concurrently), whatever the capture mode.  Device
+// allocations and graph captures of every context therefore take this one process-wide lock.
+std::recursive_mutex& alloc_capture_mutex() {
+    static std::recursive_mutex mu;  // recursive: context creation holds it around its allocations
+    return mu;
+}
+
 struct DevBuf {
     void* p = nullptr;
     size_t bytes = 0;
     int ensure(size_t n) {
         if (n <= bytes) return 0;
+        std::lock_guard<std::recursive_mutex> lk(alloc_capture_mutex());
         if (p) hipFree(p);
         p = nullptr;
         bytes = 0;
@@ -123,6 +133,7 @@ struct DevBuf {
         return 0;
     }
     void release() {
+        std::lock_guard<std::recursive_mutex> lk(alloc_capture_mutex());
         if (p) hipFree(p);
         p = nullptr;
         bytes = 0;
@@ -790,6 +801,9 @@ int orbgpu_create(const orbgpu_params* p, int device, int max_width, int max_hei
         max_height >= 4096 + 16)
         return fail(ORBGPU_ERR_INVALID, "invalid ORB parameters or sizes");
     if (int e = check_single_hip_runtime()) return e;
+    // streams, events and buffers are created under the allocation / capture lock (another
+    // thread's context may be capturing a graph)
+    std::lock_guard<std::recursive_mutex> create_lk(alloc_capture_mutex());
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
         return fail(ORBGPU_ERR_NO_DEVICE, "no HIP device");
@@ -866,8 +880,9 @@ int orbgpu_destroy(orbgpu_ctx* c) {
     hipSetDevice(c->device);
     if (c->stream) hipStreamSynchronize(c->stream);
     resolve_pending(c);
-    for (auto e : c->event_pool) hipEventDestroy(e);
     if (c->copy) hipStreamSynchronize(c->copy);
+    std::lock_guard<std::recursive_mutex> destroy_lk(alloc_capture_mutex());  // frees and destroys
+    for (auto e : c->event_pool) hipEventDestroy(e);
     DevBuf* bufs[] = {&c->input, &c->input2, &c->pyr,     &c->blur,   &c->rtab,    &c->cellkeys, &c->cellcnt,
                       &c->octws,   &c->lvlkey,  &c->lvlangle, &c->lvldesc, &c->lvlcnt, &c->status,
                       &c->outkps,  &c->outdesc, &c->outn,   &c->outmono, &c->laps,     &c->midx1,
@@ -953,11 +968,13 @@ int orbgpu_upload_images_async(orbgpu_ctx* c, const uint8_t* images, int n, int 
 int orbgpu_host_alloc(size_t bytes, void** ptr) {
     if (!ptr) return fail(ORBGPU_ERR_INVALID, "null argument");
     *ptr = nullptr;
+    std::lock_guard<std::recursive_mutex> lk(alloc_capture_mutex());
     HIP_TRY(hipHostMalloc(ptr, bytes ? bytes : 1, hipHostMallocDefault));
     return ORBGPU_OK;
 }
 
 int orbgpu_host_free(void* ptr) {
+    std::lock_guard<std::recursive_mutex> lk(alloc_capture_mutex());
     if (ptr) HIP_TRY(hipHostFree(ptr));
     return ORBGPU_OK;
 }
@@ -1213,18 +1230,22 @@ static int run_batch_impl(orbgpu_ctx* c, int n, int w, int h, const int32_t* lap
                 hipGraphExecDestroy(c->graphs[lru].exec);
                 c->graphs.erase(c->graphs.begin() + lru);
             }
-            HIP_TRY(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
-            int rr = launch_all();
-            if (!rr && with_match) rr = launch_match();
-            hipGraph_t g = nullptr;
-            const hipError_t ec = hipStreamEndCapture(s, &g);
-            if (rr || ec != hipSuccess) {
-                if (g) hipGraphDestroy(g);
-                return rr ? rr : fail(ORBGPU_ERR_HIP, std::string("hipStreamEndCapture: ") + hipGetErrorString(ec));
-            }
             hipGraphExec_t ex = nullptr;
-            const hipError_t ei = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
-            hipGraphDestroy(g);
+            hipError_t ei = hipSuccess;
+            {
+                std::lock_guard<std::recursive_mutex> lk(alloc_capture_mutex());  // no allocation mid-capture
+                HIP_TRY(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+                int rr = launch_all();
+                if (!rr && with_match) rr = launch_match();
+                hipGraph_t g = nullptr;
+                const hipError_t ec = hipStreamEndCapture(s, &g);
+                if (rr || ec != hipSuccess) {
+                    if (g) hipGraphDestroy(g);
+                    return rr ? rr : fail(ORBGPU_ERR_HIP, std::string("hipStreamEndCapture: ") + hipGetErrorString(ec));
+                }
+                ei = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
+                hipGraphDestroy(g);
+            }
             if (ei != hipSuccess)
                 return fail(ORBGPU_ERR_HIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(ei));
             orbgpu_ctx::GraphRec nr{};
