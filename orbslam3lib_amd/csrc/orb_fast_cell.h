@@ -46,6 +46,16 @@ namespace orbgpu {
 constexpr int kCellMax = 80;  // wCell, hCell < 70 (nCols = floor(W/35)) plus the 6-px overlap
 constexpr int kCellPitchSmall = 64;  // 640x480-class pyramids: every level's cells <= 55 x 58
 constexpr int kCellPitchTiny = 48;   // the leading levels of 640x480-class pyramids (cells <= 39 x 42)
+#ifndef FAST_THREADS_64
+// k_fast_cells<64>: two waves per cell.  Its cells are the largest of 640x480-class pyramids
+// (up to 55 x 58) and its launch is short, so one wave per cell left it latency-bound (0.54
+// VALU busy).  Round 5, single stream, 512 images: 1 wave 107.3 us, 2 waves 94.1, 4 waves 99.3;
+// headline +0.9% (bench A/B, 3 rounds).
+#define FAST_THREADS_64 128
+#endif
+// k_fast_cells<CP> workgroup size
+template <int CP>
+__host__ __device__ constexpr int fast_threads() { return CP == kCellPitchSmall ? FAST_THREADS_64 : FAST_THREADS; }
 // candidate list capacity for pitch P: the detection area, (P-6)^2 for the 64-byte tile, 69^2
 // for the general one (wCell, hCell <= 69: nCols = floor(W/35) >= 1)
 template <int P>
@@ -202,8 +212,8 @@ __host__ __device__ void fast_cell_stage(Pol& p, const uint8_t* src, long long p
         uint4* M128 = reinterpret_cast<uint4*>(M);
         // the first kIt chunks per thread are all loaded before any is stored, so their round
         // trips overlap (a rolled load -> wait -> store loop pays one round trip per chunk);
-        // kIt covers every chunk at FAST_THREADS threads (the device's workgroup), the loop after it the rest
-        constexpr int kIt = (CP * RQ + FAST_THREADS - 1) / FAST_THREADS;
+        // kIt covers every chunk at fast_threads<CP>() threads (the device's workgroup), the loop after it the rest
+        constexpr int kIt = (CP * RQ + fast_threads<CP>() - 1) / fast_threads<CP>();
         uint4 v[kIt];
 #pragma unroll
         for (int k = 0; k < kIt; ++k) {

@@ -890,14 +890,13 @@ hipError_t launch_pyr_tail(const BatchArgs& a, hipStream_t s) {
 // ComputeKeyPointsOctTree (ORBextractor_old.cc:807-871) with cv::FAST(cell, kps, th, true):
 // detection on [3,rows-3)x[3,cols-3) of the cell ROI, 3x3 nonmax inside the cell only, iniTh
 // then minTh if the cell yields nothing, keys emitted in row-major order.
-constexpr int kFastThreads = FAST_THREADS;  // one workgroup per cell
 #ifndef FAST_FIXED_POLICY
 #define FAST_FIXED_POLICY 1  // compile-time workgroup size in the cell code (0: blockDim, A/B only)
 #endif
 
 template <int CP>
-__global__ __launch_bounds__(kFastThreads) void k_fast_cells(BatchArgs a, int cell0, uint32_t ncell_magic) {
-    constexpr int kList = cell_list_cap<CP>();
+__global__ __launch_bounds__(fast_threads<CP>()) void k_fast_cells(BatchArgs a, int cell0, uint32_t ncell_magic) {
+    constexpr int kList = cell_list_cap<CP>(), kFastThreads = fast_threads<CP>();
     __shared__ __attribute__((aligned(16))) uint8_t T[CP * CP];
     __shared__ __attribute__((aligned(16))) uint8_t M[CP * CP];  // 16-byte rows when CP % 16 == 0
     __shared__ __attribute__((aligned(8))) uint16_t list[kList + fast_list_slack(kFastThreads / 64)];
@@ -2350,7 +2349,9 @@ hipError_t launch_fast_cells(const BatchArgs& a, int tile, hipStream_t s) {
         c1 = a.fast_n64;
     }
     if (c1 <= c0) return hipSuccess;
-    const dim3 grid(c1 - c0, a.nimages), block(kFastThreads);
+    const dim3 grid(c1 - c0, a.nimages);
+    const dim3 block(tile == kCellPitchTiny ? fast_threads<kCellPitchTiny>() : tile == kCellPitchSmall ? fast_threads<kCellPitchSmall>()
+                                                                                                      : fast_threads<kCellMax>());
     const uint32_t d = (uint32_t)(c1 - c0);
     const uint32_t magic = d > 1 ? 0xFFFFFFFFu / d + 1u : 0u;  // ceil(2^32 / d) for d >= 2
     if (tile == kCellPitchTiny) hipLaunchKernelGGL(k_fast_cells<kCellPitchTiny>, grid, block, 0, s, a, c0, magic);
