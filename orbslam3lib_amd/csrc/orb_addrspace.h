@@ -38,6 +38,18 @@ template <class T>
 struct vec4_ptr<__attribute__((address_space(3))) T*> {
     using type = __attribute__((address_space(3))) orb_u32x4*;
 };
+template <class T>
+struct vec4_ptr<const T*> {
+    using type = const orb_u32x4*;
+};
+template <class T>
+struct vec4_ptr<const __attribute__((address_space(1))) T*> {
+    using type = const __attribute__((address_space(1))) orb_u32x4*;
+};
+template <class T>
+struct vec4_ptr<const __attribute__((address_space(3))) T*> {
+    using type = const __attribute__((address_space(3))) orb_u32x4*;
+};
 template <class P>
 __host__ __device__ inline typename vec4_ptr<P>::type as_vec4(P p) {
     return reinterpret_cast<typename vec4_ptr<P>::type>(p);

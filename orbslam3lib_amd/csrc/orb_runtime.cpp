@@ -404,7 +404,8 @@ int set_geometry(orbgpu_ctx* c, int w, int h) {
         G.hCell = (int)std::ceil(height / G.nRows);
         if (G.wCell > 69 || G.hCell > 69) return fail(ORBGPU_ERR_INVALID, "cell too large");
         G.ncells = G.nCols * G.nRows;
-        G.cell_cap = ((G.wCell + 1) / 2) * ((G.hCell + 1) / 2);
+        // (a multiple of 4: k_octree reads a cell's keys as 16-byte chunks)
+        G.cell_cap = (((G.wCell + 1) / 2) * ((G.hCell + 1) / 2) + 3) & ~3;
         G.cell_first = cell_first;
         cell_first += G.ncells;
         G.cellkey_off = ck;
