@@ -678,50 +678,51 @@ __host__ __device__ __attribute__((always_inline)) inline int octree_distribute(
                 if (ntid == 0) sh->nexp = c2;
             }
             np.sync();
-            // 2. rebuild: undivided nodes keep their order after all children
+            // 2. rebuild: undivided nodes keep their order after all children; one pass over the
+            // nodes (each node's record and division rank read once) places both kinds
             {
                 const int nchild = sh->nchild;
                 int carry = 0;
                 for (int base = 0; base < size; base += NNT) {
                     const int i = base + ntid;
-                    const int v = (i < size && M.divrank[i] < 0) ? 1 : 0;
+                    const bool in = i < size;
+                    const int dr = in ? M.divrank[i] : 0;
+                    const OctNode nd = on_ld(cur, in ? i : 0);
+                    const int v = (in && dr < 0) ? 1 : 0;
                     int tot;
                     const int ex = np.scan_small(v, &tot);
                     if (v) {
                         const int pos = nchild + carry + ex;
                         M.undivpos[i] = (uint16_t)pos;
-                        on_st(nxt, pos, on_ld(cur, i));
+                        on_st(nxt, pos, nd);
                         if (!fast)
                             for (int q = 0; q < 4; ++q) cnxt[4 * pos + q] = 0;
+                    } else if (in) {
+                        int pos = M.blockoff[i];
+                        int e = M.expoff[i];
+                        for (int q = 3; q >= 0; --q) {  // push_front n1..n4 => front reads n4,n3,n2,n1
+                            const int c = ccur[4 * i + q];
+                            if (c > 0) {
+                                const OctNode ch = oct_child(nd, q, c);
+                                on_st(nxt, pos, ch);
+                                // a fresh child with >1 key is a candidate of the next round: with
+                                // the pyramid, its child counts are looked up after this phase (all
+                                // threads), which needs it above depth D
+                                if (fast) {
+                                    if (c > 1 && oct_path_depth(ch.path) >= D) sh->deep = 1;
+                                } else {
+                                    for (int qq = 0; qq < 4; ++qq) cnxt[4 * pos + qq] = 0;
+                                }
+                                M.childpos[4 * i + q] = (uint16_t)pos;
+                                ++pos;
+                            }
+                        }
+                        for (int q = 0; q < 4; ++q)  // vSizeAndPointerToNode push_back order n1..n4
+                            if (ccur[4 * i + q] > 1) vsz2[e++] = M.childpos[4 * i + q];
                     }
                     carry += tot;
                 }
                 if (ntid == 0) sh->nundiv = carry;
-            }
-            for (int i = ntid; i < size; i += NNT) {
-                if (M.divrank[i] < 0) continue;
-                int pos = M.blockoff[i];
-                int e = M.expoff[i];
-                const OctNode nd = on_ld(cur, i);
-                for (int q = 3; q >= 0; --q) {  // push_front n1..n4 => front reads n4,n3,n2,n1
-                    const int c = ccur[4 * i + q];
-                    if (c > 0) {
-                        const OctNode ch = oct_child(nd, q, c);
-                        on_st(nxt, pos, ch);
-                        // a fresh child with >1 key is a candidate of the next round: with the
-                        // pyramid, its child counts are looked up after this phase (all threads),
-                        // which needs it above depth D
-                        if (fast) {
-                            if (c > 1 && oct_path_depth(ch.path) >= D) sh->deep = 1;
-                        } else {
-                            for (int qq = 0; qq < 4; ++qq) cnxt[4 * pos + qq] = 0;
-                        }
-                        M.childpos[4 * i + q] = (uint16_t)pos;
-                        ++pos;
-                    }
-                }
-                for (int q = 0; q < 4; ++q)  // vSizeAndPointerToNode push_back order n1..n4
-                    if (ccur[4 * i + q] > 1) vsz2[e++] = M.childpos[4 * i + q];
             }
             np.sync();
             // 4. next round's state (read by every thread after the barrier)

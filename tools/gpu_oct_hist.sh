@@ -1,10 +1,10 @@
 #!/bin/bash
-# octree histogram A/B: GPU suite, one-pair phase stamps, C4 step time, octree alone, bench A/B
+# octree A/B against a variant (V): GPU suite, one-pair phase stamps, C4 step time, octree alone, bench A/B
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
 O=gpurun_out/octh
 mkdir -p $O
-V=$PWD/orbslam3lib_amd/variants/liborbgpu_histscalar.so
+V=$PWD/orbslam3lib_amd/variants/liborbgpu_head.so
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
 tail -1 $O/pytest.log
 timeout -k 10 120 python3 tools/octree_stamps.py 1 2>&1 | tail -8
