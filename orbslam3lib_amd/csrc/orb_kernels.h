@@ -119,8 +119,13 @@ struct MatchArgs {
     uint32_t* cnt;            // split launches: per (pair, query block) arrival counters (zero between
                               // launches), so the last split workgroup merges; null: k_knn2_merge does
 };
-constexpr int kKnnMaxSplit = 8;     // train-row splits of a launch with few pairs
-constexpr int kKnnSplitSlots = 8;   // pairs x splits the partial buffer holds (1 pair: 8 splits)
+#ifndef KNN_SPLIT
+// round 5, C4 step (one pair, tools/c4_time.py): 4 splits 126.6-126.9 us, 8 splits 125.2-125.5,
+// 16 splits 126.6-126.9
+#define KNN_SPLIT 8
+#endif
+constexpr int kKnnMaxSplit = KNN_SPLIT;     // train-row splits of a launch with few pairs
+constexpr int kKnnSplitSlots = KNN_SPLIT;   // pairs x splits the partial buffer holds (1 pair: KNN_SPLIT splits)
 
 // Frame::ComputeStereoMatches over a batch's device-resident results (orb_stereo.hip).
 struct StereoArgs {
