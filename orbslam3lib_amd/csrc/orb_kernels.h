@@ -201,10 +201,12 @@ constexpr int kOdKpBlock = 256 / OD_LANES;  // keypoints per k_orient_desc pass 
 #define OD_WB 16
 #endif
 constexpr int kOdWaveBatch = OD_WB;  // OD_BATCH: keypoints per wave batch
-// keypoints per k_orient_desc workgroup by default: 4 waves x one batch (OD_BATCH), or 2 passes of
-// kOdKpBlock (the per-pair kernel; round 3 single stream: 488-490 us per 512 images vs 504 at 4
-// passes, 497-504 at 1, 540 at 8)
-constexpr int kOdBlockKps = OD_BATCH ? 4 * kOdWaveBatch : 2 * kOdKpBlock;
+// keypoints per k_orient_desc workgroup by default: 4 waves x one batch (OD_BATCH), or 3 passes of
+// kOdKpBlock (the per-pair kernel).  Round 5, chunked moments, single stream per 512 images: 1 pass
+// 553 us, 2 passes 483, 3 passes 463, 4 passes 467; headline at 3 vs 2 passes +0.2 to +2.3% (bench
+// A/B, 3 rounds).  Round 3 (per-row moments) had 2 passes best.  Contexts of a few images keep 2
+// (orb_runtime.cpp set_geometry).
+constexpr int kOdBlockKps = OD_BATCH ? 4 * kOdWaveBatch : 3 * kOdKpBlock;
 
 constexpr int kOctLdsKeys = 16384;  // per-key node labels (u16) kept in LDS up to this many keys
 constexpr int kFastMergeMaxImages = 4;  // launches this small run the 48/64 FAST cells as one launch
