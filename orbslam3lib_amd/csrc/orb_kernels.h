@@ -204,7 +204,7 @@ constexpr int kOdWaveBatch = OD_WB;  // OD_BATCH: keypoints per wave batch
 // keypoints per k_orient_desc workgroup by default: 4 waves x one batch (OD_BATCH), or 3 passes of
 // kOdKpBlock (the per-pair kernel).  Round 5, chunked moments, single stream per 512 images: 1 pass
 // 553 us, 2 passes 483, 3 passes 463, 4 passes 467; headline at 3 vs 2 passes +0.2 to +2.3% (bench
-// A/B, 3 rounds).  Round 3 (per-row moments) had 2 passes best.  Contexts of a few images keep 2
+// A/B, 3 rounds).  Round 3 (per-row moments) had 2 passes best.  Contexts of a few images take 1
 // (orb_runtime.cpp set_geometry).
 constexpr int kOdBlockKps = OD_BATCH ? 4 * kOdWaveBatch : 3 * kOdKpBlock;
 

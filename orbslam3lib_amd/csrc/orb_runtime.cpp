@@ -373,11 +373,11 @@ int set_geometry(orbgpu_ctx* c, int w, int h) {
     int cc = 0, kpo = 0, cell_first = 0, tile_first = 0, od_first = 0;
     // keypoints per k_orient_desc workgroup (orb_kernels.h kOdBlockKps; ORBGPU_OD_ITERS: passes of
     // kOdKpBlock instead, for A/B).  A context that never holds more than a few images (the
-    // latency shape) keeps two passes per workgroup: more, shorter workgroups for its few
-    // keypoints (C4 step 125.4 vs 126.4 us at three passes)
+    // latency shape) takes one pass per workgroup: more, shorter workgroups for its few keypoints
+    // (C4 step 124.3 us at one pass, 125.4 at two, 126.4 at three)
     const char* odi = diag_env("ORBGPU_OD_ITERS");
     const int od_per_block = odi ? kOdKpBlock * std::max(1, atoi(odi))
-                                 : c->max_images <= kFastMergeMaxImages ? 2 * kOdKpBlock : kOdBlockKps;
+                                 : c->max_images <= kFastMergeMaxImages ? kOdKpBlock : kOdBlockKps;
     for (int l = 0; l < L; ++l) {
         LevelGeom& G = A.lv[l];
         G.w = cv_round_f((float)w * c->inv_scale[l]);   // ComputePyramid :1336
