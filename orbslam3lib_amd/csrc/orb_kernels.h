@@ -118,6 +118,7 @@ struct MatchArgs {
     uint2* part;              // [kKnnSplitSlots][out_cap] partial top-2 keys of split launches, or null
     uint32_t* cnt;            // split launches: per (pair, query block) arrival counters (zero between
                               // launches), so the last split workgroup merges; null: k_knn2_merge does
+    int cnt_slots;            // counters allocated at cnt (launch_knn2_pairs checks the grid fits)
 };
 #ifndef KNN_SPLIT
 // round 5, C4 step (one pair, tools/c4_time.py): 4 splits 126.6-126.9 us, 8 splits 125.2-125.5,
@@ -126,6 +127,14 @@ struct MatchArgs {
 #endif
 constexpr int kKnnMaxSplit = KNN_SPLIT;     // train-row splits of a launch with few pairs
 constexpr int kKnnSplitSlots = KNN_SPLIT;   // pairs x splits the partial buffer holds (1 pair: KNN_SPLIT splits)
+// queries per k_knn2_mfma_pairs workgroup (orb_kernels.hip); the grid's x extent is
+// ceil(out_cap / kKnnQueries) query blocks per pair
+constexpr int kKnnQueries = 256;
+// arrival counters of the fused split merge: one per (pair of the launch, query block); a split
+// launch has at most kKnnSplitSlots / 2 pairs (orb_runtime.cpp), sized for kKnnSplitSlots
+__host__ inline size_t knn2_counter_slots(int out_cap) {
+    return (size_t)kKnnSplitSlots * (size_t)((out_cap + kKnnQueries - 1) / kKnnQueries);
+}
 
 // Frame::ComputeStereoMatches over a batch's device-resident results (orb_stereo.hip).
 struct StereoArgs {
@@ -230,13 +239,23 @@ struct OctLayout {
 
 __host__ __device__ inline long long oct_align(long long x) { return (x + 255) & ~255LL; }
 
+// Bytes of node state per node (orb_octree.h oct_nodemem_carve: cntA / cntB 16, nodesA / nodesB
+// 16 each, divrank 4, childpos 8, five u16 arrays 10) -- the one figure both the LDS layouts and
+// the workspace below size from; orb_octree.h asserts that the carve adds up to it.
+constexpr int kOctNodeMemPerNode = 86;
+__host__ __device__ constexpr size_t oct_nodemem_bytes(int C) { return (size_t)C * kOctNodeMemPerNode + 64; }
+
 __host__ __device__ inline OctLayout oct_layout(int n_cap, int C) {
     OctLayout L;
     long long o = 0;
     L.keys = o; o = oct_align(o + 4LL * n_cap);
     L.nq = o; o = oct_align(o + 2LL * n_cap);  // used when n exceeds kOctLdsKeys
     L.nodemem = o;
-    o = oct_align(o + (long long)((size_t)C * 78 + 64));  // used when C exceeds the LDS capacity
+    // used when C exceeds the LDS capacity (k_octree_retry).  Round 3 grew OctNode from 12 to 16
+    // bytes while this reserved the old 78 B per node: levels with their node state here (above
+    // ~1000 features per level, e.g. 1920x1080 with 8200 features) wrote 8 B per node into the
+    // next level's keys, which that level's workgroup was using at the same time (round 6)
+    o = oct_align(o + (long long)oct_nodemem_bytes(C));
     L.total = o;
     return L;
 }

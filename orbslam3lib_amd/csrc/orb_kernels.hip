@@ -1856,6 +1856,7 @@ typedef int knn_v16i __attribute__((ext_vector_type(16)));
 constexpr int kKnnWaves = KNN_WAVES;     // waves per workgroup, 32 queries each
 constexpr int kKnnThreads = 64 * kKnnWaves;
 constexpr int kKnnQ = 32 * kKnnWaves;    // queries per workgroup
+static_assert(kKnnQ <= kKnnQueries, "the arrival counters (knn2_counter_slots) assume at most kKnnQueries per block");
 constexpr int kKnnPitch = 272;           // bytes per expanded train row in LDS (256 + 16: no bank conflicts)
 // 32-row tiles per LDS stage (one barrier per stage).  Round 5 (single stream, 512 images):
 // 1 tile 243-246 us, 2 tiles 251-253 us -- the barrier per tile is not what the waves wait on
@@ -2413,14 +2414,19 @@ hipError_t launch_knn2_pairs(const MatchArgs& m, int npairs, hipStream_t s) {
     // few pairs (the latency shape): the train rows split over S workgroups per query block, so
     // the launch has ~256 workgroups instead of 8 per pair, and k_knn2_merge combines the splits
     const int S = m.part ? std::max(1, std::min(kKnnMaxSplit, kKnnSplitSlots / std::max(npairs, 1))) : 1;
+    const int qblocks = (m.out_cap + kKnnQ - 1) / kKnnQ;
     if (S > 1) {
-        hipLaunchKernelGGL(k_knn2_mfma_pairs, dim3((m.out_cap + kKnnQ - 1) / kKnnQ, npairs, S), dim3(kKnnThreads), 0, s, m);
+        // the partial lists take npairs * S slots of out_cap rows, the fused merge one arrival
+        // counter per (pair, query block): refuse a launch that would index past either
+        if (npairs * S > kKnnSplitSlots || (m.cnt && (long long)npairs * qblocks > m.cnt_slots))
+            return hipErrorInvalidValue;
+        hipLaunchKernelGGL(k_knn2_mfma_pairs, dim3(qblocks, npairs, S), dim3(kKnnThreads), 0, s, m);
         if (!m.cnt) hipLaunchKernelGGL(k_knn2_merge, dim3((m.out_cap + 255) / 256, npairs), dim3(256), 0, s, m, S);
         return hipGetLastError();
     }
     MatchArgs m1 = m;
     m1.part = nullptr;
-    hipLaunchKernelGGL(k_knn2_mfma_pairs, dim3((m.out_cap + kKnnQ - 1) / kKnnQ, npairs), dim3(kKnnThreads), 0, s, m1);
+    hipLaunchKernelGGL(k_knn2_mfma_pairs, dim3(qblocks, npairs), dim3(kKnnThreads), 0, s, m1);
     return hipGetLastError();
 }
 hipError_t launch_knn2_plain(const uint8_t* q, int nq, const uint8_t* t, int nt, int32_t* i1,

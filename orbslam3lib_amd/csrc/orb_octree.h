@@ -28,6 +28,7 @@
 #include <stdint.h>
 
 #include "orb_addrspace.h"
+#include "orb_kernels.h"
 #include "orb_introsort.h"
 
 namespace orbgpu {
@@ -95,9 +96,8 @@ struct OctNodeMemT {
     asp<AS, uint16_t> vsizeB;    // [C]
 };
 
-__host__ __device__ inline size_t oct_nodemem_bytes(int C) {
-    return (size_t)C * (2 * sizeof(OctNode) + 2 * 16 + 8 + 4 + 5 * 2) + 64;
-}
+// oct_nodemem_bytes (orb_kernels.h) = C * kOctNodeMemPerNode + 64, the carve below per node:
+static_assert(2 * sizeof(OctNode) + 2 * 16 + 8 + 4 + 5 * 2 == kOctNodeMemPerNode, "node state bytes per node");
 
 // Carves an OctNodeMemT out of `base` (16-byte aligned, in address space AS).
 template <int AS>

@@ -337,7 +337,7 @@ int alloc_all(orbgpu_ctx* c, int n_images) {
     {  // split kNN2 partials, then the arrival counters of the fused merge (zeroed once: the last
        // workgroup of each query block resets its counter)
         void* before = c->mpart.p;
-        const size_t cnt_bytes = (size_t)kKnnSplitSlots * ((c->out_cap + 255) / 256 + 1) * 4;
+        const size_t cnt_bytes = knn2_counter_slots(c->out_cap) * 4;
         r |= c->mpart.ensure((size_t)kKnnSplitSlots * c->out_cap * 8 + 256 + cnt_bytes);
         if (!r && c->mpart.p != before && hipMemset(c->mpart.p, 0, c->mpart.bytes) != hipSuccess) r = -1;
     }
@@ -998,6 +998,7 @@ static MatchArgs stereo_match_args(orbgpu_ctx* c, int stereo_only) {
     m.nq = c->mnq.as<int32_t>();
     m.part = nullptr;
     m.cnt = reinterpret_cast<uint32_t*>(c->mpart.as<uint8_t>() + (size_t)kKnnSplitSlots * c->out_cap * 8 + 256);
+    m.cnt_slots = (int)knn2_counter_slots(c->out_cap);
     m.pair0 = 0;
     return m;
 }

@@ -91,6 +91,34 @@ def test_batch_knn2_past_4096_train_rows(oracle):
     np.testing.assert_array_equal(d, rd)
 
 
+@pytest.mark.parametrize("pyr", [None, "0"])
+def test_batch_1080p_8200_repeatable(oracle, monkeypatch, pyr):
+    """Levels 0-2 of a 1920x1080 / 12-level / 8200-feature frame hold more than 1024 octree nodes,
+    so k_octree_retry keeps their node state in the global workspace.  Until round 6 that region
+    was sized for 78 B per node while the carve uses 86 (orb_kernels.h oct_layout), so level l
+    wrote into level l + 1's keys while another workgroup was using them: with two chunk streams
+    the level-1 / level-2 keypoint sets changed from run to run (tools/race_probe.py).  Every image
+    of both pairs against the oracle on three runs of one context, with the count pyramid and with
+    the label passes only (ORBGPU_OCT_PYR=0)."""
+    import orbslam3lib_amd as og
+    if pyr is not None:
+        monkeypatch.setenv("ORBGPU_DIAGNOSTICS", "1")
+        monkeypatch.setenv("ORBGPU_OCT_PYR", pyr)
+    pairs = [synth.stereo_pair(1080, 1920, 60 + i) for i in range(2)]
+    imgs = np.stack([x for p in pairs for x in p])
+    refs = [oracle.extract(x, nfeatures=8200, nlevels=12) for x in imgs]
+    be = _batch(og, 1920, 1080, 12, 8200, imgs)
+    for rep in range(3):
+        be.run()
+        be.synchronize()
+        for i in range(4):
+            k, d, m = be.result(i)
+            rk, rd, rm = refs[i]
+            assert m == rm, (rep, i)
+            _same_kps(k, rk)
+            np.testing.assert_array_equal(d, rd, err_msg="run %d image %d" % (rep, i))
+
+
 def test_split_knn2_one_pair_past_4096_rows(oracle, monkeypatch):
     """A one-pair batch (the C4 shape) matches with the train rows split over 8 workgroups per
     query block, the last of which merges the partial lists (orb_kernels.hip k_knn2_mfma_pairs'
