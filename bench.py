@@ -886,8 +886,8 @@ def main():
 
     # The C4 ingest-rank path (BASELINE configs[3]) when several GPUs run: rank 0 holds
     # one 640x480 stereo pair per rank, one scatter hands each rank its pair, each rank extracts
-    # and matches it on its GPU, one gather brings every rank's results (counts, keypoints,
-    # descriptors, kNN2; orbgpu_export_batch) back to rank 0.  Reported beside the headline,
+    # and matches it on its GPU, one gather brings every rank's results (counts, then the
+    # keypoints, descriptors and kNN2 rows produced; orbgpu_export_batch) back to rank 0.  Reported beside the headline,
     # never part of it.
     ingest = None
     if world > 1:
@@ -904,10 +904,11 @@ def main():
             if -max_over_ranks(dist, -(0.0 if setup_err else 1.0)) < 1.0:
                 raise RuntimeError("ingest setup failed on a rank: %r" % (setup_err,))
             got = None
+            istats = {}
             for _ in range(4):  # the first exchanges set up the communicators and buffers
                 barrier(dist)
                 i0 = time.perf_counter()
-                got = ingest_scatter_gather(dist, ib, frames, pairs_per_rank=1, src=0)
+                got = ingest_scatter_gather(dist, ib, frames, pairs_per_rank=1, src=0, stats=istats)
                 if has_cuda:
                     torch.cuda.synchronize()
                 i1 = time.perf_counter()
@@ -926,6 +927,9 @@ def main():
                       "mfeatures_s": round(nfe / iel / 1e6, 3) if rank == 0 else None,
                       "exchange": "scatter of frames + gather of results (%s%s)"
                                   % (dist.get_backend(), ", device-resident" if has_cuda else ", host"),
+                      # the gather moves the produced rows only (orbgpu_export_batch, packed)
+                      "gathered_bytes_per_rank": istats.get("gathered_bytes_per_rank"),
+                      "capacity_layout_bytes_per_rank": istats.get("capacity_bytes_per_rank"),
                       "rank0_results_equal_local": bool(ok == 1.0) if rank == 0 else None}
             ib.close()
             del ib

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define ORBGPU_ABI_VERSION 1
+#define ORBGPU_ABI_VERSION 2  /* 2: packed orbgpu_export_batch, ORBGPU_DEVICE_CURRENT */
 
 /* Status codes (the DSP path returned 1/3/7 and callers ignored them; we never exit()). */
 enum {
@@ -65,13 +65,18 @@ typedef struct orbgpu_ctx orbgpu_ctx;
 
 /* Build a context for images up to max_width x max_height and batches of up to max_images
  * images.  Allocates all device memory once (nothing is allocated per call).  device = HIP
- * ordinal.  Replaces the ORBextractor ctor + LynxHardwareAccelerator ctor (orbslam3_open).
+ * ordinal, or ORBGPU_DEVICE_CURRENT: the calling thread's current HIP device (hipGetDevice), so a
+ * multi-camera process places each extractor on the GPU it selected before constructing it (the
+ * C++ facades pass it); orbgpu_get_device reports the ordinal a context uses.
+ * Replaces the ORBextractor ctor + LynxHardwareAccelerator ctor (orbslam3_open).
  * ORBGPU_ERR_INVALID for nlevels outside [1, 16], scale_factor not above 1 (any value above 1,
  * as ORBextractor; steps above 2 build the pyramid level by level from HBM), negative nfeatures
  * or sizes outside (0, 4112), or a pyramid level under 42 px (at the first batch of that size);
  * ORBGPU_ERR_NO_DEVICE without a HIP device. */
+#define ORBGPU_DEVICE_CURRENT (-1)
 int orbgpu_create(const orbgpu_params* params, int device, int max_width, int max_height,
                   int max_images, orbgpu_ctx** out_ctx);
+int orbgpu_get_device(const orbgpu_ctx* ctx); /* the context's HIP ordinal (ORBGPU_ERR_INVALID: null) */
 int orbgpu_destroy(orbgpu_ctx* ctx); /* orbslam3_close */
 
 /* Scale tables exactly as the ORBextractor getters return them (GetScaleFactors, ...). */
@@ -162,17 +167,23 @@ int orbgpu_match_knn2_device(orbgpu_ctx* ctx, const uint8_t* d_query, int nq, co
  *     rows of `stride` bytes) -> the context's input buffer, device to device on `stream`; the
  *     next orbgpu_run_batch / run_batch_match reads them;
  *   orbgpu_export_batch: the last batch's results of images [0, n_images) and stereo pairs
- *     [0, n_pairs) -> one device buffer (e.g. a gather's send buffer), device to device on
- *     `stream`, ordered after the batch.  Layout (out_cap = *out_cap rows per image / pair):
+ *     [0, n_pairs) -> one device buffer (e.g. a gather's send buffer, 4-byte aligned), device to
+ *     device on `stream`, ordered after the batch.  Only the rows produced are packed:
  *       int32 count[n_images], int32 mono[n_images], int32 n_queries[n_pairs],
- *       orbgpu_keypoint kps[n_images][out_cap], uint8 desc[n_images][out_cap][32],
- *       int32 idx1[n_pairs][out_cap], dist1[..], idx2[..], dist2[..]  (the last match call's);
- *     orbgpu_export_batch_bytes gives its size. */
+ *       then for each image i: orbgpu_keypoint kps[count[i]], uint8 desc[count[i]][32],
+ *       then for each pair p: int32 idx1[n_queries[p]], dist1[..], idx2[..], dist2[..]
+ *       (the last match call's).
+ *     *used = the layout's size in bytes.  The counts size it, so the call waits for the batch;
+ *     device_dst = NULL only reports *used (the size query before a collective's allocation).
+ *     A count the device replaced by a status (octree workspace overflow, output capacity) is
+ *     returned as that status (ORBGPU_ERR_OVERFLOW / ORBGPU_ERR_CAPACITY) and nothing is packed.
+ *     orbgpu_export_batch_bytes: the largest such layout (every image at the context's row
+ *     capacity), with no device access. */
 int orbgpu_ingest_images(orbgpu_ctx* ctx, const uint8_t* device_images, int n_images, int width,
                          int height, int stride, void* stream);
 size_t orbgpu_export_batch_bytes(const orbgpu_ctx* ctx, int n_images, int n_pairs);
 int orbgpu_export_batch(orbgpu_ctx* ctx, int n_images, int n_pairs, void* device_dst, size_t dst_bytes,
-                        int* out_cap, void* stream);
+                        size_t* used, void* stream);
 
 /* Batch stereo matching on device-resident results of the last orbgpu_run_batch: pair p
  * matches image 2p (query) against image 2p+1 (train), rows [mono..n) of each when

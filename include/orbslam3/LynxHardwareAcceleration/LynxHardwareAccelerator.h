@@ -96,6 +96,7 @@ private:
     };
     orbgpu_params mParams{};
     mutable orbgpu_ctx* mCtx = nullptr;
+    mutable int mDevice = ORBGPU_DEVICE_CURRENT;  // the device current at construction
     mutable int mWidth = 0, mHeight = 0;  // context capacity, per eye
     mutable int mFrameW = 0, mFrameH = 0;  // geometry of the stored frame
     std::vector<uint8_t> mStage;           // host staging of ExtractORBPair

@@ -110,6 +110,9 @@ protected:
 
     orbgpu_ctx* mCtx = nullptr;
     int mCtxW = 0, mCtxH = 0;
+    // the HIP device current when the extractor was built (ORBGPU_DEVICE_CURRENT); a context
+    // regrown for a larger image stays on it
+    int mDevice = ORBGPU_DEVICE_CURRENT;
     int mStatus = 0;
     std::vector<orbgpu_keypoint> mKps;
     std::vector<uint8_t> mDesc;

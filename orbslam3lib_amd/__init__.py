@@ -52,7 +52,10 @@ EXPORTED = [
     "orbgpu_reset_stage_times", "orbgpu_last_error", "orbgpu_abi_version",
     "orbgpu_fisheye_stereo_batch", "orbgpu_download_fisheye", "orbgpu_run_batch_match",
     "orbgpu_diagnostic_knobs", "orbgpu_ingest_images", "orbgpu_export_batch_bytes", "orbgpu_export_batch",
+    "orbgpu_get_device",
 ]
+
+DEVICE_CURRENT = -1  # ORBGPU_DEVICE_CURRENT: the calling thread's current HIP device
 
 
 class KB8Rig(C.Structure):
@@ -117,7 +120,8 @@ def load_library(path: str = LIB_PATH):
     lib.orbgpu_export_batch_bytes.restype = C.c_size_t
     lib.orbgpu_export_batch_bytes.argtypes = [C.c_void_p, C.c_int, C.c_int]
     lib.orbgpu_export_batch.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_size_t,
-                                        C.POINTER(C.c_int), C.c_void_p]
+                                        C.POINTER(C.c_size_t), C.c_void_p]
+    lib.orbgpu_get_device.argtypes = [C.c_void_p]
     for name in ("orbgpu_destroy", "orbgpu_synchronize", "orbgpu_set_profiling",
                  "orbgpu_reset_stage_times"):
         getattr(lib, name).argtypes = [C.c_void_p] + ([C.c_int] if name == "orbgpu_set_profiling" else [])
@@ -152,6 +156,52 @@ def _p(a):
     return a.ctypes.data_as(C.c_void_p)
 
 
+_COUNT_STATUS = {-5: "device workspace overflow (octree)", -2: "context output capacity exceeded"}
+
+
+def decode_export(buf, n_images, n_pairs):
+    """The packed orbgpu_export_batch layout (include/orbgpu.h) -> ([(kps, desc, mono)] per image,
+    [(idx1, dist1, idx2, dist2)] per pair).  Raises OrbGpuError on a status word in a count."""
+    b = np.ascontiguousarray(buf, dtype=np.uint8).reshape(-1)
+    hdr = 4 * (2 * n_images + n_pairs)
+    if b.size < hdr:
+        raise OrbGpuError(-2, "export buffer shorter than its header")
+    h = b[:hdr].view(np.int32)
+    counts, mono, nq = h[:n_images], h[n_images:2 * n_images], h[2 * n_images:]
+    for c in list(counts) + list(nq):
+        if c < 0:
+            code = int(c) if int(c) in _COUNT_STATUS else -2
+            raise OrbGpuError(code, _COUNT_STATUS.get(int(c), "negative row count in export"))
+    if b.size < hdr + 60 * int(counts.sum()) + 16 * int(nq.sum()):
+        raise OrbGpuError(-2, "export buffer shorter than its counts say")
+    o = hdr
+    images = []
+    for i in range(n_images):
+        n = int(counts[i])
+        kps = b[o:o + 28 * n].copy().view(KEYPOINT_DTYPE); o += 28 * n
+        desc = b[o:o + 32 * n].copy().reshape(n, 32); o += 32 * n
+        images.append((kps, desc, int(mono[i])))
+    pairs = []
+    for p in range(n_pairs):
+        n = int(nq[p])
+        m = b[o:o + 16 * n].copy().view(np.int32).reshape(4, n); o += 16 * n
+        pairs.append(tuple(m[k] for k in range(4)))
+    return images, pairs
+
+
+def encode_export(images, pairs):
+    """Host restatement of the packed layout (what orbgpu_export_batch writes) from per-image
+    (kps, desc, mono) and per-pair (idx1, dist1, idx2, dist2): the CPU stand-ins' export."""
+    parts = [np.array([len(k) for k, _, _ in images], np.int32), np.array([m for _, _, m in images], np.int32),
+             np.array([len(p[0]) for p in pairs], np.int32)]
+    for k, d, _ in images:
+        parts.append(np.ascontiguousarray(k, KEYPOINT_DTYPE).view(np.uint8).reshape(-1))
+        parts.append(np.ascontiguousarray(d, np.uint8).reshape(-1))
+    for p in pairs:
+        parts.append(np.stack([np.asarray(a, np.int32) for a in p]).reshape(-1))
+    return np.concatenate([x.view(np.uint8).reshape(-1) for x in parts])
+
+
 class _Context:
     def __init__(self, nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST, device, max_width,
                  max_height, max_images):
@@ -163,6 +213,10 @@ class _Context:
                                  int(max_height), int(max_images), C.byref(self.handle)))
         self.nlevels = int(nlevels)
         self.max_images = int(max_images)
+
+    def device(self):
+        """The HIP ordinal the context runs on (orbgpu_get_device)."""
+        return _check(_lib.orbgpu_get_device(self.handle))
 
     def close(self):
         if self.handle:
@@ -388,33 +442,32 @@ class BatchExtractor:
         self._staged = None
 
     def export_batch_bytes(self, n_images, n_pairs):
+        """The largest orbgpu_export_batch layout (every image at the context's row capacity)."""
         return int(_lib.orbgpu_export_batch_bytes(self.ctx.handle, int(n_images), int(n_pairs)))
 
+    def export_batch_size(self, n_images, n_pairs, stream=None):
+        """The exact size of the packed orbgpu_export_batch layout of the last batch (waits for it)."""
+        used = C.c_size_t(0)
+        _check(_lib.orbgpu_export_batch(self.ctx.handle, int(n_images), int(n_pairs), None, 0, C.byref(used),
+                                        C.c_void_p(stream) if stream else None))
+        return used.value
+
     def export_batch(self, device_ptr, n_images, n_pairs, nbytes, stream=None):
-        """The last batch's results of images [0, n_images) and pairs [0, n_pairs) into one device
-        buffer (orbgpu_export_batch, device to device); returns out_cap for decode_export."""
-        cap = C.c_int(0)
+        """The last batch's produced rows of images [0, n_images) and pairs [0, n_pairs) packed into
+        one device buffer (orbgpu_export_batch, device to device); returns the bytes written."""
+        used = C.c_size_t(0)
         _check(_lib.orbgpu_export_batch(self.ctx.handle, int(n_images), int(n_pairs), C.c_void_p(device_ptr),
-                                        int(nbytes), C.byref(cap), C.c_void_p(stream) if stream else None))
-        return cap.value
+                                        int(nbytes), C.byref(used), C.c_void_p(stream) if stream else None))
+        return used.value
 
     @staticmethod
-    def decode_export(buf, n_images, n_pairs, out_cap):
-        """Host view of an orbgpu_export_batch buffer (uint8 array): per image (keypoints in the
-        cv::KeyPoint layout, descriptors [n, 32], mono index) and per pair (idx1, dist1, idx2,
-        dist2) over the pair's query rows -- what result() / matches() return."""
-        b = np.ascontiguousarray(buf, dtype=np.uint8).reshape(-1)
-        o = 0
-        counts = b[o:o + 4 * n_images].view(np.int32); o += 4 * n_images
-        mono = b[o:o + 4 * n_images].view(np.int32); o += 4 * n_images
-        nq = b[o:o + 4 * n_pairs].view(np.int32); o += 4 * n_pairs
-        kps = b[o:o + 28 * out_cap * n_images].view(KEYPOINT_DTYPE).reshape(n_images, out_cap)
-        o += 28 * out_cap * n_images
-        desc = b[o:o + 32 * out_cap * n_images].reshape(n_images, out_cap, 32); o += 32 * out_cap * n_images
-        m = b[o:o + 16 * out_cap * n_pairs].view(np.int32).reshape(4, n_pairs, out_cap) if n_pairs else None
-        images = [(kps[i, :counts[i]].copy(), desc[i, :counts[i]].copy(), int(mono[i])) for i in range(n_images)]
-        pairs = [tuple(m[k, p, :nq[p]].copy() for k in range(4)) for p in range(n_pairs)]
-        return images, pairs
+    def decode_export(buf, n_images, n_pairs):
+        """Host view of an orbgpu_export_batch buffer (uint8 array, trailing padding allowed): per
+        image (keypoints in the cv::KeyPoint layout, descriptors [n, 32], mono index) and per pair
+        (idx1, dist1, idx2, dist2) over the pair's query rows -- what result() / matches() return.
+        A negative count is a device status word (-5 octree workspace overflow, -2 capacity), not
+        rows: raised as OrbGpuError, as every download path does."""
+        return decode_export(buf, n_images, n_pairs)
 
     def upload_async(self, images):
         """Stage the NEXT batch (orbgpu_upload_images_async): the copy runs beside the current

@@ -15,21 +15,6 @@
 // candidate, m > t being the segment test itself; (3) the 3x3 nonmax over the corners.
 // Policy-templated like orb_octree.h so the host harness runs the same code on the CPU.
 #pragma once
-#ifndef FAST_VAR
-#define FAST_VAR 0
-#endif
-#ifndef FAST_SINK
-#define FAST_SINK 0
-#endif
-#ifndef FAST_PRETEST8
-#define FAST_PRETEST8 0  // pre-test: 8 pixels per lane, ds_read_b64 + DPP neighbours (0: 4 per lane)
-#endif
-#ifndef FAST_2X1
-#define FAST_2X1 0  // strength phase: two single-side candidates per lane (0: one two-sided)
-#endif
-#ifndef FAST_DPP_SCAN
-#define FAST_DPP_SCAN 1  // candidate list positions by a DPP wave scan (0: bit-sliced ballots)
-#endif
 #ifndef FAST_THREADS
 // k_fast_cells workgroup: one wave per cell.  Round 5 (single stream, 512 images, k_fast_cells<48>):
 // 2 waves per cell 678-684 us, 1 wave 648-664 us, 1 wave with the fixed-size policy 652-654 us
@@ -150,7 +135,7 @@ struct CellScratch {
 // List entries past cell_list_cap on the device: each wave's list is followed by 4 spare
 // entries (the compaction writes 4 slots per lane, the ones past the lane's candidates are
 // overwritten by later lanes or land in the spare entries), then 4 sink entries.
-__host__ __device__ constexpr int fast_list_slack(int waves) { return 4 * waves + (FAST_SINK == 2 ? 512 : 4); }
+__host__ __device__ constexpr int fast_list_slack(int waves) { return 4 * waves + 4; }
 
 // The positions of the set bits of every 4-bit pre-test mask as u16 pairs (p0 | p1 << 16,
 // p2 | p3 << 16): a constant table, copied to LDS per workgroup (one load per lane, not the ~45
@@ -277,14 +262,7 @@ __host__ __device__ int fast_cell_detect(Pol& p, int sh, const CellGeom& g, int 
     const int tini = ini_th < 0 ? 0 : (ini_th > 255 ? 255 : ini_th);
     const int tmin = min_th < 0 ? 0 : (min_th > 255 ? 255 : min_th);
     const int W = p.nwaves(), w = p.wave(), L = p.wave_width(), lane = p.lane();
-#if defined(__HIP_DEVICE_COMPILE__) && FAST_PRETEST8
-    // device: the pre-test takes the 8 pixels of one 8-byte LDS pair per lane (two fw_pretest4);
-    // a wave owns a contiguous range of detection rows, and its list starts after the detection
-    // pixels of the rows before it
-    const int r0 = w * dr / W, r1 = (w + 1) * dr / W;
-    const int i0 = r0 * dc;
-    (void)lane;
-#elif defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__)
     // device: the pre-test takes 4 pixels per lane (fw_pretest4); a wave owns a contiguous
     // row-major range of (row, dword group) items, and its list starts after the detection
     // pixels of the items before it
@@ -324,108 +302,10 @@ __host__ __device__ int fast_cell_detect(Pol& p, int sh, const CellGeom& g, int 
     auto build = [&](int t) {
         int na = 0;
 #if defined(__HIP_DEVICE_COMPILE__)
-#if FAST_PRETEST8
-        {
-            // lane = (row rr of the iteration, 8-byte pair q of the LDS row): RP pairs per row
-            // cover the whole pitch, RPL rows per iteration (CP = 48: 10 rows x 6 pairs = 60
-            // lanes), so each row is read with 5 conflict-free ds_read_b64 (rows -3, -2, 0, 2, 3:
-            // 32 lanes read 32 consecutive pairs) and the dwords left / right of a pair come from
-            // the neighbouring lanes by DPP (wave_shr / wave_shl 1).  A row's first and last
-            // pairs get a neighbour of another row there, which only the halo pixels use.
-            constexpr int RP = CP / 8, RPL = 64 / RP, LN = RP * RPL;
-            const int rr = min(lane / RP, RPL - 1), q = lane - (lane / RP) * RP;
-            const uint32_t tt = (uint32_t)t * 0x00010001u, kt = (uint32_t)(255 - t) * 0x00010001u;
-            auto rank = [](uint64_t b) {  // set lanes of b below this lane
-                return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32),
-                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
-            };
-            // 0x80 in the bytes of detection columns [3 + sh, 3 + sh + dc) of this lane's pair
-            auto det_mask = [&](int b0) {
-                uint32_t m = 0;
-#pragma unroll
-                for (int j = 0; j < 4; ++j) m |= (b0 + j >= 3 + sh && b0 + j < 3 + sh + dc) ? (0x80u << (8 * j)) : 0u;
-                return m;
-            };
-            const uint32_t em0 = lane < LN ? det_mask(8 * q) : 0u, em1 = lane < LN ? det_mask(8 * q + 4) : 0u;
-            // each pair read on its own address register: the compiler would fuse two of them
-            // into a ds_read2_b64, which takes 8 LDS cycles where two ds_read_b64 take 4
-            auto ld64 = [&](int off) {
-                asm volatile("" : "+v"(off));
-                return *reinterpret_cast<const uint2*>(T + off);
-            };
-            auto shr1 = [](uint32_t v) { return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x138, 0xF, 0xF, true); };
-            auto shl1 = [](uint32_t v) { return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x130, 0xF, 0xF, true); };
-            for (int rb = r0; rb < r1; rb += RPL) {
-                const int r = rb + rr;
-                const bool in = lane < LN && r < r1;
-                const int pr = (int)__umul24((uint32_t)(min(r, r1 - 1) + 3), (uint32_t)CP) + 8 * q;  // pair in tile row r + 3
-                const uint2 C = ld64(pr), U3 = ld64(pr - 3 * CP), D3 = ld64(pr + 3 * CP);
-                const uint2 U2 = ld64(pr - 2 * CP), D2 = ld64(pr + 2 * CP);
-                const uint32_t Cl = shr1(C.y), Cr = shl1(C.x);
-                const uint32_t U2l = shr1(U2.y), U2r = shl1(U2.x), D2l = shr1(D2.y), D2r = shl1(D2.x);
-                const uint2 s0 = fw_pretest4(C.x, Cl, C.y, U3.x, D3.x, U2l, U2.x, U2.y, D2l, D2.x, D2.y, tt, kt);
-                const uint2 s1 = fw_pretest4(C.y, C.x, Cr, U3.y, D3.y, U2.x, U2.y, U2r, D2.x, D2.y, D2r, tt, kt);
-                const uint32_t m0 = in ? (s0.x | s0.y) & em0 : 0u, m1 = in ? (s1.x | s1.y) & em1 : 0u;
-                // the sides that passed, per pixel, into the strength plane (0x80 bright, 0x40 dark;
-                // 0 for every other pixel of the row): the strength phase evaluates a candidate's
-                // passing side only, and overwrites the byte with m (corner) or 0
-                if (FAST_2X1 && in)
-                    *reinterpret_cast<uint2*>(M + pr) = make_uint2((s0.y & m0) | ((s0.x & m0) >> 1),
-                                                                   (s1.y & m1) | ((s1.x & m1) >> 1));
-                // 4-bit pass masks of the two dwords (bit k = byte k) by v_dot4_u32_u8 of the 0x80 bytes
-                const uint32_t n0 = __builtin_amdgcn_udot4(m0, 0x08040201u, 0u, false) >> 7;
-                const uint32_t n1 = __builtin_amdgcn_udot4(m1, 0x08040201u, 0u, false) >> 7;
-                const int c0 = __builtin_popcount(m0), c1 = __builtin_popcount(m1), c = c0 + c1;
-                const uint64_t b0 = p.ballot(c & 1), b1 = p.ballot(c & 2), b2 = p.ballot(c & 4), b3 = p.ballot(c & 8);
-                int pos = na + rank(b0) + 2 * rank(b1) + 4 * rank(b2);
-                if (b3) pos += 8 * rank(b3);
-                // the two dwords as two list runs in row-major order: run 0 = the c0 entries of
-                // dword 0 at pos, run 1 = the c1 entries of dword 1 at pos + c0.  Each run writes 4
-                // slots in the order k = 3, 2, 1, 0, runs interleaved (run 0 then run 1 per k):
-                // the slots of a run past its entries hold garbage that a later write overwrites
-                // (its own run 1, or a later lane's run at a smaller k), or that lands in the
-                // wave's spare entries; empty runs write the sink.  Slot 3 is written only when
-                // some run of the wave has 4 entries.
-                const uint2 lv0 = cs.lut[n0], lv1 = cs.lut[n1];
-                const uint32_t base = __umul24((uint32_t)pr, 0x10001u);  // inactive lanes: c = 0
-                const uint32_t e01a = base + lv0.x, e23a = base + lv0.y;
-                const uint32_t e01b = base + 0x40004u + lv1.x, e23b = base + 0x40004u + lv1.y;
-                uint16_t* da = c0 ? list + pos : sink;
-                uint16_t* db = c1 ? list + pos + c0 : sink;
-                if (p.ballot((n0 == 15u) | (n1 == 15u))) {
-                    da[3] = (uint16_t)(e23a >> 16);
-                    asm volatile("" ::: "memory");
-                    db[3] = (uint16_t)(e23b >> 16);
-                    asm volatile("" ::: "memory");
-                }
-                da[2] = (uint16_t)e23a;
-                asm volatile("" ::: "memory");  // keep the slot order
-                db[2] = (uint16_t)e23b;
-                asm volatile("" ::: "memory");
-                da[1] = (uint16_t)(e01a >> 16);
-                asm volatile("" ::: "memory");
-                db[1] = (uint16_t)(e01b >> 16);
-                asm volatile("" ::: "memory");
-                da[0] = (uint16_t)e01a;
-                asm volatile("" ::: "memory");
-                db[0] = (uint16_t)e01b;
-                na += p.popc64(b0) + 2 * p.popc64(b1) + 4 * p.popc64(b2) + 8 * p.popc64(b3);
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the list is read by other lanes
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        }
-#else
         {
             constexpr int RW = CP / 4;
             const uint32_t* T32 = reinterpret_cast<const uint32_t*>(T);
             const uint32_t tt = (uint32_t)t * 0x00010001u, kt = (uint32_t)(255 - t) * 0x00010001u;
-#if !FAST_DPP_SCAN
-            auto rank = [](uint64_t b) {  // set lanes of b below this lane
-                return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32),
-                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
-            };
-#endif
             // this lane's item (row r, dword group q) as (q, LDS dword dw), advanced by L items
             // per iteration without a division: L = dr rows + dq groups (plus one row on wrap)
             int q = 0, dw = 0, dq = 0, ddw = 0;
@@ -446,14 +326,11 @@ __host__ __device__ int fast_cell_detect(Pol& p, int sh, const CellGeom& g, int 
                                                  T32[dw - 2 * RW - 1], T32[dw - 2 * RW], T32[dw - 2 * RW + 1],
                                                  T32[dw + 2 * RW - 1], T32[dw + 2 * RW], T32[dw + 2 * RW + 1], tt, kt);
                     m8 = (sd.x | sd.y) & cs.emask[q];  // detection pixels of the row's first / last group
-                    if (FAST_2X1)  // the passing sides into the strength plane (0x80 bright, 0x40 dark)
-                        reinterpret_cast<uint32_t*>(M)[dw] = (sd.y & m8) | ((sd.x & m8) >> 1);
                 }
                 // the 4-bit pass mask (bit k = byte k) by one v_dot4_u32_u8 of the 0x80 bytes:
                 // 128 m4, so m4's 8-byte LUT entry sits at byte offset 128 m4 >> 4 (one shift)
                 const uint32_t m4x128 = __builtin_amdgcn_udot4(m8, 0x08040201u, 0u, false);
                 const int c = __builtin_popcount(m8);
-#if FAST_DPP_SCAN
                 // this lane's list position: an inclusive scan of c over the wave by DPP (rows of
                 // 16 by row_shr 1 / 2 / 4 / 8, then row_bcast 15 / 31 across rows; 6 v_add_u32_dpp),
                 // instead of bit-sliced ballots + 6 v_mbcnt (16 VALU)
@@ -466,11 +343,6 @@ __host__ __device__ int fast_cell_detect(Pol& p, int sh, const CellGeom& g, int 
                 incl += __builtin_amdgcn_update_dpp(0, incl, 0x143, 0xC, 0xF, false); // row_bcast:31 -> rows 2, 3
                 const int pos = na + incl - c;
                 const int wave_total = __builtin_amdgcn_readlane(incl, 63);
-#else
-                const uint64_t b0 = p.ballot(c & 1), b1 = p.ballot(c & 2), b2 = p.ballot(c & 4);
-                const int pos = na + rank(b0) + 2 * rank(b1) + 4 * rank(b2);
-                const int wave_total = p.popc64(b0) + 2 * p.popc64(b1) + 4 * p.popc64(b2);
-#endif
                 // the lane's c entries 4 dw + (set bit positions), as u16 pairs from the table,
                 // written to 4 consecutive slots from pos; slots past c hold garbage that a later
                 // lane's entry overwrites (its slot index k is smaller, and the slots are written
@@ -479,28 +351,6 @@ __host__ __device__ int fast_cell_detect(Pol& p, int sh, const CellGeom& g, int 
                 const uint2 lv = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint8_t*>(cs.lut) + (m4x128 >> 4));
                 const uint32_t e01 = __umul24((uint32_t)(4 * dw), 0x10001u) + lv.x;  // v_mad_u32_u24
                 const uint32_t e23 = __umul24((uint32_t)(4 * dw), 0x10001u) + lv.y;
-#if FAST_SINK == 1  // measurement variant: lanes without candidates write nothing
-                if (c) {
-                    uint16_t* d = list + pos;
-                    d[3] = (uint16_t)(e23 >> 16);
-                    asm volatile("" ::: "memory");
-                    d[2] = (uint16_t)e23;
-                    asm volatile("" ::: "memory");
-                    d[1] = (uint16_t)(e01 >> 16);
-                    asm volatile("" ::: "memory");
-                    d[0] = (uint16_t)e01;
-                }
-#elif FAST_SINK == 2  // measurement variant: one sink column per lane (no shared address)
-                uint16_t* d = c ? list + pos : sink + 2 * lane;
-                const int st = c ? 1 : 128;
-                d[3 * st] = (uint16_t)(e23 >> 16);
-                asm volatile("" ::: "memory");
-                d[2 * st] = (uint16_t)e23;
-                asm volatile("" ::: "memory");
-                d[st] = (uint16_t)(e01 >> 16);
-                asm volatile("" ::: "memory");
-                d[0] = (uint16_t)e01;
-#else
                 uint16_t* d = c ? list + pos : sink;
                 d[3] = (uint16_t)(e23 >> 16);
                 asm volatile("" ::: "memory");  // keep the slot order (k = 3 .. 0)
@@ -509,7 +359,6 @@ __host__ __device__ int fast_cell_detect(Pol& p, int sh, const CellGeom& g, int 
                 d[1] = (uint16_t)(e01 >> 16);
                 asm volatile("" ::: "memory");
                 d[0] = (uint16_t)e01;
-#endif
                 na += wave_total;
                 q += dq;
                 dw += ddw;
@@ -522,7 +371,6 @@ __host__ __device__ int fast_cell_detect(Pol& p, int sh, const CellGeom& g, int 
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
-#endif
 #else
         for (int base = i0; base < i1; base += L) {
             const bool in = base + lane < i1;
@@ -542,53 +390,6 @@ __host__ __device__ int fast_cell_detect(Pol& p, int sh, const CellGeom& g, int 
             na += p.popc64(m);
         }
 #endif
-#if FAST_VAR == 3
-        return na;
-#endif
-#if defined(__HIP_DEVICE_COMPILE__) && FAST_2X1
-        // exact strength of every candidate (m > t <=> corner at t), corners kept in order.  A
-        // batch is 128 candidates: lane j takes candidates base + j (half 0) and base + 64 + j
-        // (half 1) and evaluates only the side each passed (fast_strength_2x1, one packed
-        // evaluation for two candidates); a batch holding a candidate that passed both sides
-        // (0.1% of candidates on the SURVEY frames) evaluates both sides of each candidate
-        // instead (fast_strength_packed).  The next batch's entries are read one batch ahead (the
-        // in-place writes of a batch land below its own end, never on entries not yet read).
-        int nb = 0;
-        auto ent = [&](int j) { return (int)list[j < na ? j : na - 1]; };
-        int oa_n = na > 0 ? ent(lane) : 0, ob_n = na > 0 ? ent(64 + lane) : 0;
-        for (int base = 0; base < na; base += 128) {
-            const int ja = base + lane, jb = base + 64 + lane;
-            const int oa = oa_n, ob = ob_n;
-            if (base + 128 < na) {
-                oa_n = ent(base + 128 + lane);
-                ob_n = ent(base + 192 + lane);
-            }
-            const int fa = M[oa], fb = M[ob];  // pass flags: 0x80 bright, 0x40 dark
-            int sa, sb;
-#if FAST_VAR == 1  // measurement variant: every candidate a corner of strength t + 1
-            sa = sb = t + 1;
-#else
-            if (p.ballot((ja < na && fa == 0xC0) || (jb < na && fb == 0xC0))) {
-                sa = fast_strength_packed<CP>(&T[oa]);
-                sb = fast_strength_packed<CP>(&T[ob]);
-            } else {
-                // the pairs are packed with a v_perm per ring point: on gfx950 a
-                // ds_read_u8_d16_hi zeroes the low half of its register instead of keeping it
-                // (tools/d16_probe.hip), so the two bytes cannot be loaded into one register
-                fast_strength_2x1<CP>(&T[oa], &T[ob], (fa & 0x80) != 0, (fb & 0x80) != 0, &sa, &sb);
-            }
-#endif
-            const bool ca = ja < na && sa > t, cb = jb < na && sb > t;
-            const uint64_t ba = p.ballot(ca), bb = p.ballot(cb);
-            // the strength plane: m for corners, 0 for the other candidates (flags cleared)
-            if (ja < na) M[oa] = (uint8_t)(ca ? sa : 0);
-            if (jb < na) M[ob] = (uint8_t)(cb ? sb : 0);
-            if (ca) list[nb + p.rank(ba)] = (uint16_t)oa;  // in place: never passes the reads
-            if (cb) list[nb + p.popc64(ba) + p.rank(bb)] = (uint16_t)ob;
-            nb += p.popc64(ba) + p.popc64(bb);
-        }
-        return nb;
-#else
         // exact strength of every candidate (m > t <=> corner at t), corners kept in order; the
         // next batch's list entries are read one batch ahead (the in-place writes of a batch
         // land below its own start, never on entries not yet read)
@@ -598,11 +399,7 @@ __host__ __device__ int fast_cell_detect(Pol& p, int sh, const CellGeom& g, int 
             const int j = base + lane;
             const int o = o_next;
             if (base + L < na) o_next = list[base + L + lane < na ? base + L + lane : na - 1];
-#if FAST_VAR == 1  // measurement variants (tools/build_variants.sh): 1 = every candidate a corner of strength t + 1
-            const int sm = t + 1;
-#else
             const int sm = fast_strength_packed<CP>(&T[o]);
-#endif
             const bool f = j < na && sm > t;
             const uint64_t m = p.ballot(j < na) & p.ballot(sm > t);  // two compares' masks, ANDed on the SALU
             if (f) {
@@ -612,7 +409,6 @@ __host__ __device__ int fast_cell_detect(Pol& p, int sh, const CellGeom& g, int 
             nb += p.popc64(m);
         }
         return nb;
-#endif
     };
     // nonmax at t for every corner of the list; the verdict is kept in bit 15 of the entry
     // (LDS offsets < 6400 use 13 bits) for the ordered write
@@ -636,9 +432,6 @@ __host__ __device__ int fast_cell_detect(Pol& p, int sh, const CellGeom& g, int 
         return make_int2(tot, before);
     };
     int nb = build(tini);
-#if FAST_VAR == 3 || FAST_VAR == 4  // measurement variants: pre-test (+ strength) at iniThFAST only
-    return nb;
-#endif
     p.sync();  // M complete: nonmax reads neighbours owned by other waves
     int2 cb = count_kept(nb, tini);
     int t = tini;
@@ -675,9 +468,6 @@ __host__ __device__ int fast_cell_run(Pol& p, const uint8_t* src, long long pitc
                                       const CellScratch& cs, uint32_t* keys_out, Ld16 ld16) {
     fast_cell_stage<CP>(p, src, pitch, sh, dword_ok, g, cs, ld16);
     p.sync();
-#if FAST_VAR == 2  // measurement variant: staging only
-    return cs.T[p.tid()] & 1;
-#endif
     return fast_cell_detect<CP>(p, sh, g, ini_th, min_th, cs, keys_out);
 }
 

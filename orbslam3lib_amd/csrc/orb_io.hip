@@ -100,4 +100,58 @@ hipError_t launch_pack_soa(const SoaArgs& a, int npairs, hipStream_t st) {
     return hipGetLastError();
 }
 
+// orbgpu_export_batch's packed layout (include/orbgpu.h), produced rows only.  blockIdx.y < nimages:
+// image y's keypoints then descriptors (15 dwords per row); otherwise pair y - nimages's four match
+// arrays (4 dwords per query row).  Each workgroup finds its unit's offset from the device counts
+// (the host checked them: no status codes); workgroup (0, 0) also writes the header.
+__global__ __launch_bounds__(256) void k_pack_export(ExportArgs a) {
+    __shared__ long long s_off;
+    const int y = blockIdx.y;
+    const bool img = y < a.nimages;
+    const int u = img ? y : y - a.nimages;
+    if (threadIdx.x == 0) s_off = 0;
+    __syncthreads();
+    {   // offset in dwords past the header: 15 per row of every earlier image (all images before a
+        // pair), 4 per query row of every earlier pair
+        long long part = 0;
+        const int nimg = img ? u : a.nimages;
+        for (int i = threadIdx.x; i < nimg; i += 256) part += 15LL * a.out_n[i];
+        if (!img)
+            for (int p = threadIdx.x; p < u; p += 256) part += 4LL * a.nq[p];
+        if (part) atomicAdd(reinterpret_cast<unsigned long long*>(&s_off), (unsigned long long)part);
+    }
+    __syncthreads();
+    uint32_t* dst = reinterpret_cast<uint32_t*>(a.dst);
+    const int hdr = 2 * a.nimages + a.npairs;
+    if (blockIdx.x == 0 && y == 0)
+        for (int i = threadIdx.x; i < hdr; i += 256)
+            dst[i] = (uint32_t)(i < a.nimages ? a.out_n[i] : i < 2 * a.nimages ? a.out_mono[i - a.nimages]
+                                                                                 : a.nq[i - 2 * a.nimages]);
+    uint32_t* out = dst + hdr + s_off;
+    const long long stride = (long long)gridDim.x * 256;
+    if (img) {
+        const long long n = a.out_n[u];
+        const uint32_t* kp = reinterpret_cast<const uint32_t*>(static_cast<const uint8_t*>(a.kps) + (long long)u * a.out_cap * 28);
+        const uint32_t* de = reinterpret_cast<const uint32_t*>(a.desc + (long long)u * a.out_cap * 32);
+        for (long long t = (long long)blockIdx.x * 256 + threadIdx.x; t < 15 * n; t += stride)
+            out[t] = t < 7 * n ? kp[t] : de[t - 7 * n];
+    } else {
+        const long long n = a.nq[u], o = (long long)u * a.out_cap;
+        for (long long t = (long long)blockIdx.x * 256 + threadIdx.x; t < 4 * n; t += stride) {
+            const long long k = t / n, r = t - k * n;
+            const int32_t* s = k == 0 ? a.idx1 : k == 1 ? a.dist1 : k == 2 ? a.idx2 : a.dist2;
+            out[t] = (uint32_t)s[o + r];
+        }
+    }
+}
+
+hipError_t launch_pack_export(const ExportArgs& a, hipStream_t st) {
+    const unsigned gy = (unsigned)(a.nimages + a.npairs);
+    if (gy == 0) return hipSuccess;
+    // enough workgroups per unit for the largest image's 15 dwords per row
+    const unsigned gx = (unsigned)std::max(1, std::min(64, (15 * a.out_cap + 1023) / 1024));
+    hipLaunchKernelGGL(k_pack_export, dim3(gx, gy), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+
 }  // namespace orbgpu

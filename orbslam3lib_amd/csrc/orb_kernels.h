@@ -67,6 +67,7 @@ struct BatchArgs {
     long long octws_img_stride;
     uint32_t* lvlkey;                // [img][level kps] packed key
     float* lvlangle;                 // [img][level kps]
+    float2* lvlsc;                   // [img][level kps] (sin, cos) of the keypoint's rotation (k_orient)
     uint8_t* lvldesc;                // [img][level kps][32]
     int lvlkp_img_stride;            // keypoints
     int32_t* lvlcnt;                 // [img][kMaxLevels]
@@ -79,7 +80,8 @@ struct BatchArgs {
     const int32_t* laps;             // [img][2]
     int total_cells, total_tiles, total_od_blocks;
     int fast_tab_off;  // rtab index of k_fast_cells' per-cell records (2 int4 per flattened cell)
-    int od_tab_off;    // rtab index of k_orient_desc's per-block records {level, 0, 0, 0}
+    int od_tab_off;    // rtab index of k_desc's per-block records {level, block, 0, 0}
+    int or_tab_off, total_or_blocks;  // k_orient's per-block records {level, block of the level}
     int fast_n48;  // k_fast_cells records [0, fast_n48) run the 48-byte FAST tile,
     int fast_n64;  // [fast_n48, fast_n64) the 64-byte one, the rest the 80-byte one (records are
                    // grouped by tile, levels in order inside each group)
@@ -199,23 +201,13 @@ struct GridArgs {
 // Octree workspace layout for one (image, level) with n_cap keys and node capacity C.  The node
 // state lives in LDS when C <= kOctLdsNodes, otherwise in the `nodemem` part of this block.
 constexpr int kOctLdsNodes = 1024;
-#ifndef OD_LANES
-#define OD_LANES 32
-#endif
-constexpr int kOdKpBlock = 256 / OD_LANES;  // keypoints per k_orient_desc pass (256 threads / lanes per keypoint)
-#ifndef OD_BATCH
-#define OD_BATCH 0  // k_orient_desc: moments, then one angle pass per batch, then descriptors (0: per pair)
-#endif
-#ifndef OD_WB
-#define OD_WB 16
-#endif
-constexpr int kOdWaveBatch = OD_WB;  // OD_BATCH: keypoints per wave batch
-// keypoints per k_orient_desc workgroup by default: 4 waves x one batch (OD_BATCH), or 3 passes of
-// kOdKpBlock (the per-pair kernel).  Round 5, chunked moments, single stream per 512 images: 1 pass
-// 553 us, 2 passes 483, 3 passes 463, 4 passes 467; headline at 3 vs 2 passes +0.2 to +2.3% (bench
-// A/B, 3 rounds).  Round 3 (per-row moments) had 2 passes best.  Contexts of a few images take 1
+constexpr int kOdKpBlock = 8;  // keypoints per k_orient_desc pass (256 threads, 32 lanes per keypoint)
+// keypoints per k_orient_desc workgroup by default: 3 passes of kOdKpBlock.  Round 5, chunked
+// moments, single stream per 512 images: 1 pass 553 us, 2 passes 483, 3 passes 463, 4 passes 467;
+// headline at 3 vs 2 passes +0.2 to +2.3% (bench A/B, 3 rounds).  Contexts of a few images take 1
 // (orb_runtime.cpp set_geometry).
-constexpr int kOdBlockKps = OD_BATCH ? 4 * kOdWaveBatch : 3 * kOdKpBlock;
+constexpr int kOdBlockKps = 3 * kOdKpBlock;
+constexpr int kOrientBlockKps = 256;  // keypoints per k_orient workgroup (4 waves x 64)
 
 constexpr int kOctLdsKeys = 16384;  // per-key node labels (u16) kept in LDS up to this many keys
 constexpr int kFastMergeMaxImages = 4;  // launches this small run the 48/64 FAST cells as one launch
@@ -355,6 +347,18 @@ hipError_t launch_sbp(const SbpArgs& a, int nframes, int max_mps, hipStream_t st
 
 hipError_t launch_sbs_split(const SbsArgs& a, hipStream_t st);
 hipError_t launch_pack_soa(const SoaArgs& a, int npairs, hipStream_t st);
+// orbgpu_export_batch (orb_io.hip k_pack_export): the produced rows of a batch, packed
+struct ExportArgs {
+    const void* kps;          // out_kps [img][out_cap] (28 B)
+    const uint8_t* desc;      // out_desc [img][out_cap][32]
+    const int32_t* out_n;     // [img] (>= 0: the host checked)
+    const int32_t* out_mono;  // [img]
+    const int32_t* nq;        // [pair]
+    const int32_t *idx1, *dist1, *idx2, *dist2;  // [pair][out_cap]
+    int out_cap, nimages, npairs;
+    void* dst;                // device buffer, 4-byte aligned
+};
+hipError_t launch_pack_export(const ExportArgs& a, hipStream_t st);
 hipError_t launch_knn2_plain(const uint8_t* q, int nq, const uint8_t* t, int nt, int32_t* i1,
                              int32_t* d1, int32_t* i2, int32_t* d2, hipStream_t s);
 

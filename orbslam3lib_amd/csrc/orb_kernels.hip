@@ -8,12 +8,11 @@
 //                          3x3 nonmax at iniTh / minTh fallback, ordered compaction (one launch
 //                          per LDS tile size)
 //   k_octree      x 1      one workgroup per (image, level): DistributeOctTree
-//   k_orient_desc x 1      32 lanes per keypoint: IC_Angle + rBRIEF 256 bit
+//   k_orient     x 1      32 lanes per keypoint for the moments, then one lane per keypoint:
+//                          IC_Angle and the sin / cos of its rotation
+//   k_desc       x 1      32 lanes per keypoint: rBRIEF 256 bit from an LDS-staged patch
 //   k_finalize    x 1      one workgroup per image: scale + mono/stereo partition
 //   k_knn2_mfma   x 1      Hamming k=2 brute force on the i8 matrix cores
-#ifndef BR_VAR
-#define BR_VAR 0
-#endif
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -47,31 +46,6 @@ __constant__ PatternTable c_pattern = make_pattern();
 // umax[] of the ORBextractor ctor (ORBextractor_old.cc:455-470) for HALF_PATCH_SIZE = 15.
 __constant__ int c_umax[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};
 
-// Byte weights for the IC_Angle moments with v_dot4_u32_u8: for disc row |v| and dword j of the
-// 32-byte window starting at u = -16: {1 inside the disc, max(u,0) inside, max(-u,0) inside}.
-struct MomentWeights {
-    uint32_t w[16][8][3];
-};
-constexpr MomentWeights make_moment_weights() {
-    MomentWeights t{};
-    const int umax[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};
-    for (int av = 0; av < 16; ++av)
-        for (int j = 0; j < 8; ++j) {
-            uint32_t one = 0, pos = 0, neg = 0;
-            for (int b = 0; b < 4; ++b) {
-                const int u = 4 * j + b - 16;
-                const bool in = (u < 0 ? -u : u) <= umax[av];
-                one |= (uint32_t)(in ? 1 : 0) << (8 * b);
-                pos |= (uint32_t)(in && u > 0 ? u : 0) << (8 * b);
-                neg |= (uint32_t)(in && u < 0 ? -u : 0) << (8 * b);
-            }
-            t.w[av][j][0] = one;
-            t.w[av][j][1] = pos;
-            t.w[av][j][2] = neg;
-        }
-    return t;
-}
-__constant__ MomentWeights c_mw = make_moment_weights();
 
 // ---------------------------------------------------------------------------------------------
 // ---------------------------------------------------------------------------------------------
@@ -225,85 +199,6 @@ __device__ inline uint4 blur_chunk(const BatchArgs& a, const BlurTile& bt, int i
     return make_uint4(v[0], v[1], v[2], v[3]);
 }
 
-// Filters one staged 128 x 32 tile (window in tin4: rows ty0-4 .., cols tx0-16 ..) and writes
-// its output rows inside [rlo, rhi).  The caller synchronizes after staging the window and
-// before the next tile reuses tin4 / hp.
-__device__ inline void blur_tile_compute(const LevelGeom& G, int tx0, int ty0, uint8_t* dst,
-                                         uint4 (*tin4)[(kBlurTW + 32) / 16],
-                                         uint4 (*hp)[kBlurTW / 4], int rlo, int rhi) {
-    constexpr int IW = kBlurTW + 32, IH = kBlurTH + 8, NRP = IH / 2;
-    const uint32_t(*tin)[IW / 4] = reinterpret_cast<const uint32_t(*)[IW / 4]>(&tin4[0][0]);
-    if (tx0 == 0 || tx0 + kBlurTW + 3 > G.w) {  // REFLECT_101 of the 3 columns past each edge
-        uint8_t* wb = reinterpret_cast<uint8_t*>(&tin4[0][0]);
-        for (int i = threadIdx.x; i < IH * 6; i += 256) {
-            const int r = i / 6, k = i - 6 * r;
-            const int xx = k < 3 ? -1 - k : G.w + (k - 3);  // plane column to fill
-            const int wx = xx - (tx0 - 16);                  // its window column
-            if (wx >= 0 && wx < IW && (k < 3 ? tx0 == 0 : true)) {
-                const int sx = refl101(xx, G.w) - (tx0 - 16);
-                wb[r * IW + wx] = wb[r * IW + sx];
-            }
-        }
-        __syncthreads();
-    }
-    // horizontal: item (row pair rp, column quad cq) -> output cols 4cq..4cq+3 need window
-    // bytes 4cq+13 .. 4cq+22 (dwords cq+3 .. cq+5)
-    for (int i = threadIdx.x; i < NRP * (kBlurTW / 4); i += 256) {
-        const int rp = i >> 5, cq = i & 31;
-        uint32_t A[3], B[3];
-#pragma unroll
-        for (int d = 0; d < 3; ++d) {
-            A[d] = tin[2 * rp][cq + 3 + d];
-            B[d] = tin[2 * rp + 1][cq + 3 + d];
-        }
-        uint32_t h[4];
-        hsum_pair(A, B, h);
-        hp[rp][cq] = make_uint4(h[0], h[1], h[2], h[3]);
-    }
-    __syncthreads();
-    // vertical: thread -> column quad cq, output rows R rg .. R rg + R - 1 (row pairs
-    // (R/2) rg .. (R/2) rg + R/2 + 3); output row r takes window rows r + 1 .. r + 7
-    constexpr int R = kBlurTH / 8;
-    const int cq = threadIdx.x & 31, rg = threadIdx.x >> 5;
-    uint32_t V[R / 2 + 4][4];
-#pragma unroll
-    for (int k = 0; k < R / 2 + 4; ++k) {
-        const uint4 q = hp[(R / 2) * rg + k][cq];
-        V[k][0] = q.x;
-        V[k][1] = q.y;
-        V[k][2] = q.z;
-        V[k][3] = q.w;
-    }
-    const u16x2 WE[4] = {as_u16x2(0u | (18u << 16)), as_u16x2(34u | (48u << 16)),
-                         as_u16x2(56u | (48u << 16)), as_u16x2(34u | (18u << 16))};
-    const u16x2 WO[4] = {as_u16x2(18u | (34u << 16)), as_u16x2(48u | (56u << 16)),
-                         as_u16x2(48u | (34u << 16)), as_u16x2(18u | (0u << 16))};
-    const int x = tx0 + 4 * cq;
-    // this thread's rows ybase .. ybase + R - 1: the ones inside [rlo, rhi) and the plane, at one
-    // compare per row; the row address from a per-thread base plus a uniform row offset
-    const int ybase = ty0 + R * rg;
-    const int ylo = max(rlo, ybase), yhi = x < G.w ? min(min(rhi, G.h), ybase + R) : ybase;
-    const int olo = ylo - ybase, ohi = yhi - ybase;
-    uint8_t* dbase = dst + plane_off(ybase, G.bpitch, x);
-#pragma unroll
-    for (int o = 0; o < R; ++o) {
-        const int k0 = (o + 1) >> 1;  // first row pair: o=0 -> 0, 1 -> 1, 2 -> 1, 3 -> 2, ...
-        uint32_t sv[4];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            uint32_t acc = 1u << 15;
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-                acc = __builtin_amdgcn_udot2(as_u16x2(V[k0 + k][c]), (o & 1) ? WO[k] : WE[k], acc, false);
-            sv[c] = acc;
-        }
-        // byte 2 of each sum is the result (sum < 2^24)
-        const uint32_t lo = __builtin_amdgcn_perm(sv[1], sv[0], 0x0c0c0602u);
-        const uint32_t hi = __builtin_amdgcn_perm(sv[3], sv[2], 0x0c0c0602u);
-        const uint32_t packed = lo | (hi << 16);
-        if (o >= olo && o < ohi) *reinterpret_cast<uint32_t*>(dbase + o * G.bpitch) = packed;
-    }
-}
 
 // The same 128 x 32 blur tile as two int8 GEMMs on the matrix cores (v_mfma_i32_32x32x32_i8; the
 // 7-tap kernel is banded, the zeros cost MFMA cycles that are otherwise idle, and the VALU keeps
@@ -322,10 +217,8 @@ __device__ inline void blur_tile_compute(const LevelGeom& G, int tx0, int ty0, u
 //     the rounded output byte (S + 2^15) >> 16 is byte 2 of 256 D2hi + D2lo + 2^16 (which stays
 //     in [-2^23, 2^23)) with bit 7 flipped.  The + 2^16 rides in K slot 4 of M-block 1 (a row >= 40
 //     that no output reads) in both lane halves: A2hi = -1 there, B = -128, 2 x 128 into D2hi.
-// Exact integer arithmetic throughout (no intermediate rounding), so bit-exact with the VALU path.
-#ifndef BLUR_MFMA
-#define BLUR_MFMA 1
-#endif
+// Exact integer arithmetic throughout (no intermediate rounding), so bit-exact with the fixed-point
+// filter the oracle restates (tests/test_blur_mfma_model.py replays the lane layouts on the CPU).
 typedef int blur_v4i __attribute__((ext_vector_type(4)));
 typedef int blur_v16i __attribute__((ext_vector_type(16)));
 struct BlurMfmaTab {
@@ -436,11 +329,6 @@ __device__ inline void blur_tile_compute_mfma(const LevelGeom& G, int tx0, int t
     for (int o = 0; o < R; ++o)
         if (o >= olo && o < ohi) *reinterpret_cast<uint32_t*>(dbase + o * G.bpitch) = ob[(R * rg + o) * (OP / 4) + cq];
 }
-#if BLUR_MFMA
-#define BLUR_TILE_COMPUTE blur_tile_compute_mfma
-#else
-#define BLUR_TILE_COMPUTE blur_tile_compute
-#endif
 
 // Persistent over the tiles of the launch (images x levels x tiles): the next tile's window
 // is loaded into registers while the current one is filtered, so the global-memory round
@@ -486,7 +374,7 @@ __global__ __launch_bounds__(256) void k_blur(BatchArgs a, int tile0, int ntile)
             }
         }
         __syncthreads();
-        BLUR_TILE_COMPUTE(G, tx0, ty0, dst, tin4, hp, 0, G.h);
+        blur_tile_compute_mfma(G, tx0, ty0, dst, tin4, hp, 0, G.h);
     }
 }
 
@@ -570,12 +458,7 @@ __device__ inline void br_tile(const BatchArgs& a, int l, bool resize, int img, 
         if (i < IH * IWQ) (&sm.tin4[0][0])[i] = pre[c];
     }
     __syncthreads();
-#if BR_VAR != 2 && BR_VAR != 3  // measurement variants (tools/build_variants.sh): 2, 3 skip the blur
-    BLUR_TILE_COMPUTE(S, bt.tx0, bt.ty0, bt.dst, sm.tin4, sm.hp, 0, S.h);  // fixes only off-plane columns
-#endif
-#if BR_VAR == 1 || BR_VAR == 3  // 1, 3 skip the resize
-    return;
-#endif
+    blur_tile_compute_mfma(S, bt.tx0, bt.ty0, bt.dst, sm.tin4, sm.hp, 0, S.h);  // fixes only off-plane columns
     if (!resize) return;
     // resize from the window: window row r = source row ty0 - 4 + r, column c = tx0 - 16 + c
     const uint8_t* wb = reinterpret_cast<const uint8_t*>(&sm.tin4[0][0]);
@@ -890,9 +773,6 @@ hipError_t launch_pyr_tail(const BatchArgs& a, hipStream_t s) {
 // ComputeKeyPointsOctTree (ORBextractor_old.cc:807-871) with cv::FAST(cell, kps, th, true):
 // detection on [3,rows-3)x[3,cols-3) of the cell ROI, 3x3 nonmax inside the cell only, iniTh
 // then minTh if the cell yields nothing, keys emitted in row-major order.
-#ifndef FAST_FIXED_POLICY
-#define FAST_FIXED_POLICY 1  // compile-time workgroup size in the cell code (0: blockDim, A/B only)
-#endif
 
 template <int CP>
 __global__ __launch_bounds__(fast_threads<CP>()) void k_fast_cells(BatchArgs a, int cell0, uint32_t ncell_magic) {
@@ -938,11 +818,7 @@ __global__ __launch_bounds__(fast_threads<CP>()) void k_fast_cells(BatchArgs a, 
         const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, roi32 + (int)off, 0, 0);
         return make_uint4(v[0], v[1], v[2], v[3]);
     };
-#if FAST_FIXED_POLICY
     FixedDevPolicy<kFastThreads> p{{scratch}};
-#else
-    DevPolicy p{scratch};
-#endif
     fast_cell_tables<CP>(g, sh, lut, emask);  // synced with the ROI staging (fast_cell_run)
     CellScratch cs{T, M, list, wcnt, lut, emask};
     const int n = fast_cell_run<CP>(p, src, G.pitch, sh, dword_ok, g, a.ini_th, a.min_th, cs, key_out, ld16);
@@ -1089,13 +965,7 @@ __global__ __launch_bounds__(NT) void k_octree(BatchArgs a, int l0, OctCfg q) {
     extern __shared__ __attribute__((aligned(16))) uint8_t nodemem_lds[];  // per-launch size
     __shared__ int scratch[16];
     __shared__ OctShared sh;
-#ifdef OCT_IMAGE_MAJOR
-    const int nl = gridDim.y, tot = gridDim.x * gridDim.y;
-    const int lg = xcd_remap(blockIdx.x + blockIdx.y * gridDim.x, tot);
-    octree_level<true>(a, a.img0 + lg / nl, l0 + lg % nl, nodemem_lds, scratch, sh, q);
-#else
     octree_level<true>(a, a.img0 + blockIdx.x, l0 + blockIdx.y, nodemem_lds, scratch, sh, q);
-#endif
 }
 
 // The levels k_octree left with kOctRetry, redone with generic pointers: a small persistent
@@ -1113,7 +983,7 @@ __global__ __launch_bounds__(512, 1) void k_octree_retry(BatchArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------------
-constexpr int kOdLanes = OD_LANES;             // lanes per keypoint (orb_kernels.h)
+constexpr int kOdLanes = 32;                   // lanes per keypoint
 constexpr int kOdPairs = 256 / kOdLanes;       // test pairs per lane
 static_assert(kOdLanes == 32, "k_orient_desc: one disc row and 8 test pairs per lane");
 static_assert(kOdKpBlock == 256 / kOdLanes, "orb_kernels.h kOdKpBlock");
@@ -1137,266 +1007,61 @@ __device__ inline int od_sum(int v) {
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
-// k_orient_desc: IC_Angle on the raw level (ORBextractor_old.cc:78-105) then
-// computeOrbDescriptor on the blurred level (:108-148): a = (float)cos, b = (float)sin of
-// angle*pi/180 (float), sample center[cvRound(x*b + y*a)*step + cvRound(x*a - y*b)].
-// 32 lanes per keypoint (two independent groups per wave): lane `sub` owns disc row v = sub - 15
-// for the moments and test pairs [8 sub, 8 sub + 8), sampled from the keypoint's blurred patch
-// staged in LDS.  The kernel waits on dependent memory round trips per keypoint (key, moment
-// rows + patch); few vector-memory instructions and registers per lane keep many of them in
-// flight.
-#ifndef OD_CHUNKS
-#define OD_CHUNKS 1  // moments from coalesced 16-byte row chunks (0: a disc row per lane, round 4)
-#endif
-#ifndef OD_PIPE
-#define OD_PIPE 1  // issue the next pair's loads before the current pair's arithmetic
-#endif
-#ifndef OD_WPE
-#define OD_WPE 4  // 106 VGPRs without spills (6: 40 spilled, 5: 6 spilled)
-#endif
-#if OD_BATCH
-// Batched per wave (orb_kernels.h kOdWaveBatch keypoints): the moments of every pair of the
-// batch first (32 lanes per keypoint, coalesced row chunks as below), their sums to LDS; then
-// ONE pass with a lane per keypoint for fastAtan2 and sin / cos (the float division and the
-// double-precision libm arithmetic, ~90 VALU, were computed by all 32 lanes of a keypoint); then
-// the descriptors of every pair from the blurred patches.  Keys are read once per batch into LDS;
-// each phase issues the next pair's loads before the current pair's arithmetic.
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OD_WPE))) void k_orient_desc(
-    BatchArgs a, uint32_t nblk_magic) {
-    __shared__ __attribute__((aligned(16))) uint8_t patch[kOdKpBlock][kOdPatchRows * kOdPatchPitch];
+// IC_Angle (ORBextractor_old.cc:78-105) and computeOrbDescriptor (:108-148) as two kernels.
+// Round 5's single kernel ran fastAtan2 + libm sinf / cosf (~150 VALU: a float division and the
+// double-precision reduction) in all 32 lanes of every keypoint; here the angle and its sin / cos
+// are computed once per keypoint, one lane each:
+//   k_orient: 32 lanes per keypoint sum the moments (coalesced row chunks, below), 64 keypoints
+//     per wave (group g of 32 lanes takes keypoints kw + 32 g + p, p = 0..31), and lane p of
+//     group g keeps the sums of pass p; then every lane turns its keypoint's m_01 / m_10 into
+//     the angle (written to lvlangle) and sin / cos of angle * pi / 180 (lvlsc);
+//   k_desc: 32 lanes per keypoint sample the 256 test pairs from the keypoint's blurred patch
+//     staged in LDS, rotated by the (sin, cos) k_orient wrote.
+// Both keep the reference's float expressions operation by operation (no contraction).
+
+// Moments from coalesced row chunks: the 31 disc rows of a keypoint are read as 16-byte aligned
+// chunks of the 48-byte window that starts at xa16 = (x - 15) & ~15 (it holds x - 15 .. x + 15
+// for every x).  Chunk slot i = sub + 32 it (it < 3) is disc row r = i / 3 (v = r - 15; r = 31
+// lies past the disc) and part i % 3, so the three lanes of a row read 48 contiguous bytes.
+// Each chunk adds its masked byte sums: s = sum of p, c = sum of (column - xa16) p over the disc
+// span |u| <= umax[|v|], i.e. chunk bytes [m, n) with m, n from the alignment a = (x - 15) & 15
+// and two per-lane constants; the byte masks of every [m, n) are an LDS table, so a chunk is one
+// b128 LDS read, 4 ANDs and 8 v_dot4_u32_u8.  Then m_10 = sum c - (15 + a) sum s and
+// m_01 = sum v s.
+constexpr int kOrWaveKps = 64;                 // keypoints per k_orient wave
+constexpr int kOrBlockKps = 4 * kOrWaveKps;    // per 256-thread workgroup
+static_assert(kOrBlockKps == kOrientBlockKps, "orb_kernels.h kOrientBlockKps");
+
+__global__ __launch_bounds__(256) void k_orient(BatchArgs a, uint32_t nblk_magic) {
     __shared__ __attribute__((aligned(16))) uint4 s_rng[17][17];  // bytes [m, n) of 16 (none if n <= m)
-    __shared__ __attribute__((aligned(16))) uint4 s_pat[kOdPairs][kOdLanes];
-    __shared__ uint32_t s_key[4][kOdWaveBatch];
-    __shared__ int2 s_mom[4][kOdWaveBatch];
-    __shared__ __attribute__((aligned(16))) float4 s_ang[4][kOdWaveBatch];  // angle, sin, cos
     const int wg = xcd_remap(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * gridDim.y);
     const int irel = gridDim.x == 1 ? wg : (int)__umulhi((uint32_t)wg, nblk_magic);
     const int img = a.img0 + irel, bx = wg - irel * (int)gridDim.x;
-    const int l = a.rtab[a.od_tab_off + bx].x;
+    const int4 rec = a.rtab[a.or_tab_off + bx];  // {level, block of the level}
+    const int l = rec.x;
     const LevelGeom G = a.lv[l];
-    const int sub = threadIdx.x % kOdLanes, grp = threadIdx.x / kOdLanes;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, half = grp & 1;
+    for (int e = threadIdx.x; e < 17 * 17; e += 256) {
+        const int m = e / 17, n = e - 17 * m;
+        uint32_t w4[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            w4[k] = 0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) w4[k] |= (4 * k + j >= m && 4 * k + j < n ? 0xFFu : 0u) << (8 * j);
+        }
+        s_rng[m][n] = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63, sub = lane & 31, grp = lane >> 5;
     const int count = a.lvlcnt[img * kMaxLevels + l];
+    const int kw = rec.y * kOrBlockKps + (threadIdx.x >> 6) * kOrWaveKps;  // the wave's first keypoint
+    if (kw >= count) return;
+    const int npass = min(32, count - kw);  // wave-uniform; group 1 runs past its keypoints
     const long long kbase = (long long)img * a.lvlkp_img_stride + G.kp_off;
     const uint8_t* lvl = a.lvl_base[l] + (long long)img * G.img_stride;
-    const uint8_t* blr = a.blur_base[l] + (long long)img * G.bimg_stride;
     const bool raw_dw = ((G.pitch | G.img_stride) & 3) == 0;
-    const __amdgpu_buffer_rsrc_t brs =
-        __builtin_amdgcn_make_buffer_rsrc((void*)blr, (short)0, G.bpitch * G.h, 0x00020000);
     const __amdgpu_buffer_rsrc_t lrs =
         __builtin_amdgcn_make_buffer_rsrc((void*)lvl, (short)0, (int)min((long long)G.pitch * G.h, 0x7fffffffLL), 0x00020000);
-    for (int e = threadIdx.x; e < 17 * 17; e += 256) {
-        const int m = e / 17, n = e - 17 * m;
-        uint32_t w4[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            w4[k] = 0;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) w4[k] |= (4 * k + j >= m && 4 * k + j < n ? 0xFFu : 0u) << (8 * j);
-        }
-        s_rng[m][n] = make_uint4(w4[0], w4[1], w4[2], w4[3]);
-    }
-    {
-        const int8_t* pv = c_pattern.v + 4 * threadIdx.x;  // x0, y0, x1, y1 of pair threadIdx.x
-        s_pat[threadIdx.x % kOdPairs][threadIdx.x / kOdPairs] = make_uint4(__float_as_uint((float)pv[0]), __float_as_uint((float)pv[2]),
-                                        __float_as_uint((float)pv[1]), __float_as_uint((float)pv[3]));
-    }
-    __syncthreads();
-    // this lane's three moment chunk slots (as the OD_CHUNKS kernel below)
-    int mv[3], mlo[3], mhi[3], mofs[3], mp16[3];
-#pragma unroll
-    for (int it = 0; it < 3; ++it) {
-        const int i = sub + 32 * it, r = i / 3, part = i - 3 * r;
-        mv[it] = r - 15;
-        const int d = r < 31 ? c_umax[mv[it] < 0 ? -mv[it] : mv[it]] : -1;
-        mlo[it] = 15 - d - 16 * part;
-        mhi[it] = 16 + d - 16 * part;
-        mofs[it] = (r < 31 ? mv[it] : 15) * G.pitch + 16 * part;
-        mp16[it] = 16 * part;
-    }
-    uint8_t* pt = patch[grp];
-    auto wave_sync = [] {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    };
-    auto moment_loads = [&](uint32_t key, uint4 mc[3]) __attribute__((always_inline)) {
-        const int x = key_x(key) + kMinBorder, y = key_y(key) + kMinBorder;
-        const int wofs = y * G.pitch + (x - 15 - ((x - 15) & 15));
-#pragma unroll
-        for (int it = 0; it < 3; ++it) {
-            if (raw_dw) {
-                const auto q = __builtin_amdgcn_raw_buffer_load_b128(lrs, wofs + mofs[it], 0, 0);
-                mc[it] = make_uint4(q[0], q[1], q[2], q[3]);
-            } else {  // level-0 rows not 4-byte aligned: bytes
-                const uint8_t* q = lvl + wofs + mofs[it];
-                uint32_t d4[4];
-#pragma unroll
-                for (int k = 0; k < 4; ++k)
-                    d4[k] = (uint32_t)q[4 * k] | ((uint32_t)q[4 * k + 1] << 8) | ((uint32_t)q[4 * k + 2] << 16) |
-                            ((uint32_t)q[4 * k + 3] << 24);
-                mc[it] = make_uint4(d4[0], d4[1], d4[2], d4[3]);
-            }
-        }
-    };
-    auto patch_loads = [&](uint32_t key, uint4 pv[kOdPatchIt]) __attribute__((always_inline)) {
-        const int x = key_x(key) + kMinBorder, y = key_y(key) + kMinBorder;
-        const int pofs = (y - kOdPatchR) * G.bpitch + ((x - kOdPatchR) & ~3);
-#pragma unroll
-        for (int it = 0; it < kOdPatchIt; ++it) {
-            const int c = sub + it * kOdLanes;
-            const int r = c / 3, part = c - 3 * r;
-            if (c < kOdPatchChunks) {
-                const auto q = __builtin_amdgcn_raw_buffer_load_b128(brs, pofs + r * G.bpitch + 16 * part, 0, 0);
-                pv[it] = make_uint4(q[0], q[1], q[2], q[3]);
-            }
-        }
-    };
-    const int wave_stride = G.od_blocks * 4 * kOdWaveBatch;
-    for (int base = ((bx - G.od_first) * 4 + w) * kOdWaveBatch; base < count; base += wave_stride) {
-        const int nkb = min(kOdWaveBatch, count - base);  // wave-uniform
-        if (lane < nkb) s_key[w][lane] = a.lvlkey[kbase + base + lane];
-        wave_sync();
-        // keypoint j + half of pair j / 2 (the odd group of a last odd pair repeats keypoint j)
-        auto key_of = [&](int j) { return s_key[w][j + half < nkb ? j + half : j]; };
-        // ---- IC_Angle moments (:78-105) of every pair
-        uint4 mc[3], mcn[3];
-        if (OD_PIPE) moment_loads(key_of(0), mc);
-        for (int j = 0; j < nkb; j += 2) {
-            const uint32_t key = key_of(j);
-            if (!OD_PIPE) moment_loads(key, mc);
-            else if (j + 2 < nkb) moment_loads(key_of(j + 2), mcn);
-            const int al = (key_x(key) + kMinBorder - 15) & 15;
-            int s_all = 0, c_all = 0, m01p = 0;
-#pragma unroll
-            for (int it = 0; it < 3; ++it) {
-                const int m = min(max(mlo[it] + al, 0), 16), n = min(max(mhi[it] + al, 0), 16);
-                const uint4 mk = s_rng[m][n];
-                const uint32_t p0 = mc[it].x & mk.x, p1 = mc[it].y & mk.y, p2 = mc[it].z & mk.z, p3 = mc[it].w & mk.w;
-                uint32_t sc = __builtin_amdgcn_udot4(p0, 0x01010101u, 0u, false);
-                sc = __builtin_amdgcn_udot4(p1, 0x01010101u, sc, false);
-                sc = __builtin_amdgcn_udot4(p2, 0x01010101u, sc, false);
-                sc = __builtin_amdgcn_udot4(p3, 0x01010101u, sc, false);
-                uint32_t cc = __builtin_amdgcn_udot4(p0, 0x03020100u, 0u, false);
-                cc = __builtin_amdgcn_udot4(p1, 0x07060504u, cc, false);
-                cc = __builtin_amdgcn_udot4(p2, 0x0B0A0908u, cc, false);
-                cc = __builtin_amdgcn_udot4(p3, 0x0F0E0D0Cu, cc, false);
-                s_all += (int)sc;
-                c_all += (int)cc + mp16[it] * (int)sc;
-                m01p += mv[it] * (int)sc;
-            }
-            const int m10 = od_sum(c_all - (15 + al) * s_all), m01 = od_sum(m01p);
-            if (sub == 0 && j + half < nkb) s_mom[w][j + half] = make_int2(m10, m01);
-            if (OD_PIPE)
-#pragma unroll
-                for (int it = 0; it < 3; ++it) mc[it] = mcn[it];
-        }
-        wave_sync();
-        // ---- angle (fastAtan2) and std::sin / std::cos (:114-115), one lane per keypoint
-        if (lane < nkb) {
-            const int2 mm = s_mom[w][lane];
-            const float angle = fast_atan2_deg((float)mm.y, (float)mm.x);
-            const float factorPI = (float)(3.14159265358979323846 / 180.0);
-            float sn, ca;
-            libm_sincosf(angle * factorPI, &sn, &ca);
-            s_ang[w][lane] = make_float4(angle, sn, ca, 0.f);
-            a.lvlangle[kbase + base + lane] = angle;
-        }
-        wave_sync();
-        // ---- computeOrbDescriptor (:108-148) of every pair: lane `sub` makes bits [8 sub, 8 sub + 8)
-        uint4 pv[kOdPatchIt], pvn[kOdPatchIt];
-        if (OD_PIPE) patch_loads(key_of(0), pv);
-        for (int j = 0; j < nkb; j += 2) {
-            const uint32_t key = key_of(j);
-            const int x = key_x(key) + kMinBorder;
-            if (!OD_PIPE) patch_loads(key, pv);
-#pragma unroll
-            for (int it = 0; it < kOdPatchIt; ++it) {
-                const int c = sub + it * kOdLanes;
-                const int r = c / 3, part = c - 3 * r;
-                if (c < kOdPatchChunks) *reinterpret_cast<uint4*>(pt + r * kOdPatchPitch + 16 * part) = pv[it];
-            }
-            if (OD_PIPE && j + 2 < nkb) patch_loads(key_of(j + 2), pvn);
-            wave_sync();
-            const float4 ag = s_ang[w][j + half < nkb ? j + half : j];
-            const float sn = ag.y, ca = ag.z;
-            const int pc = kOdPatchR * kOdPatchPitch + (x - ((x - kOdPatchR) & ~3));
-            const float magic = 12582912.0f;
-            const uint32_t kofs = (uint32_t)pc - 0x4B400000u - 0x400000u * (uint32_t)kOdPatchPitch;
-            const f32x2 snv = {sn, sn}, cav = {ca, ca}, mg = {magic, magic};
-            uint32_t bits = 0;
-#pragma unroll
-            for (int b = kOdPairs - 1; b >= 0; --b) {
-                uint4 pw = s_pat[b][sub];
-                asm volatile("" : "+v"(pw.x), "+v"(pw.y), "+v"(pw.z), "+v"(pw.w));
-                const f32x2 X = {__uint_as_float(pw.x), __uint_as_float(pw.y)};
-                const f32x2 Y = {__uint_as_float(pw.z), __uint_as_float(pw.w)};
-                const f32x2 R = (X * snv + Y * cav) + mg;
-                const f32x2 C = (X * cav - Y * snv) + mg;
-                const int o0 = (int)(__umul24(__float_as_uint(R.x), (uint32_t)kOdPatchPitch) + __float_as_uint(C.x) + kofs);
-                const int o1 = (int)(__umul24(__float_as_uint(R.y), (uint32_t)kOdPatchPitch) + __float_as_uint(C.y) + kofs);
-                bits = bits + bits + (pt[o0] < pt[o1] ? 1u : 0u);
-            }
-            if (j + half < nkb) a.lvldesc[(kbase + base + j + half) * 32 + sub] = (uint8_t)bits;
-            if (OD_PIPE)
-#pragma unroll
-                for (int it = 0; it < kOdPatchIt; ++it) pv[it] = pvn[it];
-            wave_sync();  // the group's reads of the patch are done before the next pair's stores
-        }
-    }
-}
-#elif OD_CHUNKS
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k_orient_desc(
-    BatchArgs a, uint32_t nblk_magic) {
-    // per keypoint group: the blurred patch around the keypoint, staged with 16-byte loads
-    __shared__ __attribute__((aligned(16))) uint8_t patch[kOdKpBlock][kOdPatchRows * kOdPatchPitch];
-    const int wg = xcd_remap(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * gridDim.y);
-    // wg / gridDim.x by the host's magic multiplier; the block's level from a host record (no
-    // level search with dependent kernarg loads)
-    const int irel = gridDim.x == 1 ? wg : (int)__umulhi((uint32_t)wg, nblk_magic);
-    const int img = a.img0 + irel, bx = wg - irel * (int)gridDim.x;
-    const int l = a.rtab[a.od_tab_off + bx].x;
-    const LevelGeom G = a.lv[l];
-    const int sub = threadIdx.x % kOdLanes, grp = threadIdx.x / kOdLanes;
-    const int count = a.lvlcnt[img * kMaxLevels + l];
-    const long long kbase = (long long)img * a.lvlkp_img_stride + G.kp_off;
-    const uint8_t* lvl = a.lvl_base[l] + (long long)img * G.img_stride;
-    const uint8_t* blr = a.blur_base[l] + (long long)img * G.bimg_stride;
-    const bool raw_dw = ((G.pitch | G.img_stride) & 3) == 0;
-    // raw buffer over this image's blurred level (dword 3 = gfx9 raw-buffer format word)
-    const __amdgpu_buffer_rsrc_t brs =
-        __builtin_amdgcn_make_buffer_rsrc((void*)blr, (short)0, G.bpitch * G.h, 0x00020000);
-    const int stride_k = G.od_blocks * kOdKpBlock;
-    // Moments from coalesced row chunks: the 31 disc rows of a keypoint are read as 16-byte
-    // aligned chunks of the 48-byte window that starts at xa16 = (x - 15) & ~15 (it holds
-    // x - 15 .. x + 15 for every x).  Chunk slot i = sub + 32 it (it < 3) is disc row r = i / 3
-    // (v = r - 15; r = 31 lies past the disc) and part i % 3, so the three lanes of a row read 48
-    // contiguous bytes -- one or two cache lines per row instead of three 16-byte / dword loads
-    // per row lane (round 4: ~105 of the ~160 L1 accesses per keypoint were those).  Each chunk
-    // adds its masked byte sums: s = sum of p, c = sum of (column - xa16) p over the disc span
-    // |u| <= umax[|v|], i.e. chunk bytes [m, n) with m, n from the alignment a = (x - 15) & 15 and
-    // two per-lane constants; the byte masks of every [m, n) are an LDS table, so a chunk is one
-    // b128 LDS read, 4 ANDs and 8 v_dot4_u32_u8.  Then m_10 = sum c - (15 + a) sum s and
-    // m_01 = sum v s.
-    __shared__ __attribute__((aligned(16))) uint4 s_rng[17][17];  // bytes [m, n) of 16 (none if n <= m)
-    __shared__ __attribute__((aligned(16))) uint4 s_pat[kOdPairs][kOdLanes];
-    for (int e = threadIdx.x; e < 17 * 17; e += 256) {
-        const int m = e / 17, n = e - 17 * m;
-        uint32_t w4[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            w4[k] = 0;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) w4[k] |= (4 * k + j >= m && 4 * k + j < n ? 0xFFu : 0u) << (8 * j);
-        }
-        s_rng[m][n] = make_uint4(w4[0], w4[1], w4[2], w4[3]);
-    }
-    {
-        const int8_t* pv = c_pattern.v + 4 * threadIdx.x;  // x0, y0, x1, y1 of pair threadIdx.x
-        s_pat[threadIdx.x % kOdPairs][threadIdx.x / kOdPairs] = make_uint4(__float_as_uint((float)pv[0]), __float_as_uint((float)pv[2]),
-                                        __float_as_uint((float)pv[1]), __float_as_uint((float)pv[3]));
-    }
-    __syncthreads();
     // this lane's three chunk slots: row v, chunk bytes [lo + a, hi + a) clamped to [0, 16) are
     // the disc span (lo = 15 - d - 16 part, hi = 16 + d - 16 part, d = umax[|v|], -1 past the
     // disc), the part's column offset and the byte offset from the window
@@ -1411,31 +1076,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
         mofs[it] = (r < 31 ? mv[it] : 15) * G.pitch + 16 * part;
         mp16[it] = 16 * part;
     }
-    const __amdgpu_buffer_rsrc_t lrs =
-        __builtin_amdgcn_make_buffer_rsrc((void*)lvl, (short)0, (int)min((long long)G.pitch * G.h, 0x7fffffffLL), 0x00020000);
-    uint8_t* pt = patch[grp];
-    // uniform trip count per wave so the group shuffles see all lanes
-    const int wave_first = (bx - G.od_first) * kOdKpBlock + (threadIdx.x >> 6) * 2;
-    // each iteration's key is loaded one iteration ahead, so its round trip overlaps the
-    // previous keypoint's work
-    auto key_at = [&](int kb) {
-        const int kp = kb + (grp & 1);
-        return kp < count ? a.lvlkey[kbase + kp] : a.lvlkey[kbase + kb];
-    };
-    uint32_t key_next = wave_first < count ? key_at(wave_first) : 0u;
-    for (int kb = wave_first; kb < count; kb += stride_k) {
-        const int kp = kb + (grp & 1);
-        const bool valid = kp < count;
-        const uint32_t key = key_next;
-        if (kb + stride_k < count) key_next = key_at(kb + stride_k);
+    // the wave's 64 keys in one coalesced load; pass p of group g reads lane 32 g + p's
+    const uint32_t key_l = a.lvlkey[kbase + min(kw + lane, count - 1)];
+    auto issue = [&](int p, uint4 (&mc)[3], int& al) __attribute__((always_inline)) {
+        const uint32_t k0 = __builtin_amdgcn_readlane(key_l, p), k1 = __builtin_amdgcn_readlane(key_l, p + 32);
+        const uint32_t key = grp ? k1 : k0;
         const int x = key_x(key) + kMinBorder, y = key_y(key) + kMinBorder;
-        const int al = (x - 15) & 15;
+        al = (x - 15) & 15;
         const int wofs = y * G.pitch + (x - 15 - al);  // the 48-byte window of disc row 0
-        // the three moment chunks (round trip 1) and the 37 x 37 blurred patch (rows y-18..y+18
-        // from the dword at or below x-18, 16-byte buffer loads, out-of-range bytes read as 0
-        // and never sampled) are both requested before either is used, so the two round trips
-        // overlap; window bytes past x + 15 (or past the plane: 0) only meet zero masks
-        uint4 mc[3];
 #pragma unroll
         for (int it = 0; it < 3; ++it) {
             if (raw_dw) {
@@ -1451,19 +1099,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
                 mc[it] = make_uint4(d4[0], d4[1], d4[2], d4[3]);
             }
         }
-        const int xb = (x - kOdPatchR) & ~3;
-        const int pofs = (y - kOdPatchR) * G.bpitch + xb;
-        uint4 pv[kOdPatchIt];
+    };
+    int my10 = 0, my01 = 0;
+    // two passes' rows in flight while a pass sums (a pass is ~80 VALU against a load round trip)
+    uint4 q0[3], q1[3];
+    int a0 = 0, a1 = 0;
+    issue(0, q0, a0);
+    if (npass > 1) issue(1, q1, a1);
+    for (int p = 0; p < npass; ++p) {
+        const uint4 mc[3] = {q0[0], q0[1], q0[2]};
+        const int al = a0;
 #pragma unroll
-        for (int it = 0; it < kOdPatchIt; ++it) {
-            const int c = sub + it * kOdLanes;
-            const int r = c / 3, part = c - 3 * r;
-            if (c < kOdPatchChunks) {
-                const auto q = __builtin_amdgcn_raw_buffer_load_b128(brs, pofs + r * G.bpitch + 16 * part, 0, 0);
-                pv[it] = make_uint4(q[0], q[1], q[2], q[3]);
-            }
-        }
-        // IC_Angle (:78-105) over this lane's three chunks
+        for (int it = 0; it < 3; ++it) q0[it] = q1[it];
+        a0 = a1;
+        if (p + 2 < npass) issue(p + 2, q1, a1);
         int s_all = 0, c_all = 0, m01p = 0;
 #pragma unroll
         for (int it = 0; it < 3; ++it) {
@@ -1482,61 +1131,33 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
             c_all += (int)cc + mp16[it] * (int)sc;
             m01p += mv[it] * (int)sc;
         }
-        // sums over the keypoint's lanes (DPP, no LDS round trip but the last step)
+        // sums over the keypoint's 32 lanes (DPP, and one ds_swizzle); lane p of the group keeps them
         const int m10 = od_sum(c_all - (15 + al) * s_all), m01 = od_sum(m01p);
-        const float angle = fast_atan2_deg((float)m01, (float)m10);
-        // computeOrbDescriptor (:108-148): lane `sub` makes bits [8 sub, 8 sub + 8)
+        if (sub == p) {
+            my10 = m10;
+            my01 = m01;
+        }
+    }
+    const int kp = kw + lane;  // this lane's keypoint (32 grp + sub)
+    if (kp < count) {
+        const float angle = fast_atan2_deg((float)my01, (float)my10);
         const float factorPI = (float)(3.14159265358979323846 / 180.0);
         float sn, ca;  // std::sin(float) / std::cos(float) (:114-115): libm sinf / cosf
         libm_sincosf(angle * factorPI, &sn, &ca);
-        // the patch to LDS: every sample is then an LDS byte read (4 vector-memory instructions
-        // per lane instead of one scattered byte load per sample)
-#pragma unroll
-        for (int it = 0; it < kOdPatchIt; ++it) {
-            const int c = sub + it * kOdLanes;
-            const int r = c / 3, part = c - 3 * r;
-            if (c < kOdPatchChunks) *reinterpret_cast<uint4*>(pt + r * kOdPatchPitch + 16 * part) = pv[it];
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the group's own lanes read it
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const int pc = kOdPatchR * kOdPatchPitch + (x - xb);  // patch offset of the keypoint
-        // both samples of a test pair as packed f32 (each element an IEEE single operation, no
-        // contraction): row = x*b + y*a, col = x*a - y*b as the reference's float expressions
-        // (:116-121), then cvRound by adding 1.5 * 2^23 (round to nearest even, |value| < 19),
-        // whose low 24 bits are 2^22 + the rounded value: the LDS offset is one v_mad_u32_u24 of
-        // the two bit patterns and a per-keypoint constant (no v_rndne / v_cvt per sample)
-        const float magic = 12582912.0f;
-        const uint32_t kofs = (uint32_t)pc - 0x4B400000u - 0x400000u * (uint32_t)kOdPatchPitch;
-        const f32x2 snv = {sn, sn}, cav = {ca, ca}, mg = {magic, magic};
-        uint32_t bits = 0;
-#pragma unroll
-        for (int b = kOdPairs - 1; b >= 0; --b) {  // bits = 2 bits + test, last pair first
-            uint4 pw = s_pat[b][sub];  // float bit patterns {x0, x1, y0, y1}
-            asm volatile("" : "+v"(pw.x), "+v"(pw.y), "+v"(pw.z), "+v"(pw.w));  // not hoisted
-            const f32x2 X = {__uint_as_float(pw.x), __uint_as_float(pw.y)};
-            const f32x2 Y = {__uint_as_float(pw.z), __uint_as_float(pw.w)};
-            const f32x2 R = (X * snv + Y * cav) + mg;
-            const f32x2 C = (X * cav - Y * snv) + mg;
-            // the unsigned sums wrap to the small patch offsets; index with them as int
-            const int o0 = (int)(__umul24(__float_as_uint(R.x), (uint32_t)kOdPatchPitch) + __float_as_uint(C.x) + kofs);
-            const int o1 = (int)(__umul24(__float_as_uint(R.y), (uint32_t)kOdPatchPitch) + __float_as_uint(C.y) + kofs);
-            bits = bits + bits + (pt[o0] < pt[o1] ? 1u : 0u);
-        }
-        if (valid) {
-            if (sub == 0) a.lvlangle[kbase + kp] = angle;
-            a.lvldesc[(kbase + kp) * 32 + sub] = (uint8_t)bits;
-        }
+        a.lvlangle[kbase + kp] = angle;
+        a.lvlsc[kbase + kp] = make_float2(sn, ca);
     }
 }
-#else
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k_orient_desc(
-    BatchArgs a, uint32_t nblk_magic) {
-    // per keypoint group: the blurred patch around the keypoint, staged with 16-byte loads
+
+// k_desc: 32 lanes per keypoint (two independent groups per wave): lane `sub` makes test pairs
+// [8 sub, 8 sub + 8), sampled from the keypoint's blurred 37 x 37 patch staged in LDS with 16-byte
+// buffer loads: a = (float)cos, b = (float)sin of angle * pi / 180, sample
+// center[cvRound(x*b + y*a)*step + cvRound(x*a - y*b)].  A workgroup makes several passes of 8
+// keypoints; each pass's key and (sin, cos) are loaded one pass ahead.
+__global__ __launch_bounds__(256) void k_desc(BatchArgs a, uint32_t nblk_magic) {
     __shared__ __attribute__((aligned(16))) uint8_t patch[kOdKpBlock][kOdPatchRows * kOdPatchPitch];
+    __shared__ __attribute__((aligned(16))) uint4 s_pat[kOdPairs][kOdLanes];
     const int wg = xcd_remap(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * gridDim.y);
-    // wg / gridDim.x by the host's magic multiplier; the block's level from a host record (no
-    // level search with dependent kernarg loads)
     const int irel = gridDim.x == 1 ? wg : (int)__umulhi((uint32_t)wg, nblk_magic);
     const int img = a.img0 + irel, bx = wg - irel * (int)gridDim.x;
     const int l = a.rtab[a.od_tab_off + bx].x;
@@ -1544,82 +1165,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
     const int sub = threadIdx.x % kOdLanes, grp = threadIdx.x / kOdLanes;
     const int count = a.lvlcnt[img * kMaxLevels + l];
     const long long kbase = (long long)img * a.lvlkp_img_stride + G.kp_off;
-    const uint8_t* lvl = a.lvl_base[l] + (long long)img * G.img_stride;
     const uint8_t* blr = a.blur_base[l] + (long long)img * G.bimg_stride;
-    const bool raw_dw = ((G.pitch | G.img_stride) & 3) == 0;
     // raw buffer over this image's blurred level (dword 3 = gfx9 raw-buffer format word)
     const __amdgpu_buffer_rsrc_t brs =
         __builtin_amdgcn_make_buffer_rsrc((void*)blr, (short)0, G.bpitch * G.h, 0x00020000);
     const int stride_k = G.od_blocks * kOdKpBlock;
-    // per disc row v = s - 15 (s = 0..31) and dword i of the 32-byte window u = -15..16, the byte
-    // weights restricted to |u| <= umax[|v|] (rows past v = 15 are empty): ones (sum of p) and
-    // u + 15 (sum of (u + 15) p), so each dword is one v_alignbyte and two v_dot4_u32_u8; and the
-    // test pairs (floats {x0, x1, y0, y1}: the x and y pairs are packed-f32 operands).  Both in
-    // LDS tables shared by the workgroup, index-major ([i][row], [b][sub]): the 32 lanes of a
-    // keypoint read 32 consecutive entries per instruction, conflict-free
-    __shared__ __attribute__((aligned(16))) uint2 s_w[8][32];  // {ones, u + 15} masked
-    __shared__ __attribute__((aligned(16))) uint4 s_pat[kOdPairs][kOdLanes];
     {
-        const int ts = threadIdx.x / 8, ti = threadIdx.x % 8;
-        const int v = ts - 15;
-        const int d = v > 15 ? -1 : c_umax[v < 0 ? -v : v];
-        uint32_t m = 0;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int u = 4 * ti + j - 15;
-            m |= ((u < 0 ? -u : u) <= d ? 0xFFu : 0u) << (8 * j);
-        }
-        s_w[ti][ts] = make_uint2(m & 0x01010101u, m & ((uint32_t)(4 * ti) * 0x01010101u + 0x03020100u));
         const int8_t* pv = c_pattern.v + 4 * threadIdx.x;  // x0, y0, x1, y1 of pair threadIdx.x
         s_pat[threadIdx.x % kOdPairs][threadIdx.x / kOdPairs] = make_uint4(__float_as_uint((float)pv[0]), __float_as_uint((float)pv[2]),
                                         __float_as_uint((float)pv[1]), __float_as_uint((float)pv[3]));
     }
     __syncthreads();
-    const int v = sub - 15;
-    const int vrow = v > 15 ? 0 : v;
     uint8_t* pt = patch[grp];
-    // uniform trip count per wave so the group shuffles see all lanes
+    // uniform trip count per wave so the group's lanes stay together
     const int wave_first = (bx - G.od_first) * kOdKpBlock + (threadIdx.x >> 6) * 2;
-    // each iteration's key is loaded one iteration ahead, so its round trip overlaps the
-    // previous keypoint's work
-    auto key_at = [&](int kb) {
-        const int kp = kb + (grp & 1);
-        return kp < count ? a.lvlkey[kbase + kp] : a.lvlkey[kbase + kb];
-    };
-    uint32_t key_next = wave_first < count ? key_at(wave_first) : 0u;
-    for (int kb = wave_first; kb < count; kb += stride_k) {
-        const int kp = kb + (grp & 1);
-        const bool valid = kp < count;
-        const uint32_t key = key_next;
-        if (kb + stride_k < count) key_next = key_at(kb + stride_k);
+    auto kp_at = [&](int kb) { const int kp = kb + (grp & 1); return kp < count ? kp : kb; };
+    // software pipeline over the passes: pass i + 1's patch is requested before pass i samples
+    // (its key one pass earlier still), so a pass waits on no memory round trip of its own
+    auto patch_load = [&](uint32_t key, uint4 (&pv)[kOdPatchIt]) __attribute__((always_inline)) {
         const int x = key_x(key) + kMinBorder, y = key_y(key) + kMinBorder;
-        const int x0 = x - 15;
-        const int xa = raw_dw ? (x0 & ~3) : x0;
-        const int shf = x0 - xa;
-        // the moment row (round trip 1) and the 37 x 37 blurred patch (rows y-18..y+18 from the
-        // dword at or below x-18, 16-byte buffer loads, out-of-range bytes read as 0 and never
-        // sampled) are both requested before either is used, so the two round trips overlap
-        uint32_t w[9];
-        {
-            const uint8_t* row = lvl + plane_off(y + vrow, G.pitch, 0) + xa;
-            if (raw_dw) {  // 2 x dwordx4 (+ 1 dword when the window starts past byte 1 of its
-                           // first dword: otherwise w[8] only meets the zero weight of u = 16)
-                const uint4 A = *reinterpret_cast<const uint4*>(row);
-                const uint4 B = *reinterpret_cast<const uint4*>(row + 16);
-                w[0] = A.x; w[1] = A.y; w[2] = A.z; w[3] = A.w;
-                w[4] = B.x; w[5] = B.y; w[6] = B.z; w[7] = B.w;
-                w[8] = shf > 1 ? *reinterpret_cast<const uint32_t*>(row + 32) : 0u;
-            } else {
-#pragma unroll
-                for (int i = 0; i < 9; ++i) {
-                    const uint8_t* q = row + 4 * i;
-                    w[i] = (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16) | ((uint32_t)q[3] << 24);
-                }
-            }
-        }
-        const int xb = (x - kOdPatchR) & ~3;
-        const int pofs = (y - kOdPatchR) * G.bpitch + xb;
-        uint4 pv[kOdPatchIt];
+        // the 37 x 37 blurred patch (rows y-18..y+18 from the dword at or below x-18, 16-byte
+        // buffer loads; out-of-range bytes read as 0 and are never sampled)
+        const int pofs = (y - kOdPatchR) * G.bpitch + ((x - kOdPatchR) & ~3);
 #pragma unroll
         for (int it = 0; it < kOdPatchIt; ++it) {
             const int c = sub + it * kOdLanes;
@@ -1629,24 +1196,33 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
                 pv[it] = make_uint4(q[0], q[1], q[2], q[3]);
             }
         }
-        // IC_Angle (:78-105): s = sum of p, t = sum of (u + 15) p over the row's disc span
-        uint32_t s = 0, t = 0;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const uint2 wt = s_w[i][sub];
-            const uint32_t b = __builtin_amdgcn_alignbyte(w[i + 1], w[i], shf);
-            s = __builtin_amdgcn_udot4(b, wt.x, s, false);
-            t = __builtin_amdgcn_udot4(b, wt.y, t, false);
+    };
+    uint32_t key = 0, key_n = 0;
+    float2 scv = make_float2(0.f, 0.f);
+    uint4 pv[kOdPatchIt];
+    if (wave_first < count) {
+        key = a.lvlkey[kbase + kp_at(wave_first)];
+        scv = a.lvlsc[kbase + kp_at(wave_first)];
+        if (wave_first + stride_k < count) key_n = a.lvlkey[kbase + kp_at(wave_first + stride_k)];
+        patch_load(key, pv);
+    }
+    for (int kb = wave_first; kb < count; kb += stride_k) {
+        const int kp = kb + (grp & 1);
+        const bool valid = kp < count;
+        const bool more = kb + stride_k < count;
+        uint4 pvn[kOdPatchIt];
+        uint32_t key_nn = 0;
+        float2 sc_n = make_float2(0.f, 0.f);
+        if (more) {
+            patch_load(key_n, pvn);
+            sc_n = a.lvlsc[kbase + kp_at(kb + stride_k)];
+            if (kb + 2 * stride_k < count) key_nn = a.lvlkey[kbase + kp_at(kb + 2 * stride_k)];
         }
-        // sums over the keypoint's lanes (DPP, no LDS round trip but the last step)
-        const int m10 = od_sum((int)t - 15 * (int)s), m01 = od_sum(vrow * (int)s);
-        const float angle = fast_atan2_deg((float)m01, (float)m10);
-        // computeOrbDescriptor (:108-148): lane `sub` makes bits [8 sub, 8 sub + 8)
-        const float factorPI = (float)(3.14159265358979323846 / 180.0);
-        float sn, ca;  // std::sin(float) / std::cos(float) (:114-115): libm sinf / cosf
-        libm_sincosf(angle * factorPI, &sn, &ca);
-        // the patch to LDS: every sample is then an LDS byte read (4 vector-memory instructions
-        // per lane instead of one scattered byte load per sample)
+        const int x = key_x(key) + kMinBorder;
+        const int xb = (x - kOdPatchR) & ~3;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the previous pass's samples are read
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
         for (int it = 0; it < kOdPatchIt; ++it) {
             const int c = sub + it * kOdLanes;
@@ -1664,7 +1240,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
         // the two bit patterns and a per-keypoint constant (no v_rndne / v_cvt per sample)
         const float magic = 12582912.0f;
         const uint32_t kofs = (uint32_t)pc - 0x4B400000u - 0x400000u * (uint32_t)kOdPatchPitch;
-        const f32x2 snv = {sn, sn}, cav = {ca, ca}, mg = {magic, magic};
+        const f32x2 snv = {scv.x, scv.x}, cav = {scv.y, scv.y}, mg = {magic, magic};
         uint32_t bits = 0;
 #pragma unroll
         for (int b = kOdPairs - 1; b >= 0; --b) {  // bits = 2 bits + test, last pair first
@@ -1679,13 +1255,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
             const int o1 = (int)(__umul24(__float_as_uint(R.y), (uint32_t)kOdPatchPitch) + __float_as_uint(C.y) + kofs);
             bits = bits + bits + (pt[o0] < pt[o1] ? 1u : 0u);
         }
-        if (valid) {
-            if (sub == 0) a.lvlangle[kbase + kp] = angle;
-            a.lvldesc[(kbase + kp) * 32 + sub] = (uint8_t)bits;
+        if (valid) a.lvldesc[(kbase + kp) * 32 + sub] = (uint8_t)bits;
+        if (more) {
+#pragma unroll
+            for (int it = 0; it < kOdPatchIt; ++it) pv[it] = pvn[it];
+            key = key_n;
+            key_n = key_nn;
+            scv = sc_n;
         }
     }
 }
-#endif
 
 // ---------------------------------------------------------------------------------------------
 // k_finalize: ORBextractor::operator() assembly (ORBextractor_old.cc:1130-1190): levels in
@@ -1842,34 +1421,37 @@ __device__ inline void knn2_store(uint32_t k1, uint32_t k2, int qi, int32_t* i1,
 // train rows are the two largest accumulators (no popcount, no per-pair VALU beyond the top-2
 // update).  Train rows are walked in 4096-row segments (12-bit local index); each segment's
 // winners are folded into (H << 16 | t) keys, the layout of the VALU matcher.
-//   workgroup = kKnnWaves waves x 32 queries; per 32-row train tile each wave issues 8
-//   v_mfma_i32_32x32x32_i8 (K = 256 bits): A = train tile (expanded once per workgroup into
-//   LDS, double-buffered), B = the wave's queries (expanded once into registers).
+//   workgroup = kKnnWaves waves x kKnnNB x 32 queries; per 32-row train tile each wave issues
+//   8 kKnnNB v_mfma_i32_32x32x32_i8 (K = 256 bits): A = train tile (expanded once per workgroup
+//   into LDS, double-buffered; each fragment read feeds kKnnNB MFMAs), B = the wave's queries
+//   (expanded once into registers).
 // C/D layout (cdna_hip_programming.md §3): lane l holds column l & 31 (its query) and rows
 // (reg & 3) + 8 (reg >> 2) + 4 (l >> 5) of the tile (train rows); the K order inside a
 // fragment is the same map for A and B, so any consistent bit -> element assignment is exact.
 typedef int knn_v4i __attribute__((ext_vector_type(4)));
 typedef int knn_v16i __attribute__((ext_vector_type(16)));
-#ifndef KNN_WAVES
-#define KNN_WAVES 8
+// Register blocking: each wave holds kKnnNB sets of 32 queries (B fragments), so every train
+// fragment read from LDS feeds kKnnNB MFMAs; the workgroup keeps kKnnQueries = 256 queries with
+// 8 / kKnnNB waves.
+#ifndef KNN_NB
+#define KNN_NB 2
 #endif
-constexpr int kKnnWaves = KNN_WAVES;     // waves per workgroup, 32 queries each
+constexpr int kKnnNB = KNN_NB;
+static_assert(kKnnNB == 1 || kKnnNB == 2, "query sets per wave");
+constexpr int kKnnWaves = 8 / kKnnNB;
 constexpr int kKnnThreads = 64 * kKnnWaves;
-constexpr int kKnnQ = 32 * kKnnWaves;    // queries per workgroup
-static_assert(kKnnQ <= kKnnQueries, "the arrival counters (knn2_counter_slots) assume at most kKnnQueries per block");
+constexpr int kKnnQ = 32 * kKnnNB * kKnnWaves;  // queries per workgroup
+static_assert(kKnnQ == kKnnQueries, "orb_kernels.h kKnnQueries (grid and arrival counters)");
+#ifndef KNN_WPE
+#define KNN_WPE 2
+#endif
+constexpr int kKnnWavesPerEU = KNN_WPE;  // register budget: waves per SIMD the kernel must fit
+#ifndef KNN_DBUF
+#define KNN_DBUF 1
+#endif
+constexpr bool kKnnDbuf = KNN_DBUF != 0;  // select tile i - 1 during tile i's MFMAs (two accumulator sets)
 constexpr int kKnnPitch = 272;           // bytes per expanded train row in LDS (256 + 16: no bank conflicts)
-// 32-row tiles per LDS stage (one barrier per stage).  Round 5 (single stream, 512 images):
-// 1 tile 243-246 us, 2 tiles 251-253 us -- the barrier per tile is not what the waves wait on
-#ifndef KNN_STAGE
-#define KNN_STAGE 1
-#endif
-#ifndef KNN_MFMA16
-#define KNN_MFMA16 0  // 1: v_mfma_i32_16x16x64_i8 tiles (knn2_mfma16_block)
-#endif
-constexpr int kKnnStage = KNN_STAGE;
-static_assert(kKnnStage == 1 || kKnnStage == 2 || kKnnStage == 4, "stage size");
 constexpr int kKnnSeg = 4096;            // train rows per key segment
-static_assert(kKnnWaves == 4 || kKnnWaves == 8, "expansion roles");
 
 // Descriptor dword w -> 32 int8 (-64 for a set bit, +64 otherwise; the sign is the same on both
 // operands, so the dot is still 4096 (256 - 2H)): K element 4 m + j of the dword's MFMA step is
@@ -1907,23 +1489,30 @@ __device__ inline int knn_max3_i32(int a, int b, int c) {
 
 // One workgroup: queries [qb * kKnnQ, +kKnnQ) of q against train tiles [ts, te) of t (all of
 // them unless the launch splits the train rows, ts even).  Without `part` the two best keys go
-// to i1 / d1 / i2 / d2; with it, to part[qi] (a split's partial top-2, merged by k_knn2_merge).
+// to i1 / d1 / i2 / d2; with it, to part[qi] (a split's partial top-2, merged afterwards).
+// Wave w holds query sets n = 0 .. kKnnNB - 1 of 32 queries (qb * kKnnQ + 32 (kKnnNB w + n) + r).
+// Train tiles of 32 rows are expanded once per workgroup into LDS (double-buffered, one barrier
+// per tile); each tile's body expands the next tile and loads the packed words of the one after.
 __device__ __attribute__((always_inline)) inline void knn2_mfma_block(
     const uint8_t* q, int nq, const uint8_t* t, int nt, int qb, int ts, int te, int32_t* i1, int32_t* d1,
     int32_t* i2, int32_t* d2, uint2* part, uint8_t* lds) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int r = lane & 31, h = lane >> 5;
-    const int qi = qb * kKnnQ + wave * 32 + r;
-    // B fragments: lane (r, h) of MFMA s holds bits 32 s + 16 h + [0, 16) of query qi
-    knn_v4i qf[8];
-    {
+    const int qw = qb * kKnnQ + wave * 32 * kKnnNB;  // the wave's first query
+    // B fragments: lane (r, h) of MFMA s holds bits 32 s + 16 h + [0, 16) of query qw + 32 n + r
+    knn_v4i qf[kKnnNB][8];
+#pragma unroll
+    for (int n = 0; n < kKnnNB; ++n) {
+        const int qi = qw + 32 * n + r;
         const uint4* qp = reinterpret_cast<const uint4*>(q + (long long)min(qi, max(nq - 1, 0)) * 32);
         const uint4 qa = qp[0], qc = qp[1];
         const uint32_t dw[8] = {qa.x, qa.y, qa.z, qa.w, qc.x, qc.y, qc.z, qc.w};
 #pragma unroll
-        for (int s = 0; s < 8; ++s) qf[s] = knn_expand_half(dw[s], h);
+        for (int s = 0; s < 8; ++s) qf[n][s] = knn_expand_half(dw[s], h);
     }
-    uint32_t g1 = 0xFFFFFFFFu, g2 = 0xFFFFFFFFu;  // (H << 16 | t), lexicographic min
+    uint32_t g1[kKnnNB], g2[kKnnNB];  // (H << 16 | t), lexicographic min
+#pragma unroll
+    for (int n = 0; n < kKnnNB; ++n) g1[n] = g2[n] = 0xFFFFFFFFu;
     // expansion role.  4 waves: thread -> (row tid >> 3, dword tid & 7) of a tile, two 16-byte
     // stores (threads ed >= 4 store their upper half first, so each store instruction's 8 chunks
     // start on 8 distinct 4-bank boundaries).  8 waves: thread -> (row tid >> 4, half ed & 1 of
@@ -1937,11 +1526,7 @@ __device__ __attribute__((always_inline)) inline void knn2_mfma_block(
         else
             return *reinterpret_cast<const uint32_t*>(t + (long long)row * 32 + 4 * (ed >> 1));
     };
-    // tile u's rows live in LDS stage buffer ((u - ts) / kKnnStage) & 1, slot (u - ts) % kKnnStage
-    auto tile_lds = [&](int u) __attribute__((always_inline)) {
-        const int v = u - ts;
-        return lds + (((v / kKnnStage) & 1) * kKnnStage + v % kKnnStage) * (32 * kKnnPitch);
-    };
+    auto tile_lds = [&](int u) __attribute__((always_inline)) { return lds + ((u - ts) & 1) * (32 * kKnnPitch); };
     auto store_expanded = [&](int u, uint32_t w) __attribute__((always_inline)) {
         if constexpr (kKnnWaves == 4) {
             uint8_t* dst = tile_lds(u) + er * kKnnPitch + 32 * ed;
@@ -1954,17 +1539,12 @@ __device__ __attribute__((always_inline)) inline void knn2_mfma_block(
             *reinterpret_cast<knn_v4i*>(dst) = knn_expand_half(w, ed & 1);
         }
     };
-    // Stages of kKnnStage tiles, double-buffered: the waves meet at one barrier per stage (the
-    // stage's tiles expanded, the other buffer free), and each tile's body expands the tile one
-    // stage ahead (u + kKnnStage) into the other buffer, so the expansion work per tile is the
-    // same as with one barrier per tile.  Packed train words run one tile ahead of their
-    // expansion: the word of tile u is loaded in body(u - kKnnStage - 1) and lives in
-    // pk[u & 1]; loads are unconditional (clamped rows) so waits stay counted
+    // packed train words run one tile ahead of their expansion: the word of tile u is loaded in
+    // body(u - 2) and lives in pk[u & 1]; loads are unconditional (clamped rows) so waits stay counted
     uint32_t pk0 = 0, pk1 = 0;
     if (te > ts) {
-        for (int u = ts; u < ts + kKnnStage && u < te; ++u) store_expanded(u, load_packed(u));
-        if ((ts + kKnnStage) & 1) pk1 = load_packed(ts + kKnnStage);
-        else pk0 = load_packed(ts + kKnnStage);
+        store_expanded(ts, load_packed(ts));
+        pk1 = load_packed(ts + 1);  // ts is even
     }
     // accumulator preload, the same for every tile: row(g) = (g & 3) + 8 (g >> 2) + 4 h, so
     // C0[g] = 4095 - 4 h - rowc(g) is 4095 - (tile-local row) and tile k of a segment yields
@@ -1976,270 +1556,127 @@ __device__ __attribute__((always_inline)) inline void knn2_mfma_block(
 #pragma unroll
     for (int g = 0; g < 16; ++g) C0[g] = 4095 - 4 * h - rowc(g);
     constexpr int kNone = -(1 << 30);  // below every key, and stays below after +32 per tile
+    struct Acc {
+        knn_v16i v[kKnnNB];
+    };
     for (int seg0 = (ts * 32 / kKnnSeg) * kKnnSeg; seg0 < te * 32; seg0 += kKnnSeg) {
         // this segment's tiles; keys are local to tile0 (< 4096 rows), tile0 even
         const int tile0 = max(seg0 >> 5, ts), tile1 = min(te, (seg0 + kKnnSeg) >> 5);
-        // two independent top-2 chains (even / odd accumulator rows), lexicographic max; the
-        // selection of tile ti - 1 runs while tile ti's MFMAs are in flight
-        int ka1 = kNone, ka2 = kNone, kb1 = kNone, kb2 = kNone;
+        // per query set two independent top-2 chains (even / odd accumulator rows),
+        // lexicographic max; the selection of tile ti - 1 runs while tile ti's MFMAs are in flight
+        int ka1[kKnnNB], ka2[kKnnNB], kb1[kKnnNB], kb2[kKnnNB];
+#pragma unroll
+        for (int n = 0; n < kKnnNB; ++n) ka1[n] = ka2[n] = kb1[n] = kb2[n] = kNone;
         // two candidates per step and chain (keys are distinct): the new best is max3(k1, x, y),
         // the new second max(k2, med3(k1, x, y)) -- 3 VALU per 2 candidates instead of 4
-        auto select = [&](const knn_v16i& v, bool shift) __attribute__((always_inline)) {
-            if (shift) {  // previous tile's frame -> this tile's frame
-                ka1 += 32;
-                ka2 += 32;
-                kb1 += 32;
-                kb2 += 32;
-            }
+        auto select = [&](const Acc& v, bool shift) __attribute__((always_inline)) {
 #pragma unroll
-            for (int g = 0; g < 16; g += 4) {
-                const int x0 = v[g], y0 = v[g + 1], x1 = v[g + 2], y1 = v[g + 3];
-                ka2 = max(ka2, knn_med3_i32(ka1, x0, y0));
-                ka1 = knn_max3_i32(ka1, x0, y0);
-                kb2 = max(kb2, knn_med3_i32(kb1, x1, y1));
-                kb1 = knn_max3_i32(kb1, x1, y1);
+            for (int n = 0; n < kKnnNB; ++n) {
+                if (shift) {  // previous tile's frame -> this tile's frame
+                    ka1[n] += 32;
+                    ka2[n] += 32;
+                    kb1[n] += 32;
+                    kb2[n] += 32;
+                }
+#pragma unroll
+                for (int g = 0; g < 16; g += 4) {
+                    const int x0 = v.v[n][g], y0 = v.v[n][g + 1], x1 = v.v[n][g + 2], y1 = v.v[n][g + 3];
+                    ka2[n] = max(ka2[n], knn_med3_i32(ka1[n], x0, y0));
+                    ka1[n] = knn_max3_i32(ka1[n], x0, y0);
+                    kb2[n] = max(kb2[n], knn_med3_i32(kb1[n], x1, y1));
+                    kb1[n] = knn_max3_i32(kb1[n], x1, y1);
+                }
             }
         };
-        // one tile: PAR = ti & 1 picks the accumulator and the packed words
-        auto body = [&](int ti, auto par, knn_v16i& acc, const knn_v16i& prev) __attribute__((always_inline)) {
+        // one tile: PAR = ti & 1 picks the accumulators and the packed words
+        auto body = [&](int ti, auto par, Acc& acc, const Acc& prev) __attribute__((always_inline)) {
             constexpr int PAR = decltype(par)::value;  // ti & 1 (ts is even)
-            // pk[u & 1] holds the word of tile u: this body expands tile ti + kKnnStage and loads
-            // the word of tile ti + kKnnStage + 1
-            uint32_t& pk_use = ((PAR + kKnnStage) & 1) ? pk1 : pk0;
-            uint32_t& pk_load = ((PAR + kKnnStage) & 1) ? pk0 : pk1;
-            if (kKnnStage == 1 || (PAR == 0 && (kKnnStage == 2 || (ti - ts) % kKnnStage == 0)))
-                __syncthreads();  // this stage expanded; the other buffer is free
-            pk_load = load_packed(ti + kKnnStage + 1);
+            // pk[u & 1] holds the word of tile u: this body expands tile ti + 1 and loads the word
+            // of tile ti + 2
+            uint32_t& pk_use = PAR ? pk0 : pk1;
+            uint32_t& pk_load = PAR ? pk1 : pk0;
+            __syncthreads();  // tile ti expanded; the other buffer is free
+            pk_load = load_packed(ti + 2);
             const uint8_t* ab = tile_lds(ti) + r * kKnnPitch + 16 * h;
-            {
-                const knn_v4i a = *reinterpret_cast<const knn_v4i*>(ab);
-                acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, qf[0], C0, 0, 0, 0);
-            }
 #pragma unroll
-            for (int s = 1; s < 8; ++s) {
+            for (int s = 0; s < 8; ++s) {
                 const knn_v4i a = *reinterpret_cast<const knn_v4i*>(ab + 32 * s);
-                acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, qf[s], acc, 0, 0, 0);
+#pragma unroll
+                for (int n = 0; n < kKnnNB; ++n)
+                    acc.v[n] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, qf[n][s], s ? acc.v[n] : C0, 0, 0, 0);
             }
-            if (ti > tile0) select(prev, ti - 1 > tile0);
-            if (ti + kKnnStage < te) store_expanded(ti + kKnnStage, pk_use);
+            if (kKnnDbuf && ti > tile0) select(prev, ti - 1 > tile0);
+            if (ti + 1 < te) store_expanded(ti + 1, pk_use);
             if (ti * 32 + 32 > nt) {  // partial last tile: padding rows never win
 #pragma unroll
                 for (int g = 0; g < 16; ++g)
-                    if (ti * 32 + rowc(g) + 4 * h >= nt) acc[g] = kNone;
+                    if (ti * 32 + rowc(g) + 4 * h >= nt) {
+#pragma unroll
+                        for (int n = 0; n < kKnnNB; ++n) acc.v[n][g] = kNone;
+                    }
             }
+            if (!kKnnDbuf) select(acc, ti > tile0);
         };
         using P0 = std::integral_constant<int, 0>;
         using P1 = std::integral_constant<int, 1>;
-        knn_v16i acc0, acc1;
-        int ti = tile0;
-        for (; ti + 1 < tile1; ti += 2) {
-            body(ti, P0{}, acc0, acc1);
-            body(ti + 1, P1{}, acc1, acc0);
-        }
-        if (ti < tile1) {
-            body(ti, P0{}, acc0, acc1);
-            select(acc0, ti > tile0);
-        } else if (tile1 > tile0) {
-            select(acc1, tile1 - 1 > tile0);
+        if constexpr (kKnnDbuf) {
+            Acc acc0, acc1;
+            int ti = tile0;
+            for (; ti + 1 < tile1; ti += 2) {
+                body(ti, P0{}, acc0, acc1);
+                body(ti + 1, P1{}, acc1, acc0);
+            }
+            if (ti < tile1) {
+                body(ti, P0{}, acc0, acc1);
+                select(acc0, ti > tile0);
+            } else if (tile1 > tile0) {
+                select(acc1, tile1 - 1 > tile0);
+            }
+        } else {  // one accumulator set, selected right after its tile's MFMAs
+            Acc acc;
+            int ti = tile0;
+            for (; ti + 1 < tile1; ti += 2) {
+                body(ti, P0{}, acc, acc);
+                body(ti + 1, P1{}, acc, acc);
+            }
+            if (ti < tile1) body(ti, P0{}, acc, acc);
         }
         // back to segment keys: the last selected tile is tile1 - 1
         const int unbias = 32 * (tile1 - 1 - tile0);
-        int k1 = max(ka1, kb1) - unbias;
-        int k2 = max(min(ka1, kb1), max(ka2, kb2)) - unbias;
-        // fold the segment's two winners into global (H << 16 | t) keys
-        auto fold = [&](int k) __attribute__((always_inline)) {
-            if (k < -(1 << 24)) return;  // padding rows only
-            const int tl = 4095 - (k & 4095), dotp = k >> 12;
-            const uint32_t key = ((uint32_t)((256 - dotp) >> 1) << 16) | (uint32_t)(32 * tile0 + tl);
-            g2 = med3_u32(g1, g2, key);
-            g1 = min(g1, key);
-        };
-        fold(k1);
-        fold(k2);
-    }
-    // the two lane halves saw disjoint train rows of the same query
-    const uint32_t o1 = __shfl_xor(g1, 32), o2 = __shfl_xor(g2, 32);
-    g2 = med3_u32(g1, g2, o1);
-    g1 = min(g1, o1);
-    g2 = med3_u32(g1, g2, o2);
-    g1 = min(g1, o2);
-    if (h == 0 && qi < nq) {
-        if (part) part[qi] = make_uint2(g1, g2);
-        else knn2_store(g1, g2, qi, i1, d1, i2, d2);
-    }
-}
-
-#if KNN_MFMA16
-// knn2_mfma_block on v_mfma_i32_16x16x64_i8 (same cycles per MAC as the 32x32x32 form; the
-// smaller tile draws less power, so the chip holds a higher clock under load -- MI355X_MICROARCH
-// "bare bf16 MFMA loops").  A wave still owns 32 queries and walks 32-row train tiles: per tile
-// 2 (train blocks mb) x 2 (query blocks nb) outputs of 16 x 16, each 4 MFMAs over K = 256.
-// B fragments: lane (c = lane & 15, kg = lane >> 4) of K-step s holds expanded dwords
-// 16 s + 4 kg .. + 3 of query 16 nb + c; A: train row 16 mb + c, the same 16 bytes of its expanded
-// row.  C/D (cdna_hip_programming.md §3): lane holds column c (its query) and rows 4 kg + reg.
-typedef int knn_v4 __attribute__((ext_vector_type(4)));
-__device__ __attribute__((always_inline)) inline void knn2_mfma16_block(
-    const uint8_t* q, int nq, const uint8_t* t, int nt, int qb, int ts, int te, int32_t* i1, int32_t* d1,
-    int32_t* i2, int32_t* d2, uint2* part, uint8_t* lds) {
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int c = lane & 15, kg = lane >> 4;
-    const int qw = qb * kKnnQ + wave * 32;  // the wave's first query
-    knn_v4i qf[2][4];
 #pragma unroll
-    for (int nb = 0; nb < 2; ++nb) {
-        const int qi = qw + 16 * nb + c;
-        const uint4* qp = reinterpret_cast<const uint4*>(q + (long long)min(qi, max(nq - 1, 0)) * 32);
-        const uint4 qa = qp[0], qc = qp[1];
-        const uint32_t dw[8] = {qa.x, qa.y, qa.z, qa.w, qc.x, qc.y, qc.z, qc.w};
-#pragma unroll
-        for (int s = 0; s < 4; ++s) qf[nb][s] = knn_expand_half(dw[2 * s + (kg >> 1)], kg & 1);
-    }
-    uint32_t g1[2] = {0xFFFFFFFFu, 0xFFFFFFFFu}, g2[2] = {0xFFFFFFFFu, 0xFFFFFFFFu};
-    constexpr int kPieces = kKnnThreads / 32;  // pieces per train row
-    const int er = tid / kPieces, ed = tid % kPieces;
-    auto load_packed = [&](int tile) __attribute__((always_inline)) {
-        const int row = min(tile * 32 + er, nt - 1);
-        if constexpr (kKnnWaves == 4)
-            return *reinterpret_cast<const uint32_t*>(t + (long long)row * 32 + 4 * ed);
-        else
-            return *reinterpret_cast<const uint32_t*>(t + (long long)row * 32 + 4 * (ed >> 1));
-    };
-    auto tile_lds = [&](int u) __attribute__((always_inline)) {
-        const int v = u - ts;
-        return lds + (((v / kKnnStage) & 1) * kKnnStage + v % kKnnStage) * (32 * kKnnPitch);
-    };
-    auto store_expanded = [&](int u, uint32_t w) __attribute__((always_inline)) {
-        if constexpr (kKnnWaves == 4) {
-            uint8_t* dst = tile_lds(u) + er * kKnnPitch + 32 * ed;
-            const bool kswap = ed >= 4;
-            const knn_v4i first = knn_expand_half(w, kswap ? 1 : 0), second = knn_expand_half(w, kswap ? 0 : 1);
-            *reinterpret_cast<knn_v4i*>(dst + (kswap ? 16 : 0)) = first;
-            *reinterpret_cast<knn_v4i*>(dst + (kswap ? 0 : 16)) = second;
-        } else {
-            uint8_t* dst = tile_lds(u) + er * kKnnPitch + 16 * ed;
-            *reinterpret_cast<knn_v4i*>(dst) = knn_expand_half(w, ed & 1);
-        }
-    };
-    uint32_t pk0 = 0, pk1 = 0;
-    if (te > ts) {
-        for (int u = ts; u < ts + kKnnStage && u < te; ++u) store_expanded(u, load_packed(u));
-        if ((ts + kKnnStage) & 1) pk1 = load_packed(ts + kKnnStage);
-        else pk0 = load_packed(ts + kKnnStage);
-    }
-    // preload: 4095 - (tile-local train row 16 mb + 4 kg + reg), as the 32x32 form
-    knn_v4 C0[2];
-#pragma unroll
-    for (int mb = 0; mb < 2; ++mb)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) C0[mb][g] = 4095 - 16 * mb - 4 * kg - g;
-    constexpr int kNone = -(1 << 30);
-    struct Acc {
-        knn_v4 v[2][2];  // [mb][nb]
-    };
-    for (int seg0 = (ts * 32 / kKnnSeg) * kKnnSeg; seg0 < te * 32; seg0 += kKnnSeg) {
-        const int tile0 = max(seg0 >> 5, ts), tile1 = min(te, (seg0 + kKnnSeg) >> 5);
-        int k1[2] = {kNone, kNone}, k2[2] = {kNone, kNone};  // per query block
-        auto select = [&](const Acc& v, bool shift) __attribute__((always_inline)) {
-            if (shift) {
-#pragma unroll
-                for (int nb = 0; nb < 2; ++nb) {
-                    k1[nb] += 32;
-                    k2[nb] += 32;
-                }
-            }
-#pragma unroll
-            for (int mb = 0; mb < 2; ++mb)
-#pragma unroll
-                for (int g = 0; g < 4; g += 2)
-#pragma unroll
-                    for (int nb = 0; nb < 2; ++nb) {
-                        const int x = v.v[mb][nb][g], y = v.v[mb][nb][g + 1];
-                        k2[nb] = max(k2[nb], knn_med3_i32(k1[nb], x, y));
-                        k1[nb] = knn_max3_i32(k1[nb], x, y);
-                    }
-        };
-        auto body = [&](int ti, auto par, Acc& acc, const Acc& prev) __attribute__((always_inline)) {
-            constexpr int PAR = decltype(par)::value;
-            uint32_t& pk_use = ((PAR + kKnnStage) & 1) ? pk1 : pk0;
-            uint32_t& pk_load = ((PAR + kKnnStage) & 1) ? pk0 : pk1;
-            if (kKnnStage == 1 || (PAR == 0 && (kKnnStage == 2 || (ti - ts) % kKnnStage == 0)))
-                __syncthreads();
-            pk_load = load_packed(ti + kKnnStage + 1);
-            const uint8_t* ab = tile_lds(ti) + c * kKnnPitch + 16 * kg;
-#pragma unroll
-            for (int s = 0; s < 4; ++s)
-#pragma unroll
-                for (int mb = 0; mb < 2; ++mb) {
-                    const knn_v4i a = *reinterpret_cast<const knn_v4i*>(ab + 16 * mb * kKnnPitch + 64 * s);
-#pragma unroll
-                    for (int nb = 0; nb < 2; ++nb)
-                        acc.v[mb][nb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, qf[nb][s], s ? acc.v[mb][nb] : C0[mb], 0, 0, 0);
-                }
-            if (ti > tile0) select(prev, ti - 1 > tile0);
-            if (ti + kKnnStage < te) store_expanded(ti + kKnnStage, pk_use);
-            if (ti * 32 + 32 > nt) {  // partial last tile: padding rows never win
-#pragma unroll
-                for (int mb = 0; mb < 2; ++mb)
-#pragma unroll
-                    for (int g = 0; g < 4; ++g)
-                        if (ti * 32 + 16 * mb + 4 * kg + g >= nt) acc.v[mb][0][g] = acc.v[mb][1][g] = kNone;
-            }
-        };
-        using P0 = std::integral_constant<int, 0>;
-        using P1 = std::integral_constant<int, 1>;
-        Acc acc0, acc1;
-        int ti = tile0;
-        for (; ti + 1 < tile1; ti += 2) {
-            body(ti, P0{}, acc0, acc1);
-            body(ti + 1, P1{}, acc1, acc0);
-        }
-        if (ti < tile1) {
-            body(ti, P0{}, acc0, acc1);
-            select(acc0, ti > tile0);
-        } else if (tile1 > tile0) {
-            select(acc1, tile1 - 1 > tile0);
-        }
-        const int unbias = 32 * (tile1 - 1 - tile0);
-#pragma unroll
-        for (int nb = 0; nb < 2; ++nb) {
+        for (int n = 0; n < kKnnNB; ++n) {
+            const int k1 = max(ka1[n], kb1[n]) - unbias;
+            const int k2 = max(min(ka1[n], kb1[n]), max(ka2[n], kb2[n])) - unbias;
+            // fold the segment's two winners into global (H << 16 | t) keys
             auto fold = [&](int k) __attribute__((always_inline)) {
                 if (k < -(1 << 24)) return;  // padding rows only
                 const int tl = 4095 - (k & 4095), dotp = k >> 12;
                 const uint32_t key = ((uint32_t)((256 - dotp) >> 1) << 16) | (uint32_t)(32 * tile0 + tl);
-                g2[nb] = med3_u32(g1[nb], g2[nb], key);
-                g1[nb] = min(g1[nb], key);
+                g2[n] = med3_u32(g1[n], g2[n], key);
+                g1[n] = min(g1[n], key);
             };
-            fold(k1[nb] - unbias);
-            fold(k2[nb] - unbias);
+            fold(k1);
+            fold(k2);
         }
     }
-    // the four lanes c + 16 kg saw disjoint train rows of the same queries
 #pragma unroll
-    for (int nb = 0; nb < 2; ++nb)
-#pragma unroll
-        for (int x = 16; x <= 32; x *= 2) {
-            const uint32_t o1 = __shfl_xor(g1[nb], x), o2 = __shfl_xor(g2[nb], x);
-            g2[nb] = med3_u32(g1[nb], g2[nb], o1);
-            g1[nb] = min(g1[nb], o1);
-            g2[nb] = med3_u32(g1[nb], g2[nb], o2);
-            g1[nb] = min(g1[nb], o2);
-        }
-    if (kg < 2) {  // lanes kg = 0 / 1 write query block 0 / 1
-        const int nb = kg, qi = qw + 16 * nb + c;
-        const uint32_t k1 = nb ? g1[1] : g1[0], k2 = nb ? g2[1] : g2[0];
-        if (qi < nq) {
-            if (part) part[qi] = make_uint2(k1, k2);
-            else knn2_store(k1, k2, qi, i1, d1, i2, d2);
+    for (int n = 0; n < kKnnNB; ++n) {
+        // the two lane halves saw disjoint train rows of the same query
+        const uint32_t o1 = __shfl_xor(g1[n], 32), o2 = __shfl_xor(g2[n], 32);
+        uint32_t a1 = g1[n], a2 = med3_u32(g1[n], g2[n], o1);
+        a1 = min(a1, o1);
+        a2 = med3_u32(a1, a2, o2);
+        a1 = min(a1, o2);
+        const int qi = qw + 32 * n + r;
+        if (h == 0 && qi < nq) {
+            if (part) part[qi] = make_uint2(a1, a2);
+            else knn2_store(a1, a2, qi, i1, d1, i2, d2);
         }
     }
 }
-#define KNN_BLOCK knn2_mfma16_block
-#else
-#define KNN_BLOCK knn2_mfma_block
-#endif
 
-__global__ __launch_bounds__(kKnnThreads) void k_knn2_mfma_pairs(MatchArgs m) {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * kKnnStage * 32 * kKnnPitch];
+__global__ __launch_bounds__(kKnnThreads) __attribute__((amdgpu_waves_per_eu(kKnnWavesPerEU))) void k_knn2_mfma_pairs(MatchArgs m) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * 32 * kKnnPitch];
     const int pair = m.pair0 + blockIdx.y;
     const int qimg = 2 * pair, timg = 2 * pair + 1;
     const int qn = m.out_n[qimg], tn = m.out_n[timg];
@@ -2255,7 +1692,7 @@ __global__ __launch_bounds__(kKnnThreads) void k_knn2_mfma_pairs(MatchArgs m) {
     const int npt = (((nt + 31) >> 5) + 1) >> 1, S = gridDim.z, sp = blockIdx.z;  // tile pairs
     const int ts = 2 * (npt * sp / S), te = min((nt + 31) >> 5, 2 * (npt * (sp + 1) / S));
     uint2* part = m.part ? m.part + ((long long)(blockIdx.y * S + sp)) * m.out_cap : nullptr;
-    KNN_BLOCK(q, nq, t, nt, blockIdx.x, ts, te, m.idx1 + o, m.dist1 + o, m.idx2 + o, m.dist2 + o, part, lds);
+    knn2_mfma_block(q, nq, t, nt, blockIdx.x, ts, te, m.idx1 + o, m.dist1 + o, m.idx2 + o, m.dist2 + o, part, lds);
     if (!part || !m.cnt || S == 1) return;
     // fused merge: the last of the S split workgroups of this query block merges their partial
     // top-2 lists (k_knn2_merge's work, without its launch).  The hand-off follows
@@ -2319,10 +1756,10 @@ __global__ __launch_bounds__(256) void k_knn2_merge(MatchArgs m, int nsplit) {
     knn2_store(g1, g2, qi, m.idx1 + o, m.dist1 + o, m.idx2 + o, m.dist2 + o);
 }
 
-__global__ __launch_bounds__(kKnnThreads) void k_knn2_mfma_plain(const uint8_t* q, int nq, const uint8_t* t, int nt,
+__global__ __launch_bounds__(kKnnThreads) __attribute__((amdgpu_waves_per_eu(kKnnWavesPerEU))) void k_knn2_mfma_plain(const uint8_t* q, int nq, const uint8_t* t, int nt,
                                                          int32_t* i1, int32_t* d1, int32_t* i2, int32_t* d2) {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * kKnnStage * 32 * kKnnPitch];
-    KNN_BLOCK(q, nq, t, nt, blockIdx.x, 0, (nt + 31) >> 5, i1, d1, i2, d2, nullptr, lds);
+    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * 32 * kKnnPitch];
+    knn2_mfma_block(q, nq, t, nt, blockIdx.x, 0, (nt + 31) >> 5, i1, d1, i2, d2, nullptr, lds);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2397,9 +1834,9 @@ hipError_t launch_octree(const BatchArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 hipError_t launch_orient_desc(const BatchArgs& a, hipStream_t s) {
-    const uint32_t d = (uint32_t)a.total_od_blocks;
-    const uint32_t magic = d > 1 ? 0xFFFFFFFFu / d + 1u : 0u;  // ceil(2^32 / d) for d >= 2
-    hipLaunchKernelGGL(k_orient_desc, dim3(a.total_od_blocks, a.nimages), dim3(256), 0, s, a, magic);
+    auto magic = [](uint32_t d) { return d > 1 ? 0xFFFFFFFFu / d + 1u : 0u; };  // ceil(2^32 / d) for d >= 2
+    hipLaunchKernelGGL(k_orient, dim3(a.total_or_blocks, a.nimages), dim3(256), 0, s, a, magic((uint32_t)a.total_or_blocks));
+    hipLaunchKernelGGL(k_desc, dim3(a.total_od_blocks, a.nimages), dim3(256), 0, s, a, magic((uint32_t)a.total_od_blocks));
     return hipGetLastError();
 }
 hipError_t launch_finalize(const BatchArgs& a, hipStream_t s) {

@@ -369,32 +369,6 @@ __host__ __device__ inline int fast_strength_packed(const uint8_t* c) {
     return s > 255 ? 255 : s;
 }
 
-// Two candidates in one packed evaluation, ONE polarity each (the side the pre-test passed): half
-// 0 for the pixel at ca, half 1 for cb, each half holding kFastBias + s (v - p) (s = +1 for a dark
-// candidate, -1 for a bright one) before fast_arc_maxmin.  Returns the side strengths (max over
-// arcs of the arc minimum of s (v - p); <= 0 when no arc is all on that side) in *sa / *sb.  A
-// candidate that passed only one side of the pre-test at t has strength <= t on the other side,
-// so "m > t" and m itself follow from its side alone.
-template <int STRIDE>
-__host__ __device__ inline void fast_strength_2x1(const uint8_t* ca, const uint8_t* cb, bool bright_a,
-                                                  bool bright_b, int* sa, int* sb) {
-    const int va = ca[0], vb = cb[0];
-    // x = S * P + C per half (mod 2^16): dark S = -1, C = bias + v; bright S = +1, C = bias - v
-    const orb_u16x2 S = {(unsigned short)(bright_a ? 1 : 0xFFFF), (unsigned short)(bright_b ? 1 : 0xFFFF)};
-    const orb_u16x2 C = {(unsigned short)(bright_a ? kFastBias - va : kFastBias + va),
-                         (unsigned short)(bright_b ? kFastBias - vb : kFastBias + vb)};
-    orb_u16x2 x[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        const int o = ring_dx(k) + ring_dy(k) * STRIDE;
-        const orb_u16x2 P = {(unsigned short)ca[o], (unsigned short)cb[o]};
-        x[k] = S * P + C;
-    }
-    const orb_u16x2 best = fast_arc_maxmin(x);
-    *sa = (int)best.x - kFastBias;
-    *sb = (int)best.y - kFastBias;
-}
-
 __host__ __device__ inline int fast_strength(const uint8_t* c, int stride, int t_min) {
     const int v = c[0];
     // compass pre-test: any 9-arc holds two cyclically adjacent points of {0,4,8,12}

@@ -184,7 +184,7 @@ struct orbgpu_ctx {
     long long pyr_img = 0, blur_img = 0, cellkeys_img = 0, octws_img = 0;
     int cellcnt_img = 0, lvlkp_img = 0, out_cap = 0;
     // device buffers
-    DevBuf input, pyr, blur, rtab, cellkeys, cellcnt, octws, lvlkey, lvlangle, lvldesc, lvlcnt,
+    DevBuf input, pyr, blur, rtab, cellkeys, cellcnt, octws, lvlkey, lvlangle, lvlsc, lvldesc, lvlcnt,
         status, outkps, outdesc, outn, outmono, laps, midx1, mdist1, midx2, mdist2, mnq, mpart, scratch,
         octdbg, strow, stidx, stur, stdepth, stsad, gxy, gcell, gstart, gidx, sbs, soa, m16,
         sbpmp, sbpoff, sbpcand, sbpblk, sbpmatch, sbpnm, sbplr, fel2r, fer2l, fedepth, fep3d, fecnt;
@@ -320,6 +320,7 @@ int alloc_all(orbgpu_ctx* c, int n_images) {
     r |= c->octws.ensure(ni * c->octws_img + 256);
     r |= c->lvlkey.ensure(ni * c->lvlkp_img * 4 + 256);
     r |= c->lvlangle.ensure(ni * c->lvlkp_img * 4 + 256);
+    r |= c->lvlsc.ensure(ni * c->lvlkp_img * 8 + 256);
     r |= c->lvldesc.ensure(ni * c->lvlkp_img * 32 + 256);
     r |= c->lvlcnt.ensure(ni * kMaxLevels * 4);
     r |= c->status.ensure(ni * kMaxLevels * 4);
@@ -617,6 +618,14 @@ int set_geometry(orbgpu_ctx* c, int w, int h) {
     A.od_tab_off = (int)c->rtab_host.size();
     for (int l = 0; l < L; ++l)
         for (int b = 0; b < A.lv[l].od_blocks; ++b) c->rtab_host.push_back(make_int4(l, b, 0, 0));
+    // k_orient: kOrientBlockKps keypoints per workgroup, enough blocks for the level's capacity
+    A.or_tab_off = (int)c->rtab_host.size();
+    A.total_or_blocks = 0;
+    for (int l = 0; l < L; ++l) {
+        const int nb = (A.lv[l].kp_cap + kOrientBlockKps - 1) / kOrientBlockKps;
+        for (int b = 0; b < nb; ++b) c->rtab_host.push_back(make_int4(l, b, 0, 0));
+        A.total_or_blocks += nb;
+    }
     for (int l = 0; l < L; ++l) {
         if (l > 0) A.lv[l].img_stride = c->pyr_img;
         A.lv[l].bimg_stride = c->blur_img;
@@ -640,6 +649,7 @@ int set_geometry(orbgpu_ctx* c, int w, int h) {
     A.octws_img_stride = c->octws_img;
     A.lvlkey = c->lvlkey.as<uint32_t>();
     A.lvlangle = c->lvlangle.as<float>();
+    A.lvlsc = c->lvlsc.as<float2>();
     A.lvldesc = c->lvldesc.as<uint8_t>();
     A.lvlkp_img_stride = c->lvlkp_img;
     A.lvlcnt = c->lvlcnt.as<int32_t>();
@@ -762,6 +772,30 @@ int ensure_input(orbgpu_ctx* c, int n_images, int w, int h, int slot = -1) {
     return 0;
 }
 
+// Up to k chunk streams (never more than max_images / 2), each with its join event and, once the
+// async upload exists, its slot_free event; created under the allocation / capture lock.  A new
+// stream changes the chunk layout, so the batch that asked for it forks from the main stream.
+int ensure_sub_streams(orbgpu_ctx* c, int k) {
+    k = std::min(k, std::max(1, c->max_images / 2));
+    if ((int)c->sub.size() >= k) return 0;
+    std::lock_guard<std::recursive_mutex> lk(alloc_capture_mutex());
+    HIP_TRY(hipSetDevice(c->device));
+    while ((int)c->sub.size() < k) {
+        hipStream_t st;
+        hipEvent_t jn, fr = nullptr;
+        HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+        if (hipEventCreateWithFlags(&jn, hipEventDisableTiming) != hipSuccess ||
+            (c->copy && hipEventCreateWithFlags(&fr, hipEventDisableTiming) != hipSuccess)) {
+            hipStreamDestroy(st);
+            return fail(ORBGPU_ERR_HIP, "hipEventCreate failed");
+        }
+        c->sub.push_back(st);
+        c->join.push_back(jn);
+        if (fr) c->slot_free.push_back(fr);
+    }
+    return 0;
+}
+
 // A synchronous upload / ingest replaces whatever an async upload staged for the next batch.
 int drop_pending_upload(orbgpu_ctx* c) {
     if (c->pending_slot < 0) return 0;
@@ -811,6 +845,8 @@ int orbgpu_create(const orbgpu_params* p, int device, int max_width, int max_hei
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
         return fail(ORBGPU_ERR_NO_DEVICE, "no HIP device");
+    if (device == ORBGPU_DEVICE_CURRENT && hipGetDevice(&device) != hipSuccess)
+        return fail(ORBGPU_ERR_NO_DEVICE, "hipGetDevice failed");
     if (device < 0 || device >= ndev) return fail(ORBGPU_ERR_NO_DEVICE, "bad device ordinal");
     hipDeviceProp_t prop;
     HIP_TRY(hipGetDeviceProperties(&prop, device));
@@ -842,9 +878,11 @@ int orbgpu_create(const orbgpu_params* p, int device, int max_width, int max_hei
         // process's hardware queues, which a second context (the other eye's thread) needs for its
         // own work not to queue behind this one's.
         const char* e = diag_env("ORBGPU_STREAMS");
-        // up to 3 chunk streams; run_batch_impl picks the chunk count per batch (kChunksFor)
+        // the chunk streams the largest batch takes (kChunksFor); run_batch_impl adds the third
+        // stream of a smaller batch when one first asks for it (ensure_sub_streams), so a context
+        // sized for >= 256 images that never runs a small batch holds 2 streams, not an idle third
         c->streams_forced = e != nullptr;
-        const int ns = std::max(1, std::min({8, e ? atoi(e) : 3, max_images / 2}));
+        const int ns = std::max(1, std::min({8, e ? atoi(e) : kChunksFor(max_images), max_images / 2}));
         for (int k = 1; k < ns; ++k) {
             hipStream_t st;
             if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) break;
@@ -879,6 +917,8 @@ int orbgpu_create(const orbgpu_params* p, int device, int max_width, int max_hei
     return ORBGPU_OK;
 }
 
+int orbgpu_get_device(const orbgpu_ctx* c) { return c ? c->device : fail(ORBGPU_ERR_INVALID, "null ctx"); }
+
 int orbgpu_destroy(orbgpu_ctx* c) {
     if (!c) return ORBGPU_OK;
     hipSetDevice(c->device);
@@ -888,7 +928,7 @@ int orbgpu_destroy(orbgpu_ctx* c) {
     std::lock_guard<std::recursive_mutex> destroy_lk(alloc_capture_mutex());  // frees and destroys
     for (auto e : c->event_pool) hipEventDestroy(e);
     DevBuf* bufs[] = {&c->input, &c->input2, &c->pyr,     &c->blur,   &c->rtab,    &c->cellkeys, &c->cellcnt,
-                      &c->octws,   &c->lvlkey,  &c->lvlangle, &c->lvldesc, &c->lvlcnt, &c->status,
+                      &c->octws,   &c->lvlkey,  &c->lvlangle, &c->lvlsc, &c->lvldesc, &c->lvlcnt, &c->status,
                       &c->outkps,  &c->outdesc, &c->outn,   &c->outmono, &c->laps,     &c->midx1,
                       &c->mdist1,  &c->midx2,   &c->mdist2, &c->mnq,     &c->mpart,   &c->scratch, &c->octdbg,
                       &c->strow,  &c->stidx, &c->stur,    &c->stdepth,  &c->stsad,
@@ -951,10 +991,11 @@ int orbgpu_upload_images_async(orbgpu_ctx* c, const uint8_t* images, int n, int 
     int r = ensure_input(c, n, w, h, slot);
     if (r) return r;
     HIP_TRY(hipSetDevice(c->device));
-    if (!c->copy) {
+    if (!c->copy) {  // under the allocation / capture lock: another thread may be capturing a graph
+        std::lock_guard<std::recursive_mutex> lk(alloc_capture_mutex());
         HIP_TRY(hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking));
         HIP_TRY(hipEventCreateWithFlags(&c->slot_ready, hipEventDisableTiming));
-        for (size_t k = 0; k < c->sub.size(); ++k) {
+        while (c->slot_free.size() < c->sub.size()) {
             hipEvent_t e;
             HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
             c->slot_free.push_back(e);
@@ -1062,6 +1103,8 @@ static int run_batch_impl(orbgpu_ctx* c, int n, int w, int h, const int32_t* lap
     // chunks per batch: batches of >= 128 pairs take 2 (each chunk fills the GPU); smaller ones
     // 3 (C5's 16 1080p pairs: 161 vs 154 Mfeatures/s); ORBGPU_STREAMS forces the stream count
     const int kmax = c->streams_forced ? (int)c->sub.size() : kChunksFor(n);
+    if (!stream && (n % 2) == 0 && !c->streams_forced)
+        if (int e_ = ensure_sub_streams(c, std::min(kmax, n / 2))) return e_;
     const int K = (!stream && (n % 2) == 0) ? std::min({(int)c->sub.size(), kmax, n / 2}) : 1;
     // a different sub-batch layout than last time may put an image on another stream: drain first
     if (!c->last_chunks.empty() && ((int)c->last_chunks.size() != K || c->last_images != n))
@@ -1531,6 +1574,7 @@ int orbgpu_ingest_images(orbgpu_ctx* c, const uint8_t* device_images, int n, int
     return rejoin(c, s);
 }
 
+// the packed layout's largest size (every image at the context's row capacity): no device access
 size_t orbgpu_export_batch_bytes(const orbgpu_ctx* c, int n_images, int n_pairs) {
     if (!c || n_images < 0 || n_pairs < 0) return 0;
     const size_t cap = (size_t)c->out_cap;
@@ -1539,34 +1583,47 @@ size_t orbgpu_export_batch_bytes(const orbgpu_ctx* c, int n_images, int n_pairs)
 }
 
 int orbgpu_export_batch(orbgpu_ctx* c, int n_images, int n_pairs, void* device_dst, size_t dst_bytes,
-                        int* out_cap, void* stream) {
+                        size_t* used, void* stream) {
     if (!c || n_images < 0 || n_images > c->last_images || n_pairs < 0 || n_pairs > c->last_pairs ||
         2 * n_pairs > n_images)
         return fail(ORBGPU_ERR_INVALID, "bad image / pair count");
-    if (out_cap) *out_cap = c->out_cap;
-    const size_t need = orbgpu_export_batch_bytes(c, n_images, n_pairs);
-    if (need == 0) return ORBGPU_OK;
-    if (!device_dst) return fail(ORBGPU_ERR_INVALID, "null argument");
-    if (dst_bytes < need) return fail(ORBGPU_ERR_CAPACITY, "export buffer too small");
+    if (used) *used = 0;
+    if (n_images == 0) return ORBGPU_OK;
     HIP_TRY(hipSetDevice(c->device));
-    if (!device_ptr(device_dst)) return fail(ORBGPU_ERR_INVALID, "device_dst is not device memory");
+    if (device_dst && !device_ptr(device_dst)) return fail(ORBGPU_ERR_INVALID, "device_dst is not device memory");
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
     int r = join_all(c, s);  // the outputs come from the chunk streams
     if (r) return r;
-    const size_t cap = (size_t)c->out_cap;
-    uint8_t* d = static_cast<uint8_t*>(device_dst);
-    auto put = [&](const void* src, size_t bytes) -> int {
-        if (bytes) HIP_TRY(hipMemcpyAsync(d, src, bytes, hipMemcpyDeviceToDevice, s));
-        d += bytes;
-        return 0;
-    };
-    if ((r = put(c->outn.p, 4 * (size_t)n_images)) || (r = put(c->outmono.p, 4 * (size_t)n_images)) ||
-        (r = put(c->mnq.p, 4 * (size_t)n_pairs)) ||
-        (r = put(c->outkps.p, sizeof(orbgpu_keypoint) * cap * n_images)) ||
-        (r = put(c->outdesc.p, 32 * cap * n_images)))
-        return r;
-    for (DevBuf* b : {&c->midx1, &c->mdist1, &c->midx2, &c->mdist2})
-        if ((r = put(b->p, 4 * cap * n_pairs))) return r;
+    // the produced rows size the layout: read the counts once the batch (and its match) is done
+    std::vector<int32_t> cnt((size_t)n_images + n_pairs);
+    HIP_TRY(hipMemcpyAsync(cnt.data(), c->outn.p, 4 * (size_t)n_images, hipMemcpyDeviceToHost, s));
+    if (n_pairs) HIP_TRY(hipMemcpyAsync(cnt.data() + n_images, c->mnq.p, 4 * (size_t)n_pairs, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    size_t need = 4 * (2 * (size_t)n_images + n_pairs);
+    for (int i = 0; i < n_images; ++i) {
+        if (int e = count_status(cnt[i])) return e;  // -5 / -2 status words are not row counts
+        need += (sizeof(orbgpu_keypoint) + 32) * (size_t)cnt[i];
+    }
+    for (int p = 0; p < n_pairs; ++p) need += 16 * (size_t)std::max(cnt[n_images + p], 0);
+    if (used) *used = need;
+    if (!device_dst) return rejoin(c, s);  // size query
+    if (dst_bytes < need) return fail(ORBGPU_ERR_CAPACITY, "export buffer too small");
+    if (reinterpret_cast<uintptr_t>(device_dst) % 4) return fail(ORBGPU_ERR_INVALID, "device_dst not 4-byte aligned");
+    ExportArgs x;
+    x.kps = c->outkps.p;
+    x.desc = c->outdesc.as<uint8_t>();
+    x.out_n = c->outn.as<int32_t>();
+    x.out_mono = c->outmono.as<int32_t>();
+    x.nq = c->mnq.as<int32_t>();
+    x.idx1 = c->midx1.as<int32_t>();
+    x.dist1 = c->mdist1.as<int32_t>();
+    x.idx2 = c->midx2.as<int32_t>();
+    x.dist2 = c->mdist2.as<int32_t>();
+    x.out_cap = c->out_cap;
+    x.nimages = n_images;
+    x.npairs = n_pairs;
+    x.dst = device_dst;
+    HIP_TRY(launch_pack_export(x, s));
     return rejoin(c, s);
 }
 

@@ -93,18 +93,25 @@ def cross_camera_match_device(dist, be, image=0, row0=0):
     return out
 
 
-def ingest_scatter_gather(dist, be, frames=None, pairs_per_rank=1, src=0, stereo_rows_only=False):
+def ingest_scatter_gather(dist, be, frames=None, pairs_per_rank=1, src=0, stereo_rows_only=False, stats=None):
     """The C4 ingest-rank path ("if frames are ingested on one GPU"): rank `src` holds
     the frames of every rank's stereo pairs, uint8 [world * 2P, H, W] (pair p = images 2p, 2p + 1;
     rank r owns pairs [rP, (r + 1)P)).  One scatter hands each rank its 2P images, each rank runs
     extraction + stereo kNN2 on its own GPU (BatchExtractor `be`: ingest_images -> run_match), and
-    one gather brings every rank's export_batch buffer back to `src` -- the reference hands each
-    frame's keypoints, descriptors and matches back to its one caller
-    (cpp/src/LynxHardwareAcceleration/LynxHardwareAccelerator.cpp:146-204).  Under RCCL the
-    frames and results move device to device over xGMI; under gloo the collectives are staged
-    through host tensors (the extractor still ingests from / exports to device memory when it is
-    device-resident).  Returns, on `src`, one (images, pairs) per rank as
-    BatchExtractor.decode_export gives them; None on the other ranks."""
+    one gather brings every rank's results back to `src` -- the reference hands each frame's
+    keypoints, descriptors and matches back to its one caller
+    (cpp/src/LynxHardwareAcceleration/LynxHardwareAccelerator.cpp:146-204).
+    Only the rows produced travel: each rank packs its batch with orbgpu_export_batch (counts,
+    then the keypoints, descriptors and match rows it made), the ranks agree on the largest packed
+    size and on whether every rank got that far (one max all_reduce of [failed, bytes]), and the
+    gather moves that many bytes per rank.  A rank whose ingest / extraction / export raised makes
+    every rank skip the gather and raise, so no rank is left waiting in it.  Under RCCL the frames
+    and results move device to device over xGMI; under gloo the collectives are staged through host
+    tensors (the extractor still ingests from / exports to device memory when it is
+    device-resident).  Returns, on `src`, one (images, pairs) per rank as decode_export gives them;
+    None on the other ranks.  `stats` (a dict, optional) receives the bytes each rank sent
+    (`gathered_bytes_per_rank`) and what the capacity layout would have sent
+    (`capacity_bytes_per_rank`)."""
     import torch
     world, rank = dist.get_world_size(), dist.get_rank()
     nccl = dist.get_backend() == "nccl"
@@ -119,12 +126,29 @@ def ingest_scatter_gather(dist, be, frames=None, pairs_per_rank=1, src=0, stereo
         ft = torch.as_tensor(frames).reshape(world * n_img, h, w).to(comm)
         parts = list(ft.chunk(world))
     dist.scatter(recv, parts, src=src)
-    img = recv if recv.device == dev else recv.to(dev)
-    be.ingest_images(img.data_ptr(), n_img, w, stream)
-    be.run_match(stereo_rows_only=stereo_rows_only)
-    nbytes = be.export_batch_bytes(n_img, pairs_per_rank)
-    out = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-    cap = be.export_batch(out.data_ptr(), n_img, pairs_per_rank, nbytes, stream)
+    err, local, used = None, None, 0
+    try:
+        img = recv if recv.device == dev else recv.to(dev)
+        be.ingest_images(img.data_ptr(), n_img, w, stream)
+        be.run_match(stereo_rows_only=stereo_rows_only)
+        used = be.export_batch_size(n_img, pairs_per_rank, stream)
+        local = torch.empty(max(used, 4), dtype=torch.uint8, device=dev)
+        used = be.export_batch(local.data_ptr(), n_img, pairs_per_rank, local.numel(), stream)
+    except Exception as e:  # noqa: BLE001 -- agreed on below, then re-raised
+        err = e
+    flag = torch.tensor([1 if err is not None else 0, used], dtype=torch.int64, device=comm)
+    dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+    if int(flag[0]) != 0:
+        if err is not None:
+            raise err
+        raise RuntimeError("ingest_scatter_gather: another rank failed before the gather")
+    nbytes = max(int(flag[1]), 4)
+    if stats is not None:
+        stats["gathered_bytes_per_rank"] = nbytes
+        cap = getattr(be, "export_batch_bytes", None)
+        stats["capacity_bytes_per_rank"] = int(cap(n_img, pairs_per_rank)) if cap else None
+    out = torch.zeros(nbytes, dtype=torch.uint8, device=dev)
+    out[:local.numel()] = local
     if out.device != comm:
         if out.device.type == "cuda":
             torch.cuda.current_stream().synchronize()
@@ -133,7 +157,7 @@ def ingest_scatter_gather(dist, be, frames=None, pairs_per_rank=1, src=0, stereo
     dist.gather(out, bufs, dst=src)
     if rank != src:
         return None
-    return [be.decode_export(b.cpu().numpy(), n_img, pairs_per_rank, cap) for b in bufs]
+    return [be.decode_export(b.cpu().numpy(), n_img, pairs_per_rank) for b in bufs]
 
 
 def reduce_scalar(dist, x: float, op: str = "max") -> float:

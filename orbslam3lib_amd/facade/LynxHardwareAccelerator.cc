@@ -68,8 +68,8 @@ int LynxHardwareAccelerator::ensure(int w, int h) const {
     orbgpu_destroy(mCtx);
     mCtx = nullptr;
     const int W = w > mWidth ? w : mWidth, H = h > mHeight ? h : mHeight;
-    const int r = orbgpu_create(&mParams, 0, W, H, 2, &mCtx);
-    if (r == ORBGPU_OK) mWidth = W, mHeight = H;
+    const int r = orbgpu_create(&mParams, mDevice, W, H, 2, &mCtx);  // the caller's current device
+    if (r == ORBGPU_OK) mWidth = W, mHeight = H, mDevice = orbgpu_get_device(mCtx);
     return r;
 }
 

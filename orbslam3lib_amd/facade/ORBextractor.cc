@@ -74,8 +74,10 @@ int ORBextractor::ensureContext(int w, int h) {
     mCtx = nullptr;
     orbgpu_params p{nfeatures, (float)scaleFactor, nlevels, iniThFAST, minThFAST};
     const int W = w > mCtxW ? w : mCtxW, H = h > mCtxH ? h : mCtxH;
-    mStatus = orbgpu_create(&p, 0, W, H, 2, &mCtx);
-    if (mStatus == ORBGPU_OK) mCtxW = W, mCtxH = H;
+    // the caller's current HIP device (a multi-camera process selects the GPU before constructing
+    // the extractor), kept for later regrowths
+    mStatus = orbgpu_create(&p, mDevice, W, H, 2, &mCtx);
+    if (mStatus == ORBGPU_OK) mCtxW = W, mCtxH = H, mDevice = orbgpu_get_device(mCtx);
     return mStatus;
 }
 

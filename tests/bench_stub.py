@@ -84,35 +84,33 @@ class BatchExtractor:
         a = np.ctypeslib.as_array((ctypes.c_uint8 * (n * self.height * stride)).from_address(ptr))
         self.upload(a.reshape(n, self.height, stride)[:, :, :self.width].copy())
 
-    _CAP = 64
+    def _export(self, n_img, n_pairs):
+        """The packed orbgpu_export_batch layout over the stub's results (zero keypoints)."""
+        from orbslam3lib_amd import KEYPOINT_DTYPE, encode_export
+        images = []
+        for i in range(n_img):
+            d = self.result(i)[1]
+            images.append((np.zeros(len(d), KEYPOINT_DTYPE), d, len(d)))  # mono = n, as result()
+        pairs = [self.knn_match(images[2 * p][1], images[2 * p + 1][1]) for p in range(n_pairs)]
+        return encode_export(images, pairs)
 
     def export_batch_bytes(self, n_img, n_pairs):
-        return 8 * n_img + 4 * n_pairs + self._CAP * 60 * n_img + 16 * self._CAP * n_pairs
+        return self._export(n_img, n_pairs).nbytes
+
+    def export_batch_size(self, n_img, n_pairs, stream=None):
+        return self._export(n_img, n_pairs).nbytes
 
     def export_batch(self, ptr, n_img, n_pairs, nbytes, stream=None):
-        """The orbgpu_export_batch layout over the stub's results (zero keypoints)."""
         import ctypes
-        cap = self._CAP
-        counts = np.array([self._count(i) for i in range(n_img)], np.int32)
-        parts = [counts, counts.copy(), counts[0::2][:n_pairs].copy(),  # mono = n, as result()
-                 np.zeros(28 * cap * n_img, np.uint8)]
-        desc = np.zeros((n_img, cap, 32), np.uint8)
-        for i in range(n_img):
-            desc[i, :counts[i]] = self.result(i)[1]
-        mm = np.zeros((4, n_pairs, cap), np.int32)
-        for p in range(n_pairs):
-            res = self.knn_match(self.result(2 * p)[1], self.result(2 * p + 1)[1])
-            for k in range(4):
-                mm[k, p, :len(res[k])] = res[k]
-        buf = np.concatenate([x.view(np.uint8).reshape(-1) for x in parts + [desc, mm]])
-        assert buf.nbytes == nbytes
-        ctypes.memmove(ptr, buf.ctypes.data, nbytes)
-        return cap
+        buf = self._export(n_img, n_pairs)
+        assert buf.nbytes <= nbytes
+        ctypes.memmove(ptr, buf.ctypes.data, buf.nbytes)
+        return buf.nbytes
 
     @staticmethod
-    def decode_export(buf, n_images, n_pairs, out_cap):
-        from orbslam3lib_amd import BatchExtractor as _B
-        return _B.decode_export(buf, n_images, n_pairs, out_cap)
+    def decode_export(buf, n_images, n_pairs):
+        from orbslam3lib_amd import decode_export
+        return decode_export(buf, n_images, n_pairs)
 
     def set_profiling(self, on=True, stages=None, serialize=False):
         self._prof, self._serial = bool(on), bool(serialize)

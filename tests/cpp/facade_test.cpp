@@ -106,6 +106,16 @@ int main(int argc, char** argv) {
     std::vector<uint8_t> L = texture(W, H, 7), R = texture(W, H, 8);
     ORB_SLAM3::ORBextractor ex(2000, 1.2f, 8, 20, 7);
     if (ex.GetLevels() != 8 || ex.GetScaleFactors().size() != 8) { printf("getters\n"); return 1; }
+    {   // the facades build on the caller's current HIP device (ORBGPU_DEVICE_CURRENT): on this
+        // one-GPU process that is ordinal 0, and a context made the same way reports the same one
+        orbgpu_params p{500, 1.2f, 4, 20, 7};
+        orbgpu_ctx* c = nullptr;
+        const int rc = orbgpu_create(&p, ORBGPU_DEVICE_CURRENT, 160, 120, 2, &c);
+        const int dev = rc == ORBGPU_OK ? orbgpu_get_device(c) : rc;
+        orbgpu_destroy(c);
+        if (dev != 0) { printf("current-device context on %d\n", dev); return 1; }
+        if (orbgpu_create(&p, 4096, 160, 120, 2, &c) != ORBGPU_ERR_NO_DEVICE) { printf("bad ordinal accepted\n"); return 1; }
+    }
     cv::Mat im(H, W, CV_8U, L.data(), W), desc;
     std::vector<cv::KeyPoint> kps;
     std::vector<int> lap = {0, 1000};

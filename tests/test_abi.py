@@ -39,7 +39,7 @@ def test_library_has_gfx950_code_object():
 def test_host_entry_points():
     import orbslam3lib_amd as og
     lib = og.load_library()
-    assert lib.orbgpu_abi_version() == 1
+    assert lib.orbgpu_abi_version() == 2  # 2: packed export, ORBGPU_DEVICE_CURRENT
     names = [lib.orbgpu_stage_name(i) for i in range(lib.orbgpu_num_stages())]
     assert names == [b"k_blur_resize", b"k_blur", b"k_fast_cells<48>", b"k_fast_cells<64>", b"k_fast_cells<80>", b"k_octree",
                      b"k_orient_desc", b"k_finalize", b"k_knn2", b"k_stereo", b"k_undistort_grid", b"k_sbs_split", b"k_pack_soa", b"k_sbp", b"k_fisheye_stereo",

@@ -563,9 +563,9 @@ def test_two_threads_two_contexts_concurrently(oracle):
 def test_device_ingest_and_batch_export(oracle, stereo_rows_only):
     """The C4 ingest-rank path's two entry points (dist.ingest_scatter_gather): frames already
     in device memory (a padded stride, as a collective's receive buffer may have) go in through
-    orbgpu_ingest_images, and orbgpu_export_batch writes the batch's counts, keypoints,
-    descriptors and kNN2 results into one device buffer; decoded, it equals result() /
-    matches() and the oracle, bit for bit."""
+    orbgpu_ingest_images, and orbgpu_export_batch packs the batch's counts and its produced
+    keypoints, descriptors and kNN2 rows into one device buffer of exactly that size; decoded, it
+    equals result() / matches() and the oracle, bit for bit."""
     import orbslam3lib_amd as og
     hip = _hip()
     hip.hipMalloc.argtypes = [C.POINTER(C.c_void_p), C.c_size_t]
@@ -587,16 +587,22 @@ def test_device_ingest_and_batch_export(oracle, stereo_rows_only):
         assert hip.hipMemcpy(src.value, padded.ctypes.data, padded.nbytes, 1) == 0
         be.ingest_images(src.value, 2 * P, stride=S)
         be.run_match(laps=laps, stereo_rows_only=stereo_rows_only)
-        nbytes = be.export_batch_bytes(2 * P, P)
+        nbytes = be.export_batch_size(2 * P, P)
+        # only the produced rows: the header plus 60 B per keypoint and 16 B per query row
+        ks = [be.result(i) for i in range(2 * P)]
+        assert nbytes == 4 * (4 * P + P) + sum(60 * len(k) for k, _, _ in ks) + \
+            sum(16 * len(be.matches(p)[0]) for p in range(P))
+        assert nbytes < be.export_batch_bytes(2 * P, P)
         assert hip.hipMalloc(C.byref(dst), nbytes) == 0
         bufs.append(dst)
-        cap = be.export_batch(dst.value, 2 * P, P, nbytes)
+        used = be.export_batch(dst.value, 2 * P, P, nbytes)
+        assert used == nbytes
         be.synchronize()
         host = np.zeros(nbytes, np.uint8)
         assert hip.hipMemcpy(host.ctypes.data, dst.value, nbytes, 2) == 0
-        images, pairs = og.BatchExtractor.decode_export(host, 2 * P, P, cap)
+        images, pairs = og.BatchExtractor.decode_export(host, 2 * P, P)
         for i in range(2 * P):
-            k, d, m = be.result(i)
+            k, d, m = ks[i]
             ek, ed, em = images[i]
             assert em == m
             np.testing.assert_array_equal(ek.view(np.uint8), k.view(np.uint8))
@@ -615,3 +621,24 @@ def test_device_ingest_and_batch_export(oracle, stereo_rows_only):
         be.synchronize()
         for p in bufs:
             hip.hipFree(p)
+
+
+def test_context_on_current_device():
+    """the drop-in facades build their context on the caller's current HIP
+    device (ORBGPU_DEVICE_CURRENT) instead of ordinal 0, so a multi-camera process can place an
+    extractor on the GPU it selected (LynxHardwareAccelerator.cpp:146-204 runs one session per
+    process).  Through the C ABI: ORBGPU_DEVICE_CURRENT resolves to hipGetDevice()'s ordinal and
+    orbgpu_get_device reports it; an ordinal past the device count is ORBGPU_ERR_NO_DEVICE.  (The
+    facade side is checked by tests/cpp/facade_test.cpp.)"""
+    import orbslam3lib_amd as og
+    hip = _hip()
+    cur = C.c_int(-1)
+    assert hip.hipGetDevice(C.byref(cur)) == 0
+    be = og.BatchExtractor(500, 1.2, 4, 20, 7, device=og.DEVICE_CURRENT, width=160, height=120, max_images=2)
+    assert be.ctx.device() == cur.value
+    be.close()
+    ndev = C.c_int(0)
+    assert hip.hipGetDeviceCount(C.byref(ndev)) == 0
+    with pytest.raises(og.OrbGpuError) as ei:
+        og.BatchExtractor(500, 1.2, 4, 20, 7, device=ndev.value, width=160, height=120, max_images=2)
+    assert ei.value.code == -6

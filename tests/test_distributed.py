@@ -168,7 +168,8 @@ def test_gloo_cross_camera_match_device_path_world2():
 class _HostBatch:
     """Stands in for BatchExtractor on the CPU for ingest_scatter_gather: ingest_images /
     run_match / export_batch over host addresses (the oracle as the extractor and matcher),
-    writing the orbgpu_export_batch layout that BatchExtractor.decode_export reads."""
+    writing the packed orbgpu_export_batch layout (orbslam3lib_amd.encode_export) that
+    decode_export reads."""
 
     device_resident = False
 
@@ -189,41 +190,27 @@ class _HostBatch:
         self.res = [O.extract(im, nfeatures=self.nf, nlevels=self.nl) for im in self.imgs]
         self.m = [O.knn2(self.res[2 * p][1], self.res[2 * p + 1][1]) for p in range(len(self.imgs) // 2)]
 
+    def _export(self, n_img, n_pairs):
+        from orbslam3lib_amd import encode_export
+        return encode_export(self.res[:n_img], self.m[:n_pairs])
+
     def export_batch_bytes(self, n_img, n_pairs):
-        return 8 * n_img + 4 * n_pairs + self.out_cap * 60 * n_img + 16 * self.out_cap * n_pairs
+        return self._export(n_img, n_pairs).nbytes
+
+    def export_batch_size(self, n_img, n_pairs, stream=None):
+        return self._export(n_img, n_pairs).nbytes
 
     def export_batch(self, ptr, n_img, n_pairs, nbytes, stream=None):
         import ctypes
-
-        import numpy as np
-
-        from orbslam3lib_amd import KEYPOINT_DTYPE
-        cap = self.out_cap
-        buf = np.zeros(nbytes, np.uint8)
-        o = 0
-        counts = np.array([len(r[0]) for r in self.res], np.int32)
-        buf[o:o + 4 * n_img] = counts.view(np.uint8); o += 4 * n_img
-        buf[o:o + 4 * n_img] = np.array([r[2] for r in self.res], np.int32).view(np.uint8); o += 4 * n_img
-        buf[o:o + 4 * n_pairs] = counts[0::2].view(np.uint8); o += 4 * n_pairs
-        kp = np.zeros((n_img, cap), KEYPOINT_DTYPE)
-        desc = np.zeros((n_img, cap, 32), np.uint8)
-        for i, (k, d, _) in enumerate(self.res):
-            kp[i, :len(k)] = k
-            desc[i, :len(k)] = d.reshape(-1, 32)
-        buf[o:o + kp.nbytes] = kp.view(np.uint8).reshape(-1); o += kp.nbytes
-        buf[o:o + desc.nbytes] = desc.reshape(-1); o += desc.nbytes
-        mm = np.zeros((4, n_pairs, cap), np.int32)
-        for p, res in enumerate(self.m):
-            for k in range(4):
-                mm[k, p, :len(res[k])] = res[k]
-        buf[o:o + mm.nbytes] = mm.view(np.uint8).reshape(-1)
-        ctypes.memmove(ptr, buf.ctypes.data, nbytes)
-        return cap
+        buf = self._export(n_img, n_pairs)
+        assert buf.nbytes <= nbytes
+        ctypes.memmove(ptr, buf.ctypes.data, buf.nbytes)
+        return buf.nbytes
 
     @staticmethod
-    def decode_export(buf, n_images, n_pairs, out_cap):
-        from orbslam3lib_amd import BatchExtractor
-        return BatchExtractor.decode_export(buf, n_images, n_pairs, out_cap)
+    def decode_export(buf, n_images, n_pairs):
+        from orbslam3lib_amd import decode_export
+        return decode_export(buf, n_images, n_pairs)
 
 
 def _frames_for(world, pairs, h, w):
@@ -277,3 +264,89 @@ def test_gloo_ingest_scatter_gather_world2():
         p.join(timeout=60)
         assert p.exitcode == 0
     assert all(ok for _, ok in res)
+
+
+class _FailingHostBatch(_HostBatch):
+    """_HostBatch whose extraction raises (a device error on that rank)."""
+
+    def run_match(self, stereo_rows_only=False):
+        raise RuntimeError("injected extraction failure")
+
+
+def _ingest_fail_worker(rank, world, port, q):
+    import torch.distributed as dist
+
+    from orbslam3lib_amd import dist as od
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    h, w, P = 120, 160, 1
+    frames = _frames_for(world, P, h, w) if rank == 0 else None
+    be = _FailingHostBatch(h, w) if rank == 1 else _HostBatch(h, w)
+    msg = None
+    try:
+        od.ingest_scatter_gather(dist, be, frames, pairs_per_rank=P, src=0)
+    except RuntimeError as e:
+        msg = str(e)
+    dist.barrier()  # both ranks got here: nobody is left in the gather
+    q.put((rank, msg))
+    dist.destroy_process_group()
+
+
+def test_gloo_ingest_rank_failure_world2():
+    """a rank whose extraction raises between the scatter and the gather must not leave
+    the others waiting in the gather.  ingest_scatter_gather agrees on a failure flag (max
+    all_reduce) first: rank 1 raises its own error, rank 0 (src) raises "another rank failed", and
+    both return to the caller."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ingest_fail_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=180) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[1] == "injected extraction failure"
+    assert res[0] is not None and "another rank failed" in res[0]
+
+
+def test_export_layout_roundtrip_and_status_counts():
+    """The packed orbgpu_export_batch layout (include/orbgpu.h): encode_export (the host
+    restatement) -> decode_export returns the same rows; trailing padding (the gather pads every
+    rank to the largest size) is ignored; a count holding a device status word (-5 octree
+    overflow, -2 capacity) raises OrbGpuError with that code instead of returning stale rows."""
+    import numpy as np
+
+    import orbslam3lib_amd as og
+    rng = np.random.default_rng(5)
+    images = []
+    for n in (7, 0, 12, 3):
+        k = np.zeros(n, og.KEYPOINT_DTYPE)
+        k["x"] = rng.random(n) * 600
+        k["octave"] = rng.integers(0, 8, n)
+        images.append((k, rng.integers(0, 256, (n, 32), dtype=np.uint8), n // 2))
+    pairs = [tuple(rng.integers(-1, 300, 7, dtype=np.int32) for _ in range(4)),
+             tuple(np.zeros(12, np.int32) for _ in range(4))]
+    pairs[1] = tuple(rng.integers(-1, 300, 12, dtype=np.int32) for _ in range(4))
+    buf = og.encode_export(images, pairs)
+    assert buf.nbytes == 4 * (2 * 4 + 2) + 60 * 22 + 16 * 19
+    for padded in (buf, np.concatenate([buf, np.full(100, 0xAB, np.uint8)])):
+        got_i, got_p = og.decode_export(padded, 4, 2)
+        for (k, d, m), (ek, ed, em) in zip(images, got_i):
+            assert m == em
+            np.testing.assert_array_equal(k.view(np.uint8), ek.view(np.uint8))
+            np.testing.assert_array_equal(d, ed)
+        for a, b in zip(pairs, got_p):
+            for x, y in zip(a, b):
+                np.testing.assert_array_equal(x, y)
+    for status in (-5, -2):
+        bad = buf.copy()
+        bad[4:8] = np.array([status], np.int32).view(np.uint8)  # image 1's count
+        with pytest.raises(og.OrbGpuError) as ei:
+            og.decode_export(bad, 4, 2)
+        assert ei.value.code == status
+    with pytest.raises(og.OrbGpuError):
+        og.decode_export(buf[:-1], 4, 2)  # truncated
