@@ -32,6 +32,9 @@ VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12  # 256 CU x 4 SIMD32 x 32 lanes x 2
 # dense int8 MFMA: 2x the BF16 rate per clock (MI355X_MICROARCH.md, matrix-core table: I8 32x32x32
 # takes the cycles of BF16 32x32x16), BF16 dense ~2.5 PF -> ~5.0 POPS
 MFMA_I8_PEAK_TOPS = 5000.0
+# dense block-scaled FP4 MFMA (the unit k_knn2 runs on since round 6): 4x the BF16 rate per clock
+# (32x32x64 takes the cycles of BF16 32x32x16), ~10 PF dense
+MFMA_FP4_PEAK_TOPS = 10000.0
 
 
 def level_sizes(w, h, sf=1.2, L=8):
@@ -501,11 +504,14 @@ def main():
                 row["traffic_per_launch"] = int(tb)
                 row["traffic_over_algorithmic"] = round(tb / bytes_launch, 2) if bytes_launch else None
         if name == "k_knn2":
-            # the kernel runs on the i8 matrix cores: 2 x 256 int8 ops per (query, train)
-            # pair are what it issues; the 16-op VALU popcount figure is kept beside it
+            # the kernel runs on the block-scaled FP4 matrix cores: 2 x 256 ops per
+            # (query, train) pair (one MAC per descriptor bit) are what it issues.  Priced against the
+            # dense FP4 peak; the fraction of the i8 peak (the unit of rounds 2-5) and the 16-op VALU
+            # popcount figure sit beside it
             pairs_launch = pairs_per_step / launches_per_step
-            row["Tops_i8"] = round(512.0 * pairs_launch / (avg_ms * 1e-3) / 1e12, 1)
-            row["frac_mfma_i8"] = round(row["Tops_i8"] / MFMA_I8_PEAK_TOPS, 4)
+            row["Tops_mfma"] = round(512.0 * pairs_launch / (avg_ms * 1e-3) / 1e12, 1)
+            row["frac_mfma_fp4"] = round(row["Tops_mfma"] / MFMA_FP4_PEAK_TOPS, 4)
+            row["frac_of_i8_peak"] = round(row["Tops_mfma"] / MFMA_I8_PEAK_TOPS, 4)
             row["Tops"] = round(16.0 * pairs_launch / (avg_ms * 1e-3) / 1e12, 2)
             row["frac_valu"] = round(row["Tops"] / VALU_PEAK_TOPS, 4)
         stage_rows[name] = row
@@ -530,9 +536,9 @@ def main():
                     "bytes_per_launch": r["bytes_per_launch"], "avg_us": r["avg_us"],
                     "launch": "whole batch (%d images), serialized pass, kernel alone" % n_img,
                     "launches": r["launches"], "concurrent": r.get("concurrent")}
-        elif "Tops_i8" in r:
-            roof = {"kernel": dom, "bound": "mfma_i8", "achieved": r["Tops_i8"], "peak": MFMA_I8_PEAK_TOPS,
-                    "unit": "Tops/s", "frac": r["frac_mfma_i8"], "traffic": r.get("traffic_per_launch"),
+        elif "Tops_mfma" in r:
+            roof = {"kernel": dom, "bound": "mfma_fp4", "achieved": r["Tops_mfma"], "peak": MFMA_FP4_PEAK_TOPS,
+                    "unit": "Tops/s", "frac": r["frac_mfma_fp4"], "traffic": r.get("traffic_per_launch"),
                     "avg_us": r["avg_us"]}
         else:
             roof = {"kernel": dom, "bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS,
@@ -575,13 +581,14 @@ def main():
                      "definition": "SQ_ACTIVE_INST_VALU x 4 / (1024 SIMDs x GRBM_GUI_ACTIVE / 8), "
                                    "whole-batch launches, kernel alone"}
 
-    # the matcher's own roofline (north_star: "Hamming BFMatch"): it runs on the int8 matrix cores
+    # the matcher's own roofline (north_star: "Hamming BFMatch"): it runs on the FP4 matrix cores
     kr = stage_rows.get("k_knn2")
     roof_knn = None
-    if kr and "Tops_i8" in kr:
-        roof_knn = {"kernel": "k_knn2", "bound": "mfma_i8", "achieved": kr["Tops_i8"], "peak": MFMA_I8_PEAK_TOPS,
-                    "unit": "Tops/s", "frac": kr["frac_mfma_i8"], "avg_us": kr["avg_us"],
-                    "ops_per_pair": 512, "valu_equivalent_Tops": kr["Tops"], "frac_valu_int32": kr["frac_valu"]}
+    if kr and "Tops_mfma" in kr:
+        roof_knn = {"kernel": "k_knn2", "bound": "mfma_fp4", "achieved": kr["Tops_mfma"], "peak": MFMA_FP4_PEAK_TOPS,
+                    "unit": "Tops/s", "frac": kr["frac_mfma_fp4"], "avg_us": kr["avg_us"],
+                    "ops_per_pair": 512, "frac_of_i8_peak": kr["frac_of_i8_peak"], "i8_peak": MFMA_I8_PEAK_TOPS,
+                    "valu_equivalent_Tops": kr["Tops"], "frac_valu_int32": kr["frac_valu"]}
 
     # Frame::ComputeStereoMatches on the same resident batch, timed on its own
     # (not part of the headline step): EuRoC-like rig, baseline 0.11 m, fx 435.2

@@ -67,7 +67,6 @@ struct BatchArgs {
     long long octws_img_stride;
     uint32_t* lvlkey;                // [img][level kps] packed key
     float* lvlangle;                 // [img][level kps]
-    float2* lvlsc;                   // [img][level kps] (sin, cos) of the keypoint's rotation (k_orient)
     uint8_t* lvldesc;                // [img][level kps][32]
     int lvlkp_img_stride;            // keypoints
     int32_t* lvlcnt;                 // [img][kMaxLevels]
@@ -80,8 +79,7 @@ struct BatchArgs {
     const int32_t* laps;             // [img][2]
     int total_cells, total_tiles, total_od_blocks;
     int fast_tab_off;  // rtab index of k_fast_cells' per-cell records (2 int4 per flattened cell)
-    int od_tab_off;    // rtab index of k_desc's per-block records {level, block, 0, 0}
-    int or_tab_off, total_or_blocks;  // k_orient's per-block records {level, block of the level}
+    int od_tab_off;    // rtab index of k_orient_desc's per-block records {level, block, 0, 0}
     int fast_n48;  // k_fast_cells records [0, fast_n48) run the 48-byte FAST tile,
     int fast_n64;  // [fast_n48, fast_n64) the 64-byte one, the rest the 80-byte one (records are
                    // grouped by tile, levels in order inside each group)
@@ -207,7 +205,6 @@ constexpr int kOdKpBlock = 8;  // keypoints per k_orient_desc pass (256 threads,
 // headline at 3 vs 2 passes +0.2 to +2.3% (bench A/B, 3 rounds).  Contexts of a few images take 1
 // (orb_runtime.cpp set_geometry).
 constexpr int kOdBlockKps = 3 * kOdKpBlock;
-constexpr int kOrientBlockKps = 256;  // keypoints per k_orient workgroup (4 waves x 64)
 
 constexpr int kOctLdsKeys = 16384;  // per-key node labels (u16) kept in LDS up to this many keys
 constexpr int kFastMergeMaxImages = 4;  // launches this small run the 48/64 FAST cells as one launch

@@ -8,9 +8,7 @@
 //                          3x3 nonmax at iniTh / minTh fallback, ordered compaction (one launch
 //                          per LDS tile size)
 //   k_octree      x 1      one workgroup per (image, level): DistributeOctTree
-//   k_orient     x 1      32 lanes per keypoint for the moments, then one lane per keypoint:
-//                          IC_Angle and the sin / cos of its rotation
-//   k_desc       x 1      32 lanes per keypoint: rBRIEF 256 bit from an LDS-staged patch
+//   k_orient_desc x 1      32 lanes per keypoint: IC_Angle + rBRIEF 256 bit
 //   k_finalize    x 1      one workgroup per image: scale + mono/stereo partition
 //   k_knn2_mfma   x 1      Hamming k=2 brute force on the i8 matrix cores
 #include <hip/hip_runtime.h>
@@ -1007,39 +1005,48 @@ __device__ inline int od_sum(int v) {
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
-// IC_Angle (ORBextractor_old.cc:78-105) and computeOrbDescriptor (:108-148) as two kernels.
-// Round 5's single kernel ran fastAtan2 + libm sinf / cosf (~150 VALU: a float division and the
-// double-precision reduction) in all 32 lanes of every keypoint; here the angle and its sin / cos
-// are computed once per keypoint, one lane each:
-//   k_orient: 32 lanes per keypoint sum the moments (coalesced row chunks, below), 64 keypoints
-//     per wave (group g of 32 lanes takes keypoints kw + 32 g + p, p = 0..31), and lane p of
-//     group g keeps the sums of pass p; then every lane turns its keypoint's m_01 / m_10 into
-//     the angle (written to lvlangle) and sin / cos of angle * pi / 180 (lvlsc);
-//   k_desc: 32 lanes per keypoint sample the 256 test pairs from the keypoint's blurred patch
-//     staged in LDS, rotated by the (sin, cos) k_orient wrote.
-// Both keep the reference's float expressions operation by operation (no contraction).
-
-// Moments from coalesced row chunks: the 31 disc rows of a keypoint are read as 16-byte aligned
-// chunks of the 48-byte window that starts at xa16 = (x - 15) & ~15 (it holds x - 15 .. x + 15
-// for every x).  Chunk slot i = sub + 32 it (it < 3) is disc row r = i / 3 (v = r - 15; r = 31
-// lies past the disc) and part i % 3, so the three lanes of a row read 48 contiguous bytes.
-// Each chunk adds its masked byte sums: s = sum of p, c = sum of (column - xa16) p over the disc
-// span |u| <= umax[|v|], i.e. chunk bytes [m, n) with m, n from the alignment a = (x - 15) & 15
-// and two per-lane constants; the byte masks of every [m, n) are an LDS table, so a chunk is one
-// b128 LDS read, 4 ANDs and 8 v_dot4_u32_u8.  Then m_10 = sum c - (15 + a) sum s and
-// m_01 = sum v s.
-constexpr int kOrWaveKps = 64;                 // keypoints per k_orient wave
-constexpr int kOrBlockKps = 4 * kOrWaveKps;    // per 256-thread workgroup
-static_assert(kOrBlockKps == kOrientBlockKps, "orb_kernels.h kOrientBlockKps");
-
-__global__ __launch_bounds__(256) void k_orient(BatchArgs a, uint32_t nblk_magic) {
-    __shared__ __attribute__((aligned(16))) uint4 s_rng[17][17];  // bytes [m, n) of 16 (none if n <= m)
+// k_orient_desc: IC_Angle on the raw level (ORBextractor_old.cc:78-105) then
+// computeOrbDescriptor on the blurred level (:108-148): a = (float)cos, b = (float)sin of
+// angle*pi/180 (float), sample center[cvRound(x*b + y*a)*step + cvRound(x*a - y*b)].
+// 32 lanes per keypoint (two independent groups per wave): lane `sub` owns disc row v = sub - 15
+// for the moments and test pairs [8 sub, 8 sub + 8), sampled from the keypoint's blurred patch
+// staged in LDS.  The kernel waits on dependent memory round trips per keypoint (key, moment
+// rows + patch); few vector-memory instructions and registers per lane keep many of them in
+// flight.
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k_orient_desc(
+    BatchArgs a, uint32_t nblk_magic) {
+    // per keypoint group: the blurred patch around the keypoint, staged with 16-byte loads
+    __shared__ __attribute__((aligned(16))) uint8_t patch[kOdKpBlock][kOdPatchRows * kOdPatchPitch];
     const int wg = xcd_remap(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * gridDim.y);
+    // wg / gridDim.x by the host's magic multiplier; the block's level from a host record (no
+    // level search with dependent kernarg loads)
     const int irel = gridDim.x == 1 ? wg : (int)__umulhi((uint32_t)wg, nblk_magic);
     const int img = a.img0 + irel, bx = wg - irel * (int)gridDim.x;
-    const int4 rec = a.rtab[a.or_tab_off + bx];  // {level, block of the level}
-    const int l = rec.x;
+    const int l = a.rtab[a.od_tab_off + bx].x;
     const LevelGeom G = a.lv[l];
+    const int sub = threadIdx.x % kOdLanes, grp = threadIdx.x / kOdLanes;
+    const int count = a.lvlcnt[img * kMaxLevels + l];
+    const long long kbase = (long long)img * a.lvlkp_img_stride + G.kp_off;
+    const uint8_t* lvl = a.lvl_base[l] + (long long)img * G.img_stride;
+    const uint8_t* blr = a.blur_base[l] + (long long)img * G.bimg_stride;
+    const bool raw_dw = ((G.pitch | G.img_stride) & 3) == 0;
+    // raw buffer over this image's blurred level (dword 3 = gfx9 raw-buffer format word)
+    const __amdgpu_buffer_rsrc_t brs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)blr, (short)0, G.bpitch * G.h, 0x00020000);
+    const int stride_k = G.od_blocks * kOdKpBlock;
+    // Moments from coalesced row chunks: the 31 disc rows of a keypoint are read as 16-byte
+    // aligned chunks of the 48-byte window that starts at xa16 = (x - 15) & ~15 (it holds
+    // x - 15 .. x + 15 for every x).  Chunk slot i = sub + 32 it (it < 3) is disc row r = i / 3
+    // (v = r - 15; r = 31 lies past the disc) and part i % 3, so the three lanes of a row read 48
+    // contiguous bytes -- one or two cache lines per row instead of three 16-byte / dword loads
+    // per row lane (round 4: ~105 of the ~160 L1 accesses per keypoint were those).  Each chunk
+    // adds its masked byte sums: s = sum of p, c = sum of (column - xa16) p over the disc span
+    // |u| <= umax[|v|], i.e. chunk bytes [m, n) with m, n from the alignment a = (x - 15) & 15 and
+    // two per-lane constants; the byte masks of every [m, n) are an LDS table, so a chunk is one
+    // b128 LDS read, 4 ANDs and 8 v_dot4_u32_u8.  Then m_10 = sum c - (15 + a) sum s and
+    // m_01 = sum v s.
+    __shared__ __attribute__((aligned(16))) uint4 s_rng[17][17];  // bytes [m, n) of 16 (none if n <= m)
+    __shared__ __attribute__((aligned(16))) uint4 s_pat[kOdPairs][kOdLanes];
     for (int e = threadIdx.x; e < 17 * 17; e += 256) {
         const int m = e / 17, n = e - 17 * m;
         uint32_t w4[4];
@@ -1051,17 +1058,12 @@ __global__ __launch_bounds__(256) void k_orient(BatchArgs a, uint32_t nblk_magic
         }
         s_rng[m][n] = make_uint4(w4[0], w4[1], w4[2], w4[3]);
     }
+    {
+        const int8_t* pv = c_pattern.v + 4 * threadIdx.x;  // x0, y0, x1, y1 of pair threadIdx.x
+        s_pat[threadIdx.x % kOdPairs][threadIdx.x / kOdPairs] = make_uint4(__float_as_uint((float)pv[0]), __float_as_uint((float)pv[2]),
+                                        __float_as_uint((float)pv[1]), __float_as_uint((float)pv[3]));
+    }
     __syncthreads();
-    const int lane = threadIdx.x & 63, sub = lane & 31, grp = lane >> 5;
-    const int count = a.lvlcnt[img * kMaxLevels + l];
-    const int kw = rec.y * kOrBlockKps + (threadIdx.x >> 6) * kOrWaveKps;  // the wave's first keypoint
-    if (kw >= count) return;
-    const int npass = min(32, count - kw);  // wave-uniform; group 1 runs past its keypoints
-    const long long kbase = (long long)img * a.lvlkp_img_stride + G.kp_off;
-    const uint8_t* lvl = a.lvl_base[l] + (long long)img * G.img_stride;
-    const bool raw_dw = ((G.pitch | G.img_stride) & 3) == 0;
-    const __amdgpu_buffer_rsrc_t lrs =
-        __builtin_amdgcn_make_buffer_rsrc((void*)lvl, (short)0, (int)min((long long)G.pitch * G.h, 0x7fffffffLL), 0x00020000);
     // this lane's three chunk slots: row v, chunk bytes [lo + a, hi + a) clamped to [0, 16) are
     // the disc span (lo = 15 - d - 16 part, hi = 16 + d - 16 part, d = umax[|v|], -1 past the
     // disc), the part's column offset and the byte offset from the window
@@ -1076,14 +1078,31 @@ __global__ __launch_bounds__(256) void k_orient(BatchArgs a, uint32_t nblk_magic
         mofs[it] = (r < 31 ? mv[it] : 15) * G.pitch + 16 * part;
         mp16[it] = 16 * part;
     }
-    // the wave's 64 keys in one coalesced load; pass p of group g reads lane 32 g + p's
-    const uint32_t key_l = a.lvlkey[kbase + min(kw + lane, count - 1)];
-    auto issue = [&](int p, uint4 (&mc)[3], int& al) __attribute__((always_inline)) {
-        const uint32_t k0 = __builtin_amdgcn_readlane(key_l, p), k1 = __builtin_amdgcn_readlane(key_l, p + 32);
-        const uint32_t key = grp ? k1 : k0;
+    const __amdgpu_buffer_rsrc_t lrs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)lvl, (short)0, (int)min((long long)G.pitch * G.h, 0x7fffffffLL), 0x00020000);
+    uint8_t* pt = patch[grp];
+    // uniform trip count per wave so the group shuffles see all lanes
+    const int wave_first = (bx - G.od_first) * kOdKpBlock + (threadIdx.x >> 6) * 2;
+    // each iteration's key is loaded one iteration ahead, so its round trip overlaps the
+    // previous keypoint's work
+    auto key_at = [&](int kb) {
+        const int kp = kb + (grp & 1);
+        return kp < count ? a.lvlkey[kbase + kp] : a.lvlkey[kbase + kb];
+    };
+    uint32_t key_next = wave_first < count ? key_at(wave_first) : 0u;
+    for (int kb = wave_first; kb < count; kb += stride_k) {
+        const int kp = kb + (grp & 1);
+        const bool valid = kp < count;
+        const uint32_t key = key_next;
+        if (kb + stride_k < count) key_next = key_at(kb + stride_k);
         const int x = key_x(key) + kMinBorder, y = key_y(key) + kMinBorder;
-        al = (x - 15) & 15;
+        const int al = (x - 15) & 15;
         const int wofs = y * G.pitch + (x - 15 - al);  // the 48-byte window of disc row 0
+        // the three moment chunks (round trip 1) and the 37 x 37 blurred patch (rows y-18..y+18
+        // from the dword at or below x-18, 16-byte buffer loads, out-of-range bytes read as 0
+        // and never sampled) are both requested before either is used, so the two round trips
+        // overlap; window bytes past x + 15 (or past the plane: 0) only meet zero masks
+        uint4 mc[3];
 #pragma unroll
         for (int it = 0; it < 3; ++it) {
             if (raw_dw) {
@@ -1099,20 +1118,19 @@ __global__ __launch_bounds__(256) void k_orient(BatchArgs a, uint32_t nblk_magic
                 mc[it] = make_uint4(d4[0], d4[1], d4[2], d4[3]);
             }
         }
-    };
-    int my10 = 0, my01 = 0;
-    // two passes' rows in flight while a pass sums (a pass is ~80 VALU against a load round trip)
-    uint4 q0[3], q1[3];
-    int a0 = 0, a1 = 0;
-    issue(0, q0, a0);
-    if (npass > 1) issue(1, q1, a1);
-    for (int p = 0; p < npass; ++p) {
-        const uint4 mc[3] = {q0[0], q0[1], q0[2]};
-        const int al = a0;
+        const int xb = (x - kOdPatchR) & ~3;
+        const int pofs = (y - kOdPatchR) * G.bpitch + xb;
+        uint4 pv[kOdPatchIt];
 #pragma unroll
-        for (int it = 0; it < 3; ++it) q0[it] = q1[it];
-        a0 = a1;
-        if (p + 2 < npass) issue(p + 2, q1, a1);
+        for (int it = 0; it < kOdPatchIt; ++it) {
+            const int c = sub + it * kOdLanes;
+            const int r = c / 3, part = c - 3 * r;
+            if (c < kOdPatchChunks) {
+                const auto q = __builtin_amdgcn_raw_buffer_load_b128(brs, pofs + r * G.bpitch + 16 * part, 0, 0);
+                pv[it] = make_uint4(q[0], q[1], q[2], q[3]);
+            }
+        }
+        // IC_Angle (:78-105) over this lane's three chunks
         int s_all = 0, c_all = 0, m01p = 0;
 #pragma unroll
         for (int it = 0; it < 3; ++it) {
@@ -1131,98 +1149,15 @@ __global__ __launch_bounds__(256) void k_orient(BatchArgs a, uint32_t nblk_magic
             c_all += (int)cc + mp16[it] * (int)sc;
             m01p += mv[it] * (int)sc;
         }
-        // sums over the keypoint's 32 lanes (DPP, and one ds_swizzle); lane p of the group keeps them
+        // sums over the keypoint's lanes (DPP, no LDS round trip but the last step)
         const int m10 = od_sum(c_all - (15 + al) * s_all), m01 = od_sum(m01p);
-        if (sub == p) {
-            my10 = m10;
-            my01 = m01;
-        }
-    }
-    const int kp = kw + lane;  // this lane's keypoint (32 grp + sub)
-    if (kp < count) {
-        const float angle = fast_atan2_deg((float)my01, (float)my10);
+        const float angle = fast_atan2_deg((float)m01, (float)m10);
+        // computeOrbDescriptor (:108-148): lane `sub` makes bits [8 sub, 8 sub + 8)
         const float factorPI = (float)(3.14159265358979323846 / 180.0);
         float sn, ca;  // std::sin(float) / std::cos(float) (:114-115): libm sinf / cosf
         libm_sincosf(angle * factorPI, &sn, &ca);
-        a.lvlangle[kbase + kp] = angle;
-        a.lvlsc[kbase + kp] = make_float2(sn, ca);
-    }
-}
-
-// k_desc: 32 lanes per keypoint (two independent groups per wave): lane `sub` makes test pairs
-// [8 sub, 8 sub + 8), sampled from the keypoint's blurred 37 x 37 patch staged in LDS with 16-byte
-// buffer loads: a = (float)cos, b = (float)sin of angle * pi / 180, sample
-// center[cvRound(x*b + y*a)*step + cvRound(x*a - y*b)].  A workgroup makes several passes of 8
-// keypoints; each pass's key and (sin, cos) are loaded one pass ahead.
-__global__ __launch_bounds__(256) void k_desc(BatchArgs a, uint32_t nblk_magic) {
-    __shared__ __attribute__((aligned(16))) uint8_t patch[kOdKpBlock][kOdPatchRows * kOdPatchPitch];
-    __shared__ __attribute__((aligned(16))) uint4 s_pat[kOdPairs][kOdLanes];
-    const int wg = xcd_remap(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * gridDim.y);
-    const int irel = gridDim.x == 1 ? wg : (int)__umulhi((uint32_t)wg, nblk_magic);
-    const int img = a.img0 + irel, bx = wg - irel * (int)gridDim.x;
-    const int l = a.rtab[a.od_tab_off + bx].x;
-    const LevelGeom G = a.lv[l];
-    const int sub = threadIdx.x % kOdLanes, grp = threadIdx.x / kOdLanes;
-    const int count = a.lvlcnt[img * kMaxLevels + l];
-    const long long kbase = (long long)img * a.lvlkp_img_stride + G.kp_off;
-    const uint8_t* blr = a.blur_base[l] + (long long)img * G.bimg_stride;
-    // raw buffer over this image's blurred level (dword 3 = gfx9 raw-buffer format word)
-    const __amdgpu_buffer_rsrc_t brs =
-        __builtin_amdgcn_make_buffer_rsrc((void*)blr, (short)0, G.bpitch * G.h, 0x00020000);
-    const int stride_k = G.od_blocks * kOdKpBlock;
-    {
-        const int8_t* pv = c_pattern.v + 4 * threadIdx.x;  // x0, y0, x1, y1 of pair threadIdx.x
-        s_pat[threadIdx.x % kOdPairs][threadIdx.x / kOdPairs] = make_uint4(__float_as_uint((float)pv[0]), __float_as_uint((float)pv[2]),
-                                        __float_as_uint((float)pv[1]), __float_as_uint((float)pv[3]));
-    }
-    __syncthreads();
-    uint8_t* pt = patch[grp];
-    // uniform trip count per wave so the group's lanes stay together
-    const int wave_first = (bx - G.od_first) * kOdKpBlock + (threadIdx.x >> 6) * 2;
-    auto kp_at = [&](int kb) { const int kp = kb + (grp & 1); return kp < count ? kp : kb; };
-    // software pipeline over the passes: pass i + 1's patch is requested before pass i samples
-    // (its key one pass earlier still), so a pass waits on no memory round trip of its own
-    auto patch_load = [&](uint32_t key, uint4 (&pv)[kOdPatchIt]) __attribute__((always_inline)) {
-        const int x = key_x(key) + kMinBorder, y = key_y(key) + kMinBorder;
-        // the 37 x 37 blurred patch (rows y-18..y+18 from the dword at or below x-18, 16-byte
-        // buffer loads; out-of-range bytes read as 0 and are never sampled)
-        const int pofs = (y - kOdPatchR) * G.bpitch + ((x - kOdPatchR) & ~3);
-#pragma unroll
-        for (int it = 0; it < kOdPatchIt; ++it) {
-            const int c = sub + it * kOdLanes;
-            const int r = c / 3, part = c - 3 * r;
-            if (c < kOdPatchChunks) {
-                const auto q = __builtin_amdgcn_raw_buffer_load_b128(brs, pofs + r * G.bpitch + 16 * part, 0, 0);
-                pv[it] = make_uint4(q[0], q[1], q[2], q[3]);
-            }
-        }
-    };
-    uint32_t key = 0, key_n = 0;
-    float2 scv = make_float2(0.f, 0.f);
-    uint4 pv[kOdPatchIt];
-    if (wave_first < count) {
-        key = a.lvlkey[kbase + kp_at(wave_first)];
-        scv = a.lvlsc[kbase + kp_at(wave_first)];
-        if (wave_first + stride_k < count) key_n = a.lvlkey[kbase + kp_at(wave_first + stride_k)];
-        patch_load(key, pv);
-    }
-    for (int kb = wave_first; kb < count; kb += stride_k) {
-        const int kp = kb + (grp & 1);
-        const bool valid = kp < count;
-        const bool more = kb + stride_k < count;
-        uint4 pvn[kOdPatchIt];
-        uint32_t key_nn = 0;
-        float2 sc_n = make_float2(0.f, 0.f);
-        if (more) {
-            patch_load(key_n, pvn);
-            sc_n = a.lvlsc[kbase + kp_at(kb + stride_k)];
-            if (kb + 2 * stride_k < count) key_nn = a.lvlkey[kbase + kp_at(kb + 2 * stride_k)];
-        }
-        const int x = key_x(key) + kMinBorder;
-        const int xb = (x - kOdPatchR) & ~3;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the previous pass's samples are read
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // the patch to LDS: every sample is then an LDS byte read (4 vector-memory instructions
+        // per lane instead of one scattered byte load per sample)
 #pragma unroll
         for (int it = 0; it < kOdPatchIt; ++it) {
             const int c = sub + it * kOdLanes;
@@ -1240,7 +1175,7 @@ __global__ __launch_bounds__(256) void k_desc(BatchArgs a, uint32_t nblk_magic) 
         // the two bit patterns and a per-keypoint constant (no v_rndne / v_cvt per sample)
         const float magic = 12582912.0f;
         const uint32_t kofs = (uint32_t)pc - 0x4B400000u - 0x400000u * (uint32_t)kOdPatchPitch;
-        const f32x2 snv = {scv.x, scv.x}, cav = {scv.y, scv.y}, mg = {magic, magic};
+        const f32x2 snv = {sn, sn}, cav = {ca, ca}, mg = {magic, magic};
         uint32_t bits = 0;
 #pragma unroll
         for (int b = kOdPairs - 1; b >= 0; --b) {  // bits = 2 bits + test, last pair first
@@ -1255,13 +1190,9 @@ __global__ __launch_bounds__(256) void k_desc(BatchArgs a, uint32_t nblk_magic) 
             const int o1 = (int)(__umul24(__float_as_uint(R.y), (uint32_t)kOdPatchPitch) + __float_as_uint(C.y) + kofs);
             bits = bits + bits + (pt[o0] < pt[o1] ? 1u : 0u);
         }
-        if (valid) a.lvldesc[(kbase + kp) * 32 + sub] = (uint8_t)bits;
-        if (more) {
-#pragma unroll
-            for (int it = 0; it < kOdPatchIt; ++it) pv[it] = pvn[it];
-            key = key_n;
-            key_n = key_nn;
-            scv = sc_n;
+        if (valid) {
+            if (sub == 0) a.lvlangle[kbase + kp] = angle;
+            a.lvldesc[(kbase + kp) * 32 + sub] = (uint8_t)bits;
         }
     }
 }
@@ -1414,269 +1345,186 @@ __device__ inline void knn2_store(uint32_t k1, uint32_t k2, int qi, int32_t* i1,
 }
 
 // ---------------------------------------------------------------------------------------------
-// k_knn2_mfma: BFMatcher(NORM_HAMMING).knnMatch(k=2) on the matrix cores.  With every descriptor
-// bit b mapped to +-64 (int8), the i8 MFMA dot of a train row t and a query q is
-// 4096 * (256 - 2 * Hamming(t, q)); the accumulator is preloaded with 4095 - (t mod 4096), so
-// acc = 4096 * (256 - 2H) + 4095 - t_local orders exactly like (H, t) ascending and the best two
-// train rows are the two largest accumulators (no popcount, no per-pair VALU beyond the top-2
-// update).  Train rows are walked in 4096-row segments (12-bit local index); each segment's
-// winners are folded into (H << 16 | t) keys, the layout of the VALU matcher.
-//   workgroup = kKnnWaves waves x kKnnNB x 32 queries; per 32-row train tile each wave issues
-//   8 kKnnNB v_mfma_i32_32x32x32_i8 (K = 256 bits): A = train tile (expanded once per workgroup
-//   into LDS, double-buffered; each fragment read feeds kKnnNB MFMAs), B = the wave's queries
+// k_knn2_mfma: BFMatcher(NORM_HAMMING).knnMatch(k=2) on the block-scaled FP4 matrix cores.
+// Every descriptor bit becomes one e2m1 element, +1 (0x2) for a clear bit and -1 (0xA) for a set
+// one, on both operands; with an E8M0 scale of 2^6 per 32-element block on each side,
+// v_mfma_scale_f32_32x32x64_f8f6f4 gives 4096 * (64 - 2 H) over its K = 64 bits, so a train tile
+// of 32 rows against 32 queries is 4 MFMAs over the 256 bits, at twice the MACs per cycle of the
+// i8 form (MI355X_MICROARCH.md: FP4 32x32x64 takes the cycles of BF16 32x32x16).  The f32
+// accumulator is preloaded with 4095 - (t mod 4096), so acc = 4096 (256 - 2H) + 4095 - t_local
+// (every value an integer below 2^24, exact) orders like (H, t) ascending and the best two train
+// rows are the two largest accumulators: no popcount, no per-pair VALU beyond the top-2 update.
+// Train rows are walked in 4096-row segments (12-bit local index); each segment's winners are
+// folded into (H << 16 | t) keys.
+//   workgroup = 8 waves x 32 queries; per 32-row train tile each wave issues 4 MFMAs: A = the
+//   train tile (expanded once per workgroup into LDS, double-buffered), B = the wave's queries
 //   (expanded once into registers).
 // C/D layout (cdna_hip_programming.md §3): lane l holds column l & 31 (its query) and rows
-// (reg & 3) + 8 (reg >> 2) + 4 (l >> 5) of the tile (train rows); the K order inside a
-// fragment is the same map for A and B, so any consistent bit -> element assignment is exact.
-typedef int knn_v4i __attribute__((ext_vector_type(4)));
-typedef int knn_v16i __attribute__((ext_vector_type(16)));
-// Register blocking: each wave holds kKnnNB sets of 32 queries (B fragments), so every train
-// fragment read from LDS feeds kKnnNB MFMAs; the workgroup keeps kKnnQueries = 256 queries with
-// 8 / kKnnNB waves.
-#ifndef KNN_NB
-#define KNN_NB 2
-#endif
-constexpr int kKnnNB = KNN_NB;
-static_assert(kKnnNB == 1 || kKnnNB == 2, "query sets per wave");
-constexpr int kKnnWaves = 8 / kKnnNB;
+// (reg & 3) + 8 (reg >> 2) + 4 (l >> 5) of the tile (train rows); the K order inside a fragment is
+// the same map for A and B, so any consistent bit -> element assignment is exact.
+// Measured and replaced (round 6, single stream, 512 images): the i8 form
+// (v_mfma_i32_32x32x32_i8, bits as +-64 bytes, 8 MFMAs per tile) 230-238 us against 159-167 us;
+// two query sets per wave on the i8 form (each LDS-read train fragment feeding two MFMAs; 186
+// VGPRs, 2 waves per SIMD) 256 us, and with one accumulator set selected after its own tile 237 us.
+// Round 2's FP4 attempt lost to its nibble expansion; here a dword expands to its 32 nibbles with
+// one shift and one v_and_or_b32 per 8 nibbles.
+typedef int knn_v8i __attribute__((ext_vector_type(8)));
+typedef float knn_v16f __attribute__((ext_vector_type(16)));
+constexpr int kKnnWaves = 8;
 constexpr int kKnnThreads = 64 * kKnnWaves;
-constexpr int kKnnQ = 32 * kKnnNB * kKnnWaves;  // queries per workgroup
+constexpr int kKnnQ = 32 * kKnnWaves;    // queries per workgroup
 static_assert(kKnnQ == kKnnQueries, "orb_kernels.h kKnnQueries (grid and arrival counters)");
-#ifndef KNN_WPE
-#define KNN_WPE 2
-#endif
-constexpr int kKnnWavesPerEU = KNN_WPE;  // register budget: waves per SIMD the kernel must fit
-#ifndef KNN_DBUF
-#define KNN_DBUF 1
-#endif
-constexpr bool kKnnDbuf = KNN_DBUF != 0;  // select tile i - 1 during tile i's MFMAs (two accumulator sets)
-constexpr int kKnnPitch = 272;           // bytes per expanded train row in LDS (256 + 16: no bank conflicts)
 constexpr int kKnnSeg = 4096;            // train rows per key segment
-
-// Descriptor dword w -> 32 int8 (-64 for a set bit, +64 otherwise; the sign is the same on both
-// operands, so the dot is still 4096 (256 - 2H)): K element 4 m + j of the dword's MFMA step is
-// bit m + 8 j, i.e. expanded dword m = ((w << (7 - m)) & 0x80808080) | 0x40404040 -- one shift and
-// one v_and_or_b32 per 4 bytes (round 4: bit k -> byte k through a 24-bit multiply, ~5 VALU).
-// Any bit -> K assignment is exact as long as queries and train rows share it.
-__device__ inline uint32_t knn_bytes_of(uint32_t ws) {
-    uint32_t r;  // one v_and_or_b32 (the compiler splits it into v_and + v_or)
-    asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(ws), "v"(0x80808080u), "v"(0x40404040u));
+constexpr int kKnnPitch4 = 144;          // bytes per expanded train row (128 + 16: conflict-free b128 reads)
+// bit 3 of each nibble from ws, nibble = 0x2 (+1) or 0xA (-1): one v_and_or_b32
+__device__ inline uint32_t knn_nib_of(uint32_t ws) {
+    uint32_t r;
+    asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(ws), "v"(0x88888888u), "v"(0x22222222u));
     return r;
 }
-// half hh (K elements 16 hh .. 16 hh + 15) of dword w: expanded dwords m = 4 hh .. 4 hh + 3
-__device__ inline knn_v4i knn_expand_half(uint32_t w, int hh) {
-    const uint32_t ws = w << (4 - 4 * hh);  // now every m of this half needs shift 3 - (m - 4 hh)
-    knn_v4i v;
-    v[0] = (int)knn_bytes_of(ws << 3);
-    v[1] = (int)knn_bytes_of(ws << 2);
-    v[2] = (int)knn_bytes_of(ws << 1);
-    v[3] = (int)knn_bytes_of(ws);
+// 8 nibbles of output dword m (m = 0..3) = bits m, m + 4, .., m + 28 of w, each +1 (0x2) or -1 (0xA)
+__device__ inline knn_v8i knn4_expand(uint32_t w) {
+    knn_v8i v;
+    v[0] = (int)knn_nib_of(w << 3);
+    v[1] = (int)knn_nib_of(w << 2);
+    v[2] = (int)knn_nib_of(w << 1);
+    v[3] = (int)knn_nib_of(w);
+    v[4] = v[5] = v[6] = v[7] = 0;  // the e2m1 form reads four registers
     return v;
 }
-
-// v_med3_i32 / v_max3_i32 as single instructions (the compiler's CSE of max(k1, x) otherwise
-// splits the pair into two v_max_i32 plus a v_med3_i32)
-__device__ inline int knn_med3_i32(int a, int b, int c) {
-    int r;
-    asm("v_med3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+__device__ inline float knn_med3_f32(float a, float b, float c) {
+    float r;
+    asm("v_med3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
     return r;
 }
-__device__ inline int knn_max3_i32(int a, int b, int c) {
-    int r;
-    asm("v_max3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+__device__ inline float knn_max3_f32(float a, float b, float c) {
+    float r;
+    asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
     return r;
 }
-
-// One workgroup: queries [qb * kKnnQ, +kKnnQ) of q against train tiles [ts, te) of t (all of
-// them unless the launch splits the train rows, ts even).  Without `part` the two best keys go
-// to i1 / d1 / i2 / d2; with it, to part[qi] (a split's partial top-2, merged afterwards).
-// Wave w holds query sets n = 0 .. kKnnNB - 1 of 32 queries (qb * kKnnQ + 32 (kKnnNB w + n) + r).
-// Train tiles of 32 rows are expanded once per workgroup into LDS (double-buffered, one barrier
-// per tile); each tile's body expands the next tile and loads the packed words of the one after.
-__device__ __attribute__((always_inline)) inline void knn2_mfma_block(
+__device__ __attribute__((always_inline)) inline void knn2_fp4_block(
     const uint8_t* q, int nq, const uint8_t* t, int nt, int qb, int ts, int te, int32_t* i1, int32_t* d1,
     int32_t* i2, int32_t* d2, uint2* part, uint8_t* lds) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int r = lane & 31, h = lane >> 5;
-    const int qw = qb * kKnnQ + wave * 32 * kKnnNB;  // the wave's first query
-    // B fragments: lane (r, h) of MFMA s holds bits 32 s + 16 h + [0, 16) of query qw + 32 n + r
-    knn_v4i qf[kKnnNB][8];
-#pragma unroll
-    for (int n = 0; n < kKnnNB; ++n) {
-        const int qi = qw + 32 * n + r;
+    const int qi = qb * kKnnQ + wave * 32 + r;
+    // B fragments: lane (r, h) of MFMA s holds bits 64 s + 32 h + [0, 32) = dword 2 s + h of query qi
+    knn_v8i qf[4];
+    {
         const uint4* qp = reinterpret_cast<const uint4*>(q + (long long)min(qi, max(nq - 1, 0)) * 32);
         const uint4 qa = qp[0], qc = qp[1];
-        const uint32_t dw[8] = {qa.x, qa.y, qa.z, qa.w, qc.x, qc.y, qc.z, qc.w};
-#pragma unroll
-        for (int s = 0; s < 8; ++s) qf[n][s] = knn_expand_half(dw[s], h);
+        qf[0] = knn4_expand(h ? qa.y : qa.x);
+        qf[1] = knn4_expand(h ? qa.w : qa.z);
+        qf[2] = knn4_expand(h ? qc.y : qc.x);
+        qf[3] = knn4_expand(h ? qc.w : qc.z);
     }
-    uint32_t g1[kKnnNB], g2[kKnnNB];  // (H << 16 | t), lexicographic min
-#pragma unroll
-    for (int n = 0; n < kKnnNB; ++n) g1[n] = g2[n] = 0xFFFFFFFFu;
-    // expansion role.  4 waves: thread -> (row tid >> 3, dword tid & 7) of a tile, two 16-byte
-    // stores (threads ed >= 4 store their upper half first, so each store instruction's 8 chunks
-    // start on 8 distinct 4-bank boundaries).  8 waves: thread -> (row tid >> 4, half ed & 1 of
-    // dword ed >> 1), one 16-byte store (8 lanes write 128 contiguous bytes: conflict-free).
-    constexpr int kPieces = kKnnThreads / 32;  // pieces per train row
-    const int er = tid / kPieces, ed = tid % kPieces;
+    uint32_t g1 = 0xFFFFFFFFu, g2 = 0xFFFFFFFFu;
+    // expansion: threads < 256 take (row tid >> 3, dword tid & 7) of a tile, one 16-byte store
+    // (8 lanes write 128 contiguous bytes)
+    const int er = tid >> 3, ed = tid & 7;
+    const bool expander = tid < 256;
     auto load_packed = [&](int tile) __attribute__((always_inline)) {
         const int row = min(tile * 32 + er, nt - 1);
-        if constexpr (kKnnWaves == 4)
-            return *reinterpret_cast<const uint32_t*>(t + (long long)row * 32 + 4 * ed);
-        else
-            return *reinterpret_cast<const uint32_t*>(t + (long long)row * 32 + 4 * (ed >> 1));
+        return expander ? *reinterpret_cast<const uint32_t*>(t + (long long)row * 32 + 4 * ed) : 0u;
     };
-    auto tile_lds = [&](int u) __attribute__((always_inline)) { return lds + ((u - ts) & 1) * (32 * kKnnPitch); };
+    auto tile_lds = [&](int u) __attribute__((always_inline)) { return lds + ((u - ts) & 1) * (32 * kKnnPitch4); };
     auto store_expanded = [&](int u, uint32_t w) __attribute__((always_inline)) {
-        if constexpr (kKnnWaves == 4) {
-            uint8_t* dst = tile_lds(u) + er * kKnnPitch + 32 * ed;
-            const bool kswap = ed >= 4;
-            const knn_v4i first = knn_expand_half(w, kswap ? 1 : 0), second = knn_expand_half(w, kswap ? 0 : 1);
-            *reinterpret_cast<knn_v4i*>(dst + (kswap ? 16 : 0)) = first;
-            *reinterpret_cast<knn_v4i*>(dst + (kswap ? 0 : 16)) = second;
-        } else {
-            uint8_t* dst = tile_lds(u) + er * kKnnPitch + 16 * ed;
-            *reinterpret_cast<knn_v4i*>(dst) = knn_expand_half(w, ed & 1);
+        if (expander) {
+            const knn_v8i v = knn4_expand(w);
+            *reinterpret_cast<uint4*>(tile_lds(u) + er * kKnnPitch4 + 16 * ed) = make_uint4(v[0], v[1], v[2], v[3]);
         }
     };
-    // packed train words run one tile ahead of their expansion: the word of tile u is loaded in
-    // body(u - 2) and lives in pk[u & 1]; loads are unconditional (clamped rows) so waits stay counted
     uint32_t pk0 = 0, pk1 = 0;
     if (te > ts) {
         store_expanded(ts, load_packed(ts));
         pk1 = load_packed(ts + 1);  // ts is even
     }
-    // accumulator preload, the same for every tile: row(g) = (g & 3) + 8 (g >> 2) + 4 h, so
-    // C0[g] = 4095 - 4 h - rowc(g) is 4095 - (tile-local row) and tile k of a segment yields
-    // acc = key + 32 k, key = 4096 (256 - 2H) + 4095 - (segment-local row).  The running top-2
-    // keys are kept in the frame of the tile being selected (+32 per tile) instead of
-    // re-preloading 16 accumulators per tile.
     auto rowc = [](int g) { return (g & 3) + 8 * (g >> 2); };
-    knn_v16i C0;
+    knn_v16f C0;
 #pragma unroll
-    for (int g = 0; g < 16; ++g) C0[g] = 4095 - 4 * h - rowc(g);
-    constexpr int kNone = -(1 << 30);  // below every key, and stays below after +32 per tile
-    struct Acc {
-        knn_v16i v[kKnnNB];
-    };
+    for (int g = 0; g < 16; ++g) C0[g] = (float)(4095 - 4 * h - rowc(g));
+    const float kNone = -1073741824.0f;  // -2^30: below every key, and stays below after +32 per tile
     for (int seg0 = (ts * 32 / kKnnSeg) * kKnnSeg; seg0 < te * 32; seg0 += kKnnSeg) {
-        // this segment's tiles; keys are local to tile0 (< 4096 rows), tile0 even
         const int tile0 = max(seg0 >> 5, ts), tile1 = min(te, (seg0 + kKnnSeg) >> 5);
-        // per query set two independent top-2 chains (even / odd accumulator rows),
-        // lexicographic max; the selection of tile ti - 1 runs while tile ti's MFMAs are in flight
-        int ka1[kKnnNB], ka2[kKnnNB], kb1[kKnnNB], kb2[kKnnNB];
+        float ka1 = kNone, ka2 = kNone, kb1 = kNone, kb2 = kNone;
+        auto select = [&](const knn_v16f& v, bool shift) __attribute__((always_inline)) {
+            if (shift) {
+                ka1 += 32.f;
+                ka2 += 32.f;
+                kb1 += 32.f;
+                kb2 += 32.f;
+            }
 #pragma unroll
-        for (int n = 0; n < kKnnNB; ++n) ka1[n] = ka2[n] = kb1[n] = kb2[n] = kNone;
-        // two candidates per step and chain (keys are distinct): the new best is max3(k1, x, y),
-        // the new second max(k2, med3(k1, x, y)) -- 3 VALU per 2 candidates instead of 4
-        auto select = [&](const Acc& v, bool shift) __attribute__((always_inline)) {
-#pragma unroll
-            for (int n = 0; n < kKnnNB; ++n) {
-                if (shift) {  // previous tile's frame -> this tile's frame
-                    ka1[n] += 32;
-                    ka2[n] += 32;
-                    kb1[n] += 32;
-                    kb2[n] += 32;
-                }
-#pragma unroll
-                for (int g = 0; g < 16; g += 4) {
-                    const int x0 = v.v[n][g], y0 = v.v[n][g + 1], x1 = v.v[n][g + 2], y1 = v.v[n][g + 3];
-                    ka2[n] = max(ka2[n], knn_med3_i32(ka1[n], x0, y0));
-                    ka1[n] = knn_max3_i32(ka1[n], x0, y0);
-                    kb2[n] = max(kb2[n], knn_med3_i32(kb1[n], x1, y1));
-                    kb1[n] = knn_max3_i32(kb1[n], x1, y1);
-                }
+            for (int g = 0; g < 16; g += 4) {
+                const float x0 = v[g], y0 = v[g + 1], x1 = v[g + 2], y1 = v[g + 3];
+                ka2 = fmaxf(ka2, knn_med3_f32(ka1, x0, y0));
+                ka1 = knn_max3_f32(ka1, x0, y0);
+                kb2 = fmaxf(kb2, knn_med3_f32(kb1, x1, y1));
+                kb1 = knn_max3_f32(kb1, x1, y1);
             }
         };
-        // one tile: PAR = ti & 1 picks the accumulators and the packed words
-        auto body = [&](int ti, auto par, Acc& acc, const Acc& prev) __attribute__((always_inline)) {
-            constexpr int PAR = decltype(par)::value;  // ti & 1 (ts is even)
-            // pk[u & 1] holds the word of tile u: this body expands tile ti + 1 and loads the word
-            // of tile ti + 2
+        auto body = [&](int ti, auto par, knn_v16f& acc, const knn_v16f& prev) __attribute__((always_inline)) {
+            constexpr int PAR = decltype(par)::value;
             uint32_t& pk_use = PAR ? pk0 : pk1;
             uint32_t& pk_load = PAR ? pk1 : pk0;
             __syncthreads();  // tile ti expanded; the other buffer is free
             pk_load = load_packed(ti + 2);
-            const uint8_t* ab = tile_lds(ti) + r * kKnnPitch + 16 * h;
+            const uint8_t* ab = tile_lds(ti) + r * kKnnPitch4 + 16 * h;
 #pragma unroll
-            for (int s = 0; s < 8; ++s) {
-                const knn_v4i a = *reinterpret_cast<const knn_v4i*>(ab + 32 * s);
-#pragma unroll
-                for (int n = 0; n < kKnnNB; ++n)
-                    acc.v[n] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, qf[n][s], s ? acc.v[n] : C0, 0, 0, 0);
+            for (int s = 0; s < 4; ++s) {
+                const uint4 a4 = *reinterpret_cast<const uint4*>(ab + 32 * s);
+                const knn_v8i a = {(int)a4.x, (int)a4.y, (int)a4.z, (int)a4.w, 0, 0, 0, 0};
+                acc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, qf[s], s ? acc : C0, 4, 4, 0, 133, 0, 133);
             }
-            if (kKnnDbuf && ti > tile0) select(prev, ti - 1 > tile0);
+            if (ti > tile0) select(prev, ti - 1 > tile0);
             if (ti + 1 < te) store_expanded(ti + 1, pk_use);
             if (ti * 32 + 32 > nt) {  // partial last tile: padding rows never win
 #pragma unroll
                 for (int g = 0; g < 16; ++g)
-                    if (ti * 32 + rowc(g) + 4 * h >= nt) {
-#pragma unroll
-                        for (int n = 0; n < kKnnNB; ++n) acc.v[n][g] = kNone;
-                    }
+                    if (ti * 32 + rowc(g) + 4 * h >= nt) acc[g] = kNone;
             }
-            if (!kKnnDbuf) select(acc, ti > tile0);
         };
         using P0 = std::integral_constant<int, 0>;
         using P1 = std::integral_constant<int, 1>;
-        if constexpr (kKnnDbuf) {
-            Acc acc0, acc1;
-            int ti = tile0;
-            for (; ti + 1 < tile1; ti += 2) {
-                body(ti, P0{}, acc0, acc1);
-                body(ti + 1, P1{}, acc1, acc0);
-            }
-            if (ti < tile1) {
-                body(ti, P0{}, acc0, acc1);
-                select(acc0, ti > tile0);
-            } else if (tile1 > tile0) {
-                select(acc1, tile1 - 1 > tile0);
-            }
-        } else {  // one accumulator set, selected right after its tile's MFMAs
-            Acc acc;
-            int ti = tile0;
-            for (; ti + 1 < tile1; ti += 2) {
-                body(ti, P0{}, acc, acc);
-                body(ti + 1, P1{}, acc, acc);
-            }
-            if (ti < tile1) body(ti, P0{}, acc, acc);
+        knn_v16f acc0, acc1;
+        int ti = tile0;
+        for (; ti + 1 < tile1; ti += 2) {
+            body(ti, P0{}, acc0, acc1);
+            body(ti + 1, P1{}, acc1, acc0);
         }
-        // back to segment keys: the last selected tile is tile1 - 1
+        if (ti < tile1) {
+            body(ti, P0{}, acc0, acc1);
+            select(acc0, ti > tile0);
+        } else if (tile1 > tile0) {
+            select(acc1, tile1 - 1 > tile0);
+        }
         const int unbias = 32 * (tile1 - 1 - tile0);
-#pragma unroll
-        for (int n = 0; n < kKnnNB; ++n) {
-            const int k1 = max(ka1[n], kb1[n]) - unbias;
-            const int k2 = max(min(ka1[n], kb1[n]), max(ka2[n], kb2[n])) - unbias;
-            // fold the segment's two winners into global (H << 16 | t) keys
-            auto fold = [&](int k) __attribute__((always_inline)) {
-                if (k < -(1 << 24)) return;  // padding rows only
-                const int tl = 4095 - (k & 4095), dotp = k >> 12;
-                const uint32_t key = ((uint32_t)((256 - dotp) >> 1) << 16) | (uint32_t)(32 * tile0 + tl);
-                g2[n] = med3_u32(g1[n], g2[n], key);
-                g1[n] = min(g1[n], key);
-            };
-            fold(k1);
-            fold(k2);
-        }
+        const int k1 = (int)fmaxf(ka1, kb1) - unbias;
+        const int k2 = (int)fmaxf(fminf(ka1, kb1), fmaxf(ka2, kb2)) - unbias;
+        auto fold = [&](int k) __attribute__((always_inline)) {
+            if (k < -(1 << 24)) return;  // padding rows only
+            const int tl = 4095 - (k & 4095), dotp = k >> 12;
+            const uint32_t key = ((uint32_t)((256 - dotp) >> 1) << 16) | (uint32_t)(32 * tile0 + tl);
+            g2 = med3_u32(g1, g2, key);
+            g1 = min(g1, key);
+        };
+        fold(k1);
+        fold(k2);
     }
-#pragma unroll
-    for (int n = 0; n < kKnnNB; ++n) {
-        // the two lane halves saw disjoint train rows of the same query
-        const uint32_t o1 = __shfl_xor(g1[n], 32), o2 = __shfl_xor(g2[n], 32);
-        uint32_t a1 = g1[n], a2 = med3_u32(g1[n], g2[n], o1);
-        a1 = min(a1, o1);
-        a2 = med3_u32(a1, a2, o2);
-        a1 = min(a1, o2);
-        const int qi = qw + 32 * n + r;
-        if (h == 0 && qi < nq) {
-            if (part) part[qi] = make_uint2(a1, a2);
-            else knn2_store(a1, a2, qi, i1, d1, i2, d2);
-        }
+    const uint32_t o1 = __shfl_xor(g1, 32), o2 = __shfl_xor(g2, 32);
+    g2 = med3_u32(g1, g2, o1);
+    g1 = min(g1, o1);
+    g2 = med3_u32(g1, g2, o2);
+    g1 = min(g1, o2);
+    if (h == 0 && qi < nq) {
+        if (part) part[qi] = make_uint2(g1, g2);
+        else knn2_store(g1, g2, qi, i1, d1, i2, d2);
     }
 }
+constexpr int kKnnLdsBytes = 2 * 32 * kKnnPitch4;  // two expanded train tiles
 
-__global__ __launch_bounds__(kKnnThreads) __attribute__((amdgpu_waves_per_eu(kKnnWavesPerEU))) void k_knn2_mfma_pairs(MatchArgs m) {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * 32 * kKnnPitch];
+__global__ __launch_bounds__(kKnnThreads) void k_knn2_mfma_pairs(MatchArgs m) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kKnnLdsBytes];
     const int pair = m.pair0 + blockIdx.y;
     const int qimg = 2 * pair, timg = 2 * pair + 1;
     const int qn = m.out_n[qimg], tn = m.out_n[timg];
@@ -1692,7 +1540,7 @@ __global__ __launch_bounds__(kKnnThreads) __attribute__((amdgpu_waves_per_eu(kKn
     const int npt = (((nt + 31) >> 5) + 1) >> 1, S = gridDim.z, sp = blockIdx.z;  // tile pairs
     const int ts = 2 * (npt * sp / S), te = min((nt + 31) >> 5, 2 * (npt * (sp + 1) / S));
     uint2* part = m.part ? m.part + ((long long)(blockIdx.y * S + sp)) * m.out_cap : nullptr;
-    knn2_mfma_block(q, nq, t, nt, blockIdx.x, ts, te, m.idx1 + o, m.dist1 + o, m.idx2 + o, m.dist2 + o, part, lds);
+    knn2_fp4_block(q, nq, t, nt, blockIdx.x, ts, te, m.idx1 + o, m.dist1 + o, m.idx2 + o, m.dist2 + o, part, lds);
     if (!part || !m.cnt || S == 1) return;
     // fused merge: the last of the S split workgroups of this query block merges their partial
     // top-2 lists (k_knn2_merge's work, without its launch).  The hand-off follows
@@ -1756,10 +1604,10 @@ __global__ __launch_bounds__(256) void k_knn2_merge(MatchArgs m, int nsplit) {
     knn2_store(g1, g2, qi, m.idx1 + o, m.dist1 + o, m.idx2 + o, m.dist2 + o);
 }
 
-__global__ __launch_bounds__(kKnnThreads) __attribute__((amdgpu_waves_per_eu(kKnnWavesPerEU))) void k_knn2_mfma_plain(const uint8_t* q, int nq, const uint8_t* t, int nt,
+__global__ __launch_bounds__(kKnnThreads) void k_knn2_mfma_plain(const uint8_t* q, int nq, const uint8_t* t, int nt,
                                                          int32_t* i1, int32_t* d1, int32_t* i2, int32_t* d2) {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * 32 * kKnnPitch];
-    knn2_mfma_block(q, nq, t, nt, blockIdx.x, 0, (nt + 31) >> 5, i1, d1, i2, d2, nullptr, lds);
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kKnnLdsBytes];
+    knn2_fp4_block(q, nq, t, nt, blockIdx.x, 0, (nt + 31) >> 5, i1, d1, i2, d2, nullptr, lds);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1834,9 +1682,9 @@ hipError_t launch_octree(const BatchArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 hipError_t launch_orient_desc(const BatchArgs& a, hipStream_t s) {
-    auto magic = [](uint32_t d) { return d > 1 ? 0xFFFFFFFFu / d + 1u : 0u; };  // ceil(2^32 / d) for d >= 2
-    hipLaunchKernelGGL(k_orient, dim3(a.total_or_blocks, a.nimages), dim3(256), 0, s, a, magic((uint32_t)a.total_or_blocks));
-    hipLaunchKernelGGL(k_desc, dim3(a.total_od_blocks, a.nimages), dim3(256), 0, s, a, magic((uint32_t)a.total_od_blocks));
+    const uint32_t d = (uint32_t)a.total_od_blocks;
+    const uint32_t magic = d > 1 ? 0xFFFFFFFFu / d + 1u : 0u;  // ceil(2^32 / d) for d >= 2
+    hipLaunchKernelGGL(k_orient_desc, dim3(a.total_od_blocks, a.nimages), dim3(256), 0, s, a, magic);
     return hipGetLastError();
 }
 hipError_t launch_finalize(const BatchArgs& a, hipStream_t s) {

@@ -184,7 +184,7 @@ struct orbgpu_ctx {
     long long pyr_img = 0, blur_img = 0, cellkeys_img = 0, octws_img = 0;
     int cellcnt_img = 0, lvlkp_img = 0, out_cap = 0;
     // device buffers
-    DevBuf input, pyr, blur, rtab, cellkeys, cellcnt, octws, lvlkey, lvlangle, lvlsc, lvldesc, lvlcnt,
+    DevBuf input, pyr, blur, rtab, cellkeys, cellcnt, octws, lvlkey, lvlangle, lvldesc, lvlcnt,
         status, outkps, outdesc, outn, outmono, laps, midx1, mdist1, midx2, mdist2, mnq, mpart, scratch,
         octdbg, strow, stidx, stur, stdepth, stsad, gxy, gcell, gstart, gidx, sbs, soa, m16,
         sbpmp, sbpoff, sbpcand, sbpblk, sbpmatch, sbpnm, sbplr, fel2r, fer2l, fedepth, fep3d, fecnt;
@@ -320,7 +320,6 @@ int alloc_all(orbgpu_ctx* c, int n_images) {
     r |= c->octws.ensure(ni * c->octws_img + 256);
     r |= c->lvlkey.ensure(ni * c->lvlkp_img * 4 + 256);
     r |= c->lvlangle.ensure(ni * c->lvlkp_img * 4 + 256);
-    r |= c->lvlsc.ensure(ni * c->lvlkp_img * 8 + 256);
     r |= c->lvldesc.ensure(ni * c->lvlkp_img * 32 + 256);
     r |= c->lvlcnt.ensure(ni * kMaxLevels * 4);
     r |= c->status.ensure(ni * kMaxLevels * 4);
@@ -618,14 +617,6 @@ int set_geometry(orbgpu_ctx* c, int w, int h) {
     A.od_tab_off = (int)c->rtab_host.size();
     for (int l = 0; l < L; ++l)
         for (int b = 0; b < A.lv[l].od_blocks; ++b) c->rtab_host.push_back(make_int4(l, b, 0, 0));
-    // k_orient: kOrientBlockKps keypoints per workgroup, enough blocks for the level's capacity
-    A.or_tab_off = (int)c->rtab_host.size();
-    A.total_or_blocks = 0;
-    for (int l = 0; l < L; ++l) {
-        const int nb = (A.lv[l].kp_cap + kOrientBlockKps - 1) / kOrientBlockKps;
-        for (int b = 0; b < nb; ++b) c->rtab_host.push_back(make_int4(l, b, 0, 0));
-        A.total_or_blocks += nb;
-    }
     for (int l = 0; l < L; ++l) {
         if (l > 0) A.lv[l].img_stride = c->pyr_img;
         A.lv[l].bimg_stride = c->blur_img;
@@ -649,7 +640,6 @@ int set_geometry(orbgpu_ctx* c, int w, int h) {
     A.octws_img_stride = c->octws_img;
     A.lvlkey = c->lvlkey.as<uint32_t>();
     A.lvlangle = c->lvlangle.as<float>();
-    A.lvlsc = c->lvlsc.as<float2>();
     A.lvldesc = c->lvldesc.as<uint8_t>();
     A.lvlkp_img_stride = c->lvlkp_img;
     A.lvlcnt = c->lvlcnt.as<int32_t>();
@@ -928,7 +918,7 @@ int orbgpu_destroy(orbgpu_ctx* c) {
     std::lock_guard<std::recursive_mutex> destroy_lk(alloc_capture_mutex());  // frees and destroys
     for (auto e : c->event_pool) hipEventDestroy(e);
     DevBuf* bufs[] = {&c->input, &c->input2, &c->pyr,     &c->blur,   &c->rtab,    &c->cellkeys, &c->cellcnt,
-                      &c->octws,   &c->lvlkey,  &c->lvlangle, &c->lvlsc, &c->lvldesc, &c->lvlcnt, &c->status,
+                      &c->octws,   &c->lvlkey,  &c->lvlangle, &c->lvldesc, &c->lvlcnt, &c->status,
                       &c->outkps,  &c->outdesc, &c->outn,   &c->outmono, &c->laps,     &c->midx1,
                       &c->mdist1,  &c->midx2,   &c->mdist2, &c->mnq,     &c->mpart,   &c->scratch, &c->octdbg,
                       &c->strow,  &c->stidx, &c->stur,    &c->stdepth,  &c->stsad,

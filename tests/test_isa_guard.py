@@ -19,7 +19,7 @@ LIB = os.path.join(ROOT, "orbslam3lib_amd", "liborbgpu.so")
 OBJDUMP = "/opt/rocm/lib/llvm/bin/llvm-objdump"
 
 # mangled-name fragments of the LDS-resident kernels (every instantiation of each)
-LDS_KERNELS = ("k_pyr_tail", "k_blur_resize", "6k_blurE", "k_fast_cells", "8k_orientE", "6k_descE",
+LDS_KERNELS = ("k_pyr_tail", "k_blur_resize", "6k_blurE", "k_fast_cells", "k_orient_desc",
                "k_knn2_mfma_pairs", "k_knn2_mfma_plain", "k_finalize")
 
 
