@@ -109,6 +109,17 @@ def pmc_valu_table(root):
         txt = open(paths[-1]).read()
     except OSError:
         return {}, None
+    # the counters describe one binary; use them only for the library loaded now
+    import hashlib
+    m = re.search(r"^# liborbgpu.so sha256 ([0-9a-f]{64})", txt, re.M)
+    lib = os.environ.get("ORBGPU_LIB") or os.path.join(root, "orbslam3lib_amd", "liborbgpu.so")
+    try:
+        cur = hashlib.sha256(open(lib, "rb").read()).hexdigest()
+    except OSError:
+        cur = None
+    if not m or m.group(1) != cur:
+        return {}, "%s (stale: recorded for %s, loaded %s)" % (
+            os.path.relpath(paths[-1], root), m.group(1)[:12] if m else "no library hash", (cur or "?")[:12])
     for block in re.split(r"\n(?=\S)", txt):
         lines = block.strip().split("\n")
         name = lines[0].replace("void ", "").replace("orbgpu::", "").strip()
@@ -571,6 +582,8 @@ def main():
         vt, vsrc = pmc_valu_table(ROOT)
     except Exception:
         vt, vsrc = {}, None
+    if dom is not None and not vt and vsrc:
+        roof_valu = {"kernel": dom, "bound": "valu", "stale": True, "source": vsrc}
     if dom is not None and dom in vt:
         v = vt[dom]
         roof_valu = {"kernel": dom, "bound": "valu", "busy": v["valu_busy"],

@@ -11,7 +11,7 @@ import csv, glob, sys
 rows = list(csv.DictReader(open(glob.glob(sys.argv[1] + "/**/run_kernel_trace.csv", recursive=True)[0])))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 # steps start at the first k_blur_resize after a k_knn2
-starts = [i for i, r in enumerate(rows) if "k_blur_resize" in r["Kernel_Name"] and (i == 0 or "knn2" in rows[i - 1]["Kernel_Name"])]
+starts = [i for i, r in enumerate(rows) if ("k_blur_resize" in r["Kernel_Name"] or "k_pyr_chain" in r["Kernel_Name"]) and (i == 0 or "knn2" in rows[i - 1]["Kernel_Name"])]
 for s0, s1 in zip(starts[-4:-1], starts[-3:]):
     t0 = int(rows[s0]["Start_Timestamp"]); t1 = int(rows[s1]["Start_Timestamp"])
     print("step %.1f us" % ((t1 - t0) / 1e3))

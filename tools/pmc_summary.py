@@ -3,6 +3,12 @@ import csv, glob, os, sys
 from collections import defaultdict
 
 root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
+# the binary these counters describe (bench.py uses them only for the same liborbgpu.so)
+import hashlib
+lib = os.environ.get("ORBGPU_LIB") or os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                                   "orbslam3lib_amd", "liborbgpu.so")
+if os.path.exists(lib):
+    print("# liborbgpu.so sha256 %s" % hashlib.sha256(open(lib, "rb").read()).hexdigest())
 acc = defaultdict(lambda: defaultdict(list))
 for f in glob.glob(os.path.join(root, "p*", "**", "*counter_collection.csv"), recursive=True):
     for r in csv.DictReader(open(f)):
