@@ -101,6 +101,8 @@ struct BatchArgs {
     int tail0;
     int tail_lds, tail_buf1, tail_tab, tail_maxq, tail_maxrows;  // its LDS layout (bytes / entries)
     int tail_min;              // launches of fewer images take the per-level path (host only)
+    int fuse_out;              // no image of the batch has a lapping area: k_orient_desc writes the
+                               // assembled outputs and counts, k_finalize does not run
 };
 
 struct MatchArgs {

@@ -1005,6 +1005,13 @@ __device__ inline int od_sum(int v) {
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
+// cv::KeyPoint as written to the outputs (orbgpu_keypoint): pt.x, pt.y, size, angle, response,
+// octave, class_id
+struct KP28 {
+    float x, y, size, angle, response;
+    int32_t octave, class_id;
+};
+
 // k_orient_desc: IC_Angle on the raw level (ORBextractor_old.cc:78-105) then
 // computeOrbDescriptor on the blurred level (:108-148): a = (float)cos, b = (float)sin of
 // angle*pi/180 (float), sample center[cvRound(x*b + y*a)*step + cvRound(x*a - y*b)].
@@ -1034,6 +1041,32 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
     const __amdgpu_buffer_rsrc_t brs =
         __builtin_amdgcn_make_buffer_rsrc((void*)blr, (short)0, G.bpitch * G.h, 0x00020000);
     const int stride_k = G.od_blocks * kOdKpBlock;
+    // a.fuse_out (every image of the batch has no lapping area, so every keypoint is mono): the
+    // assembly of k_finalize (ORBextractor_old.cc:1130-1190) is done here -- keypoint j of level l
+    // goes to output row off[l] + j, with pt *= mvScaleFactor[l], size, octave, class_id -1 --
+    // and k_finalize does not run.  off[l] and the image's total come from the level counts (16
+    // scalar loads); a level the octree could not finish or a total past out_cap writes the status
+    // word instead, as k_finalize does.
+    int out_row0 = 0;
+    bool out_ok = false;
+    if (a.fuse_out) {
+        int total = 0;
+        bool bad = false;
+#pragma unroll
+        for (int k = 0; k < kMaxLevels; ++k)
+            if (k < a.nlevels) {
+                if (k < l) out_row0 += a.lvlcnt[img * kMaxLevels + k];
+                total += a.lvlcnt[img * kMaxLevels + k];
+                bad |= a.status[img * kMaxLevels + k] != 0;
+            }
+        out_ok = !bad && total <= a.out_cap;
+        if (bx == 0 && threadIdx.x == 0) {  // one workgroup per image writes the counts
+            a.out_n[img] = bad ? -5 : total > a.out_cap ? -2 : total;
+            a.out_mono[img] = out_ok ? total : 0;
+        }
+    }
+    KP28* const out_kp = reinterpret_cast<KP28*>(a.out_kps) + (long long)img * a.out_cap + out_row0;
+    uint8_t* const out_d = a.out_desc + ((long long)img * a.out_cap + out_row0) * 32;
     // Moments from coalesced row chunks: the 31 disc rows of a keypoint are read as 16-byte
     // aligned chunks of the 48-byte window that starts at xa16 = (x - 15) & ~15 (it holds
     // x - 15 .. x + 15 for every x).  Chunk slot i = sub + 32 it (it < 3) is disc row r = i / 3
@@ -1190,9 +1223,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
             const int o1 = (int)(__umul24(__float_as_uint(R.y), (uint32_t)kOdPatchPitch) + __float_as_uint(C.y) + kofs);
             bits = bits + bits + (pt[o0] < pt[o1] ? 1u : 0u);
         }
-        if (valid) {
+        if (valid && !out_ok) {  // the level arrays, for k_finalize (or a status image)
             if (sub == 0) a.lvlangle[kbase + kp] = angle;
             a.lvldesc[(kbase + kp) * 32 + sub] = (uint8_t)bits;
+        }
+        if (valid) {
+            if (out_ok) {  // the assembled output row (k_finalize's arithmetic): lanes 0-6 its 7 dwords
+                out_d[kp * 32 + sub] = (uint8_t)bits;
+                if (sub < 7) {
+                    float px = (float)(x), py = (float)(y);
+                    if (l != 0) {
+                        px = px * G.scale;
+                        py = py * G.scale;
+                    }
+                    const uint32_t w7[7] = {__float_as_uint(px), __float_as_uint(py), __float_as_uint((float)G.patch),
+                                            __float_as_uint(angle), __float_as_uint((float)key_resp(key)),
+                                            (uint32_t)l, 0xFFFFFFFFu};
+                    uint32_t v = w7[0];
+#pragma unroll
+                    for (int k = 1; k < 7; ++k) v = sub == k ? w7[k] : v;
+                    reinterpret_cast<uint32_t*>(out_kp + kp)[sub] = v;
+                }
+            }
         }
     }
 }
@@ -1201,10 +1253,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
 // k_finalize: ORBextractor::operator() assembly (ORBextractor_old.cc:1130-1190): levels in
 // order, pt *= mvScaleFactor[level] for level > 0, keypoints inside [lap0, lap1] written from
 // the back, the others from the front; returns monoIndex.
-struct KP28 {
-    float x, y, size, angle, response;
-    int32_t octave, class_id;
-};
 
 // The image's keypoints are walked as one sequence (level l's keypoint j at off[l] + j), in
 // batches of kFinU chunks of kFinThreads whose loads are all issued before the first chunk's partition,

@@ -46,7 +46,8 @@ const char* const kDiagKnobs[] = {"ORBGPU_OD_ITERS",      "ORBGPU_OCT_SMALL_LDS"
                                   "ORBGPU_OCT_SPLIT",     "ORBGPU_OCT_GENERIC",   "ORBGPU_OCT_PYR",
                                   "ORBGPU_FAST_PITCH",    "ORBGPU_STREAMS",       "ORBGPU_ISOLATE",
                                   "ORBGPU_STAGGER",       "ORBGPU_OCT_STAMPS",    "ORBGPU_GRAPH",
-                                  "ORBGPU_KNN_NOSPLIT",   "ORBGPU_NO_TAIL",       "ORBGPU_TAIL_MIN"};
+                                  "ORBGPU_KNN_NOSPLIT",   "ORBGPU_NO_TAIL",       "ORBGPU_TAIL_MIN",
+                                  "ORBGPU_NO_FUSE_OUT"};
 
 bool diagnostics_on() {
     const char* g = getenv("ORBGPU_DIAGNOSTICS");
@@ -220,10 +221,12 @@ struct orbgpu_ctx {
     // alternating input slots (async uploads) or match variants replay instead of recapturing
     bool streams_forced = false;  // ORBGPU_STREAMS (diagnostics): every sub stream is a chunk
     bool use_graph = true;   // ORBGPU_GRAPH=0 launches every kernel directly (A/B)
-    struct GraphRec { int key[6]; hipGraphExec_t exec; unsigned long long used; };
+    struct GraphRec { int key[7]; hipGraphExec_t exec; unsigned long long used; };
     std::vector<GraphRec> graphs;
     unsigned long long graph_tick = 0;
     bool knn_nosplit = false;  // ORBGPU_KNN_NOSPLIT (read once at create): no split kNN2 launches
+    bool no_fuse_out = false;  // ORBGPU_NO_FUSE_OUT: k_finalize assembles even without lapping areas
+    bool last_fused = false;   // the last batch's outputs were assembled by k_orient_desc
     std::vector<int32_t> laps_host;  // lapping areas currently in `laps` (device), per image
     bool need_fork = true;           // the main stream holds work the sub streams must wait for
     bool stagger = true;             // ORBGPU_STAGGER=0: the chunks start every layout in lockstep
@@ -896,6 +899,7 @@ int orbgpu_create(const orbgpu_params* p, int device, int max_width, int max_hei
         c->oct_stamps = diag_env("ORBGPU_OCT_STAMPS") != nullptr;
         if (const char* g = diag_env("ORBGPU_GRAPH")) c->use_graph = atoi(g) != 0;
         c->knn_nosplit = diag_env("ORBGPU_KNN_NOSPLIT") != nullptr;
+        c->no_fuse_out = diag_env("ORBGPU_NO_FUSE_OUT") != nullptr;
     }
     int r = ensure_input(c, 1, max_width, max_height);
     if (!r) r = set_geometry(c, max_width, max_height);
@@ -1066,6 +1070,15 @@ static int run_batch_impl(orbgpu_ctx* c, int n, int w, int h, const int32_t* lap
     A.nimages = n;
     A.img0 = 0;
     A.octdbg = nullptr;
+    // no image with a lapping area a keypoint can fall in (every x is >= minBorderX = 16): every
+    // keypoint is mono and k_orient_desc writes the assembled outputs itself (no k_finalize)
+    A.fuse_out = 1;
+    for (int i = 0; i < n; ++i) {
+        const int l0 = c->laps_host[2 * i], l1 = c->laps_host[2 * i + 1];
+        if (l1 >= kMinBorder && l0 <= l1) A.fuse_out = 0;
+    }
+    if (c->no_fuse_out) A.fuse_out = 0;
+    c->last_fused = A.fuse_out != 0;  // orbgpu_get_level_keypoints reads the outputs then
     if (c->oct_stamps) {  // diagnostic build of the octree phase clocks
         const size_t bytes = (size_t)n * kMaxLevels * 8 * 8;
         if (!c->octdbg.ensure(bytes)) {
@@ -1239,7 +1252,8 @@ static int run_batch_impl(orbgpu_ctx* c, int n, int w, int h, const int32_t* lap
         }
         if ((r = each(ST_OCTREE, [](const BatchArgs& B, hipStream_t st) { return launch_octree(B, st); }))) return r;
         if ((r = each(ST_ORIENT, [](const BatchArgs& B, hipStream_t st) { return launch_orient_desc(B, st); }))) return r;
-        if ((r = each(ST_FINAL, [](const BatchArgs& B, hipStream_t st) { return launch_finalize(B, st); }))) return r;
+        if (!A.fuse_out)
+            if ((r = each(ST_FINAL, [](const BatchArgs& B, hipStream_t st) { return launch_finalize(B, st); }))) return r;
         return 0;
     };
     // One stream, no caller stream, no instrumentation (the single-pair / latency shape, e.g.
@@ -1255,7 +1269,7 @@ static int run_batch_impl(orbgpu_ctx* c, int n, int w, int h, const int32_t* lap
         return 0;
     };
     if (graphable) {
-        const int key[6] = {n, w, h, c->in_slot, with_match ? match_pairs : 0, with_match ? stereo_only : 0};
+        const int key[7] = {n, w, h, c->in_slot, with_match ? match_pairs : 0, with_match ? stereo_only : 0, A.fuse_out};
         orbgpu_ctx::GraphRec* rec = nullptr;
         for (auto& g : c->graphs)
             if (std::memcmp(key, g.key, sizeof key) == 0) rec = &g;
@@ -1478,9 +1492,17 @@ int orbgpu_get_level_keypoints(orbgpu_ctx* c, int img, orbgpu_keypoint* kps, uin
         const size_t base = (size_t)img * c->lvlkp_img + G.kp_off;
         if (m) {
             D2H(keys.data(), c->lvlkey.as<uint32_t>() + base, 4 * m);
-            D2H(ang.data(), c->lvlangle.as<float>() + base, 4 * m);
-            if (desc)
-                D2H(desc + 32 * (size_t)off, c->lvldesc.as<uint8_t>() + base * 32, 32 * (size_t)m);
+            if (c->last_fused) {  // k_orient_desc wrote the assembled rows (all mono, level order) only
+                const size_t row = (size_t)img * c->out_cap + off;
+                std::vector<orbgpu_keypoint> ok(m);
+                D2H(ok.data(), c->outkps.as<orbgpu_keypoint>() + row, sizeof(orbgpu_keypoint) * m);
+                for (int i = 0; i < m; ++i) ang[i] = ok[i].angle;
+                if (desc) D2H(desc + 32 * (size_t)off, c->outdesc.as<uint8_t>() + row * 32, 32 * (size_t)m);
+            } else {
+                D2H(ang.data(), c->lvlangle.as<float>() + base, 4 * m);
+                if (desc)
+                    D2H(desc + 32 * (size_t)off, c->lvldesc.as<uint8_t>() + base * 32, 32 * (size_t)m);
+            }
         }
         for (int i = 0; i < m; ++i) {
             orbgpu_keypoint& k = kps[off + i];

@@ -642,3 +642,47 @@ def test_context_on_current_device():
     with pytest.raises(og.OrbGpuError) as ei:
         og.BatchExtractor(500, 1.2, 4, 20, 7, device=ndev.value, width=160, height=120, max_images=2)
     assert ei.value.code == -6
+
+
+def test_fused_assembly_equals_finalize(oracle, monkeypatch):
+    """Batches with no lapping area (every keypoint mono) are assembled by k_orient_desc itself
+    (BatchArgs.fuse_out: rows off[l] + j, pt *= mvScaleFactor[l], ORBextractor_old.cc:1130-1190)
+    and k_finalize does not run; a lapping area anywhere in the batch, or ORBGPU_NO_FUSE_OUT,
+    takes k_finalize.  The two give the same counts, keypoints and descriptors, the level
+    keypoints (orbgpu_get_level_keypoints, read from the assembled rows when fused) agree, and
+    a later batch with lapping areas on the same context still matches the oracle."""
+    import orbslam3lib_amd as og
+    imgs = np.stack([x for i in range(3) for x in synth.stereo_pair(480, 640, 190 + i)])
+    be = _batch(og, 640, 480, 8, 2000, imgs)
+    be.run()
+    be.synchronize()
+    fused = [be.result(i) for i in range(len(imgs))]
+    laps = np.array([[0, 0], [60, 590]] * 3, np.int32)
+    be.run(laps=laps)  # k_finalize path on the same context
+    be.synchronize()
+    for i in range(len(imgs)):
+        k, d, m = be.result(i)
+        rk, rd, rm = oracle.extract(imgs[i], nfeatures=2000, lap=tuple(laps[i]))
+        assert m == rm
+        np.testing.assert_array_equal(d, rd.reshape(-1, 32))
+    monkeypatch.setenv("ORBGPU_DIAGNOSTICS", "1")
+    monkeypatch.setenv("ORBGPU_NO_FUSE_OUT", "1")
+    be2 = _batch(og, 640, 480, 8, 2000, imgs)
+    be2.run()
+    be2.synchronize()
+    for i in range(len(imgs)):
+        k, d, m = be2.result(i)
+        fk, fd, fm = fused[i]
+        assert m == fm == len(fk)
+        np.testing.assert_array_equal(k.view(np.uint8), fk.view(np.uint8))
+        np.testing.assert_array_equal(d, fd)
+    monkeypatch.delenv("ORBGPU_NO_FUSE_OUT")
+    ex = og.ORBextractor(2000, 1.2, 8, 20, 7, max_width=640, max_height=480, max_images=1)
+    kp, d, m = ex(imgs[0])
+    lk = ex.level_keypoints(0)
+    rk, rd, rm = oracle.extract(imgs[0], nfeatures=2000)
+    np.testing.assert_array_equal(d, rd.reshape(-1, 32))
+    # all mono: the level keypoints in level order are the output rows (level coordinates)
+    np.testing.assert_array_equal(np.concatenate([x[1] for x in lk]), d)
+    np.testing.assert_array_equal(np.concatenate([x[0]["angle"] for x in lk]), kp["angle"])
+    np.testing.assert_array_equal(np.concatenate([x[0]["octave"] for x in lk]), kp["octave"])
