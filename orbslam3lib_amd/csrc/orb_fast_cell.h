@@ -106,11 +106,11 @@ __device__ inline uint2 fw_pretest4(uint32_t C, uint32_t Cm, uint32_t Cp, uint32
     const uint32_t nhi = __builtin_amdgcn_perm(nhO, nhE, 0x06020400u);
     auto nd = [&](uint32_t p) { return __builtin_amdgcn_lerp(p, nlo, 0x01010101u); };  // bit 7: p >= lo
     auto br = [&](uint32_t p) { return __builtin_amdgcn_lerp(p, nhi, 0u); };          // bit 7: p > hi
-    // dark: every pair has a point < lo  <=>  no pair has both points >= lo
-    uint32_t x = nd(R3) & nd(L3);
-    x = (nd(D3) & nd(U3)) | x;
-    x = (nd(DR) & nd(UL)) | x;
-    x = (nd(UR) & nd(DL)) | x;
+    // dark: every pair has a point < lo  <=>  no pair has both points >= lo (the 3-input OR as
+    // v_bitop3_b32, a full-rate op, where the compiler's v_or3_b32 issues at the slow rate:
+    // profiles/r06/valu_rates.json)
+    const uint32_t x = __builtin_amdgcn_bitop3_b32(nd(R3) & nd(L3), nd(D3) & nd(U3), nd(DR) & nd(UL), 0xfe) |
+                       (nd(UR) & nd(DL));
     // bright: every pair has a point > hi
     uint32_t y = br(R3) | br(L3);
     y = (br(D3) | br(U3)) & y;
@@ -304,28 +304,34 @@ __host__ __device__ int fast_cell_detect(Pol& p, int sh, const CellGeom& g, int 
 #if defined(__HIP_DEVICE_COMPILE__)
         {
             constexpr int RW = CP / 4;
-            const uint32_t* T32 = reinterpret_cast<const uint32_t*>(T);
+            const uint8_t* const Tb = T;
+            const uint8_t* const Eb = reinterpret_cast<const uint8_t*>(cs.emask);
+            auto T32 = [&](int byte_off) { return *reinterpret_cast<const uint32_t*>(Tb + byte_off); };
             const uint32_t tt = (uint32_t)t * 0x00010001u, kt = (uint32_t)(255 - t) * 0x00010001u;
-            // this lane's item (row r, dword group q) as (q, LDS dword dw), advanced by L items
-            // per iteration without a division: L = dr rows + dq groups (plus one row on wrap)
-            int q = 0, dw = 0, dq = 0, ddw = 0;
+            // this lane's item (row r, dword group q) as byte offsets (qb = 4 q into the edge-mask
+            // table, db = 4 dw into T: the LDS addresses themselves, no per-item shift), advanced by
+            // L items per iteration without a division: L = dr rows + dq groups (plus one row on wrap)
+            int qb = 0, db = 0, dqb = 0, ddb = 0;
             if (ng > 0) {
                 const int i = j0 + lane;
                 const int r = (int)(((float)i + 0.5f) * inv_ng);  // exact: i < 69 * 19 + 64
-                q = i - __mul24(r, ng);                           // (24-bit products: full rate)
-                dw = __mul24(r + 3, RW) + g0 + q;
+                const int q = i - __mul24(r, ng);                 // (24-bit products: full rate)
+                qb = 4 * q;
+                db = 4 * (__mul24(r + 3, RW) + g0 + q);
                 const int dr = (int)(((float)L + 0.5f) * inv_ng);
-                dq = L - __mul24(dr, ng);
-                ddw = __mul24(dr, RW) + dq;
+                const int dq = L - __mul24(dr, ng);
+                dqb = 4 * dq;
+                ddb = 4 * (__mul24(dr, RW) + dq);
             }
+            const int ngb = 4 * ng, wrapb = 4 * (RW - ng);
             for (int base = j0; base < j1; base += L) {
-                const int i = base + lane;
                 uint32_t m8 = 0;  // 0x80 per passing pixel
-                if (i < j1) {
-                    const uint2 sd = fw_pretest4(T32[dw], T32[dw - 1], T32[dw + 1], T32[dw - 3 * RW], T32[dw + 3 * RW],
-                                                 T32[dw - 2 * RW - 1], T32[dw - 2 * RW], T32[dw - 2 * RW + 1],
-                                                 T32[dw + 2 * RW - 1], T32[dw + 2 * RW], T32[dw + 2 * RW + 1], tt, kt);
-                    m8 = (sd.x | sd.y) & cs.emask[q];  // detection pixels of the row's first / last group
+                if (lane < j1 - base) {
+                    const uint2 sd = fw_pretest4(T32(db), T32(db - 4), T32(db + 4), T32(db - 12 * RW), T32(db + 12 * RW),
+                                                 T32(db - 8 * RW - 4), T32(db - 8 * RW), T32(db - 8 * RW + 4),
+                                                 T32(db + 8 * RW - 4), T32(db + 8 * RW), T32(db + 8 * RW + 4), tt, kt);
+                    // detection pixels of the row's first / last group
+                    m8 = (sd.x | sd.y) & *reinterpret_cast<const uint32_t*>(Eb + qb);
                 }
                 // the 4-bit pass mask (bit k = byte k) by one v_dot4_u32_u8 of the 0x80 bytes:
                 // 128 m4, so m4's 8-byte LUT entry sits at byte offset 128 m4 >> 4 (one shift)
@@ -341,17 +347,17 @@ __host__ __device__ int fast_cell_detect(Pol& p, int sh, const CellGeom& g, int 
                 incl += __builtin_amdgcn_update_dpp(0, incl, 0x118, 0xF, 0xF, true);  // row_shr:8
                 incl += __builtin_amdgcn_update_dpp(0, incl, 0x142, 0xA, 0xF, false); // row_bcast:15 -> rows 1, 3
                 incl += __builtin_amdgcn_update_dpp(0, incl, 0x143, 0xC, 0xF, false); // row_bcast:31 -> rows 2, 3
-                const int pos = na + incl - c;
                 const int wave_total = __builtin_amdgcn_readlane(incl, 63);
                 // the lane's c entries 4 dw + (set bit positions), as u16 pairs from the table,
-                // written to 4 consecutive slots from pos; slots past c hold garbage that a later
-                // lane's entry overwrites (its slot index k is smaller, and the slots are written
-                // in the order k = 3, 2, 1, 0) or that lands in the wave's spare entries; lanes
-                // without candidates write the sink
+                // written to 4 consecutive slots from na + incl - c; slots past c hold garbage that
+                // a later lane's entry overwrites (its slot index k is smaller, and the slots are
+                // written in the order k = 3, 2, 1, 0) or that lands in the wave's spare entries;
+                // lanes without candidates write the sink
                 const uint2 lv = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint8_t*>(cs.lut) + (m4x128 >> 4));
-                const uint32_t e01 = __umul24((uint32_t)(4 * dw), 0x10001u) + lv.x;  // v_mad_u32_u24
-                const uint32_t e23 = __umul24((uint32_t)(4 * dw), 0x10001u) + lv.y;
-                uint16_t* d = c ? list + pos : sink;
+                const uint32_t e01 = __umul24((uint32_t)db, 0x10001u) + lv.x;  // v_mad_u32_u24
+                const uint32_t e23 = __umul24((uint32_t)db, 0x10001u) + lv.y;
+                uint16_t* const lw = list + na;  // wave-uniform
+                uint16_t* d = c ? lw + (incl - c) : sink;
                 d[3] = (uint16_t)(e23 >> 16);
                 asm volatile("" ::: "memory");  // keep the slot order (k = 3 .. 0)
                 d[2] = (uint16_t)e23;
@@ -360,11 +366,11 @@ __host__ __device__ int fast_cell_detect(Pol& p, int sh, const CellGeom& g, int 
                 asm volatile("" ::: "memory");
                 d[0] = (uint16_t)e01;
                 na += wave_total;
-                q += dq;
-                dw += ddw;
-                if (q >= ng) {
-                    q -= ng;
-                    dw += RW - ng;
+                qb += dqb;
+                db += ddb;
+                if (qb >= ngb) {
+                    qb -= ngb;
+                    db += wrapb;
                 }
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the list is read by other lanes

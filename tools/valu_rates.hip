@@ -42,6 +42,38 @@ OP_KERNEL(k_mul_f32, "v_mul_f32 %0, %0, %1")
 OP_KERNEL(k_mad_u32_u24, "v_mad_u32_u24 %0, %0, %1, %0")
 OP_KERNEL(k_add3_u32, "v_add3_u32 %0, %0, %1, %0")
 OP_KERNEL(k_sad_u8, "v_sad_u8 %0, %0, %1, %0")
+OP_KERNEL(k_sub_u32, "v_sub_u32 %0, %0, %1")
+OP_KERNEL(k_and_b32, "v_and_b32 %0, %0, %1")
+OP_KERNEL(k_or_b32, "v_or_b32 %0, %0, %1")
+OP_KERNEL(k_xor_b32, "v_xor_b32 %0, %0, %1")
+OP_KERNEL(k_lshlrev_b32, "v_lshlrev_b32 %0, 1, %0")
+OP_KERNEL(k_lshrrev_b32, "v_lshrrev_b32 %0, 1, %0")
+OP_KERNEL(k_cndmask_b32, "v_cndmask_b32 %0, %0, %1, vcc")
+OP_KERNEL(k_cmp_gt_u32, "v_cmp_gt_u32 vcc, %0, %1")
+OP_KERNEL(k_max_i32, "v_max_i32 %0, %0, %1")
+OP_KERNEL(k_min_u32, "v_min_u32 %0, %0, %1")
+OP_KERNEL(k_max_f32, "v_max_f32 %0, %0, %1")
+OP_KERNEL(k_add_f32, "v_add_f32 %0, %0, %1")
+OP_KERNEL(k_fma_f32, "v_fma_f32 %0, %0, %1, %0")
+OP_KERNEL(k_max3_f32, "v_max3_f32 %0, %0, %1, %0")
+OP_KERNEL(k_med3_u32, "v_med3_u32 %0, %0, %1, %0")
+OP_KERNEL(k_and_or_b32, "v_and_or_b32 %0, %0, %1, %0")
+OP_KERNEL(k_or3_b32, "v_or3_b32 %0, %0, %1, %0")
+OP_KERNEL(k_lshl_add_u32, "v_lshl_add_u32 %0, %0, 1, %1")
+OP_KERNEL(k_lshl_or_b32, "v_lshl_or_b32 %0, %0, 1, %1")
+OP_KERNEL(k_mul_u32_u24, "v_mul_u32_u24 %0, %0, %1")
+OP_KERNEL(k_mul_lo_u32, "v_mul_lo_u32 %0, %0, %1")
+OP_KERNEL(k_bfe_u32, "v_bfe_u32 %0, %0, %1, 8")
+OP_KERNEL(k_bcnt_u32, "v_bcnt_u32_b32 %0, %0, %1")
+OP_KERNEL(k_cvt_f32_u32, "v_cvt_f32_u32 %0, %0")
+OP_KERNEL(k_mov_b32, "v_mov_b32 %0, %1")
+OP_KERNEL(k_add_dpp, "v_add_u32_dpp %0, %0, %0 row_shr:1 row_mask:0xf bank_mask:0xf")
+OP_KERNEL(k_pk_add_u16, "v_pk_add_u16 %0, %0, %1")
+OP_KERNEL(k_pk_max_f16, "v_pk_max_f16 %0, %0, %1")
+OP_KERNEL(k_max_u16, "v_max_u16 %0, %0, %1")
+OP_KERNEL(k_mul_hi_u32_u24, "v_mul_hi_u32_u24 %0, %0, %1")
+OP_KERNEL(k_cvt_pk_u8_f32, "v_cvt_pk_u8_f32 %0, %1, 1, %0")
+OP_KERNEL(k_readfirstlane, "v_mbcnt_lo_u32_b32 %0, %0, %1")
 
 // 64-bit operands (register pairs): packed f32 and f64
 #define OP_KERNEL64(NAME, ASM)                                                            \
@@ -66,6 +98,7 @@ OP_KERNEL(k_sad_u8, "v_sad_u8 %0, %0, %1, %0")
 OP_KERNEL64(k_pk_mul_f32, "v_pk_mul_f32 %0, %0, %1")
 OP_KERNEL64(k_pk_add_f32, "v_pk_add_f32 %0, %0, %1")
 OP_KERNEL64(k_mul_f64, "v_mul_f64 %0, %0, %1")
+OP_KERNEL64(k_pk_fma_f32, "v_pk_fma_f32 %0, %0, %1, %0")
 
 typedef void (*kfn)(uint32_t*, int, uint32_t);
 
@@ -78,7 +111,7 @@ int main() {
         {"v_dot4_u32_u8", k_dot4_u32_u8}, {"v_pk_mad_u16", k_pk_mad_u16}, {"v_mov_b32_dpp wave_shr", k_mov_dpp},
         {"v_mul_f32", k_mul_f32}, {"v_mad_u32_u24", k_mad_u32_u24}, {"v_add3_u32", k_add3_u32},
         {"v_sad_u8", k_sad_u8}, {"v_pk_mul_f32", k_pk_mul_f32}, {"v_pk_add_f32", k_pk_add_f32},
-        {"v_mul_f64", k_mul_f64}};
+        {"v_mul_f64", k_mul_f64}, {"v_pk_fma_f32", k_pk_fma_f32}, {"v_sub_u32", k_sub_u32}, {"v_and_b32", k_and_b32}, {"v_or_b32", k_or_b32}, {"v_xor_b32", k_xor_b32}, {"v_lshlrev_b32", k_lshlrev_b32}, {"v_lshrrev_b32", k_lshrrev_b32}, {"v_cndmask_b32", k_cndmask_b32}, {"v_cmp_gt_u32", k_cmp_gt_u32}, {"v_max_i32", k_max_i32}, {"v_min_u32", k_min_u32}, {"v_max_f32", k_max_f32}, {"v_add_f32", k_add_f32}, {"v_fma_f32", k_fma_f32}, {"v_max3_f32", k_max3_f32}, {"v_med3_u32", k_med3_u32}, {"v_and_or_b32", k_and_or_b32}, {"v_or3_b32", k_or3_b32}, {"v_lshl_add_u32", k_lshl_add_u32}, {"v_lshl_or_b32", k_lshl_or_b32}, {"v_mul_u32_u24", k_mul_u32_u24}, {"v_mul_lo_u32", k_mul_lo_u32}, {"v_bfe_u32", k_bfe_u32}, {"v_bcnt_u32_b32", k_bcnt_u32}, {"v_cvt_f32_u32", k_cvt_f32_u32}, {"v_mov_b32", k_mov_b32}, {"v_add_u32_dpp row_shr", k_add_dpp}, {"v_pk_add_u16", k_pk_add_u16}, {"v_pk_max_f16", k_pk_max_f16}, {"v_max_u16", k_max_u16}, {"v_mul_hi_u32_u24", k_mul_hi_u32_u24}, {"v_cvt_pk_u8_f32", k_cvt_pk_u8_f32}, {"v_mbcnt_lo_u32_b32", k_readfirstlane}};
     hipDeviceProp_t prop;
     hipGetDeviceProperties(&prop, 0);
     const int cus = prop.multiProcessorCount;
