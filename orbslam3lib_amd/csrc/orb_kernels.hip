@@ -1209,19 +1209,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
         const float magic = 12582912.0f;
         const uint32_t kofs = (uint32_t)pc - 0x4B400000u - 0x400000u * (uint32_t)kOdPatchPitch;
         const f32x2 snv = {sn, sn}, cav = {ca, ca}, mg = {magic, magic};
+        // the LDS address of a sample is v_mad_u32_u24(R, pitch, C) + kpb, the patch base folded
+        // into the per-keypoint constant: one full-rate v_add_u32 per sample where the compiler's
+        // own association gave a v_add3_u32 (slow class, profiles/r06/valu_rates.json)
+        typedef const __attribute__((address_space(3))) uint8_t lds_u8;
+        const uint32_t kpb = kofs + (uint32_t)(uintptr_t)(lds_u8*)pt;
         uint32_t bits = 0;
 #pragma unroll
-        for (int b = kOdPairs - 1; b >= 0; --b) {  // bits = 2 bits + test, last pair first
+        for (int b = kOdPairs - 1; b >= 0; --b) {  // bit b of the byte is pair b's test
             uint4 pw = s_pat[b][sub];  // float bit patterns {x0, x1, y0, y1}
             asm volatile("" : "+v"(pw.x), "+v"(pw.y), "+v"(pw.z), "+v"(pw.w));  // not hoisted
             const f32x2 X = {__uint_as_float(pw.x), __uint_as_float(pw.y)};
             const f32x2 Y = {__uint_as_float(pw.z), __uint_as_float(pw.w)};
             const f32x2 R = (X * snv + Y * cav) + mg;
             const f32x2 C = (X * cav - Y * snv) + mg;
-            // the unsigned sums wrap to the small patch offsets; index with them as int
-            const int o0 = (int)(__umul24(__float_as_uint(R.x), (uint32_t)kOdPatchPitch) + __float_as_uint(C.x) + kofs);
-            const int o1 = (int)(__umul24(__float_as_uint(R.y), (uint32_t)kOdPatchPitch) + __float_as_uint(C.y) + kofs);
-            bits = bits + bits + (pt[o0] < pt[o1] ? 1u : 0u);
+            // the unsigned sums wrap to the small patch offsets
+            uint32_t m0 = __umul24(__float_as_uint(R.x), (uint32_t)kOdPatchPitch) + __float_as_uint(C.x);
+            uint32_t m1 = __umul24(__float_as_uint(R.y), (uint32_t)kOdPatchPitch) + __float_as_uint(C.y);
+            asm volatile("" : "+v"(m0), "+v"(m1));  // keep the mad's addend C (not re-associated)
+            const uint32_t p0 = *(lds_u8*)(uintptr_t)(m0 + kpb), p1 = *(lds_u8*)(uintptr_t)(m1 + kpb);
+            // p0 < p1 <=> the sign of p0 - p1: shifted to bit b and merged by one v_bitop3
+            // (A | (B & C)) -- full-rate ops instead of v_cmp + v_cndmask + a shift-or
+            bits = __builtin_amdgcn_bitop3_b32(bits, (p0 - p1) >> (31 - b), 1u << b, 0xf8);
         }
         if (valid && !out_ok) {  // the level arrays, for k_finalize (or a status image)
             if (sub == 0) a.lvlangle[kbase + kp] = angle;
