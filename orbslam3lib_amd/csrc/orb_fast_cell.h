@@ -249,9 +249,15 @@ __host__ __device__ void fast_cell_stage(Pol& p, const uint8_t* src, long long p
 // The detection pixels are split into one contiguous row-major range per wave, so the wave
 // lists concatenated in wave order are row-major: ordered output needs only a prefix over waves.
 // Runs on a staged ROI (fast_cell_stage + sync); returns the cell's kept count.
-template <int CP, class Pol>
+// kCap: the candidate list's capacity.  Below cell_list_cap<CP>() (one wave per cell only: the
+// small-list k_fast_cells<48>, whose 1 KB list lets 27 instead of 19 workgroups share a CU) a
+// pre-test pass whose candidates would not fit returns kFastOverflow before writing past the
+// list, and the cell is redone by the full-list kernel.
+constexpr int kFastOverflow = -1;
+template <int CP, int kCap = cell_list_cap<CP>(), class Pol>
 __host__ __device__ int fast_cell_detect(Pol& p, int sh, const CellGeom& g, int ini_th, int min_th,
                                          const CellScratch& cs, uint32_t* keys_out) {
+    static_assert(kCap <= cell_list_cap<CP>(), "list capacity");
     const int rows = g.rows, cols = g.cols;
     uint8_t* T = cs.T;
     uint8_t* M = cs.M;
@@ -287,7 +293,7 @@ __host__ __device__ int fast_cell_detect(Pol& p, int sh, const CellGeom& g, int 
 #endif
 #if defined(__HIP_DEVICE_COMPILE__)
     uint16_t* list = cs.list + i0 + 4 * w;  // 4 spare entries after each wave's list
-    uint16_t* sink = cs.list + cell_list_cap<CP>() + 4 * W;  // 4 entries (fast_list_slack)
+    uint16_t* sink = cs.list + kCap + 4 * W;  // 4 entries (fast_list_slack)
 #else
     uint16_t* list = cs.list + i0;
 #endif
@@ -348,6 +354,10 @@ __host__ __device__ int fast_cell_detect(Pol& p, int sh, const CellGeom& g, int 
                 incl += __builtin_amdgcn_update_dpp(0, incl, 0x142, 0xA, 0xF, false); // row_bcast:15 -> rows 1, 3
                 incl += __builtin_amdgcn_update_dpp(0, incl, 0x143, 0xC, 0xF, false); // row_bcast:31 -> rows 2, 3
                 const int wave_total = __builtin_amdgcn_readlane(incl, 63);
+                if (kCap < cell_list_cap<CP>() && na + wave_total > kCap) {  // wave-uniform
+                    na = kFastOverflow;
+                    break;
+                }
                 // the lane's c entries 4 dw + (set bit positions), as u16 pairs from the table,
                 // written to 4 consecutive slots from na + incl - c; slots past c hold garbage that
                 // a later lane's entry overwrites (its slot index k is smaller, and the slots are
@@ -376,6 +386,7 @@ __host__ __device__ int fast_cell_detect(Pol& p, int sh, const CellGeom& g, int 
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the list is read by other lanes
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (kCap < cell_list_cap<CP>() && na == kFastOverflow) return kFastOverflow;
         }
 #else
         for (int base = i0; base < i1; base += L) {
@@ -438,6 +449,7 @@ __host__ __device__ int fast_cell_detect(Pol& p, int sh, const CellGeom& g, int 
         return make_int2(tot, before);
     };
     int nb = build(tini);
+    if (kCap < cell_list_cap<CP>() && nb == kFastOverflow) return kFastOverflow;
     p.sync();  // M complete: nonmax reads neighbours owned by other waves
     int2 cb = count_kept(nb, tini);
     int t = tini;
@@ -446,6 +458,7 @@ __host__ __device__ int fast_cell_detect(Pol& p, int sh, const CellGeom& g, int 
         p.sync();
         if (tmin < tini) {
             nb = build(tmin);
+            if (kCap < cell_list_cap<CP>() && nb == kFastOverflow) return kFastOverflow;
             p.sync();
         }
         cb = count_kept(nb, t);
@@ -468,13 +481,13 @@ __host__ __device__ int fast_cell_detect(Pol& p, int sh, const CellGeom& g, int 
     return cb.x;
 }
 
-template <int CP, class Pol, class Ld16>
+template <int CP, int kCap = cell_list_cap<CP>(), class Pol, class Ld16>
 __host__ __device__ int fast_cell_run(Pol& p, const uint8_t* src, long long pitch, int sh,
                                       bool dword_ok, const CellGeom& g, int ini_th, int min_th,
                                       const CellScratch& cs, uint32_t* keys_out, Ld16 ld16) {
     fast_cell_stage<CP>(p, src, pitch, sh, dword_ok, g, cs, ld16);
     p.sync();
-    return fast_cell_detect<CP>(p, sh, g, ini_th, min_th, cs, keys_out);
+    return fast_cell_detect<CP, kCap>(p, sh, g, ini_th, min_th, cs, keys_out);
 }
 
 }  // namespace orbgpu

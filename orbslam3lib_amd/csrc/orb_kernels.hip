@@ -772,21 +772,13 @@ hipError_t launch_pyr_tail(const BatchArgs& a, hipStream_t s) {
 // detection on [3,rows-3)x[3,cols-3) of the cell ROI, 3x3 nonmax inside the cell only, iniTh
 // then minTh if the cell yields nothing, keys emitted in row-major order.
 
-template <int CP>
-__global__ __launch_bounds__(fast_threads<CP>()) void k_fast_cells(BatchArgs a, int cell0, uint32_t ncell_magic) {
-    constexpr int kList = cell_list_cap<CP>(), kFastThreads = fast_threads<CP>();
-    __shared__ __attribute__((aligned(16))) uint8_t T[CP * CP];
-    __shared__ __attribute__((aligned(16))) uint8_t M[CP * CP];  // 16-byte rows when CP % 16 == 0
-    __shared__ __attribute__((aligned(8))) uint16_t list[kList + fast_list_slack(kFastThreads / 64)];
-    __shared__ uint2 lut[16];
-    __shared__ uint32_t emask[32];
-    __shared__ int32_t wcnt[kFastThreads / 64];
-    __shared__ int scratch[16];
-    const int wg = xcd_remap(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * gridDim.y);
-    // wg / gridDim.x by the host's magic multiplier (exact for wg < 2^32 / gridDim.x)
-    const int irel = gridDim.x == 1 ? wg : (int)__umulhi((uint32_t)wg, ncell_magic);
-    const int img = a.img0 + irel;
-    const int gcell = cell0 + (wg - irel * (int)gridDim.x);  // flattened over the levels
+// One cell of image img (flattened cell index gcell) with a candidate list of kCap entries;
+// returns the kept count (written to the cell's count) or kFastOverflow (nothing written).
+template <int CP, int kCap>
+__device__ __attribute__((always_inline)) inline int fast_cell_one(const BatchArgs& a, int img, int gcell, uint8_t* T,
+                                                                   uint8_t* M, uint16_t* list, uint2* lut,
+                                                                   uint32_t* emask, int32_t* wcnt, int* scratch) {
+    constexpr int kFastThreads = fast_threads<CP>();
     // the cell's record (host: the cell loop's geometry, :807-821)
     const int4 e0 = a.rtab[a.fast_tab_off + 2 * gcell];
     const int4 e1 = a.rtab[a.fast_tab_off + 2 * gcell + 1];
@@ -800,7 +792,7 @@ __global__ __launch_bounds__(fast_threads<CP>()) void k_fast_cells(BatchArgs a, 
     g.minBorder = kMinBorder;
     if (e1.z) {  // :812, :821
         if (threadIdx.x == 0) *cnt_out = 0;
-        return;
+        return 0;
     }
     g.rows = e0.w & 0xFFFF;
     g.cols = e0.w >> 16;
@@ -819,8 +811,70 @@ __global__ __launch_bounds__(fast_threads<CP>()) void k_fast_cells(BatchArgs a, 
     FixedDevPolicy<kFastThreads> p{{scratch}};
     fast_cell_tables<CP>(g, sh, lut, emask);  // synced with the ROI staging (fast_cell_run)
     CellScratch cs{T, M, list, wcnt, lut, emask};
-    const int n = fast_cell_run<CP>(p, src, G.pitch, sh, dword_ok, g, a.ini_th, a.min_th, cs, key_out, ld16);
-    if (threadIdx.x == 0) *cnt_out = n;
+    const int n = fast_cell_run<CP, kCap>(p, src, G.pitch, sh, dword_ok, g, a.ini_th, a.min_th, cs, key_out, ld16);
+    if (n != kFastOverflow && threadIdx.x == 0) *cnt_out = n;
+    return n;
+}
+
+// k_fast_cells<CP, kSmall>: one workgroup per (image, cell) of the tile's cells.  kSmall (the
+// 48-byte tile of launches of more than kFastMergeMaxImages images): a kFastSmallList-entry
+// candidate list (LDS 5.9 instead of 8.4 KB per workgroup: 27 instead of 19 resident per CU;
+// round 6: one workgroup per CU more or less moved this kernel by ~20%).  A cell whose pre-test
+// passes more pixels than that (none of the bench frames' cells at iniThFAST, where the most is
+// 441 of 1225) is queued (a.fast_ovf, per-launch slice by img0) and redone by k_fast_cells_ovf.
+template <int CP, bool kSmall>
+__global__ __launch_bounds__(fast_threads<CP>()) void k_fast_cells(BatchArgs a, int cell0, uint32_t ncell_magic) {
+    constexpr int kList = kSmall ? kFastSmallList : cell_list_cap<CP>(), kFastThreads = fast_threads<CP>();
+    static_assert(!kSmall || kFastThreads == 64, "the small list is one wave's");
+    __shared__ __attribute__((aligned(16))) uint8_t T[CP * CP];
+    __shared__ __attribute__((aligned(16))) uint8_t M[CP * CP];  // 16-byte rows when CP % 16 == 0
+    __shared__ __attribute__((aligned(8))) uint16_t list[kList + fast_list_slack(kFastThreads / 64)];
+    __shared__ uint2 lut[16];
+    __shared__ uint32_t emask[32];
+    __shared__ int32_t wcnt[kFastThreads / 64];
+    __shared__ int scratch[16];
+    const int wg = xcd_remap(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * gridDim.y);
+    // wg / gridDim.x by the host's magic multiplier (exact for wg < 2^32 / gridDim.x)
+    const int irel = gridDim.x == 1 ? wg : (int)__umulhi((uint32_t)wg, ncell_magic);
+    const int img = a.img0 + irel;
+    const int gcell = cell0 + (wg - irel * (int)gridDim.x);  // flattened over the levels
+    const int n = (kSmall && a.fast_ovf_all) ? kFastOverflow  // diagnostics: every cell to the full-list pass
+                                             : fast_cell_one<CP, kList>(a, img, gcell, T, M, list, lut, emask, wcnt, scratch);
+    if (kSmall && n == kFastOverflow && threadIdx.x == 0) {
+        const int q = __hip_atomic_fetch_add(a.fast_ovf_cnt + 2 * a.img0, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        a.fast_ovf[(long long)a.img0 * a.fast_n48 + q] = make_int2(img, gcell);
+    }
+}
+
+// The cells k_fast_cells<CP, true> queued, with the full candidate list: a small grid walks the
+// launch's queue (the count is read after the queueing launch finished: same stream); the last
+// workgroup to finish resets the count and its own arrival counter for the next launch.
+template <int CP>
+__global__ __launch_bounds__(fast_threads<CP>()) void k_fast_cells_ovf(BatchArgs a) {
+    constexpr int kList = cell_list_cap<CP>(), kFastThreads = fast_threads<CP>();
+    __shared__ __attribute__((aligned(16))) uint8_t T[CP * CP];
+    __shared__ __attribute__((aligned(16))) uint8_t M[CP * CP];
+    __shared__ __attribute__((aligned(8))) uint16_t list[kList + fast_list_slack(kFastThreads / 64)];
+    __shared__ uint2 lut[16];
+    __shared__ uint32_t emask[32];
+    __shared__ int32_t wcnt[kFastThreads / 64];
+    __shared__ int scratch[16];
+    int* const cnt = a.fast_ovf_cnt + 2 * a.img0;  // [0] queued cells, [1] finished workgroups
+    const int nq = __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int q = blockIdx.x; q < nq; q += gridDim.x) {
+        const int2 e = a.fast_ovf[(long long)a.img0 * a.fast_n48 + q];
+        fast_cell_one<CP, kList>(a, e.x, e.y, T, M, list, lut, emask, wcnt, scratch);
+        __syncthreads();  // the LDS scratch is reused by the next cell
+    }
+    if (threadIdx.x == 0) {
+        // every workgroup has read the count once it arrives here (the loop above depends on the
+        // value), so the last one may clear both; the counters order nothing else (relaxed)
+        const int done = __hip_atomic_fetch_add(cnt + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (done == (int)gridDim.x - 1) {
+            __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(cnt + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1685,7 +1739,7 @@ hipError_t launch_fast_cells(const BatchArgs& a, int tile, hipStream_t s) {
     fast_cell_range(a, tile, &c0, &c1);
     // a launch of a few images (the latency shape) leaves the GPU mostly idle: the 48- and 64-byte
     // cells go in ONE 64-byte launch instead of two back to back (every 48 cell fits 64)
-    const bool merge = a.nimages <= kFastMergeMaxImages && a.fast_n48 > 0 && a.fast_n64 > a.fast_n48;
+    const bool merge = a.nimages <= kFastMergeMaxImages && a.fast_small <= 0 && a.fast_n48 > 0 && a.fast_n64 > a.fast_n48;
     if (merge && tile == kCellPitchSmall) return hipSuccess;  // done by the 48 launch
     if (merge && tile == kCellPitchTiny) {
         tile = kCellPitchSmall;
@@ -1697,9 +1751,15 @@ hipError_t launch_fast_cells(const BatchArgs& a, int tile, hipStream_t s) {
                                                                                                       : fast_threads<kCellMax>());
     const uint32_t d = (uint32_t)(c1 - c0);
     const uint32_t magic = d > 1 ? 0xFFFFFFFFu / d + 1u : 0u;  // ceil(2^32 / d) for d >= 2
-    if (tile == kCellPitchTiny) hipLaunchKernelGGL(k_fast_cells<kCellPitchTiny>, grid, block, 0, s, a, c0, magic);
-    else if (tile == kCellPitchSmall) hipLaunchKernelGGL(k_fast_cells<kCellPitchSmall>, grid, block, 0, s, a, c0, magic);
-    else hipLaunchKernelGGL(k_fast_cells<kCellMax>, grid, block, 0, s, a, c0, magic);
+    // the small-list 48-byte kernel and its overflow pass for the batch shape (a.fast_small)
+    const bool small = tile == kCellPitchTiny && a.fast_ovf &&
+                       (a.fast_small > 0 || (a.fast_small < 0 && a.nimages > kFastMergeMaxImages));
+    if (small) {
+        hipLaunchKernelGGL((k_fast_cells<kCellPitchTiny, true>), grid, block, 0, s, a, c0, magic);
+        hipLaunchKernelGGL(k_fast_cells_ovf<kCellPitchTiny>, dim3(kFastOvfBlocks), block, 0, s, a);
+    } else if (tile == kCellPitchTiny) hipLaunchKernelGGL((k_fast_cells<kCellPitchTiny, false>), grid, block, 0, s, a, c0, magic);
+    else if (tile == kCellPitchSmall) hipLaunchKernelGGL((k_fast_cells<kCellPitchSmall, false>), grid, block, 0, s, a, c0, magic);
+    else hipLaunchKernelGGL((k_fast_cells<kCellMax, false>), grid, block, 0, s, a, c0, magic);
     return hipGetLastError();
 }
 hipError_t launch_octree(const BatchArgs& a, hipStream_t s) {

@@ -47,7 +47,7 @@ const char* const kDiagKnobs[] = {"ORBGPU_OD_ITERS",      "ORBGPU_OCT_SMALL_LDS"
                                   "ORBGPU_FAST_PITCH",    "ORBGPU_STREAMS",       "ORBGPU_ISOLATE",
                                   "ORBGPU_STAGGER",       "ORBGPU_OCT_STAMPS",    "ORBGPU_GRAPH",
                                   "ORBGPU_KNN_NOSPLIT",   "ORBGPU_NO_TAIL",       "ORBGPU_TAIL_MIN",
-                                  "ORBGPU_NO_FUSE_OUT"};
+                                  "ORBGPU_NO_FUSE_OUT",   "ORBGPU_FAST_SMALL",    "ORBGPU_FAST_OVF_ALL"};
 
 bool diagnostics_on() {
     const char* g = getenv("ORBGPU_DIAGNOSTICS");
@@ -187,7 +187,7 @@ struct orbgpu_ctx {
     // device buffers
     DevBuf input, pyr, blur, rtab, cellkeys, cellcnt, octws, lvlkey, lvlangle, lvldesc, lvlcnt,
         status, outkps, outdesc, outn, outmono, laps, midx1, mdist1, midx2, mdist2, mnq, mpart, scratch,
-        octdbg, strow, stidx, stur, stdepth, stsad, gxy, gcell, gstart, gidx, sbs, soa, m16,
+        octdbg, fastovf, strow, stidx, stur, stdepth, stsad, gxy, gcell, gstart, gidx, sbs, soa, m16,
         sbpmp, sbpoff, sbpcand, sbpblk, sbpmatch, sbpnm, sbplr, fel2r, fer2l, fedepth, fep3d, fecnt;
     float grid_bounds[4] = {0, 0, 0, 0}, grid_inv[2] = {0, 0};  // of the last undistort_grid
     int sbp_frames = 0, sbp_step = 1, sbp_two_cam = 0;
@@ -226,6 +226,8 @@ struct orbgpu_ctx {
     unsigned long long graph_tick = 0;
     bool knn_nosplit = false;  // ORBGPU_KNN_NOSPLIT (read once at create): no split kNN2 launches
     bool no_fuse_out = false;  // ORBGPU_NO_FUSE_OUT: k_finalize assembles even without lapping areas
+    int fast_small = -1;       // ORBGPU_FAST_SMALL: the small-list FAST kernel never (0) / always (1)
+    bool fast_ovf_all = false;  // ORBGPU_FAST_OVF_ALL: every small-list cell through the overflow pass
     bool last_fused = false;   // the last batch's outputs were assembled by k_orient_desc
     std::vector<int32_t> laps_host;  // lapping areas currently in `laps` (device), per image
     bool need_fork = true;           // the main stream holds work the sub streams must wait for
@@ -337,6 +339,13 @@ int alloc_all(orbgpu_ctx* c, int n_images) {
     r |= c->midx2.ensure(np * c->out_cap * 4 + 256);
     r |= c->mdist2.ensure(np * c->out_cap * 4 + 256);
     r |= c->mnq.ensure(np * 4 + 64);
+    {  // FAST overflow queue [img][fast_n48] (image, cell) and two counters per image slot (zeroed
+       // once: k_fast_cells_ovf's last workgroup resets its launch's pair)
+        void* before = c->fastovf.p;
+        const size_t ent = ni * (size_t)std::max(c->A.fast_n48, 1) * 8;
+        r |= c->fastovf.ensure(ent + ni * 8 + 256);
+        if (!r && c->fastovf.p != before && hipMemset(c->fastovf.p, 0, c->fastovf.bytes) != hipSuccess) r = -1;
+    }
     {  // split kNN2 partials, then the arrival counters of the fused merge (zeroed once: the last
        // workgroup of each query block resets its counter)
         void* before = c->mpart.p;
@@ -653,6 +662,11 @@ int set_geometry(orbgpu_ctx* c, int w, int h) {
     A.out_n = c->outn.as<int32_t>();
     A.out_mono = c->outmono.as<int32_t>();
     A.laps = c->laps.as<int32_t>();
+    A.fast_ovf = c->fastovf.as<int2>();
+    A.fast_ovf_cnt = reinterpret_cast<int*>(c->fastovf.as<uint8_t>() + (size_t)std::max(c->max_images, 1) *
+                                                                           std::max(A.fast_n48, 1) * 8);
+    A.fast_small = c->fast_small;
+    A.fast_ovf_all = c->fast_ovf_all ? 1 : 0;
     c->gw = w;
     c->gh = h;
     return 0;
@@ -900,6 +914,8 @@ int orbgpu_create(const orbgpu_params* p, int device, int max_width, int max_hei
         if (const char* g = diag_env("ORBGPU_GRAPH")) c->use_graph = atoi(g) != 0;
         c->knn_nosplit = diag_env("ORBGPU_KNN_NOSPLIT") != nullptr;
         c->no_fuse_out = diag_env("ORBGPU_NO_FUSE_OUT") != nullptr;
+        if (const char* f = diag_env("ORBGPU_FAST_SMALL")) c->fast_small = atoi(f) != 0 ? 1 : 0;
+        c->fast_ovf_all = diag_env("ORBGPU_FAST_OVF_ALL") != nullptr;
     }
     int r = ensure_input(c, 1, max_width, max_height);
     if (!r) r = set_geometry(c, max_width, max_height);
@@ -924,7 +940,7 @@ int orbgpu_destroy(orbgpu_ctx* c) {
     DevBuf* bufs[] = {&c->input, &c->input2, &c->pyr,     &c->blur,   &c->rtab,    &c->cellkeys, &c->cellcnt,
                       &c->octws,   &c->lvlkey,  &c->lvlangle, &c->lvldesc, &c->lvlcnt, &c->status,
                       &c->outkps,  &c->outdesc, &c->outn,   &c->outmono, &c->laps,     &c->midx1,
-                      &c->mdist1,  &c->midx2,   &c->mdist2, &c->mnq,     &c->mpart,   &c->scratch, &c->octdbg,
+                      &c->mdist1,  &c->midx2,   &c->mdist2, &c->mnq,     &c->mpart,   &c->scratch, &c->octdbg, &c->fastovf,
                       &c->strow,  &c->stidx, &c->stur,    &c->stdepth,  &c->stsad,
                       &c->gxy,     &c->gcell,  &c->gstart, &c->gidx,    &c->sbs,      &c->soa,
                       &c->m16,     &c->sbpmp,  &c->sbpoff, &c->sbpcand, &c->sbpblk,  &c->sbpmatch,

@@ -686,3 +686,44 @@ def test_fused_assembly_equals_finalize(oracle, monkeypatch):
     np.testing.assert_array_equal(np.concatenate([x[1] for x in lk]), d)
     np.testing.assert_array_equal(np.concatenate([x[0]["angle"] for x in lk]), kp["angle"])
     np.testing.assert_array_equal(np.concatenate([x[0]["octave"] for x in lk]), kp["octave"])
+
+
+def test_fast_small_list_and_overflow_pass(oracle, monkeypatch):
+    """k_fast_cells<48>'s small-list form (512 candidates, the batch shape's FAST) and the
+    full-list pass over the cells it queues (k_fast_cells_ovf).  Forced on for a small batch
+    (ORBGPU_FAST_SMALL=1), including frames of uniform noise whose cells pass far more than 512
+    pixels of the pre-test, and with every cell sent through the overflow pass
+    (ORBGPU_FAST_OVF_ALL=1): the same keypoints and descriptors as the full-list kernel, on
+    repeated batches of one context (the queue counters reset themselves), and the oracle's."""
+    import orbslam3lib_amd as og
+    rng = np.random.default_rng(77)
+    noise = [rng.integers(0, 256, (480, 640), dtype=np.uint8) for _ in range(2)]
+    imgs = np.stack([x for i in range(2) for x in synth.stereo_pair(480, 640, 400 + i)] + noise)
+
+    def run_all(be):
+        out = []
+        for _ in range(2):  # twice on one context
+            be.run()
+            be.synchronize()
+            out.append([be.result(i) for i in range(len(imgs))])
+        return out
+
+    ref = run_all(_batch(og, 640, 480, 8, 2000, imgs))
+    for i in (0, len(imgs) - 1):
+        k, d, m = ref[0][i]
+        rk, rd, rm = oracle.extract(imgs[i], nfeatures=2000)
+        assert m == rm
+        np.testing.assert_array_equal(d, rd.reshape(-1, 32))
+    monkeypatch.setenv("ORBGPU_DIAGNOSTICS", "1")
+    monkeypatch.setenv("ORBGPU_FAST_SMALL", "1")
+    for ovf_all in (False, True):
+        if ovf_all:
+            monkeypatch.setenv("ORBGPU_FAST_OVF_ALL", "1")
+        got = run_all(_batch(og, 640, 480, 8, 2000, imgs))
+        for rep in range(2):
+            for i in range(len(imgs)):
+                k, d, m = got[rep][i]
+                fk, fd, fm = ref[0][i]
+                assert m == fm, (ovf_all, rep, i)
+                np.testing.assert_array_equal(k.view(np.uint8), fk.view(np.uint8))
+                np.testing.assert_array_equal(d, fd)
