@@ -120,6 +120,7 @@ def pmc_valu_table(root):
     if not m or m.group(1) != cur:
         return {}, "%s (stale: recorded for %s, loaded %s)" % (
             os.path.relpath(paths[-1], root), m.group(1)[:12] if m else "no library hash", (cur or "?")[:12])
+    acc = {}
     for block in re.split(r"\n(?=\S)", txt):
         lines = block.strip().split("\n")
         name = lines[0].replace("void ", "").replace("orbgpu::", "").strip()
@@ -134,6 +135,12 @@ def pmc_valu_table(root):
         for pre, st in (("k_knn2", "k_knn2"), ("k_octree", "k_octree"), ("k_finalize", "k_finalize")):
             if name.startswith(pre):
                 stage = st
+        # the small-list FAST kernel and its overflow pass make one stage (k_fast_cells<48>)
+        stage = re.sub(r"^k_fast_cells(?:_ovf)?<(\d+)(?:, (?:true|false))?>$", r"k_fast_cells<\1>", stage)
+        tot = acc.setdefault(stage, {})
+        for k, v in c.items():
+            tot[k] = tot.get(k, 0.0) + v
+    for stage, c in acc.items():
         cyc = c["GRBM_GUI_ACTIVE"] / 8.0
         out[stage] = {"valu_busy": round(c["SQ_ACTIVE_INST_VALU"] * 4.0 / 1024.0 / cyc, 3),
                       "valu_instr_per_launch": c.get("SQ_INSTS_VALU")}

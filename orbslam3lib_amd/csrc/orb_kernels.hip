@@ -860,7 +860,10 @@ __global__ __launch_bounds__(fast_threads<CP>()) void k_fast_cells_ovf(BatchArgs
     __shared__ int32_t wcnt[kFastThreads / 64];
     __shared__ int scratch[16];
     int* const cnt = a.fast_ovf_cnt + 2 * a.img0;  // [0] queued cells, [1] finished workgroups
-    const int nq = __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // written by the previous launch on this stream (complete before this one starts): a plain
+    // load; with nothing queued (the usual case) the launch ends here, no counter to reset
+    const int nq = *cnt;
+    if (nq == 0) return;
     for (int q = blockIdx.x; q < nq; q += gridDim.x) {
         const int2 e = a.fast_ovf[(long long)a.img0 * a.fast_n48 + q];
         fast_cell_one<CP, kList>(a, e.x, e.y, T, M, list, lut, emask, wcnt, scratch);

@@ -19,8 +19,11 @@ import re
 
 
 def stage_name(kernel):
+    """The bench stage a kernel belongs to: k_octree<NT> -> k_octree, k_knn2_mfma_pairs -> k_knn2,
+    k_fast_cells<48, true> and its overflow pass k_fast_cells_ovf<48> -> k_fast_cells<48>."""
     k = kernel.split("(")[0].replace("orbgpu::", "").replace("void ", "").strip()
     k = re.sub(r"^k_octree<\d+>$", "k_octree", k)
+    k = re.sub(r"^k_fast_cells(?:_ovf)?<(\d+)(?:, (?:true|false))?>$", r"k_fast_cells<\1>", k)
     return {"k_knn2_mfma_pairs": "k_knn2"}.get(k, k)
 
 
