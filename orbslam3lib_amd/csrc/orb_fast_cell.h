@@ -130,6 +130,7 @@ struct CellScratch {
     // u16 pairs (p0 | p1 << 16, p2 | p3 << 16), and the detection-pixel mask of each dword group
     const uint2* lut = nullptr;  // [16]
     const uint32_t* emask = nullptr;  // [ng <= 20]: 0x80 in the bytes of detection pixels
+    int32_t* wovf = nullptr;          // [waves]: capped lists, a wave's overflow flag
 };
 
 // List entries past cell_list_cap on the device: each wave's list is followed by 4 spare
@@ -258,6 +259,7 @@ template <int CP, int kCap = cell_list_cap<CP>(), class Pol>
 __host__ __device__ int fast_cell_detect(Pol& p, int sh, const CellGeom& g, int ini_th, int min_th,
                                          const CellScratch& cs, uint32_t* keys_out) {
     static_assert(kCap <= cell_list_cap<CP>(), "list capacity");
+    constexpr bool kCapped = kCap < cell_list_cap<CP>();
     const int rows = g.rows, cols = g.cols;
     uint8_t* T = cs.T;
     uint8_t* M = cs.M;
@@ -268,6 +270,7 @@ __host__ __device__ int fast_cell_detect(Pol& p, int sh, const CellGeom& g, int 
     const int tini = ini_th < 0 ? 0 : (ini_th > 255 ? 255 : ini_th);
     const int tmin = min_th < 0 ? 0 : (min_th > 255 ? 255 : min_th);
     const int W = p.nwaves(), w = p.wave(), L = p.wave_width(), lane = p.lane();
+    (void)lane;
 #if defined(__HIP_DEVICE_COMPILE__)
     // device: the pre-test takes 4 pixels per lane (fw_pretest4); a wave owns a contiguous
     // row-major range of (row, dword group) items, and its list starts after the detection
@@ -292,7 +295,9 @@ __host__ __device__ int fast_cell_detect(Pol& p, int sh, const CellGeom& g, int 
     const int i0 = w * nd / W, i1 = (w + 1) * nd / W;  // nd <= 4900, W <= 16: no overflow
 #endif
 #if defined(__HIP_DEVICE_COMPILE__)
-    uint16_t* list = cs.list + i0 + 4 * w;  // 4 spare entries after each wave's list
+    // 4 spare entries after each wave's list; a capped list gives each wave kCap / W entries
+    const int capw = kCap / W;
+    uint16_t* list = cs.list + (kCapped ? w * capw : i0) + 4 * w;
     uint16_t* sink = cs.list + kCap + 4 * W;  // 4 entries (fast_list_slack)
 #else
     uint16_t* list = cs.list + i0;
@@ -354,7 +359,7 @@ __host__ __device__ int fast_cell_detect(Pol& p, int sh, const CellGeom& g, int 
                 incl += __builtin_amdgcn_update_dpp(0, incl, 0x142, 0xA, 0xF, false); // row_bcast:15 -> rows 1, 3
                 incl += __builtin_amdgcn_update_dpp(0, incl, 0x143, 0xC, 0xF, false); // row_bcast:31 -> rows 2, 3
                 const int wave_total = __builtin_amdgcn_readlane(incl, 63);
-                if (kCap < cell_list_cap<CP>() && na + wave_total > kCap) {  // wave-uniform
+                if (kCapped && na + wave_total > capw) {  // wave-uniform
                     na = kFastOverflow;
                     break;
                 }
@@ -386,7 +391,7 @@ __host__ __device__ int fast_cell_detect(Pol& p, int sh, const CellGeom& g, int 
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the list is read by other lanes
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            if (kCap < cell_list_cap<CP>() && na == kFastOverflow) return kFastOverflow;
+            if (kCapped && na == kFastOverflow) return kFastOverflow;
         }
 #else
         for (int base = i0; base < i1; base += L) {
@@ -448,8 +453,17 @@ __host__ __device__ int fast_cell_detect(Pol& p, int sh, const CellGeom& g, int 
         }
         return make_int2(tot, before);
     };
+    // a capped list: the workgroup agrees on an overflow of any wave before its next barrier
+    auto overflowed = [&](int nbw) {
+        if (W == 1) return nbw == kFastOverflow;
+        if (lane == 0) cs.wovf[w] = nbw == kFastOverflow ? 1 : 0;
+        p.sync();
+        int any = 0;
+        for (int v = 0; v < W; ++v) any |= cs.wovf[v];
+        return any != 0;
+    };
     int nb = build(tini);
-    if (kCap < cell_list_cap<CP>() && nb == kFastOverflow) return kFastOverflow;
+    if (kCapped && overflowed(nb)) return kFastOverflow;
     p.sync();  // M complete: nonmax reads neighbours owned by other waves
     int2 cb = count_kept(nb, tini);
     int t = tini;
@@ -458,7 +472,7 @@ __host__ __device__ int fast_cell_detect(Pol& p, int sh, const CellGeom& g, int 
         p.sync();
         if (tmin < tini) {
             nb = build(tmin);
-            if (kCap < cell_list_cap<CP>() && nb == kFastOverflow) return kFastOverflow;
+            if (kCapped && overflowed(nb)) return kFastOverflow;
             p.sync();
         }
         cb = count_kept(nb, t);

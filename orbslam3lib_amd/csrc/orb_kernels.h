@@ -83,12 +83,13 @@ struct BatchArgs {
     int fast_n48;  // k_fast_cells records [0, fast_n48) run the 48-byte FAST tile,
     int fast_n64;  // [fast_n48, fast_n64) the 64-byte one, the rest the 80-byte one (records are
                    // grouped by tile, levels in order inside each group)
-    // k_fast_cells' small-list path (48-byte tile): queued overflow cells [img][fast_n48] as
+    // k_fast_cells' small-list path (48- and 64-byte tiles): queued overflow cells [img][fast_qcap] as
     // (image, cell), counters [2 * img0] per launch (queued, finished overflow workgroups);
     // fast_small: -1 for launches of more than kFastMergeMaxImages images, 0 never, 1 always
     // (diagnostics); fast_ovf_all (diagnostics): every small-path cell goes to the overflow pass
     int2* fast_ovf;
     int* fast_ovf_cnt;
+    int fast_qcap;  // queue entries per image: the larger tile's cell count
     int fast_small, fast_ovf_all;
     unsigned long long* octdbg;      // diagnostic: [img][kMaxLevels][8] phase clocks, or null
     int oct_lds_nodes;               // node capacity of k_octree's dynamic LDS (0: all global)
@@ -217,7 +218,9 @@ constexpr int kOdBlockKps = 3 * kOdKpBlock;
 
 constexpr int kOctLdsKeys = 16384;  // per-key node labels (u16) kept in LDS up to this many keys
 constexpr int kFastMergeMaxImages = 4;  // launches this small run the 48/64 FAST cells as one launch
-constexpr int kFastSmallList = 512;     // candidate list of the small-list k_fast_cells<48> (orb_kernels.hip)
+// candidate list of the small-list k_fast_cells<48> / <64> (orb_kernels.hip), split over the waves
+template <int CP>
+constexpr int kFastSmallList() { return CP == 48 ? 512 : 1280; }
 constexpr int kFastOvfBlocks = 32;      // workgroups of k_fast_cells_ovf
 constexpr int kOctSmallThreads = 256;  // default workgroup size of the short-level k_octree launch
 constexpr int kOctSmallMinImages = 32;  // launches with fewer images keep the 512-thread shape

@@ -777,7 +777,8 @@ hipError_t launch_pyr_tail(const BatchArgs& a, hipStream_t s) {
 template <int CP, int kCap>
 __device__ __attribute__((always_inline)) inline int fast_cell_one(const BatchArgs& a, int img, int gcell, uint8_t* T,
                                                                    uint8_t* M, uint16_t* list, uint2* lut,
-                                                                   uint32_t* emask, int32_t* wcnt, int* scratch) {
+                                                                   uint32_t* emask, int32_t* wcnt, int32_t* wovf,
+                                                                   int* scratch) {
     constexpr int kFastThreads = fast_threads<CP>();
     // the cell's record (host: the cell loop's geometry, :807-821)
     const int4 e0 = a.rtab[a.fast_tab_off + 2 * gcell];
@@ -810,28 +811,28 @@ __device__ __attribute__((always_inline)) inline int fast_cell_one(const BatchAr
     };
     FixedDevPolicy<kFastThreads> p{{scratch}};
     fast_cell_tables<CP>(g, sh, lut, emask);  // synced with the ROI staging (fast_cell_run)
-    CellScratch cs{T, M, list, wcnt, lut, emask};
+    CellScratch cs{T, M, list, wcnt, lut, emask, wovf};
     const int n = fast_cell_run<CP, kCap>(p, src, G.pitch, sh, dword_ok, g, a.ini_th, a.min_th, cs, key_out, ld16);
     if (n != kFastOverflow && threadIdx.x == 0) *cnt_out = n;
     return n;
 }
 
 // k_fast_cells<CP, kSmall>: one workgroup per (image, cell) of the tile's cells.  kSmall (the
-// 48-byte tile of launches of more than kFastMergeMaxImages images): a kFastSmallList-entry
-// candidate list (LDS 5.9 instead of 8.4 KB per workgroup: 27 instead of 19 resident per CU;
-// round 6: one workgroup per CU more or less moved this kernel by ~20%).  A cell whose pre-test
-// passes more pixels than that (none of the bench frames' cells at iniThFAST, where the most is
-// 441 of 1225) is queued (a.fast_ovf, per-launch slice by img0) and redone by k_fast_cells_ovf.
+// 48- and 64-byte tiles of launches of more than kFastMergeMaxImages images): a capped candidate
+// list, kFastSmallList<CP> entries split over the waves (48: LDS 5.9 instead of 8.4 KB per
+// workgroup, 26 instead of 19 resident per CU; 64: 11 instead of 15.2 KB; round 6: residency
+// moves this kernel by up to ~20%).  A cell whose pre-test passes more pixels than fit (none of
+// the bench frames' cells at iniThFAST, where the most is 441 of 1225 in a 48-byte cell) is
+// queued (a.fast_ovf, per-launch slice by img0) and redone by k_fast_cells_ovf.
 template <int CP, bool kSmall>
 __global__ __launch_bounds__(fast_threads<CP>()) void k_fast_cells(BatchArgs a, int cell0, uint32_t ncell_magic) {
-    constexpr int kList = kSmall ? kFastSmallList : cell_list_cap<CP>(), kFastThreads = fast_threads<CP>();
-    static_assert(!kSmall || kFastThreads == 64, "the small list is one wave's");
+    constexpr int kList = kSmall ? kFastSmallList<CP>() : cell_list_cap<CP>(), kFastThreads = fast_threads<CP>();
     __shared__ __attribute__((aligned(16))) uint8_t T[CP * CP];
     __shared__ __attribute__((aligned(16))) uint8_t M[CP * CP];  // 16-byte rows when CP % 16 == 0
     __shared__ __attribute__((aligned(8))) uint16_t list[kList + fast_list_slack(kFastThreads / 64)];
     __shared__ uint2 lut[16];
     __shared__ uint32_t emask[32];
-    __shared__ int32_t wcnt[kFastThreads / 64];
+    __shared__ int32_t wcnt[kFastThreads / 64], wovf[kFastThreads / 64];
     __shared__ int scratch[16];
     const int wg = xcd_remap(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * gridDim.y);
     // wg / gridDim.x by the host's magic multiplier (exact for wg < 2^32 / gridDim.x)
@@ -839,10 +840,10 @@ __global__ __launch_bounds__(fast_threads<CP>()) void k_fast_cells(BatchArgs a, 
     const int img = a.img0 + irel;
     const int gcell = cell0 + (wg - irel * (int)gridDim.x);  // flattened over the levels
     const int n = (kSmall && a.fast_ovf_all) ? kFastOverflow  // diagnostics: every cell to the full-list pass
-                                             : fast_cell_one<CP, kList>(a, img, gcell, T, M, list, lut, emask, wcnt, scratch);
+                                             : fast_cell_one<CP, kList>(a, img, gcell, T, M, list, lut, emask, wcnt, wovf, scratch);
     if (kSmall && n == kFastOverflow && threadIdx.x == 0) {
         const int q = __hip_atomic_fetch_add(a.fast_ovf_cnt + 2 * a.img0, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        a.fast_ovf[(long long)a.img0 * a.fast_n48 + q] = make_int2(img, gcell);
+        a.fast_ovf[(long long)a.img0 * a.fast_qcap + q] = make_int2(img, gcell);
     }
 }
 
@@ -857,7 +858,7 @@ __global__ __launch_bounds__(fast_threads<CP>()) void k_fast_cells_ovf(BatchArgs
     __shared__ __attribute__((aligned(8))) uint16_t list[kList + fast_list_slack(kFastThreads / 64)];
     __shared__ uint2 lut[16];
     __shared__ uint32_t emask[32];
-    __shared__ int32_t wcnt[kFastThreads / 64];
+    __shared__ int32_t wcnt[kFastThreads / 64], wovf[kFastThreads / 64];
     __shared__ int scratch[16];
     int* const cnt = a.fast_ovf_cnt + 2 * a.img0;  // [0] queued cells, [1] finished workgroups
     // written by the previous launch on this stream (complete before this one starts): a plain
@@ -865,8 +866,8 @@ __global__ __launch_bounds__(fast_threads<CP>()) void k_fast_cells_ovf(BatchArgs
     const int nq = *cnt;
     if (nq == 0) return;
     for (int q = blockIdx.x; q < nq; q += gridDim.x) {
-        const int2 e = a.fast_ovf[(long long)a.img0 * a.fast_n48 + q];
-        fast_cell_one<CP, kList>(a, e.x, e.y, T, M, list, lut, emask, wcnt, scratch);
+        const int2 e = a.fast_ovf[(long long)a.img0 * a.fast_qcap + q];
+        fast_cell_one<CP, kList>(a, e.x, e.y, T, M, list, lut, emask, wcnt, wovf, scratch);
         __syncthreads();  // the LDS scratch is reused by the next cell
     }
     if (threadIdx.x == 0) {
@@ -1754,12 +1755,17 @@ hipError_t launch_fast_cells(const BatchArgs& a, int tile, hipStream_t s) {
                                                                                                       : fast_threads<kCellMax>());
     const uint32_t d = (uint32_t)(c1 - c0);
     const uint32_t magic = d > 1 ? 0xFFFFFFFFu / d + 1u : 0u;  // ceil(2^32 / d) for d >= 2
-    // the small-list 48-byte kernel and its overflow pass for the batch shape (a.fast_small)
-    const bool small = tile == kCellPitchTiny && a.fast_ovf &&
+    // the small-list 48- and 64-byte kernels and their overflow passes for the batch shape
+    // (a.fast_small); the two tiles' launches share the queue slot (one after the other on the
+    // stream, each overflow pass resets it)
+    const bool small = (tile == kCellPitchTiny || tile == kCellPitchSmall) && a.fast_ovf &&
                        (a.fast_small > 0 || (a.fast_small < 0 && a.nimages > kFastMergeMaxImages));
-    if (small) {
+    if (small && tile == kCellPitchTiny) {
         hipLaunchKernelGGL((k_fast_cells<kCellPitchTiny, true>), grid, block, 0, s, a, c0, magic);
         hipLaunchKernelGGL(k_fast_cells_ovf<kCellPitchTiny>, dim3(kFastOvfBlocks), block, 0, s, a);
+    } else if (small) {
+        hipLaunchKernelGGL((k_fast_cells<kCellPitchSmall, true>), grid, block, 0, s, a, c0, magic);
+        hipLaunchKernelGGL(k_fast_cells_ovf<kCellPitchSmall>, dim3(kFastOvfBlocks), block, 0, s, a);
     } else if (tile == kCellPitchTiny) hipLaunchKernelGGL((k_fast_cells<kCellPitchTiny, false>), grid, block, 0, s, a, c0, magic);
     else if (tile == kCellPitchSmall) hipLaunchKernelGGL((k_fast_cells<kCellPitchSmall, false>), grid, block, 0, s, a, c0, magic);
     else hipLaunchKernelGGL((k_fast_cells<kCellMax, false>), grid, block, 0, s, a, c0, magic);

@@ -342,7 +342,7 @@ int alloc_all(orbgpu_ctx* c, int n_images) {
     {  // FAST overflow queue [img][fast_n48] (image, cell) and two counters per image slot (zeroed
        // once: k_fast_cells_ovf's last workgroup resets its launch's pair)
         void* before = c->fastovf.p;
-        const size_t ent = ni * (size_t)std::max(c->A.fast_n48, 1) * 8;
+        const size_t ent = ni * (size_t)std::max(c->A.fast_qcap, 1) * 8;
         r |= c->fastovf.ensure(ent + ni * 8 + 256);
         if (!r && c->fastovf.p != before && hipMemset(c->fastovf.p, 0, c->fastovf.bytes) != hipSuccess) r = -1;
     }
@@ -624,6 +624,7 @@ int set_geometry(orbgpu_ctx* c, int w, int h) {
     }
     A.fast_n48 = tier_end[0];
     A.fast_n64 = tier_end[1];
+    A.fast_qcap = std::max(tier_end[0], tier_end[1] - tier_end[0]);
     A.total_tiles = tile_first;
     A.total_od_blocks = od_first;
     A.od_tab_off = (int)c->rtab_host.size();
@@ -664,7 +665,7 @@ int set_geometry(orbgpu_ctx* c, int w, int h) {
     A.laps = c->laps.as<int32_t>();
     A.fast_ovf = c->fastovf.as<int2>();
     A.fast_ovf_cnt = reinterpret_cast<int*>(c->fastovf.as<uint8_t>() + (size_t)std::max(c->max_images, 1) *
-                                                                           std::max(A.fast_n48, 1) * 8);
+                                                                           std::max(A.fast_qcap, 1) * 8);
     A.fast_small = c->fast_small;
     A.fast_ovf_all = c->fast_ovf_all ? 1 : 0;
     c->gw = w;
