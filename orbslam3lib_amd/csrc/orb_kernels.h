@@ -89,7 +89,7 @@ struct BatchArgs {
     // (diagnostics); fast_ovf_all (diagnostics): every small-path cell goes to the overflow pass
     int2* fast_ovf;
     int* fast_ovf_cnt;
-    int fast_qcap;  // queue entries per image: the larger tile's cell count
+    int fast_qcap;  // queue entries per image: the 48- and 64-byte tiles' cells
     int fast_small, fast_ovf_all;
     unsigned long long* octdbg;      // diagnostic: [img][kMaxLevels][8] phase clocks, or null
     int oct_lds_nodes;               // node capacity of k_octree's dynamic LDS (0: all global)

@@ -1760,12 +1760,17 @@ hipError_t launch_fast_cells(const BatchArgs& a, int tile, hipStream_t s) {
     // stream, each overflow pass resets it)
     const bool small = (tile == kCellPitchTiny || tile == kCellPitchSmall) && a.fast_ovf &&
                        (a.fast_small > 0 || (a.fast_small < 0 && a.nimages > kFastMergeMaxImages));
+    // one overflow pass after both tiles: the 64-byte full-list kernel redoes the cells either
+    // queued (every 48-byte cell fits the 64-byte tile, as in the merged launch of small batches)
+    const dim3 oblock(fast_threads<kCellPitchSmall>());
     if (small && tile == kCellPitchTiny) {
         hipLaunchKernelGGL((k_fast_cells<kCellPitchTiny, true>), grid, block, 0, s, a, c0, magic);
-        hipLaunchKernelGGL(k_fast_cells_ovf<kCellPitchTiny>, dim3(kFastOvfBlocks), block, 0, s, a);
+        int d0, d1;
+        fast_cell_range(a, kCellPitchSmall, &d0, &d1);
+        if (d1 <= d0) hipLaunchKernelGGL(k_fast_cells_ovf<kCellPitchSmall>, dim3(kFastOvfBlocks), oblock, 0, s, a);
     } else if (small) {
         hipLaunchKernelGGL((k_fast_cells<kCellPitchSmall, true>), grid, block, 0, s, a, c0, magic);
-        hipLaunchKernelGGL(k_fast_cells_ovf<kCellPitchSmall>, dim3(kFastOvfBlocks), block, 0, s, a);
+        hipLaunchKernelGGL(k_fast_cells_ovf<kCellPitchSmall>, dim3(kFastOvfBlocks), oblock, 0, s, a);
     } else if (tile == kCellPitchTiny) hipLaunchKernelGGL((k_fast_cells<kCellPitchTiny, false>), grid, block, 0, s, a, c0, magic);
     else if (tile == kCellPitchSmall) hipLaunchKernelGGL((k_fast_cells<kCellPitchSmall, false>), grid, block, 0, s, a, c0, magic);
     else hipLaunchKernelGGL((k_fast_cells<kCellMax, false>), grid, block, 0, s, a, c0, magic);

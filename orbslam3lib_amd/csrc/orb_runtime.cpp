@@ -624,7 +624,7 @@ int set_geometry(orbgpu_ctx* c, int w, int h) {
     }
     A.fast_n48 = tier_end[0];
     A.fast_n64 = tier_end[1];
-    A.fast_qcap = std::max(tier_end[0], tier_end[1] - tier_end[0]);
+    A.fast_qcap = tier_end[1];  // the 48- and 64-byte tiles' cells share one queue per launch
     A.total_tiles = tile_first;
     A.total_od_blocks = od_first;
     A.od_tab_off = (int)c->rtab_host.size();
