@@ -30,19 +30,24 @@ allrows = list(csv.DictReader(open(sys.argv[2])))
 rows = [r for r in allrows if stage_of(r["Kernel_Name"]) == name or
         (name not in ("k_fast_cells<48>", "k_fast_cells<64>", "k_fast_cells<80>") and name in r["Kernel_Name"])]
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-# a small-list k_fast_cells<48> launch is followed on its stream by its overflow pass: the stage the
-# bench times (HIP events around both) ends with that pass
-ovf = sorted((r for r in allrows if "k_fast_cells_ovf<" in r["Kernel_Name"]), key=lambda r: int(r["Start_Timestamp"]))
+# the overflow pass of the small-list FAST kernels runs right after the last FAST launch of a
+# step on its stream (the 64-byte one): the stage the bench times (HIP events around its
+# launches) ends with that pass, so it is added where it is the next kernel on the stream
+by_stream = {}
+for r in sorted(allrows, key=lambda r: int(r["Start_Timestamp"])):
+    by_stream.setdefault(r["Stream_Id"], []).append(r)
+nxt = {}
+for lst in by_stream.values():
+    for a, b in zip(lst, lst[1:]):
+        nxt[id(a)] = b
 grid = lambda r: (r["Grid_Size_X"], r["Grid_Size_Y"], r["Grid_Size_Z"])
 
 
 def dur(r):
     end = int(r["End_Timestamp"])
-    if name.startswith("k_fast_cells") and ", true>" in r["Kernel_Name"]:
-        for o in ovf:
-            if o["Stream_Id"] == r["Stream_Id"] and int(o["Start_Timestamp"]) >= end:
-                end = int(o["End_Timestamp"])
-                break
+    b = nxt.get(id(r))
+    if b is not None and "k_fast_cells_ovf<" in b["Kernel_Name"]:
+        end = int(b["End_Timestamp"])
     return (end - int(r["Start_Timestamp"])) / 1e3
 n_ser = roof.get("launches") or 3  # serialized launches (3 steps x launches per step)
 per_step = max(1, n_ser // 3)
