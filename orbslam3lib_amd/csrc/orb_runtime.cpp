@@ -339,7 +339,7 @@ int alloc_all(orbgpu_ctx* c, int n_images) {
     r |= c->midx2.ensure(np * c->out_cap * 4 + 256);
     r |= c->mdist2.ensure(np * c->out_cap * 4 + 256);
     r |= c->mnq.ensure(np * 4 + 64);
-    {  // FAST overflow queue [img][fast_n48] (image, cell) and two counters per image slot (zeroed
+    {  // FAST overflow queue [img][fast_qcap] (image, cell) and two counters per image slot (zeroed
        // once: k_fast_cells_ovf's last workgroup resets its launch's pair)
         void* before = c->fastovf.p;
         const size_t ent = ni * (size_t)std::max(c->A.fast_qcap, 1) * 8;
