@@ -625,39 +625,61 @@ __device__ inline void tail_blur(const uint8_t* buf, int P, const LevelGeom& G, 
                          as_u16x2(56u | (48u << 16)), as_u16x2(34u | (18u << 16))};
     const u16x2 WO[4] = {as_u16x2(18u | (34u << 16)), as_u16x2(48u | (56u << 16)),
                          as_u16x2(48u | (34u << 16)), as_u16x2(18u | (0u << 16))};
-    auto row = [&](int y) { return buf + __mul24(min(max(refl101(y, G.h), 0), G.h - 1), P); };
+    // REFLECT_101 of rows -4 .. h + 4 as min(|y|, 2h - 2 - |y|): one reflection suffices, every
+    // level has >= 2 kEdge + 4 rows (the host's level check); rows >= 0 skip the |y|
+    const int h2 = 2 * G.h - 2;
+    auto row = [&](int y) {
+        const int ay = max(y, -y);
+        return buf + __mul24(min(ay, h2 - ay), P);
+    };
+    auto row_lo = [&](int y) { return buf + __mul24(min(y, h2 - y), P); };
     for (int t0 = 0; t0 < nq * nseg; t0 += kTailThreads) {
         const int t = t0 + (int)threadIdx.x;
         const int sg = t / nq, cq = t - sg * nq;  // one division per task
         if (sg >= nseg) break;
         const int y0 = sg * R, y1 = min(y0 + R, G.h);
-        uint32_t V[5][4];
+        // the last five row pairs' sums in five register sets, the loop unrolled by five so that
+        // each step names them in rotated order (no register moves between rows)
+        uint32_t V0[4], V1[4], V2[4], V3[4], V4[4];
+        tail_hpair(row(y0 - 4), row(y0 - 3), cq, V0);
+        tail_hpair(row(y0 - 2), row(y0 - 1), cq, V1);
+        tail_hpair(row(y0), row(y0 + 1), cq, V2);
+        tail_hpair(row(y0 + 2), row(y0 + 3), cq, V3);
+        uint8_t* d = dst + plane_off(y0, G.bpitch, 4 * cq);
+        using Pair4 = uint32_t[4];
+        // output row from pairs p0 .. p3 (weights W): 4 columns, bytes 2 of the sums
+        auto vsum = [&](const Pair4& p0, const Pair4& p1, const Pair4& p2, const Pair4& p3, const u16x2* W) {
+            uint32_t sv[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) tail_hpair(row(y0 - 4 + 2 * j), row(y0 - 3 + 2 * j), cq, V[j]);
-        const int x = 4 * cq;
-        uint8_t* d = dst + plane_off(y0, G.bpitch, x);
-        for (int y = y0; y < y1; y += 2) {
-            tail_hpair(row(y + 4), row(y + 5), cq, V[4]);  // pair m + 4
-#pragma unroll
-            for (int o = 0; o < 2; ++o) {
-                uint32_t sv[4];
-#pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    uint32_t acc = 1u << 15;
-#pragma unroll
-                    for (int k = 0; k < 4; ++k)
-                        acc = __builtin_amdgcn_udot2(as_u16x2(V[o + k][c]), o ? WO[k] : WE[k], acc, false);
-                    sv[c] = acc;
-                }
-                const uint32_t lo = __builtin_amdgcn_perm(sv[1], sv[0], 0x0c0c0602u);
-                const uint32_t hi = __builtin_amdgcn_perm(sv[3], sv[2], 0x0c0c0602u);
-                if (y + o < y1) *reinterpret_cast<uint32_t*>(d + o * G.bpitch) = lo | (hi << 16);
+            for (int c = 0; c < 4; ++c) {
+                uint32_t acc = 1u << 15;
+                acc = __builtin_amdgcn_udot2(as_u16x2(p0[c]), W[0], acc, false);
+                acc = __builtin_amdgcn_udot2(as_u16x2(p1[c]), W[1], acc, false);
+                acc = __builtin_amdgcn_udot2(as_u16x2(p2[c]), W[2], acc, false);
+                acc = __builtin_amdgcn_udot2(as_u16x2(p3[c]), W[3], acc, false);
+                sv[c] = acc;
             }
+            return __builtin_amdgcn_perm(sv[1], sv[0], 0x0c0c0602u) | __builtin_amdgcn_perm(sv[3], sv[2], 0x06020c0cu);
+        };
+        // rows y, y + 1 from pairs m .. m + 3 (even weights) and m + 1 .. m + 4 (odd), pair m + 4
+        // (rows y + 4, y + 5) loaded into n
+        auto step = [&](const Pair4& a, const Pair4& b, const Pair4& c, const Pair4& e, Pair4& n, int y) {
+            tail_hpair(row_lo(y + 4), row_lo(y + 5), cq, n);
+            *reinterpret_cast<uint32_t*>(d) = vsum(a, b, c, e, WE);
+            if (y + 1 < y1) *reinterpret_cast<uint32_t*>(d + G.bpitch) = vsum(b, c, e, n, WO);
             d += 2 * G.bpitch;
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-#pragma unroll
-                for (int c = 0; c < 4; ++c) V[j][c] = V[j + 1][c];
+        };
+        for (int y = y0;;) {  // y0 < y1: at least one step
+            step(V0, V1, V2, V3, V4, y);
+            if ((y += 2) >= y1) break;
+            step(V1, V2, V3, V4, V0, y);
+            if ((y += 2) >= y1) break;
+            step(V2, V3, V4, V0, V1, y);
+            if ((y += 2) >= y1) break;
+            step(V3, V4, V0, V1, V2, y);
+            if ((y += 2) >= y1) break;
+            step(V4, V0, V1, V2, V3, y);
+            if ((y += 2) >= y1) break;
         }
     }
 }
