@@ -39,7 +39,6 @@ constexpr PatternTable make_pattern() {
     for (int i = 0; i < 1024; ++i) t.v[i] = (int8_t)(hexval(h[2 * i]) * 16 + hexval(h[2 * i + 1]));
     return t;
 }
-__constant__ PatternTable c_pattern = make_pattern();
 
 // umax[] of the ORBextractor ctor (ORBextractor_old.cc:455-470) for HALF_PATCH_SIZE = 15.
 __constant__ int c_umax[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};
@@ -1085,6 +1084,33 @@ __device__ inline int od_sum(int v) {
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
+// k_orient_desc's two LDS tables, built at compile time and copied once per workgroup (building
+// them in the kernel took ~200 VALU per wave, comparable to a whole keypoint pass):
+//   rng[m * 17 + n]: 0xFF in bytes [m, n) of a 16-byte chunk (none if n <= m);
+//   pat[b * kOdLanes + lane]: float bit patterns {x0, x1, y0, y1} of test pair 8 lane + b.
+struct OdTables {
+    uint32_t rng[17 * 17][4];
+    uint32_t pat[kOdPairs * kOdLanes][4];
+};
+constexpr OdTables make_od_tables() {
+    OdTables t{};
+    for (int m = 0; m < 17; ++m)
+        for (int n = 0; n < 17; ++n)
+            for (int j = 0; j < 16; ++j)
+                if (j >= m && j < n) t.rng[m * 17 + n][j >> 2] |= 0xFFu << (8 * (j & 3));
+    const PatternTable pt = make_pattern();
+    for (int b = 0; b < kOdPairs; ++b)
+        for (int lane = 0; lane < kOdLanes; ++lane) {
+            const int8_t* pv = pt.v + 4 * (kOdPairs * lane + b);  // x0, y0, x1, y1
+            t.pat[b * kOdLanes + lane][0] = __builtin_bit_cast(uint32_t, (float)pv[0]);
+            t.pat[b * kOdLanes + lane][1] = __builtin_bit_cast(uint32_t, (float)pv[2]);
+            t.pat[b * kOdLanes + lane][2] = __builtin_bit_cast(uint32_t, (float)pv[1]);
+            t.pat[b * kOdLanes + lane][3] = __builtin_bit_cast(uint32_t, (float)pv[3]);
+        }
+    return t;
+}
+__constant__ OdTables c_od_tab = make_od_tables();
+
 // cv::KeyPoint as written to the outputs (orbgpu_keypoint): pt.x, pt.y, size, angle, response,
 // octave, class_id
 struct KP28 {
@@ -1160,22 +1186,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
     // m_01 = sum v s.
     __shared__ __attribute__((aligned(16))) uint4 s_rng[17][17];  // bytes [m, n) of 16 (none if n <= m)
     __shared__ __attribute__((aligned(16))) uint4 s_pat[kOdPairs][kOdLanes];
-    for (int e = threadIdx.x; e < 17 * 17; e += 256) {
-        const int m = e / 17, n = e - 17 * m;
-        uint32_t w4[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            w4[k] = 0;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) w4[k] |= (4 * k + j >= m && 4 * k + j < n ? 0xFFu : 0u) << (8 * j);
-        }
-        s_rng[m][n] = make_uint4(w4[0], w4[1], w4[2], w4[3]);
-    }
-    {
-        const int8_t* pv = c_pattern.v + 4 * threadIdx.x;  // x0, y0, x1, y1 of pair threadIdx.x
-        s_pat[threadIdx.x % kOdPairs][threadIdx.x / kOdPairs] = make_uint4(__float_as_uint((float)pv[0]), __float_as_uint((float)pv[2]),
-                                        __float_as_uint((float)pv[1]), __float_as_uint((float)pv[3]));
-    }
+    static_assert(kOdPairs * kOdLanes == 256 && 17 * 17 <= 2 * 256, "table copy: one / two entries per thread");
+    const uint4* rng_src = reinterpret_cast<const uint4*>(c_od_tab.rng);
+    const uint4 rng0 = rng_src[threadIdx.x];
+    const uint4 pat0 = reinterpret_cast<const uint4*>(c_od_tab.pat)[threadIdx.x];
+    if (threadIdx.x < 17 * 17 - 256) (&s_rng[0][0])[threadIdx.x + 256] = rng_src[threadIdx.x + 256];
+    (&s_rng[0][0])[threadIdx.x] = rng0;
+    (&s_pat[0][0])[threadIdx.x] = pat0;
     __syncthreads();
     // this lane's three chunk slots: row v, chunk bytes [lo + a, hi + a) clamped to [0, 16) are
     // the disc span (lo = 15 - d - 16 part, hi = 16 + d - 16 part, d = umax[|v|], -1 past the
