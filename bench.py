@@ -675,16 +675,23 @@ def main():
             ur_u = be.stereo_result(u)[0] if stereo is not None else None
             uniq_mps.append(synth.map_points(xy_u, kl_u["octave"], dl_u, ur_u, n=args.map_points, seed=7 + u))
         mp_list = [uniq_mps[p % U] for p in range(P)]
+        # the timed calls pass the points in the ABI's form (one array + offsets, as a caller that
+        # keeps its local map packed would); the list form adds a host concatenation per call
+        mp_rows = (np.concatenate(mp_list), np.concatenate([[0], np.cumsum([len(m) for m in mp_list])]))
         use_ur = stereo is not None
         be.undistort_grid(EUROC_K, EUROC_D)
         be.search_by_projection(mp_list, image_step=2, use_uright=use_ur)
         be.synchronize()
+        t_l0 = time.perf_counter()
+        be.search_by_projection(mp_list, image_step=2, use_uright=use_ur)
+        be.synchronize()
+        t_list = time.perf_counter() - t_l0
         be.set_profiling(True, stages=["k_sbp"])
         be.reset_stage_times()
         barrier(dist)
         q0 = time.perf_counter()
         for _ in range(args.steps):
-            be.search_by_projection(mp_list, image_step=2, use_uright=use_ur)
+            be.search_by_projection(mp_rows, image_step=2, use_uright=use_ur)
         be.synchronize()
         q1 = time.perf_counter()
         q_el = max_over_ranks(dist, q1 - q0)
@@ -697,6 +704,7 @@ def main():
                "value": round(sum_over_ranks(dist, n_mp) / (k_ms * 1e-3) / 1e6, 3) if k_ms else None,
                "unit": "Mmappoints/s", "kernel_ms_per_step": round(k_ms, 4) if k_ms else None,
                "call_ms_per_step": round(q_el / args.steps * 1e3, 4),
+               "call_ms_list_form": round(t_list * 1e3, 4),
                "map_points_per_frame": args.map_points, "frames_per_step": P, "nmatches_frame0": nm0}
         # the two-camera form (Nleft != -1, the fisheye rig): grids on the raw positions, both
         # windows per point, stereo partners from a synthetic one-to-one pairing

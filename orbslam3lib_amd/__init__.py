@@ -635,17 +635,34 @@ class BatchExtractor:
                                               C.byref(n)))
         return tuple(a[:n.value] for a in r)
 
-    def search_by_projection(self, map_points, image_step=2, use_uright=True, kp_block=None, th=1.0,
-                             nnratio=0.8, far_points=False, th_far=50.0, stream=None):
-        """ORBmatcher(nnratio).SearchByProjection(F, vpMapPoints, th, bFarPoints, thFarPoints)
-        (ORBmatcher.cc:44-214) for frames f = images f * image_step after undistort_grid();
-        map_points: list (one per frame) of MAP_POINT_DTYPE arrays; kp_block: optional list of u8
-        arrays (1 = keypoint already holds a map point with observations)."""
+    @staticmethod
+    def _map_point_rows(map_points):
+        """(points, offsets, n_frames) for the C ABI: map_points is either a list (one per frame)
+        of MAP_POINT_DTYPE arrays, concatenated here, or a tuple (points, offsets) already in the
+        ABI's form -- every frame's points in one MAP_POINT_DTYPE array and int32 offsets [n + 1] --
+        which is passed through without a host copy."""
+        if isinstance(map_points, tuple):
+            mps, off = map_points
+            mps = np.ascontiguousarray(mps, MAP_POINT_DTYPE)
+            off = np.ascontiguousarray(off, np.int32)
+            if off.ndim != 1 or len(off) < 1 or off[0] != 0 or off[-1] != len(mps) or np.any(np.diff(off) < 0):
+                raise ValueError("map point offsets must start at 0, not decrease and end at len(points)")
+            return mps, off, len(off) - 1
         nf = len(map_points)
         mps = np.ascontiguousarray(np.concatenate([np.asarray(m, MAP_POINT_DTYPE) for m in map_points])
                                    if nf else np.zeros(0, MAP_POINT_DTYPE))
         off = np.zeros(nf + 1, np.int32)
         off[1:] = np.cumsum([len(m) for m in map_points])
+        return mps, off, nf
+
+    def search_by_projection(self, map_points, image_step=2, use_uright=True, kp_block=None, th=1.0,
+                             nnratio=0.8, far_points=False, th_far=50.0, stream=None):
+        """ORBmatcher(nnratio).SearchByProjection(F, vpMapPoints, th, bFarPoints, thFarPoints)
+        (ORBmatcher.cc:44-214) for frames f = images f * image_step after undistort_grid();
+        map_points: list (one per frame) of MAP_POINT_DTYPE arrays, or (points, offsets) with every
+        frame's points in one array (_map_point_rows); kp_block: optional list of u8 arrays (1 =
+        keypoint already holds a map point with observations)."""
+        mps, off, nf = self._map_point_rows(map_points)
         blk, stride = None, 0
         if kp_block is not None:
             stride = max(1, max(len(b) for b in kp_block))
@@ -662,12 +679,8 @@ class BatchExtractor:
         """The two-camera SearchByProjection (Nleft != -1, ORBmatcher.cc:59-214) on every stereo
         pair of the last run() (grids from undistort_grid(K, ())); left_to_right / right_to_left:
         per pair int32 arrays (mvLeftToRightMatch / mvRightToLeftMatch); kp_block per pair over
-        Nleft + Nright keypoints."""
-        nf = len(map_points)
-        mps = np.ascontiguousarray(np.concatenate([np.asarray(m, MAP_POINT_DTYPE) for m in map_points])
-                                   if nf else np.zeros(0, MAP_POINT_DTYPE))
-        off = np.zeros(nf + 1, np.int32)
-        off[1:] = np.cumsum([len(m) for m in map_points])
+        Nleft + Nright keypoints; map_points as for search_by_projection."""
+        mps, off, nf = self._map_point_rows(map_points)
 
         def rows(lst, dtype, fill):
             if lst is None:

@@ -126,6 +126,39 @@ def _gpu_case(oracle, be, n_frames, stereo, th, far, th_far, blocked, n_mp, seed
         gm, gnm = be.projection_matches(f)
         np.testing.assert_array_equal(gm, m, err_msg="frame %d" % f)
         assert gnm == nm, (f, gnm, nm)
+    # the same call with the points already in the ABI's form (one array + offsets)
+    off = np.concatenate([[0], np.cumsum([len(x) for x in mps_all])]).astype(np.int32)
+    be.search_by_projection((np.concatenate(mps_all), off), image_step=2, use_uright=stereo,
+                            kp_block=blks if blocked else None, th=th, nnratio=0.8, far_points=far,
+                            th_far=th_far)
+    be.synchronize()
+    for f, (kps, desc, xy, ur) in enumerate(frames):
+        _, b, _, cs, ci = oracle.undistort_grid(kps, K_, D_, 640, 480)
+        m, nm = oracle.search_by_projection(mps_all[f], xy, kps["octave"], desc, ur, b, cs, ci, blks[f], th,
+                                            0.8, far, th_far)
+        gm, gnm = be.projection_matches(f)
+        np.testing.assert_array_equal(gm, m, err_msg="frame %d (points + offsets)" % f)
+        assert gnm == nm
+
+
+def test_map_point_rows_forms():
+    """The wrapper's two map-point forms give the ABI the same (points, offsets); malformed
+    offsets are refused before any device call."""
+    import orbslam3lib_amd as og
+    rng = np.random.default_rng(3)
+    parts = []
+    for n in (5, 0, 7):
+        a = np.zeros(n, og.MAP_POINT_DTYPE)
+        a.view(np.uint8)[:] = rng.integers(0, 256, a.nbytes, dtype=np.uint8)
+        parts.append(a)
+    m1, o1, n1 = og.BatchExtractor._map_point_rows(parts)
+    m2, o2, n2 = og.BatchExtractor._map_point_rows((np.concatenate(parts), np.array([0, 5, 5, 12])))
+    assert n1 == n2 == 3 and o1.dtype == o2.dtype == np.int32
+    np.testing.assert_array_equal(o1, o2)
+    assert m1.tobytes() == m2.tobytes()
+    for bad in ([1, 5, 5, 12], [0, 5, 4, 12], [0, 5, 5, 11]):
+        with pytest.raises(ValueError):
+            og.BatchExtractor._map_point_rows((np.concatenate(parts), np.array(bad)))
 
 
 @pytest.mark.gpu
